@@ -1,0 +1,101 @@
+/*
+ * smg.h -- C-ABI of libsmg.so, the MI355X (gfx950) kernels of the SM_distributed molecule-annotation
+ * hot path: ion-image generation (formula_imager_segm.compute_sf_images) and MSM scoring
+ * (formula_img_validator.sf_image_metrics).
+ *
+ * Conventions
+ *  - every entry point returns an int status (SMG_OK = 0, < 0 on error); the message of the last
+ *    error on the calling thread is returned by smg_last_error();
+ *  - the caller owns every buffer; pointers marked "device" are HBM pointers (e.g. torch
+ *    tensor.data_ptr()), sizes are int64_t, `stream` is a hipStream_t passed as void* (NULL = the
+ *    null stream).  Hot entry points never allocate: size the workspace with the matching
+ *    *_workspace_size() call first;
+ *  - all calls are asynchronous on `stream` and re-entrant (no global mutable state except the
+ *    thread-local error string).
+ *
+ * Each entry point cites the reference interface it replaces (paths under frulo/SM_distributed).
+ */
+#ifndef SMG_H
+#define SMG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SMG_OK 0
+#define SMG_ERR_INVALID (-1)     /* bad argument / shape */
+#define SMG_ERR_HIP (-2)         /* HIP runtime error */
+#define SMG_ERR_WORKSPACE (-3)   /* workspace too small */
+#define SMG_ERR_UNSUPPORTED (-4) /* configuration not implemented */
+
+/* per-ion flags written by smg_ion_metrics */
+#define SMG_ION_HAS_HITS 0x1u    /* >= 1 window with >= 1 point: the ion gets a row (formula_img_validator.py:115-118) */
+#define SMG_ION_DENSE 0x2u       /* scored by the dense (global-scratch) path instead of the LDS path */
+#define SMG_ION_CHAOS_NAN 0x4u   /* raw measure_of_chaos was NaN (empty / < 4 positive pixels) */
+
+/* hit formats accepted by smg_ion_metrics */
+#define SMG_HITS_PACKED_F32 0    /* uint64: low 32 bits pixel index, high 32 bits float32 intensity */
+#define SMG_HITS_SPLIT_F64 1     /* uint32 pixel[] + double intensity[] */
+
+const char* smg_version(void);
+const char* smg_last_error(void);
+
+/* Pack one dataset into the resident hit layout: hit[i] = pixel_map[spectrum(i)] | f32bits(ints[i]) << 32.
+ * Replaces the (sp_id -> pixel) join of formula_imager_segm.py:60-63 (_sp_df_gen) /
+ * dataset.py:68-75 (get_norm_img_pixel_inds).  sp_off: device int64[n_spectra+1];
+ * pixel_map: device int32[n_spectra]; ints: device float[n_points]; hits: device uint64[n_points]. */
+int smg_pack_hits(const int64_t* sp_off, const int32_t* pixel_map, int64_t n_spectra,
+                  const float* ints, int64_t n_points, uint64_t* hits, void* stream);
+
+/* Global m/z sort of the packed points (the pandas sort_values('mz') of formula_imager_segm.py:73-74,
+ * done once over the whole dataset instead of per m/z segment).  Keys are positive float32 m/z. */
+int smg_sort_points_workspace_size(int64_t n_points, size_t* bytes);
+int smg_sort_points(const float* mz, const uint64_t* hits, int64_t n_points,
+                    float* mz_sorted, uint64_t* hits_sorted, void* workspace, size_t workspace_bytes,
+                    void* stream);
+
+/* Window search (formula_imager_segm.py:79-82): lower = mz - mz*ppm*1e-6, upper = mz + mz*ppm*1e-6
+ * in float64, lo = searchsorted(mz_sorted, lower, 'left'), hi = searchsorted(mz_sorted, upper, 'right'),
+ * compared in float64.  If `order` is non-NULL, thread t handles window order[t] (pass windows in
+ * m/z order for cache locality); results are written at the window's own index. */
+int smg_window_bounds(const double* peak_mz, const int64_t* order, int64_t n_windows, double ppm,
+                      const float* mz_sorted, int64_t n_points, int64_t* lo, int64_t* hi, void* stream);
+
+/* Fused ion imaging + MSM scoring (replaces formula_imager_segm.py:84-109 _gen_iso_images COO
+ * construction + _img_pairs_to_list, and formula_img_validator.py:72-84,93-122 compute/sf_image_metrics).
+ * Ion i owns windows [ion_win_off[i], ion_win_off[i+1]) in peak_i order; window w's image is the set
+ * of points [lo[w], hi[w]) of the m/z-sorted hit array (duplicate pixels summed, as coo.toarray()).
+ * theor_int[w] is the theoretical intensity of window w (FormulasSegm.get_sf_peak_ints).
+ * Outputs (device, [n_ion]): cleaned chaos / spatial / spectral (ImgMeasures.to_tuple semantics),
+ * msm = chaos*spatial*spectral, and SMG_ION_* flags.
+ * connectivity (4 or 8) and erosion_border (0 or 1) select the measure_of_chaos variant (default 4, 0).
+ * ion_order (optional, int64[n_ions]) is the processing order (pass ions sorted by principal m/z so
+ * concurrently scored ions share cached windows); outputs are always written at the ion's own index.
+ * do_preprocessing != 0 applies the q-th-percentile hot-spot clip (dense path). */
+int smg_ion_metrics_workspace_size(int64_t n_ions, int32_t nrows, int32_t ncols, size_t* bytes);
+int smg_ion_metrics(int32_t hit_format, const void* hits, const double* hit_vals,
+                    const int64_t* lo, const int64_t* hi, const int64_t* ion_win_off,
+                    const double* theor_int, const int64_t* ion_order, int64_t n_ions, int32_t nrows, int32_t ncols,
+                    int32_t nlevels, double q, int32_t do_preprocessing,
+                    int32_t connectivity, int32_t erosion_border,
+                    double* out_chaos, double* out_spatial, double* out_spectral, double* out_msm,
+                    uint32_t* out_flags, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Legacy imager (formula_imager.py:9-38 _get_nonzero_ints / _sample_spectrum): for every spectrum s and
+ * window j, v = cum_ints[searchsorted(mzs, upper_j, 'right')] - cum_ints[searchsorted(mzs, lower_j, 'left')],
+ * emitted as (j, s, v) when v > 0.001.  sp_off: int64[n_spectra+1] into mzs; cum_ints has one extra
+ * leading element per spectrum (offset sp_off[s] + s).  Writes up to `capacity` triples (unordered) and
+ * the total count to *count (device int64). */
+int smg_sample_spectra(const int64_t* sp_off, const double* mzs, const double* cum_ints, int64_t n_spectra,
+                       const double* lower, const double* upper, int64_t n_windows,
+                       int64_t* out_window, int64_t* out_spectrum, double* out_value, int64_t capacity,
+                       int64_t* count, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SMG_H */

@@ -1,0 +1,77 @@
+"""ctypes binding of libsmg.so (declared in include/smg.h).
+
+The product path has no CPU fallback: if the shared library is missing or cannot be loaded,
+``lib()`` raises ``SmgLibraryError`` and every device entry point fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsmg.so")
+
+SMG_OK = 0
+SMG_ION_HAS_HITS = 0x1
+SMG_ION_DENSE = 0x2
+SMG_ION_CHAOS_NAN = 0x4
+SMG_HITS_PACKED_F32 = 0
+SMG_HITS_SPLIT_F64 = 1
+
+# every symbol include/smg.h declares, with its ctypes prototype
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_D = ctypes.c_double
+_SZ = ctypes.c_size_t
+PROTOTYPES = {
+    "smg_version": (ctypes.c_char_p, []),
+    "smg_last_error": (ctypes.c_char_p, []),
+    "smg_pack_hits": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _P, _P]),
+    "smg_sort_points_workspace_size": (ctypes.c_int, [_I64, ctypes.POINTER(_SZ)]),
+    "smg_sort_points": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _SZ, _P]),
+    "smg_window_bounds": (ctypes.c_int, [_P, _P, _I64, _D, _P, _I64, _P, _P, _P]),
+    "smg_ion_metrics_workspace_size": (ctypes.c_int, [_I64, _I32, _I32, ctypes.POINTER(_SZ)]),
+    "smg_ion_metrics": (ctypes.c_int, [_I32, _P, _P, _P, _P, _P, _P, _P, _I64, _I32, _I32, _I32, _D, _I32,
+                                       _I32, _I32, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "smg_sample_spectra": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _I64, _P, _P, _P, _I64, _P, _P]),
+}
+
+
+class SmgLibraryError(ImportError):
+    pass
+
+
+class SmgError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise SmgLibraryError(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(there is no CPU fallback for the device path)")
+        try:
+            handle = ctypes.CDLL(LIB_PATH)
+        except OSError as e:  # pragma: no cover - depends on the machine
+            raise SmgLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        for name, (res, args) in PROTOTYPES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str = "smg call"):
+    if rc != SMG_OK:
+        msg = lib().smg_last_error().decode(errors="replace")
+        raise SmgError(f"{what} failed with status {rc}: {msg}")
+
+
+def version() -> str:
+    return lib().smg_version().decode()

@@ -1,0 +1,1012 @@
+// Fused ion imaging + MSM scoring on gfx950.
+//
+// One ion = K theoretical isotope windows.  Window w's image is the run [lo[w], hi[w]) of the
+// m/z-sorted hit array (pixel, intensity); duplicate pixels are summed (coo.toarray()).
+// Replaces, in frulo/SM_distributed:
+//   formula_imager_segm.py:84-92   per-window COO construction   (_gen_iso_images)
+//   formula_imager_segm.py:95-109  per-ion image list             (_img_pairs_to_list)
+//   formula_img_validator.py:72-84 compute(): spectral / spatial / chaos
+//   pyImagingMSpec 0.1.1 isotope_pattern_match / isotope_image_correlation,
+//   cpyImagingMSpec 0.0.4 measure_of_chaos   (restated, see oracle/msm_oracle.py)
+//
+// Two paths:
+//  * LDS path (ion_lds_kernel): one 256-thread workgroup per ion.  The principal image lives in LDS
+//    as a pixel bitmap + per-64-bit-word popcount prefix (rank) + f64 values in rank order.  The
+//    other isotope windows are streamed once and joined against it (spectral sums, Pearson sums);
+//    their own duplicate pixels are found with a hashed two-bit filter.  measure_of_chaos uses the
+//    threshold decomposition of flat morphology: the per-level dilate(cross)/erode(box) equals
+//    thresholding eL = erode_box(dilate_cross(L)) of the per-pixel level index L, so
+//    sum_levels #components = sum_p eL(p) - weight(maximum spanning forest), computed with one
+//    Kruskal pass (levels descending) over an LDS union-find.  Candidates for eL > 0 are found from
+//    7x7 bit windows of the bitmap, so isolated pixels cost ~14 LDS reads.
+//  * dense path (ion_dense_kernel): persistent workgroups with a global-memory scratch slot of
+//    N_px-sized images, for ions that do not fit the LDS path (principal window > CAP points, too
+//    many E pixels / suspects, images larger than 2^18 pixels).
+#include <stdarg.h>
+
+#include "smg_common.hpp"
+
+namespace smg {
+
+constexpr int BLOCK = 256;
+constexpr int NW = BLOCK / WAVE;
+constexpr int CAP = 4096;            // max points in the principal window on the LDS path
+constexpr int R0 = CAP / BLOCK;      // principal-window points held per thread
+constexpr int MAXK = 8;              // windows per ion on the LDS path
+constexpr int MAXK_DENSE = 32;       // windows per ion supported at all
+constexpr int FILT_WORDS = 2048;     // 65536-bit duplicate filter, two of them
+constexpr int FILT_BITS = FILT_WORDS * 32;
+constexpr int SUSP_CAP = 512;
+constexpr int NPX_LDS_MAX = 1 << 18; // images up to 262144 pixels use the LDS path
+
+enum { C_NSUSP = 0, C_NE, C_EMAX, C_ABORT, C_NCTR = 8 };
+
+struct Params {
+  int32_t nrows, ncols, npx;
+  int32_t nlevels;
+  int32_t connectivity;
+  int32_t erosion_border;
+  double step;  // np.linspace(0, 1, nlevels) step
+};
+
+template <int FMT>
+struct Hits;
+
+template <>
+struct Hits<SMG_HITS_PACKED_F32> {
+  const uint64_t* h;
+  const double* unused;
+  __device__ __forceinline__ void get(int64_t i, uint32_t& p, double& v) const {
+    const uint64_t x = h[i];
+    p = (uint32_t)x;
+    v = (double)__uint_as_float((uint32_t)(x >> 32));
+  }
+};
+
+template <>
+struct Hits<SMG_HITS_SPLIT_F64> {
+  const uint32_t* pix;
+  const double* val;
+  __device__ __forceinline__ void get(int64_t i, uint32_t& p, double& v) const {
+    p = pix[i];
+    v = val[i];
+  }
+};
+
+// level index L = #{i : linspace(0,1,n)[i] < v/vmax}  (measure_of_chaos: bw = im_clean > level)
+__device__ __forceinline__ int level_of(double v, double vmax, const Params& P) {
+  const double norm = v / vmax;
+  int L = 0;
+  for (int i = 0; i < P.nlevels; ++i) {
+    const double lev = (P.nlevels > 1 && i == P.nlevels - 1) ? 1.0 : (double)i * P.step;
+    L += (lev < norm) ? 1 : 0;
+  }
+  return L;
+}
+
+__device__ __forceinline__ double clean(double v) {  // ImgMeasures._replace_nan
+  return (v == 0.0 || isnan(v) || isinf(v)) ? 0.0 : v;
+}
+
+// formula_img_validator.py:78-84 + the restated pyImagingMSpec functions; writes the outputs.
+__device__ void finalize_ion(int K, const double* __restrict__ t, const double* s, double sx, double sxx,
+                             const double* sy, const double* syy, const double* sxy, double npx,
+                             double chaos_raw, int64_t ion, uint32_t flags, double* oc, double* osp,
+                             double* osc, double* omsm, uint32_t* oflags) {
+  // isotope_pattern_match
+  double tt = 0.0, ss = 0.0;
+  for (int k = 0; k < K; ++k) {
+    tt += t[k] * t[k];
+    ss += s[k] * s[k];
+  }
+  const double nt = sqrt(tt), ns = sqrt(ss);
+  double acc = 0.0;
+  for (int k = 0; k < K; ++k) acc += fabs(t[k] / nt - s[k] / ns);
+  double spectral = 1.0 - acc / (double)K;
+  if (spectral == 1.0) spectral = 0.0;
+
+  // isotope_image_correlation: np.corrcoef rows, weights = theor[1:]
+  double spatial = 0.0;
+  if (K >= 2) {
+    const double n1 = npx - 1.0;
+    const double sxx_c = (sxx - sx * sx / npx) / n1;
+    const double sd0 = sqrt(sxx_c);
+    double num = 0.0, den = 0.0;
+    for (int k = 1; k < K; ++k) {
+      const double syy_c = (syy[k] - sy[k] * sy[k] / npx) / n1;
+      const double sxy_c = (sxy[k] - sx * sy[k] / npx) / n1;
+      double r = sxy_c / sqrt(syy_c) / sd0;
+      if (!isnan(r)) r = r > 1.0 ? 1.0 : (r < -1.0 ? -1.0 : r);
+      if (isinf(r)) r = 0.0;
+      num += r * t[k];
+      den += t[k];
+    }
+    spatial = num / den;
+  }
+
+  double chaos = chaos_raw;
+  if (!isnan(chaos) && fabs(chaos - 1.0) <= 1e-8 + 1e-5) chaos = 0.0;  // np.isclose(moc, 1.0)
+
+  chaos = clean(chaos);
+  spatial = clean(spatial);
+  spectral = clean(spectral);
+  oc[ion] = chaos;
+  osp[ion] = spatial;
+  osc[ion] = spectral;
+  omsm[ion] = chaos * spatial * spectral;
+  oflags[ion] = flags;
+}
+
+__device__ __forceinline__ double block_max(double v, double* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  v = wave_max(v);
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  double m = scratch[0];
+  for (int w = 1; w < NW; ++w) m = scratch[w] > m ? scratch[w] : m;
+  __syncthreads();
+  return m;
+}
+
+// ---------------------------------------------------------------------------------------------
+// LDS bitmap + rank helpers
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool bm_test(const uint32_t* bm, int p) { return (bm[p >> 5] >> (p & 31)) & 1u; }
+
+__device__ __forceinline__ int bm_rank(const uint32_t* bm, const uint16_t* pf, int p) {
+  const uint64_t w = reinterpret_cast<const uint64_t*>(bm)[p >> 6];
+  const uint64_t m = (p & 63) ? (w & ((1ull << (p & 63)) - 1ull)) : 0ull;
+  return (int)pf[p >> 6] + __popcll(m);
+}
+
+// exclusive popcount prefix over the first n64 64-bit words: each wave scans a contiguous range
+// 64 words at a time (lane-parallel), then wave offsets are added.  Returns the total.
+__device__ int bm_build_prefix(const uint32_t* bm, uint16_t* pf, int n64, int* wscratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(bm);
+  const int span = ((n64 + NW - 1) / NW + 63) & ~63;
+  const int a = wid * span;
+  const int b = min(n64, a + span);
+  int carry = 0;
+  for (int base = a; base < b; base += 64) {
+    const int j = base + lane;
+    const int c = (j < b) ? __popcll(bm64[j]) : 0;
+    int inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    if (j < b) pf[j] = (uint16_t)(carry + inc - c);
+    carry += __shfl(inc, 63, 64);
+  }
+  if (lane == 0) wscratch[wid] = carry;
+  __syncthreads();
+  int off = 0, tot = 0;
+  for (int w = 0; w < NW; ++w) {
+    const int c = wscratch[w];
+    if (w < wid) off += c;
+    tot += c;
+  }
+  if (off) {
+    for (int j = a + lane; j < b; j += 64) pf[j] = (uint16_t)(pf[j] + off);
+  }
+  __syncthreads();
+  return tot;
+}
+
+// bits of image row `row`, columns c0..c0+6 (bit j <-> column c0+j); 0 outside the image
+__device__ __forceinline__ uint32_t bits7(const uint32_t* bm, int row, int c0, const Params& P) {
+  if (row < 0 || row >= P.nrows) return 0u;
+  const int lc = c0 < 0 ? 0 : c0;
+  const int hc = (c0 + 6) < (P.ncols - 1) ? (c0 + 6) : (P.ncols - 1);
+  if (lc > hc) return 0u;
+  const int start = row * P.ncols + lc;
+  const int n = hc - lc + 1;
+  const int w = start >> 5, off = start & 31;
+  const uint64_t v = (uint64_t)bm[w] | ((uint64_t)bm[w + 1] << 32);
+  const uint32_t bits = (uint32_t)(v >> off) & ((1u << n) - 1u);
+  return bits << (lc - c0);
+}
+
+__device__ __forceinline__ uint32_t uf_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ uint32_t uf_find(uint32_t* par, uint32_t x) {
+  while (true) {
+    const uint32_t p = uf_load(&par[x]);
+    if (p == x) return x;
+    const uint32_t g = uf_load(&par[p]);
+    if (g != p) __hip_atomic_store(&par[x], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    x = g;
+  }
+}
+
+// returns true if a and b were in different trees (one successful link)
+__device__ __forceinline__ bool uf_unite(uint32_t* par, uint32_t a, uint32_t b) {
+  while (true) {
+    a = uf_find(par, a);
+    b = uf_find(par, b);
+    if (a == b) return false;
+    if (a < b) {
+      const uint32_t t = a;
+      a = b;
+      b = t;
+    }
+    const uint32_t old = atomicCAS(&par[a], a, b);
+    if (old == a) return true;
+  }
+}
+
+struct LdsLayout {
+  int w32;        // bitmap words incl. padding (multiple of 4)
+  size_t o_pf, o_vals, o_L, o_filt, o_susp_pix, o_susp_val, o_red, o_stats, o_ctr, o_wsc, bytes;
+};
+
+static inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+static LdsLayout lds_layout(int npx) {
+  LdsLayout L;
+  const int words = (npx + 31) / 32 + 2;
+  L.w32 = (words + 3) & ~3;
+  size_t o = al16((size_t)L.w32 * 4);
+  L.o_pf = o;
+  o = al16(o + (size_t)(L.w32 / 2) * 2);
+  L.o_vals = o;
+  o = al16(o + (size_t)CAP * 8);
+  L.o_L = o;
+  o = al16(o + (size_t)CAP);
+  L.o_filt = o;
+  o = al16(o + (size_t)2 * FILT_WORDS * 4);
+  L.o_susp_pix = o;
+  o = al16(o + (size_t)SUSP_CAP * 4);
+  L.o_susp_val = o;
+  o = al16(o + (size_t)SUSP_CAP * 8);
+  L.o_red = o;
+  o = al16(o + (size_t)8 * NW * 8);
+  L.o_stats = o;
+  o = al16(o + (size_t)4 * MAXK * 8);
+  L.o_ctr = o;
+  o = al16(o + (size_t)C_NCTR * 4);
+  L.o_wsc = o;
+  o = al16(o + (size_t)NW * 4);
+  L.bytes = o;
+  return L;
+}
+
+__device__ __forceinline__ uint32_t filt_hash(uint32_t p, int npx) {
+  return npx <= FILT_BITS ? p : ((p * 2654435761u) >> 16);
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(BLOCK) ion_lds_kernel(
+    Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
+    const int64_t* __restrict__ ion_off, const double* __restrict__ theor, const int64_t* __restrict__ ion_order,
+    int64_t n_ions, Params P, LdsLayout LL, double* __restrict__ oc, double* __restrict__ osp,
+    double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags,
+    uint32_t* __restrict__ dense_list, uint32_t* __restrict__ dense_count) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* Hbm = reinterpret_cast<uint32_t*>(smem);
+  uint16_t* pf = reinterpret_cast<uint16_t*>(smem + LL.o_pf);
+  double* vals = reinterpret_cast<double*>(smem + LL.o_vals);
+  uint8_t* Lv = reinterpret_cast<uint8_t*>(smem + LL.o_L);
+  uint32_t* filtA = reinterpret_cast<uint32_t*>(smem + LL.o_filt);
+  uint32_t* filtD = filtA + FILT_WORDS;
+  uint32_t* susp_pix = reinterpret_cast<uint32_t*>(smem + LL.o_susp_pix);
+  double* susp_val = reinterpret_cast<double*>(smem + LL.o_susp_val);
+  double* red = reinterpret_cast<double*>(smem + LL.o_red);
+  double* stats = reinterpret_cast<double*>(smem + LL.o_stats);  // s, sy, syy, sxy  x MAXK
+  int* ctr = reinterpret_cast<int*>(smem + LL.o_ctr);
+  int* wsc = reinterpret_cast<int*>(smem + LL.o_wsc);
+  // E-phase aliases
+  uint32_t* epix = reinterpret_cast<uint32_t*>(vals);                 // append order
+  uint8_t* eL8 = reinterpret_cast<uint8_t*>(vals) + (size_t)CAP * 4;  // append order
+  uint32_t* epix_r = filtA;                                           // rank order (needs 4*CAP bytes)
+  uint8_t* eLr = Lv;                                                  // rank order
+  uint32_t* par = reinterpret_cast<uint32_t*>(vals);                  // rank order (after epix consumed)
+
+  const int tid = threadIdx.x;
+  const int64_t ion = ion_order ? ion_order[blockIdx.x] : (int64_t)blockIdx.x;
+  if (ion >= n_ions) return;
+  const int64_t w0 = ion_off[ion];
+  const int K = (int)(ion_off[ion + 1] - w0);
+
+  uint32_t flags = 0;
+  for (int k = 0; k < K && k < MAXK_DENSE; ++k)
+    if (hi[w0 + k] > lo[w0 + k]) flags |= SMG_ION_HAS_HITS;
+  if (K == 0) {
+    if (tid == 0) {
+      oc[ion] = osp[ion] = osc[ion] = omsm[ion] = 0.0;
+      oflags[ion] = 0;
+    }
+    return;
+  }
+  const int64_t lo0 = lo[w0];
+  const int n0 = (int)min<int64_t>(hi[w0] - lo0, (int64_t)CAP + 1);
+  if (K > MAXK || n0 > CAP) {
+    if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
+    return;
+  }
+
+  // ---- phase 1: principal image -> bitmap, rank prefix, f64 values -------------------------
+  {
+    uint4* z = reinterpret_cast<uint4*>(Hbm);
+    for (int i = tid; i < LL.w32 / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
+    uint4* zf = reinterpret_cast<uint4*>(filtA);
+    for (int i = tid; i < FILT_WORDS / 2; i += BLOCK) zf[i] = make_uint4(0, 0, 0, 0);
+    if (tid < C_NCTR) ctr[tid] = 0;
+  }
+  uint32_t hp[R0];
+  double hv[R0];
+#pragma unroll
+  for (int j = 0; j < R0; ++j) {
+    const int i = tid + j * BLOCK;
+    if (i < n0) hits.get(lo0 + i, hp[j], hv[j]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < R0; ++j) {
+    const int i = tid + j * BLOCK;
+    if (i < n0) atomicOr(&Hbm[hp[j] >> 5], 1u << (hp[j] & 31));
+  }
+  __syncthreads();
+  const int n64 = (P.npx + 63) / 64;
+  const int nnz = bm_build_prefix(Hbm, pf, n64, wsc);
+  for (int r = tid; r < nnz; r += BLOCK) vals[r] = 0.0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < R0; ++j) {
+    const int i = tid + j * BLOCK;
+    if (i < n0) atomicAdd(&vals[bm_rank(Hbm, pf, (int)hp[j])], hv[j]);
+  }
+  __syncthreads();
+
+  // ---- phase 2: principal-image statistics ---------------------------------------------------
+  double sx, sxx, s0, npos, vmax;
+  {
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    double mx = -INFINITY;
+    for (int r = tid; r < nnz; r += BLOCK) {
+      const double v = vals[r];
+      acc[0] += v;
+      acc[1] += v * v;
+      if (v > 0.0) {
+        acc[2] += v;
+        acc[3] += 1.0;
+      }
+      mx = v > mx ? v : mx;
+    }
+    block_sum<BLOCK, 4>(acc, red);
+    sx = acc[0];
+    sxx = acc[1];
+    s0 = acc[2];
+    npos = acc[3];
+    vmax = block_max(mx, red);
+  }
+  const bool chaos_ok = (sx > 0.0) && (npos >= 4.0);
+
+  // ---- phase 3: level index per principal pixel ------------------------------------------------
+  if (chaos_ok) {
+    for (int r = tid; r < nnz; r += BLOCK) Lv[r] = (uint8_t)level_of(vals[r], vmax, P);
+  }
+
+  // ---- phase 5: stream the other isotope windows, join against the principal image ------------
+  for (int k = 1; k < K; ++k) {
+    const int64_t a = lo[w0 + k], b = hi[w0 + k];
+    double psy = 0.0, psyy = 0.0, psxy = 0.0, psk = 0.0;
+    for (int64_t i = a + tid; i < b; i += BLOCK) {
+      uint32_t p;
+      double v;
+      hits.get(i, p, v);
+      double x = 0.0;
+      if (bm_test(Hbm, (int)p)) x = vals[bm_rank(Hbm, pf, (int)p)];
+      psy += v;
+      psxy += x * v;
+      if (x > 0.0) psk += v;
+      const uint32_t h = filt_hash(p, P.npx);
+      const uint32_t bit = 1u << (h & 31);
+      const uint32_t old = atomicOr(&filtA[h >> 5], bit);
+      if (old & bit) atomicOr(&filtD[h >> 5], bit);
+    }
+    __syncthreads();
+    for (int64_t i = a + tid; i < b; i += BLOCK) {
+      uint32_t p;
+      double v;
+      hits.get(i, p, v);
+      const uint32_t h = filt_hash(p, P.npx);
+      if ((filtD[h >> 5] >> (h & 31)) & 1u) {
+        const int s = atomicAdd(&ctr[C_NSUSP], 1);
+        if (s < SUSP_CAP) {
+          susp_pix[s] = p;
+          susp_val[s] = v;
+        }
+      } else {
+        psyy += v * v;
+      }
+    }
+    __syncthreads();
+    const int ns = ctr[C_NSUSP];
+    {
+      uint4* zf = reinterpret_cast<uint4*>(filtA);
+      for (int i = tid; i < FILT_WORDS / 2; i += BLOCK) zf[i] = make_uint4(0, 0, 0, 0);
+    }
+    if (ns <= SUSP_CAP) {
+      for (int s = tid; s < ns; s += BLOCK) {
+        const uint32_t ps = susp_pix[s];
+        bool first = true;
+        double sum = 0.0;
+        for (int u = 0; u < ns; ++u) {
+          if (susp_pix[u] == ps) {
+            if (u < s) {
+              first = false;
+              break;
+            }
+            sum += susp_val[u];
+          }
+        }
+        if (first) psyy += sum * sum;
+      }
+    }
+    double acc[4] = {psy, psyy, psxy, psk};
+    block_sum<BLOCK, 4>(acc, red);  // contains barriers: every thread has read ctr[C_NSUSP]
+    if (ns > SUSP_CAP) {
+      if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
+      return;
+    }
+    if (tid == 0) {
+      stats[0 * MAXK + k] = acc[3];
+      stats[1 * MAXK + k] = acc[0];
+      stats[2 * MAXK + k] = acc[1];
+      stats[3 * MAXK + k] = acc[2];
+      ctr[C_NSUSP] = 0;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 4a: chaos candidates (pixels with eL >= 1) -----------------------------------------
+  double chaos_raw = NAN;
+  if (chaos_ok) {
+    const int w32u = (P.npx + 31) / 32;
+    for (int w = tid; w < w32u; w += BLOCK) {
+      uint32_t bits = Hbm[w];
+      while (bits) {
+        const int bpos = __ffs(bits) - 1;
+        bits &= bits - 1u;
+        const int s = w * 32 + bpos;
+        const int rs = s / P.ncols, cs = s - rs * P.ncols;
+        uint32_t H[7];
+#pragma unroll
+        for (int d = 0; d < 7; ++d) H[d] = bits7(Hbm, rs - 3 + d, cs - 3, P);
+        uint32_t cv = 0;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+          const int c = cs - 3 + j;
+          if (c >= 0 && c < P.ncols) cv |= 1u << j;
+        }
+        uint32_t D[7];
+        D[0] = D[6] = 0;
+#pragma unroll
+        for (int d = 1; d <= 5; ++d) {
+          const int row = rs - 3 + d;
+          const bool rv = row >= 0 && row < P.nrows;
+          uint32_t x = (H[d] | (H[d] << 1) | (H[d] >> 1) | H[d - 1] | H[d + 1]) & cv;
+          if (!rv) x = 0;
+          if (P.erosion_border) x |= rv ? (~cv & 0x7Fu) : 0x7Fu;
+          D[d] = x & 0x7Fu;
+        }
+        auto hb = [&](int dr, int dc) -> uint32_t { return (H[3 + dr] >> (3 + dc)) & 1u; };
+        const int cand_dr[5] = {0, 0, 0, -1, 1};
+        const int cand_dc[5] = {0, 1, -1, 0, 0};
+#pragma unroll
+        for (int ci = 0; ci < 5; ++ci) {
+          const int dr = cand_dr[ci], dc = cand_dc[ci];
+          const int rp = rs + dr, cp = cs + dc;
+          if (rp < 0 || rp >= P.nrows || cp < 0 || cp >= P.ncols) continue;
+          bool owner;
+          if (ci == 0) owner = !hb(-1, 0) && !hb(0, -1);
+          else if (ci == 1) owner = !hb(-1, 1);
+          else if (ci == 2) owner = !hb(-1, -1) && !hb(0, -2) && !hb(0, -1);
+          else if (ci == 3) owner = !hb(-2, 0) && !hb(-1, -1) && !hb(-1, 0) && !hb(-1, 1);
+          else owner = true;
+          if (!owner) continue;
+          bool pass = true;
+#pragma unroll
+          for (int e = -1; e <= 1; ++e) pass = pass && (((D[3 + dr + e] >> (3 + dc - 1)) & 7u) == 7u);
+          if (!pass) continue;
+          // exact eL(p) = min_{q in N9(p)} max_{q' in N4[q]} L(q')
+          int lv[5][5];
+#pragma unroll
+          for (int a = -2; a <= 2; ++a)
+#pragma unroll
+            for (int b = -2; b <= 2; ++b) {
+              lv[a + 2][b + 2] = 0;
+              if ((a == -2 || a == 2) && (b == -2 || b == 2)) continue;
+              if (hb(dr + a, dc + b)) {
+                const int q = (rp + a) * P.ncols + (cp + b);
+                lv[a + 2][b + 2] = Lv[bm_rank(Hbm, pf, q)];
+              }
+            }
+          int mn = 1 << 20;
+#pragma unroll
+          for (int qa = -1; qa <= 1; ++qa)
+#pragma unroll
+            for (int qb = -1; qb <= 1; ++qb) {
+              const int rq = rp + qa, cq = cp + qb;
+              if (rq < 0 || rq >= P.nrows || cq < 0 || cq >= P.ncols) {
+                if (!P.erosion_border) mn = 0;
+                continue;
+              }
+              int dl = lv[qa + 2][qb + 2];
+              dl = max(dl, lv[qa + 1][qb + 2]);
+              dl = max(dl, lv[qa + 3][qb + 2]);
+              dl = max(dl, lv[qa + 2][qb + 1]);
+              dl = max(dl, lv[qa + 2][qb + 3]);
+              mn = min(mn, dl);
+            }
+          if (mn >= 1 && mn < (1 << 20)) {
+            const int idx = atomicAdd(&ctr[C_NE], 1);
+            if (idx < CAP) {
+              epix[idx] = (uint32_t)(rp * P.ncols + cp);
+              eL8[idx] = (uint8_t)mn;
+            }
+            atomicMax(&ctr[C_EMAX], mn);
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- phase 4b: Kruskal over eL (levels descending) with an LDS union-find -------------------
+    const int m = ctr[C_NE];
+    if (m > CAP) {
+      if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
+      return;
+    }
+    double sum_c = 0.0;
+    if (m > 0) {
+      uint4* z = reinterpret_cast<uint4*>(Hbm);
+      for (int i = tid; i < LL.w32 / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
+      __syncthreads();
+      for (int i = tid; i < m; i += BLOCK) atomicOr(&Hbm[epix[i] >> 5], 1u << (epix[i] & 31));
+      __syncthreads();
+      bm_build_prefix(Hbm, pf, n64, wsc);
+      for (int i = tid; i < m; i += BLOCK) {
+        const uint32_t p = epix[i];
+        const int r = bm_rank(Hbm, pf, (int)p);
+        epix_r[r] = p;
+        eLr[r] = eL8[i];
+      }
+      __syncthreads();
+      for (int r = tid; r < m; r += BLOCK) par[r] = (uint32_t)r;
+      __syncthreads();
+      const int emax = ctr[C_EMAX];
+      double wsum = 0.0, esum = 0.0;
+      for (int r = tid; r < m; r += BLOCK) esum += (double)eLr[r];
+      for (int t = emax; t >= 1; --t) {
+        for (int r = tid; r < m; r += BLOCK) {
+          const int e = eLr[r];
+          if (e < t) continue;
+          const int p = (int)epix_r[r];
+          const int rp = p / P.ncols, cp = p - rp * P.ncols;
+          int nb[4];
+          int nn = 0;
+          if (cp + 1 < P.ncols) nb[nn++] = p + 1;
+          if (rp + 1 < P.nrows) {
+            nb[nn++] = p + P.ncols;
+            if (P.connectivity == 8) {
+              if (cp > 0) nb[nn++] = p + P.ncols - 1;
+              if (cp + 1 < P.ncols) nb[nn++] = p + P.ncols + 1;
+            }
+          }
+          for (int j = 0; j < nn; ++j) {
+            const int q = nb[j];
+            if (!bm_test(Hbm, q)) continue;
+            const int rq = bm_rank(Hbm, pf, q);
+            const int eq = eLr[rq];
+            if ((e < eq ? e : eq) == t) {
+              if (uf_unite(par, (uint32_t)r, (uint32_t)rq)) wsum += (double)t;
+            }
+          }
+        }
+        __syncthreads();
+      }
+      double acc[2] = {esum, wsum};
+      block_sum<BLOCK, 2>(acc, red);
+      sum_c = acc[0] - acc[1];
+    }
+    chaos_raw = 1.0 - sum_c / (double)P.nlevels / npos;
+  } else {
+    flags |= SMG_ION_CHAOS_NAN;
+  }
+
+  if (tid == 0) {
+    double t[MAXK], s[MAXK], sy[MAXK], syy[MAXK], sxy[MAXK];
+    for (int k = 0; k < K; ++k) {
+      t[k] = theor[w0 + k];
+      if (k == 0) {
+        s[k] = s0;
+        sy[k] = syy[k] = sxy[k] = 0.0;
+      } else {
+        s[k] = stats[0 * MAXK + k];
+        sy[k] = stats[1 * MAXK + k];
+        syy[k] = stats[2 * MAXK + k];
+        sxy[k] = stats[3 * MAXK + k];
+      }
+    }
+    finalize_ion(K, t, s, sx, sxx, sy, syy, sxy, (double)P.npx, chaos_raw, ion, flags, oc, osp, osc, omsm,
+                 oflags);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// dense path: persistent workgroups, one global scratch slot each
+// ---------------------------------------------------------------------------------------------
+struct DenseSlot {
+  double* x;
+  double* y;
+  uint32_t* par;
+  uint32_t* elist;
+  uint8_t* L8;
+  uint8_t* T8;
+  uint8_t* E8;
+};
+
+static inline size_t dense_slot_bytes(int npx) {
+  return al16((size_t)npx * 8) * 2 + al16((size_t)npx * 4) * 2 + al16((size_t)npx) * 3 + 256;
+}
+
+__device__ __forceinline__ DenseSlot dense_slot(unsigned char* base, int npx) {
+  DenseSlot S;
+  auto a16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  size_t o = 0;
+  S.x = reinterpret_cast<double*>(base + o);
+  o += a16((size_t)npx * 8);
+  S.y = reinterpret_cast<double*>(base + o);
+  o += a16((size_t)npx * 8);
+  S.par = reinterpret_cast<uint32_t*>(base + o);
+  o += a16((size_t)npx * 4);
+  S.elist = reinterpret_cast<uint32_t*>(base + o);
+  o += a16((size_t)npx * 4);
+  S.L8 = base + o;
+  o += a16((size_t)npx);
+  S.T8 = base + o;
+  o += a16((size_t)npx);
+  S.E8 = base + o;
+  return S;
+}
+
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint32_t guf_find(uint32_t* par, uint32_t x) {
+  while (true) {
+    const uint32_t p = ld_agent(&par[x]);
+    if (p == x) return x;
+    const uint32_t g = ld_agent(&par[p]);
+    if (g != p) __hip_atomic_store(&par[x], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    x = g;
+  }
+}
+
+__device__ __forceinline__ bool guf_unite(uint32_t* par, uint32_t a, uint32_t b) {
+  while (true) {
+    a = guf_find(par, a);
+    b = guf_find(par, b);
+    if (a == b) return false;
+    if (a < b) {
+      const uint32_t t = a;
+      a = b;
+      b = t;
+    }
+    const uint32_t old = atomicCAS(&par[a], a, b);
+    if (old == a) return true;
+  }
+}
+
+template <int FMT>
+__device__ void scatter_window(const Hits<FMT>& hits, int64_t a, int64_t b, double* img) {
+  for (int64_t i = a + threadIdx.x; i < b; i += BLOCK) {
+    uint32_t p;
+    double v;
+    hits.get(i, p, v);
+    atomicAdd(&img[p], v);
+  }
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
+    Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
+    const int64_t* __restrict__ ion_off, const double* __restrict__ theor, int64_t n_ions, Params P,
+    const uint32_t* __restrict__ dense_list, const uint32_t* __restrict__ dense_count, uint32_t* next,
+    unsigned char* scratch, size_t slot_bytes, double* __restrict__ oc, double* __restrict__ osp,
+    double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags) {
+  __shared__ double red[8 * NW];
+  __shared__ double kst[4 * MAXK_DENSE];
+  __shared__ int sh_ion;
+  __shared__ int sh_ctr[4];
+  const int tid = threadIdx.x;
+  DenseSlot S = dense_slot(scratch + (size_t)blockIdx.x * slot_bytes, P.npx);
+  const int npx = P.npx;
+  const uint32_t total = *dense_count;
+
+  while (true) {
+    if (tid == 0) {
+      const uint32_t k = atomicAdd(next, 1u);
+      sh_ion = (k < total) ? (int)dense_list[k] : -1;
+      sh_ctr[0] = 0;
+      sh_ctr[1] = 0;
+    }
+    __syncthreads();
+    const int64_t ion = sh_ion;
+    if (ion < 0) break;
+    const int64_t w0 = ion_off[ion];
+    const int K = (int)(ion_off[ion + 1] - w0);
+    uint32_t flags = SMG_ION_DENSE;
+    for (int k = 0; k < K && k < MAXK_DENSE; ++k)
+      if (hi[w0 + k] > lo[w0 + k]) flags |= SMG_ION_HAS_HITS;
+    if (K > MAXK_DENSE || K == 0) {
+      if (tid == 0) {
+        oc[ion] = osp[ion] = osc[ion] = omsm[ion] = 0.0;
+        oflags[ion] = (K == 0) ? 0u : (flags | 0x80000000u);
+      }
+      __syncthreads();
+      continue;
+    }
+
+    // principal image (agent fences: plain zero stores must land in L2 before the L2 atomics,
+    // and the atomics before the loads that follow)
+    for (int p = tid; p < npx; p += BLOCK) S.x[p] = 0.0;
+    __threadfence();
+    __syncthreads();
+    scatter_window<FMT>(hits, lo[w0], hi[w0], S.x);
+    __threadfence();
+    __syncthreads();
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    double mx = -INFINITY;
+    for (int p = tid; p < npx; p += BLOCK) {
+      const double v = ld_agent(&S.x[p]);
+      acc[0] += v;
+      acc[1] += v * v;
+      if (v > 0.0) {
+        acc[2] += v;
+        acc[3] += 1.0;
+      }
+      mx = v > mx ? v : mx;
+    }
+    block_sum<BLOCK, 4>(acc, red);
+    const double sx = acc[0], sxx = acc[1], s0 = acc[2], npos = acc[3];
+    const double vmax = block_max(mx, red);
+    const bool chaos_ok = (sx > 0.0) && (npos >= 4.0);
+
+    // other windows
+    for (int k = 1; k < K; ++k) {
+      for (int p = tid; p < npx; p += BLOCK) S.y[p] = 0.0;
+      __threadfence();
+      __syncthreads();
+      scatter_window<FMT>(hits, lo[w0 + k], hi[w0 + k], S.y);
+      __threadfence();
+      __syncthreads();
+      double a2[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int p = tid; p < npx; p += BLOCK) {
+        const double y = ld_agent(&S.y[p]);
+        const double x = ld_agent(&S.x[p]);
+        a2[0] += y;
+        a2[1] += y * y;
+        a2[2] += x * y;
+        if (x > 0.0) a2[3] += y;
+      }
+      block_sum<BLOCK, 4>(a2, red);
+      if (tid == 0) {
+        kst[0 * MAXK_DENSE + k] = a2[3];
+        kst[1 * MAXK_DENSE + k] = a2[0];
+        kst[2 * MAXK_DENSE + k] = a2[1];
+        kst[3 * MAXK_DENSE + k] = a2[2];
+      }
+    }
+    __syncthreads();
+
+    double chaos_raw = NAN;
+    if (chaos_ok) {
+      const int nr = P.nrows, nc = P.ncols;
+      for (int p = tid; p < npx; p += BLOCK) S.L8[p] = (uint8_t)level_of(ld_agent(&S.x[p]), vmax, P);
+      __syncthreads();
+      for (int p = tid; p < npx; p += BLOCK) {  // dilation with the 4-cross (outside = 0)
+        const int r = p / nc, c = p - r * nc;
+        int d = S.L8[p];
+        if (r > 0) d = max(d, (int)S.L8[p - nc]);
+        if (r + 1 < nr) d = max(d, (int)S.L8[p + nc]);
+        if (c > 0) d = max(d, (int)S.L8[p - 1]);
+        if (c + 1 < nc) d = max(d, (int)S.L8[p + 1]);
+        S.T8[p] = (uint8_t)d;
+      }
+      __syncthreads();
+      for (int p = tid; p < npx; p += BLOCK) {  // erosion with the 3x3 box
+        const int r = p / nc, c = p - r * nc;
+        int e = 1 << 20;
+        for (int a = -1; a <= 1; ++a)
+          for (int b = -1; b <= 1; ++b) {
+            const int rr = r + a, cc = c + b;
+            if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) {
+              if (!P.erosion_border) e = 0;
+              continue;
+            }
+            e = min(e, (int)S.T8[rr * nc + cc]);
+          }
+        if (e >= (1 << 20)) e = 0;
+        S.E8[p] = (uint8_t)e;
+        if (e >= 1) {
+          const int idx = atomicAdd(&sh_ctr[0], 1);
+          S.elist[idx] = (uint32_t)p;
+          S.par[p] = (uint32_t)p;
+          atomicMax(&sh_ctr[1], e);
+        }
+      }
+      __threadfence();
+      __syncthreads();
+      const int m = sh_ctr[0], emax = sh_ctr[1];
+      double esum = 0.0, wsum = 0.0;
+      for (int i = tid; i < m; i += BLOCK) esum += (double)S.E8[S.elist[i]];
+      for (int t = emax; t >= 1; --t) {
+        for (int i = tid; i < m; i += BLOCK) {
+          const int p = (int)S.elist[i];
+          const int e = S.E8[p];
+          if (e < t) continue;
+          const int r = p / nc, c = p - r * nc;
+          int nb[4];
+          int nn = 0;
+          if (c + 1 < nc) nb[nn++] = p + 1;
+          if (r + 1 < nr) {
+            nb[nn++] = p + nc;
+            if (P.connectivity == 8) {
+              if (c > 0) nb[nn++] = p + nc - 1;
+              if (c + 1 < nc) nb[nn++] = p + nc + 1;
+            }
+          }
+          for (int j = 0; j < nn; ++j) {
+            const int q = nb[j];
+            const int eq = S.E8[q];
+            if (eq >= 1 && (e < eq ? e : eq) == t) {
+              if (guf_unite(S.par, (uint32_t)p, (uint32_t)q)) wsum += (double)t;
+            }
+          }
+        }
+        __syncthreads();
+      }
+      double a3[2] = {esum, wsum};
+      block_sum<BLOCK, 2>(a3, red);
+      chaos_raw = 1.0 - (a3[0] - a3[1]) / (double)P.nlevels / npos;
+    } else {
+      flags |= SMG_ION_CHAOS_NAN;
+    }
+
+    if (tid == 0) {
+      double t[MAXK_DENSE], s[MAXK_DENSE], sy[MAXK_DENSE], syy[MAXK_DENSE], sxy[MAXK_DENSE];
+      for (int k = 0; k < K; ++k) {
+        t[k] = theor[w0 + k];
+        if (k == 0) {
+          s[k] = s0;
+          sy[k] = syy[k] = sxy[k] = 0.0;
+        } else {
+          s[k] = kst[0 * MAXK_DENSE + k];
+          sy[k] = kst[1 * MAXK_DENSE + k];
+          syy[k] = kst[2 * MAXK_DENSE + k];
+          sxy[k] = kst[3 * MAXK_DENSE + k];
+        }
+      }
+      finalize_ion(K, t, s, sx, sxx, sy, syy, sxy, (double)npx, chaos_raw, ion, flags, oc, osp, osc, omsm,
+                   oflags);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void list_all_kernel(uint32_t* list, uint32_t* count, const int64_t* ion_order, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) list[i] = (uint32_t)(ion_order ? ion_order[i] : i);
+  if (i == 0) *count = (uint32_t)n;
+}
+
+static constexpr int DENSE_SLOTS = 256;
+static constexpr size_t WS_HEADER = 256;
+
+static size_t ws_bytes_for(int64_t n_ions, int npx) {
+  return WS_HEADER + al16((size_t)n_ions * 4) + (size_t)DENSE_SLOTS * dense_slot_bytes(npx);
+}
+
+template <int FMT>
+static int launch_metrics(Hits<FMT> hits, const int64_t* lo, const int64_t* hi, const int64_t* ion_off,
+                          const double* theor, const int64_t* ion_order, int64_t n_ions, const Params& P,
+                          double* oc, double* osp, double* osc, double* omsm, uint32_t* oflags,
+                          unsigned char* ws, hipStream_t st) {
+  uint32_t* dense_count = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* next = dense_count + 1;
+  uint32_t* dense_list = reinterpret_cast<uint32_t*>(ws + WS_HEADER);
+  unsigned char* slots = ws + WS_HEADER + al16((size_t)n_ions * 4);
+  const size_t slot_bytes = dense_slot_bytes(P.npx);
+  SMG_HIP(hipMemsetAsync(ws, 0, WS_HEADER, st));
+  if (P.npx <= NPX_LDS_MAX) {
+    LdsLayout LL = lds_layout(P.npx);
+    SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ion_lds_kernel<FMT>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)LL.bytes));
+    hipLaunchKernelGGL(ion_lds_kernel<FMT>, dim3((unsigned)n_ions), dim3(BLOCK), LL.bytes, st, hits, lo, hi,
+                       ion_off, theor, ion_order, n_ions, P, LL, oc, osp, osc, omsm, oflags, dense_list,
+                       dense_count);
+    SMG_LAUNCH_CHECK();
+  } else {
+    hipLaunchKernelGGL(list_all_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, dense_list,
+                       dense_count, ion_order, n_ions);
+    SMG_LAUNCH_CHECK();
+  }
+  const int nslots = (int)(n_ions < DENSE_SLOTS ? n_ions : DENSE_SLOTS);
+  hipLaunchKernelGGL(ion_dense_kernel<FMT>, dim3((unsigned)nslots), dim3(BLOCK), 0, st, hits, lo, hi, ion_off,
+                     theor, n_ions, P, dense_list, dense_count, next, slots, slot_bytes, oc, osp, osc, omsm,
+                     oflags);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+}  // namespace smg
+
+using namespace smg;
+
+extern "C" {
+
+int smg_ion_metrics_workspace_size(int64_t n_ions, int32_t nrows, int32_t ncols, size_t* bytes) {
+  SMG_CHECK_ARG(bytes && n_ions >= 0 && nrows > 0 && ncols > 0, "bad arguments");
+  SMG_CHECK_ARG((int64_t)nrows * ncols < (1ll << 31), "image too large");
+  *bytes = ws_bytes_for(n_ions, nrows * ncols);
+  return SMG_OK;
+}
+
+int smg_ion_metrics(int32_t hit_format, const void* hits, const double* hit_vals, const int64_t* lo,
+                    const int64_t* hi, const int64_t* ion_win_off, const double* theor_int,
+                    const int64_t* ion_order, int64_t n_ions, int32_t nrows, int32_t ncols, int32_t nlevels,
+                    double q, int32_t do_preprocessing, int32_t connectivity, int32_t erosion_border,
+                    double* out_chaos, double* out_spatial, double* out_spectral, double* out_msm,
+                    uint32_t* out_flags, void* workspace, size_t workspace_bytes, void* stream) {
+  (void)q;
+  SMG_CHECK_ARG(n_ions >= 0 && n_ions < (1ll << 31), "n_ions out of range");
+  if (n_ions == 0) return SMG_OK;
+  SMG_CHECK_ARG(nrows > 0 && ncols > 0 && (int64_t)nrows * ncols < (1ll << 31), "bad image shape");
+  SMG_CHECK_ARG(nlevels >= 1 && nlevels <= 254, "nlevels must be in [1, 254]");
+  SMG_CHECK_ARG(connectivity == 4 || connectivity == 8, "connectivity must be 4 or 8");
+  SMG_CHECK_ARG(erosion_border == 0 || erosion_border == 1, "erosion_border must be 0 or 1");
+  SMG_CHECK_ARG(hit_format == SMG_HITS_PACKED_F32 || hit_format == SMG_HITS_SPLIT_F64, "bad hit_format");
+  SMG_CHECK_ARG(lo && hi && ion_win_off && theor_int && out_chaos && out_spatial && out_spectral && out_msm &&
+                    out_flags && workspace,
+                "null pointer");
+  if (do_preprocessing) {
+    set_error("do_preprocessing (q-percentile hot-spot clip) is not implemented on the device path yet");
+    return SMG_ERR_UNSUPPORTED;
+  }
+  const size_t need = ws_bytes_for(n_ions, nrows * ncols);
+  if (workspace_bytes < need) {
+    set_error("ion_metrics workspace too small: %zu < %zu", workspace_bytes, need);
+    return SMG_ERR_WORKSPACE;
+  }
+  Params P;
+  P.nrows = nrows;
+  P.ncols = ncols;
+  P.npx = nrows * ncols;
+  P.nlevels = nlevels;
+  P.connectivity = connectivity;
+  P.erosion_border = erosion_border;
+  P.step = nlevels > 1 ? 1.0 / (double)(nlevels - 1) : 0.0;
+  unsigned char* ws = reinterpret_cast<unsigned char*>(workspace);
+  hipStream_t st = as_stream(stream);
+  if (hit_format == SMG_HITS_PACKED_F32) {
+    SMG_CHECK_ARG(hits != nullptr, "null hits");
+    Hits<SMG_HITS_PACKED_F32> h{reinterpret_cast<const uint64_t*>(hits), nullptr};
+    return launch_metrics<SMG_HITS_PACKED_F32>(h, lo, hi, ion_win_off, theor_int, ion_order, n_ions, P, out_chaos,
+                                               out_spatial, out_spectral, out_msm, out_flags, ws, st);
+  }
+  SMG_CHECK_ARG(hits != nullptr && hit_vals != nullptr, "null hits");
+  Hits<SMG_HITS_SPLIT_F64> h{reinterpret_cast<const uint32_t*>(hits), hit_vals};
+  return launch_metrics<SMG_HITS_SPLIT_F64>(h, lo, hi, ion_win_off, theor_int, ion_order, n_ions, P, out_chaos,
+                                            out_spatial, out_spectral, out_msm, out_flags, ws, st);
+}
+
+}  // extern "C"

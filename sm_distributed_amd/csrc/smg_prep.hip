@@ -1,0 +1,228 @@
+// Peak-list preparation on gfx950: hit packing, global m/z sort, ppm-window search, legacy sampler.
+//
+// Reference behaviour (frulo/SM_distributed):
+//   formula_imager_segm.py:60-63  _sp_df_gen   (sp_id -> pixel join)
+//   formula_imager_segm.py:73-74  sort_values('mz') per segment/chunk
+//   formula_imager_segm.py:79-82  f64 ppm bounds + searchsorted('l' / 'r')
+//   formula_imager.py:9-38        legacy prefix-sum sampler
+#include <cstring>
+#include <stdarg.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "smg_common.hpp"
+
+namespace smg {
+
+static thread_local std::string g_last_error;
+
+void set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+}
+
+// ---------------------------------------------------------------------------------------------
+// pack: one thread per spectrum-chunk.  Each block handles one spectrum at a time (grid-stride),
+// streaming its intensities with coalesced loads and writing 8-byte hits.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) pack_hits_kernel(const int64_t* __restrict__ sp_off,
+                                                        const int32_t* __restrict__ pixel_map,
+                                                        int64_t n_spectra,
+                                                        const float* __restrict__ ints,
+                                                        uint64_t* __restrict__ hits) {
+  for (int64_t s = blockIdx.x; s < n_spectra; s += gridDim.x) {
+    const int64_t a = sp_off[s], b = sp_off[s + 1];
+    const uint64_t pix = (uint32_t)pixel_map[s];
+    for (int64_t i = a + threadIdx.x; i < b; i += blockDim.x) {
+      hits[i] = pix | ((uint64_t)__float_as_uint(ints[i]) << 32);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// window search.  Bounds are computed exactly as the reference lambda evaluates them
+// (`mz - mz*ppm*1e-6`: ((mz*ppm)*1e-6) then subtract; the library is built with
+// -ffp-contract=off so no FMA changes the rounding), compared in f64 against the f32 keys.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t lower_bound_f64(const float* __restrict__ a, int64_t n, double x) {
+  int64_t lo = 0, len = n;
+  while (len > 0) {
+    const int64_t half = len >> 1;
+    const int64_t mid = lo + half;
+    if ((double)a[mid] < x) {
+      lo = mid + 1;
+      len -= half + 1;
+    } else {
+      len = half;
+    }
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int64_t upper_bound_f64(const float* __restrict__ a, int64_t n, double x) {
+  int64_t lo = 0, len = n;
+  while (len > 0) {
+    const int64_t half = len >> 1;
+    const int64_t mid = lo + half;
+    if ((double)a[mid] <= x) {
+      lo = mid + 1;
+      len -= half + 1;
+    } else {
+      len = half;
+    }
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(256) window_bounds_kernel(const double* __restrict__ peak_mz,
+                                                            const int64_t* __restrict__ order,
+                                                            int64_t n_windows, double ppm,
+                                                            const float* __restrict__ mz_sorted,
+                                                            int64_t n_points, int64_t* __restrict__ lo,
+                                                            int64_t* __restrict__ hi) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_windows) return;
+  const int64_t w = order ? order[t] : t;
+  const double mz = peak_mz[w];
+  const double d = mz * ppm * 1e-6;
+  const double lower = mz - d;
+  const double upper = mz + d;
+  lo[w] = lower_bound_f64(mz_sorted, n_points, lower);
+  hi[w] = upper_bound_f64(mz_sorted, n_points, upper);
+}
+
+// ---------------------------------------------------------------------------------------------
+// legacy sampler: one wave per (spectrum, window-chunk); each lane one window.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t lb_d(const double* a, int64_t n, double x) {
+  int64_t lo = 0, len = n;
+  while (len > 0) {
+    int64_t half = len >> 1, mid = lo + half;
+    if (a[mid] < x) { lo = mid + 1; len -= half + 1; } else { len = half; }
+  }
+  return lo;
+}
+__device__ __forceinline__ int64_t ub_d(const double* a, int64_t n, double x) {
+  int64_t lo = 0, len = n;
+  while (len > 0) {
+    int64_t half = len >> 1, mid = lo + half;
+    if (a[mid] <= x) { lo = mid + 1; len -= half + 1; } else { len = half; }
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(256) sample_spectra_kernel(
+    const int64_t* __restrict__ sp_off, const double* __restrict__ mzs, const double* __restrict__ cum,
+    int64_t n_spectra, const double* __restrict__ lower, const double* __restrict__ upper,
+    int64_t n_windows, int64_t* __restrict__ ow, int64_t* __restrict__ os, double* __restrict__ ov,
+    int64_t capacity, unsigned long long* __restrict__ count) {
+  const int64_t s = blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_spectra || j >= n_windows) return;
+  const int64_t a = sp_off[s], n = sp_off[s + 1] - a;
+  const double* m = mzs + a;
+  const double* c = cum + a + s;  // n+1 cumulative values
+  const double v = c[ub_d(m, n, upper[j])] - c[lb_d(m, n, lower[j])];
+  if (v > 0.001) {
+    const unsigned long long k = atomicAdd(count, 1ull);
+    if ((int64_t)k < capacity) {
+      ow[k] = j;
+      os[k] = s;
+      ov[k] = v;
+    }
+  }
+}
+
+}  // namespace smg
+
+using namespace smg;
+
+extern "C" {
+
+const char* smg_version(void) { return "smg 0.1.0 (gfx950)"; }
+
+const char* smg_last_error(void) { return g_last_error.c_str(); }
+
+int smg_pack_hits(const int64_t* sp_off, const int32_t* pixel_map, int64_t n_spectra, const float* ints,
+                  int64_t n_points, uint64_t* hits, void* stream) {
+  SMG_CHECK_ARG(n_spectra >= 0 && n_points >= 0, "negative sizes");
+  if (n_spectra == 0 || n_points == 0) return SMG_OK;
+  SMG_CHECK_ARG(sp_off && pixel_map && ints && hits, "null pointer");
+  const int64_t grid = n_spectra < (1 << 20) ? n_spectra : (1 << 20);
+  hipLaunchKernelGGL(pack_hits_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream), sp_off,
+                     pixel_map, n_spectra, ints, hits);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_sort_points_workspace_size(int64_t n_points, size_t* bytes) {
+  SMG_CHECK_ARG(bytes != nullptr && n_points >= 0, "bad arguments");
+  size_t tb = 0;
+  const uint32_t* kin = nullptr;
+  uint32_t* kout = nullptr;
+  const uint64_t* vin = nullptr;
+  uint64_t* vout = nullptr;
+  hipError_t e = rocprim::radix_sort_pairs(nullptr, tb, kin, kout, vin, vout, (size_t)n_points, 0, 31,
+                                           (hipStream_t)0, false);
+  if (e != hipSuccess) {
+    set_error("rocprim workspace query failed: %s", hipGetErrorString(e));
+    return SMG_ERR_HIP;
+  }
+  *bytes = tb + 256;
+  return SMG_OK;
+}
+
+int smg_sort_points(const float* mz, const uint64_t* hits, int64_t n_points, float* mz_sorted,
+                    uint64_t* hits_sorted, void* workspace, size_t workspace_bytes, void* stream) {
+  SMG_CHECK_ARG(n_points >= 0, "negative n_points");
+  if (n_points == 0) return SMG_OK;
+  SMG_CHECK_ARG(mz && hits && mz_sorted && hits_sorted && workspace, "null pointer");
+  size_t need = 0;
+  int rc = smg_sort_points_workspace_size(n_points, &need);
+  if (rc) return rc;
+  if (workspace_bytes < need) {
+    set_error("sort workspace too small: %zu < %zu", workspace_bytes, need);
+    return SMG_ERR_WORKSPACE;
+  }
+  size_t tb = need - 256;
+  // positive float32 keys order like their bit patterns; bit 31 (sign) is always 0
+  SMG_HIP(rocprim::radix_sort_pairs(workspace, tb, reinterpret_cast<const uint32_t*>(mz),
+                                    reinterpret_cast<uint32_t*>(mz_sorted), hits, hits_sorted,
+                                    (size_t)n_points, 0, 31, as_stream(stream), false));
+  return SMG_OK;
+}
+
+int smg_window_bounds(const double* peak_mz, const int64_t* order, int64_t n_windows, double ppm,
+                      const float* mz_sorted, int64_t n_points, int64_t* lo, int64_t* hi, void* stream) {
+  SMG_CHECK_ARG(n_windows >= 0 && n_points >= 0, "negative sizes");
+  if (n_windows == 0) return SMG_OK;
+  SMG_CHECK_ARG(peak_mz && lo && hi && (mz_sorted || n_points == 0), "null pointer");
+  const int64_t grid = (n_windows + 255) / 256;
+  hipLaunchKernelGGL(window_bounds_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream), peak_mz,
+                     order, n_windows, ppm, mz_sorted, n_points, lo, hi);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_sample_spectra(const int64_t* sp_off, const double* mzs, const double* cum_ints, int64_t n_spectra,
+                       const double* lower, const double* upper, int64_t n_windows, int64_t* out_window,
+                       int64_t* out_spectrum, double* out_value, int64_t capacity, int64_t* count,
+                       void* stream) {
+  SMG_CHECK_ARG(n_spectra >= 0 && n_windows >= 0 && capacity >= 0, "negative sizes");
+  SMG_CHECK_ARG(count != nullptr, "null count");
+  SMG_HIP(hipMemsetAsync(count, 0, sizeof(int64_t), as_stream(stream)));
+  if (n_spectra == 0 || n_windows == 0) return SMG_OK;
+  SMG_CHECK_ARG(n_spectra < 65536, "n_spectra too large for the legacy sampler grid");
+  dim3 grid((unsigned)((n_windows + 255) / 256), (unsigned)n_spectra);
+  hipLaunchKernelGGL(sample_spectra_kernel, grid, dim3(256), 0, as_stream(stream), sp_off, mzs, cum_ints,
+                     n_spectra, lower, upper, n_windows, out_window, out_spectrum, out_value, capacity,
+                     reinterpret_cast<unsigned long long*>(count));
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+}  // extern "C"

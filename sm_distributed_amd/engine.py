@@ -1,0 +1,235 @@
+"""Device pipeline of the hot path: resident peak list -> m/z sort -> window search -> fused ion metrics.
+
+This is the layer the reference-API mirror (formula_imager_segm / formula_img_validator) sits on.
+Every call goes through libsmg.so (include/smg.h) on the current torch stream; torch is used only for
+HBM allocation and streams.  There is no CPU fallback: on a machine without a GPU these functions raise.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError("sm_distributed_amd device path needs a ROCm GPU (no CPU fallback)")
+    lib()  # fail loudly if libsmg.so is missing
+
+
+_ws_cache: dict = {}
+
+
+def workspace(nbytes: int, device, tag: str) -> torch.Tensor:
+    """Grow-only per-(tag, device) workspace so hot calls do not allocate."""
+    key = (tag, str(device))
+    t = _ws_cache.get(key)
+    if t is None or t.numel() < nbytes:
+        t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+        _ws_cache[key] = t
+    return t
+
+
+@dataclass
+class DevicePeaks:
+    """The dataset resident in HBM.
+
+    ``mz``: float32[N]; ``hits``: int64[N] holding uint64 ``pixel | f32bits(intensity) << 32``; both in
+    dataset (spectrum) order.  ``mz_sorted``/``hits_sorted`` are the m/z-sorted copies made by ``sort``.
+    """
+    mz: torch.Tensor
+    hits: torch.Tensor
+    nrows: int
+    ncols: int
+    mz_sorted: torch.Tensor | None = None
+    hits_sorted: torch.Tensor | None = None
+
+    @property
+    def n_points(self) -> int:
+        return int(self.mz.numel())
+
+    @property
+    def device(self):
+        return self.mz.device
+
+    @classmethod
+    def from_arrays(cls, sp_off, mz, ints, pixel_map, dims, device="cuda", stream=None) -> "DevicePeaks":
+        require_gpu()
+        mz = np.ascontiguousarray(mz, dtype=np.float32)
+        if mz.size and not (np.all(mz > 0) and np.all(np.isfinite(mz))):
+            raise ValueError("m/z values must be positive and finite")
+        d_off = torch.from_numpy(np.ascontiguousarray(sp_off, dtype=np.int64)).to(device)
+        d_pix = torch.from_numpy(np.ascontiguousarray(pixel_map, dtype=np.int32)).to(device)
+        d_ints = torch.from_numpy(np.ascontiguousarray(ints, dtype=np.float32)).to(device)
+        d_mz = torch.from_numpy(mz).to(device)
+        hits = torch.empty(mz.shape[0], dtype=torch.int64, device=device)
+        check(lib().smg_pack_hits(_p(d_off), _p(d_pix), len(pixel_map), _p(d_ints), mz.shape[0], _p(hits),
+                                  _stream(stream)), "smg_pack_hits")
+        return cls(mz=d_mz, hits=hits, nrows=int(dims[0]), ncols=int(dims[1]))
+
+    @classmethod
+    def from_device(cls, mz: torch.Tensor, hits: torch.Tensor, dims) -> "DevicePeaks":
+        return cls(mz=mz, hits=hits, nrows=int(dims[0]), ncols=int(dims[1]))
+
+    def sort(self, stream=None) -> "DevicePeaks":
+        n = self.n_points
+        if self.mz_sorted is None or self.mz_sorted.numel() != n:
+            self.mz_sorted = torch.empty_like(self.mz)
+            self.hits_sorted = torch.empty_like(self.hits)
+        if n == 0:
+            return self
+        sz = ctypes.c_size_t(0)
+        check(lib().smg_sort_points_workspace_size(n, ctypes.byref(sz)), "smg_sort_points_workspace_size")
+        ws = workspace(sz.value, self.device, "sort")
+        check(lib().smg_sort_points(_p(self.mz), _p(self.hits), n, _p(self.mz_sorted), _p(self.hits_sorted),
+                                    _p(ws), ws.numel(), _stream(stream)), "smg_sort_points")
+        return self
+
+
+@dataclass
+class DeviceIons:
+    """Theoretical windows of a batch of ions, ion-major (FormulasSegm.get_sf_peak_df / get_sf_peak_ints).
+
+    ``win_off``: int64[n_ion+1]; ``peak_mz``/``theor``: float64[n_win]; ``win_order``: windows sorted by
+    m/z (the reference's sf_peak_df order); ``ion_order``: ions sorted by principal m/z.
+    """
+    win_off: torch.Tensor
+    peak_mz: torch.Tensor
+    theor: torch.Tensor
+    win_order: torch.Tensor
+    ion_order: torch.Tensor
+    n_ions: int
+    n_windows: int
+    max_k: int
+
+    @classmethod
+    def from_arrays(cls, win_off, peak_mz, theor, device="cuda") -> "DeviceIons":
+        win_off = np.ascontiguousarray(win_off, dtype=np.int64)
+        peak_mz = np.ascontiguousarray(peak_mz, dtype=np.float64)
+        theor = np.ascontiguousarray(theor, dtype=np.float64)
+        n_ions = len(win_off) - 1
+        K = np.diff(win_off)
+        if n_ions and K.max(initial=0) > 32:
+            raise ValueError("at most 32 theoretical peaks per ion are supported")
+        win_order = np.argsort(peak_mz, kind="stable").astype(np.int64)
+        first = np.full(n_ions, np.inf)
+        nz = K > 0
+        first[nz] = peak_mz[win_off[:-1][nz]]
+        ion_order = np.argsort(first, kind="stable").astype(np.int64)
+        t = lambda a: torch.from_numpy(a).to(device)
+        return cls(win_off=t(win_off), peak_mz=t(peak_mz), theor=t(theor), win_order=t(win_order),
+                   ion_order=t(ion_order), n_ions=n_ions, n_windows=int(win_off[-1]) if n_ions else 0,
+                   max_k=int(K.max(initial=0)))
+
+
+def window_bounds(peaks: DevicePeaks, ions: DeviceIons, ppm: float, stream=None):
+    """searchsorted of formula_imager_segm.py:79-82 for every window -> (lo, hi) int64 device tensors."""
+    assert peaks.mz_sorted is not None, "call peaks.sort() first"
+    lo = torch.empty(ions.n_windows, dtype=torch.int64, device=peaks.device)
+    hi = torch.empty_like(lo)
+    check(lib().smg_window_bounds(_p(ions.peak_mz), _p(ions.win_order), ions.n_windows, float(ppm),
+                                  _p(peaks.mz_sorted), peaks.n_points, _p(lo), _p(hi), _stream(stream)),
+          "smg_window_bounds")
+    return lo, hi
+
+
+@dataclass
+class IonMetrics:
+    chaos: torch.Tensor
+    spatial: torch.Tensor
+    spectral: torch.Tensor
+    msm: torch.Tensor
+    flags: torch.Tensor
+
+    def to_numpy(self):
+        return {k: getattr(self, k).cpu().numpy() for k in ("chaos", "spatial", "spectral", "msm", "flags")}
+
+
+def ion_metrics_raw(hit_format: int, hits: torch.Tensor, hit_vals, lo, hi, win_off, theor, ion_order,
+                    n_ions: int, nrows: int, ncols: int, nlevels: int = 30, q: float = 99.0,
+                    do_preprocessing: bool = False, connectivity: int = 4, erosion_border: int = 0,
+                    out: IonMetrics | None = None, stream=None) -> IonMetrics:
+    device = lo.device
+    if out is None:
+        f64 = lambda: torch.empty(n_ions, dtype=torch.float64, device=device)
+        out = IonMetrics(f64(), f64(), f64(), f64(), torch.empty(n_ions, dtype=torch.int32, device=device))
+    if n_ions == 0:
+        return out
+    sz = ctypes.c_size_t(0)
+    check(lib().smg_ion_metrics_workspace_size(n_ions, nrows, ncols, ctypes.byref(sz)),
+          "smg_ion_metrics_workspace_size")
+    ws = workspace(sz.value, device, "metrics")
+    check(lib().smg_ion_metrics(hit_format, _p(hits), _p(hit_vals), _p(lo), _p(hi), _p(win_off), _p(theor),
+                                _p(ion_order), n_ions, nrows, ncols, nlevels, float(q), int(bool(do_preprocessing)),
+                                connectivity, erosion_border, _p(out.chaos), _p(out.spatial), _p(out.spectral),
+                                _p(out.msm), _p(out.flags), _p(ws), ws.numel(), _stream(stream)),
+          "smg_ion_metrics")
+    return out
+
+
+def ion_metrics(peaks: DevicePeaks, ions: DeviceIons, lo, hi, nlevels=30, q=99.0, do_preprocessing=False,
+                connectivity=4, erosion_border=0, out=None, stream=None) -> IonMetrics:
+    """Fused imaging + MSM scoring of every ion (one launch for the LDS path, one for the dense path)."""
+    return ion_metrics_raw(_lib.SMG_HITS_PACKED_F32, peaks.hits_sorted, None, lo, hi, ions.win_off, ions.theor,
+                           ions.ion_order, ions.n_ions, peaks.nrows, peaks.ncols, nlevels, q, do_preprocessing,
+                           connectivity, erosion_border, out, stream)
+
+
+def run_hot_path(peaks: DevicePeaks, ions: DeviceIons, ppm: float, nlevels: int = 30, **kw):
+    """One full pass: sort -> window search -> fused metrics (all on the current stream)."""
+    peaks.sort()
+    lo, hi = window_bounds(peaks, ions, ppm)
+    return ion_metrics(peaks, ions, lo, hi, nlevels=nlevels, **kw), lo, hi
+
+
+def metrics_from_images(ion_images, nrows, ncols, nlevels=30, q=99.0, do_preprocessing=False, connectivity=4,
+                        erosion_border=0, device="cuda"):
+    """Score explicit sparse images (the generic ``compute(iso_images_sparse, sf_ints)`` path).
+
+    ``ion_images``: iterable of ``(imgs, sf_ints)``; ``imgs`` is a list of scipy sparse matrices or None,
+    padded to len(sf_ints) as formula_img_validator.py:73-75 does.  Values keep float64.
+    Returns numpy arrays (chaos, spatial, spectral, msm, flags).
+    """
+    require_gpu()
+    pix_l, val_l, lo_l, hi_l, th_l, off = [], [], [], [], [], [0]
+    pos = 0
+    for imgs, sf_ints in ion_images:
+        imgs = list(imgs) + [None] * (len(sf_ints) - len(imgs))
+        for img, t in zip(imgs, sf_ints):
+            lo_l.append(pos)
+            if img is not None:
+                c = img.tocoo()
+                p = (c.row.astype(np.int64) * ncols + c.col.astype(np.int64))
+                pix_l.append(p.astype(np.uint32))
+                val_l.append(c.data.astype(np.float64))
+                pos += p.shape[0]
+            hi_l.append(pos)
+            th_l.append(float(t))
+        off.append(len(lo_l))
+    n_ions = len(off) - 1
+    if n_ions == 0:
+        return {k: np.zeros(0) for k in ("chaos", "spatial", "spectral", "msm", "flags")}
+    pix = np.concatenate(pix_l) if pix_l else np.zeros(1, np.uint32)
+    val = np.concatenate(val_l) if val_l else np.zeros(1, np.float64)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(device)
+    d_pix = t(pix.view(np.int32), np.int32)
+    d_val = t(val, np.float64)
+    res = ion_metrics_raw(_lib.SMG_HITS_SPLIT_F64, d_pix, d_val, t(lo_l, np.int64), t(hi_l, np.int64),
+                          t(off, np.int64), t(th_l, np.float64), None, n_ions, nrows, ncols, nlevels, q,
+                          do_preprocessing, connectivity, erosion_border)
+    torch.cuda.synchronize()
+    return res.to_numpy()

@@ -1,0 +1,144 @@
+"""Shared seeded parity cases: the same inputs feed the oracle (CPU) and the device path (GPU)."""
+from __future__ import annotations
+
+import numpy as np
+import pandas as pd
+
+from sm_distributed_amd import synthetic as syn
+
+
+def subset_ions(ions: syn.IonTable, idx) -> syn.IonTable:
+    idx = np.asarray(idx)
+    K = np.diff(ions.win_off)[idx]
+    off = np.zeros(len(idx) + 1, np.int64)
+    np.cumsum(K, out=off[1:])
+    sel = np.concatenate([np.arange(ions.win_off[i], ions.win_off[i + 1]) for i in idx]) if len(idx) else np.zeros(0, np.int64)
+    return syn.IonTable(sf_ids=ions.sf_ids[idx], adducts=ions.adducts[idx], win_off=off,
+                        peak_mz=ions.peak_mz[sel], peak_int=ions.peak_int[sel],
+                        target_adducts=ions.target_adducts, decoy_sample_size=ions.decoy_sample_size, td=ions.td)
+
+
+def sf_peak_df(ions: syn.IonTable) -> pd.DataFrame:
+    """FormulasSegm.get_sf_peak_df (formulas_segm.py:56-63): one row per theoretical peak, sorted by mz."""
+    K = np.diff(ions.win_off)
+    owner = np.repeat(np.arange(ions.n_ions), K)
+    peak_i = np.arange(ions.n_windows) - np.repeat(ions.win_off[:-1], K)
+    df = pd.DataFrame({"sf_id": ions.sf_ids[owner], "adduct": ions.adducts[owner], "peak_i": peak_i,
+                       "mz": ions.peak_mz})
+    return df.sort_values(by="mz", kind="stable")
+
+
+def sf_peak_ints(ions: syn.IonTable) -> dict:
+    return {(s, a): ions.peak_int[ions.win_off[i]:ions.win_off[i + 1]].tolist()
+            for i, (s, a) in enumerate(zip(ions.sf_ids, ions.adducts))}
+
+
+def add_duplicates(ds: syn.SpectraSet, frac: float, seed: int) -> syn.SpectraSet:
+    """Duplicate a fraction of points inside their own spectrum at m/z*(1+1e-7): same-window duplicate pixels."""
+    rng = np.random.default_rng(seed)
+    sp_of = np.repeat(np.arange(ds.n_spectra), np.diff(ds.sp_off))
+    pick = rng.random(ds.n_points) < frac
+    mz = np.concatenate([ds.mz, (ds.mz[pick].astype(np.float64) * (1 + 1e-7)).astype(np.float32)])
+    ints = np.concatenate([ds.ints, (ds.ints[pick] * rng.uniform(0.5, 2.0, pick.sum())).astype(np.float32)])
+    sp = np.concatenate([sp_of, sp_of[pick]])
+    order = np.lexsort((mz, sp))
+    sp, mz, ints = sp[order], mz[order], ints[order]
+    off = np.zeros(ds.n_spectra + 1, np.int64)
+    np.cumsum(np.bincount(sp, minlength=ds.n_spectra), out=off[1:])
+    return syn.SpectraSet(sp_off=off, mz=mz, ints=ints, coords=ds.coords)
+
+
+def boundary_ions(ds: syn.SpectraSet, ppm: float, n: int, seed: int) -> syn.IonTable:
+    """Ions whose windows have a data point exactly on the f64 lower or upper bound (inclusive window)."""
+    rng = np.random.default_rng(seed)
+    xs = ds.mz[rng.choice(ds.n_points, size=2 * n, replace=False)].astype(np.float64)
+    mzs = []
+    for j, x in enumerate(xs):
+        want_lower = j % 2 == 0
+        M = x / (1 - ppm * 1e-6) if want_lower else x / (1 + ppm * 1e-6)
+        found = None
+        for _ in range(2000):
+            d = M * ppm * 1e-6
+            b = (M - d) if want_lower else (M + d)
+            if b == x:
+                found = M
+                break
+            M = np.nextafter(M, np.inf if b < x else -np.inf)
+        if found is not None:
+            mzs.append(found)
+        if len(mzs) >= n:
+            break
+    mzs = np.array(mzs)
+    k = 4
+    win_off = np.arange(len(mzs) + 1, dtype=np.int64) * k
+    peak_mz = (mzs[:, None] + np.arange(k)[None, :] * syn.ISOTOPE_SPACING).ravel()
+    peak_int = np.tile(np.array([100.0, 40.0, 12.0, 3.0]), len(mzs))
+    return syn.IonTable(sf_ids=np.arange(len(mzs), dtype=np.int64) + 900000,
+                        adducts=np.array(['+H'] * len(mzs), dtype=object), win_off=win_off, peak_mz=peak_mz,
+                        peak_int=peak_int, td=(np.zeros(0), np.zeros(0), np.zeros(0)))
+
+
+def make_case(name: str):
+    """Returns (spectra, ions, ppm, kwargs) for a named parity case."""
+    if name == "basic":
+        ions = syn.make_ion_table(30, seed=1, decoy_seed=2)
+        ds = syn.make_dataset_np(32, 32, 500, seed=3, ions=ions, plant_fraction=0.3, plant_seed=4)
+        return ds, ions, 20.0, {}
+    if name == "zeros_rect":
+        ions = syn.make_ion_table(20, seed=11, decoy_seed=12)
+        ds = syn.make_dataset_np(24, 40, 400, seed=13, ions=ions, plant_fraction=0.4, plant_seed=14,
+                                 blob_sigma=(1.0, 4.0), zero_fraction=0.2)
+        return ds, ions, 30.0, {}
+    if name == "dups":
+        ions = syn.make_ion_table(20, seed=21, decoy_seed=22)
+        ds = syn.make_dataset_np(30, 30, 600, seed=23, ions=ions, plant_fraction=0.4, plant_seed=24)
+        return add_duplicates(ds, 0.2, 25), ions, 25.0, {}
+    if name == "row":
+        ions = syn.make_ion_table(15, seed=31, decoy_seed=32)
+        ds = syn.make_dataset_np(1, 300, 800, seed=33, ions=ions, plant_fraction=0.5, plant_seed=34)
+        return ds, ions, 40.0, {}
+    if name == "column":
+        ions = syn.make_ion_table(15, seed=41, decoy_seed=42)
+        ds = syn.make_dataset_np(200, 1, 800, seed=43, ions=ions, plant_fraction=0.5, plant_seed=44)
+        return ds, ions, 40.0, {}
+    if name == "row_border1":
+        ds, ions, ppm, _ = make_case("row")
+        return ds, ions, ppm, {"erosion_border": 1}
+    if name == "conn8_border1":
+        ds, ions, ppm, _ = make_case("basic")
+        return ds, ions, ppm, {"connectivity": 8, "erosion_border": 1}
+    if name == "nlevels":
+        ds, ions, ppm, _ = make_case("zeros_rect")
+        return ds, ions, ppm, {"nlevels": 7}
+    if name == "nlevels1":
+        ds, ions, ppm, _ = make_case("basic")
+        return ds, ions, ppm, {"nlevels": 1}
+    if name == "big_window":   # principal window > LDS capacity -> dense path
+        ions = syn.make_ion_table(6, seed=51, decoy_seed=52)
+        ds = syn.make_dataset_np(80, 80, 60, seed=53, ions=ions, plant_fraction=1.0, plant_seed=54,
+                                 blob_sigma=(150.0, 200.0))
+        return ds, ions, 10.0, {}
+    if name == "large_image":  # > 2^18 pixels -> dense path for every ion
+        full = syn.make_ion_table(2, seed=61, decoy_seed=62)
+        tgt = np.nonzero(np.isin(full.adducts, list(full.target_adducts)))[0][:4]
+        ions = subset_ions(full, np.concatenate([tgt, [0, 1]]))
+        ds = syn.make_dataset_np(520, 520, 3, seed=63, ions=ions, plant_fraction=1.0, plant_seed=64,
+                                 blob_sigma=(3.0, 8.0))
+        return ds, ions, 50.0, {}
+    if name == "boundary":
+        ds = syn.make_dataset_np(16, 16, 300, seed=71)
+        return ds, boundary_ions(ds, 5.0, 40, 72), 5.0, {}
+    raise KeyError(name)
+
+
+CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels", "nlevels1", "big_window",
+         "large_image", "boundary"]
+
+
+def oracle_run(ds, ions, ppm, nlevels=30, connectivity=4, erosion_border=0):
+    from oracle import msm_oracle as O
+    pm, dims = ds.pixel_map_dims()
+    imgs = O.compute_sf_images(ds.spectra(), pm, dims, sf_peak_df(ions), ppm)
+    df = O.sf_image_metrics(imgs, sf_peak_ints(ions), dims[0], dims[1], nlevels, connectivity=connectivity,
+                            erosion_border=erosion_border)
+    return imgs, df
