@@ -1,0 +1,248 @@
+#!/usr/bin/env python
+"""bench.py -- MSM-scored ions/sec of the molecule-annotation hot path on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over the resident dataset: global m/z sort of every centroid ->
+ppm-window search for every theoretical peak -> fused ion imaging + MSM scoring of every ion
+(formula_imager_segm.compute_sf_images + formula_img_validator.sf_image_metrics), plus, for N > 1, the
+RCCL all-gather of the per-ion metric rows.  Workload (config 3 of BASELINE.json, per GPU): 500x500-px
+synthetic dataset, Poisson(2000) centroids per spectrum (~5e8 points, generated in HBM), 20,000 synthetic
+formulas x (+H, +Na, +K targets + distinct decoys, 20 decoy draws per target as fdr.py does), ppm 2,
+nlevels 30.  N > 1: weak scaling, each rank scores its own 20,000-formula shard against the replicated
+dataset.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]   (N > 1 under torch.distributed.run)
+Prints ONE JSON line on rank 0 (see README/DESIGN.md for the fields).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "MSM-scored ions/sec (HMDB×3 adducts, 250k-px synth) + imaging-kernel HBM GB/s"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n-sf", type=int, default=20000)
+    ap.add_argument("--nrows", type=int, default=500)
+    ap.add_argument("--ncols", type=int, default=500)
+    ap.add_argument("--peaks", type=float, default=2000.0)
+    ap.add_argument("--ppm", type=float, default=2.0)
+    ap.add_argument("--nlevels", type=int, default=30)
+    ap.add_argument("--plant-fraction", type=float, default=0.02)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-ions", type=int, default=256)
+    ap.add_argument("--cpu-workers", type=int, default=8)
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from sm_distributed_amd import engine as E
+    from sm_distributed_amd import synthetic as syn
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+
+    t_setup = time.perf_counter()
+    ions = syn.make_ion_table(args.n_sf, seed=43 + 7919 * rank, decoy_seed=44 + 7919 * rank,
+                              sf_id_offset=rank * args.n_sf)
+    mz, hits, dims, info = syn.make_dataset_torch(args.nrows, args.ncols, args.peaks, seed=42, device=device,
+                                                  ions=ions, plant_fraction=args.plant_fraction,
+                                                  plant_seed=45 + rank)
+    peaks = E.DevicePeaks.from_device(mz, hits, dims)
+    dions = E.DeviceIons.from_arrays(ions.win_off, ions.peak_mz, ions.peak_int, device=device)
+    n_ions = dions.n_ions
+    f64 = lambda: torch.empty(n_ions, dtype=torch.float64, device=device)
+    out = E.IonMetrics(f64(), f64(), f64(), f64(), torch.empty(n_ions, dtype=torch.int32, device=device))
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s: {info['n_points']:,} points, "
+        f"{n_ions:,} ions, {dions.n_windows:,} windows, planted {info['n_planted_ions']} ions")
+
+    # rows gathered to every rank (RCCL all_gather over xGMI) when N > 1
+    if world > 1:
+        cnt = torch.tensor([n_ions], device=device, dtype=torch.int64)
+        cnts = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(cnts, cnt)
+        n_max = int(max(c.item() for c in cnts))
+        send = torch.zeros(n_max, 5, dtype=torch.float64, device=device)
+        recv = torch.empty(world * n_max, 5, dtype=torch.float64, device=device)
+
+    n_ev = 5
+    events = []
+
+    def step(timed):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(n_ev)] if timed else None
+        if ev:
+            ev[0].record()
+        peaks.sort()
+        if ev:
+            ev[1].record()
+        lo, hi = E.window_bounds(peaks, dions, args.ppm)
+        if ev:
+            ev[2].record()
+        E.ion_metrics(peaks, dions, lo, hi, nlevels=args.nlevels, out=out)
+        if ev:
+            ev[3].record()
+        if world > 1:
+            send[:n_ions, 0] = out.chaos
+            send[:n_ions, 1] = out.spatial
+            send[:n_ions, 2] = out.spectral
+            send[:n_ions, 3] = out.msm
+            send[:n_ions, 4] = out.flags.to(torch.float64)
+            dist.all_gather_into_tensor(recv, send)
+        if ev:
+            ev[4].record()
+            events.append(ev)
+        return lo, hi
+
+    for _ in range(args.warmup):
+        lo, hi = step(False)
+    torch.cuda.synchronize()
+    if args.warmup == 0:
+        lo, hi = step(False)
+        torch.cuda.synchronize()
+    sum_hits = int((hi - lo).sum().item())
+    n_scored = int(((out.flags & 1) != 0).sum().item())
+    n_dense = int(((out.flags & 2) != 0).sum().item())
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        sc = torch.tensor([n_scored], dtype=torch.int64, device=device)
+        dist.all_reduce(sc)
+        n_scored_total = int(sc.item())
+    else:
+        n_scored_total = n_scored
+    ms_per_step = elapsed / max(args.steps, 1) * 1e3
+
+    stage_names = ["sort", "window_search", "ion_metrics", "gather"]
+    stages = {n: 0.0 for n in stage_names}
+    for ev in events:
+        for j, n in enumerate(stage_names):
+            stages[n] += ev[j].elapsed_time(ev[j + 1])
+    stages = {n: v / max(len(events), 1) for n, v in stages.items()}
+
+    # algorithmic bytes per launch
+    alg = {
+        "ion_metrics": 8.0 * sum_hits,                   # one 8-B (pixel, f32) hit read per window point
+        "sort": 24.0 * info["n_points"],                 # read + write of (f32 key, 8-B hit) once
+        "window_search": 24.0 * dions.n_windows,         # peak m/z in, (lo, hi) out
+    }
+    dominant = max(("sort", "window_search", "ion_metrics"), key=lambda n: stages[n])
+    kernel_rows = {n: {"ms": stages[n], "alg_bytes": alg[n],
+                       "achieved_GBs": (alg[n] / (stages[n] * 1e-3) / 1e9) if stages[n] > 0 else None}
+                   for n in ("sort", "window_search", "ion_metrics")}
+    ach = kernel_rows[dominant]["achieved_GBs"]
+    roofline = {"bound": "hbm", "kernel": dominant, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (ach / HBM_PEAK_GBS) if ach else None, "traffic": None,
+                "imaging_kernel": {"kernel": "ion_metrics", "achieved": kernel_rows["ion_metrics"]["achieved_GBs"],
+                                   "frac": (kernel_rows["ion_metrics"]["achieved_GBs"] or 0) / HBM_PEAK_GBS}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, ions, mz, hits, dims, out)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": n_scored_total / (ms_per_step * 1e-3),
+            "unit": "ions/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {
+                "workload": (f"config3 per GPU: {args.nrows}x{args.ncols} px, Poisson({args.peaks:g}) centroids/"
+                             f"spectrum, {args.n_sf} formulas x (+H,+Na,+K + distinct decoys), ppm {args.ppm:g}, "
+                             f"nlevels {args.nlevels}"),
+                "n_points": info["n_points"], "n_ions": n_ions, "n_scored_ions_per_step": n_scored_total,
+                "n_windows": dions.n_windows, "sum_window_points": sum_hits, "n_dense_path_ions": n_dense,
+                "parallelism": f"ion shards x{world}, dataset replicated",
+            },
+            "stages_ms": stages,
+            "kernels": kernel_rows,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, ions, mz, hits, dims, out):
+    """Oracle on host cores over a bounded sample: ions whose principal m/z lies in [500, 505)."""
+    import torch
+
+    from oracle import cpu_baseline as CB
+    rng = np.random.default_rng(7)
+    first = ions.peak_mz[ions.win_off[:-1]]
+    cand = np.nonzero((first >= 500.0) & (first < 505.0))[0]
+    pick = np.sort(rng.choice(cand, size=min(args.cpu_ions, len(cand)), replace=False))
+    lo_b = min(ions.peak_mz[ions.win_off[i]] for i in pick) * (1 - 2 * args.ppm * 1e-6) - 1e-3
+    hi_b = max(ions.peak_mz[ions.win_off[i + 1] - 1] for i in pick) * (1 + 2 * args.ppm * 1e-6) + 1e-3
+    sel = (mz >= lo_b) & (mz <= hi_b)
+    b_mz = mz[sel].cpu().numpy()
+    b_hits = hits[sel].cpu().numpy().view(np.uint64)
+    b_pix = (b_hits & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    b_int = (b_hits >> np.uint64(32)).astype(np.uint32).view(np.float32)
+    tasks = [(int(i), ions.peak_mz[ions.win_off[i]:ions.win_off[i + 1]].copy(),
+              ions.peak_int[ions.win_off[i]:ions.win_off[i + 1]].copy()) for i in pick]
+    workers = max(1, min(args.cpu_workers, os.cpu_count() or 1))
+    rows, wall, per = CB.run_pool(b_pix, b_mz, b_int, dims, args.ppm, args.nlevels, tasks, workers)
+    # live cross-check of the GPU metrics on the sample
+    g = {k: getattr(out, k).cpu().numpy() for k in ("chaos", "spatial", "spectral")}
+    err = 0.0
+    for ion_id, c, s, p in rows:
+        err = max(err, abs(c - g["chaos"][ion_id]), abs(s - g["spatial"][ion_id]), abs(p - g["spectral"][ion_id]))
+    return {"value": len(rows) / wall, "unit": "ions/s", "cores": workers, "kind": "port",
+            "sample": (f"{len(pick)} ions ({len(rows)} scored) with principal m/z in [500,505) of the same dataset; each worker sorts "
+                       f"the {b_mz.size:,}-point m/z segment, then images+scores its ions (oracle/cpu_baseline.py); "
+                       f"wall {wall:.1f}s"),
+            "sample_rows": len(rows), "sample_max_abs_err_vs_gpu": err}
+
+
+if __name__ == "__main__":
+    main()

@@ -245,3 +245,67 @@ def _plant_np(ions: IonTable, nrows, ncols, fraction, seed, blob_sigma, mz_range
     if not sp_l:
         return np.zeros(0, np.int64), np.zeros(0, np.float32), np.zeros(0, np.float32)
     return np.concatenate(sp_l), np.concatenate(mz_l), np.concatenate(in_l)
+
+
+def make_dataset_torch(nrows: int, ncols: int, peaks_per_spectrum: float, seed: int = 42, device="cuda",
+                       mz_range=(100.0, 1000.0), ions: IonTable | None = None, plant_fraction: float = 0.02,
+                       plant_seed: int = 45, blob_sigma=(3.0, 12.0)):
+    """Config-3 style dataset generated directly in HBM (same recipe as make_dataset_np, torch RNG).
+
+    Returns ``(mz f32[N], hits int64[N], dims, info)`` in the resident layout (hits = pixel | f32 << 32),
+    spectrum-major (dataset order); pixel = spectrum index (row-major grid, dataset.py:52-66).
+    """
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    n_sp = nrows * ncols
+    counts = torch.poisson(torch.full((n_sp,), float(peaks_per_spectrum), device=device, dtype=torch.float32),
+                           generator=g).to(torch.int64)
+    n = int(counts.sum().item())
+    mz = (torch.rand(n, generator=g, dtype=torch.float64, device=device) * (mz_range[1] - mz_range[0])
+          + mz_range[0]).to(torch.float32)
+    ints = torch.exp(torch.randn(n, generator=g, dtype=torch.float32, device=device) * 1.5 + 6.0)
+    pix = torch.repeat_interleave(torch.arange(n_sp, device=device, dtype=torch.int64), counts)
+    extra_pix, extra_mz, extra_int = [], [], []
+    n_planted = 0
+    if ions is not None and plant_fraction > 0:
+        rng = np.random.default_rng(plant_seed)
+        tgt = np.nonzero(np.isin(ions.adducts, list(ions.target_adducts)))[0]
+        n_pl = max(1, int(round(plant_fraction * len(tgt)))) if len(tgt) else 0
+        chosen = rng.choice(tgt, size=n_pl, replace=False) if n_pl else []
+        gp = torch.Generator(device=device)
+        gp.manual_seed(plant_seed)
+        for ion in chosen:
+            cy, cx = rng.uniform(0, nrows), rng.uniform(0, ncols)
+            sig = rng.uniform(*blob_sigma)
+            amp = float(rng.lognormal(8.0, 0.5))
+            r0, r1 = max(0, int(cy - 4 * sig)), min(nrows, int(cy + 4 * sig) + 1)
+            c0, c1 = max(0, int(cx - 4 * sig)), min(ncols, int(cx + 4 * sig) + 1)
+            yy = torch.arange(r0, r1, device=device, dtype=torch.float64)[:, None]
+            xx = torch.arange(c0, c1, device=device, dtype=torch.float64)[None, :]
+            gauss = torch.exp(-((yy - cy) ** 2 + (xx - cx) ** 2) / (2 * sig * sig))
+            sel = torch.rand(gauss.shape, generator=gp, device=device, dtype=torch.float64) < gauss
+            rr, cc = torch.nonzero(sel, as_tuple=True)
+            if rr.numel() == 0:
+                continue
+            p = (rr + r0) * ncols + (cc + c0)
+            gv = gauss[rr, cc]
+            a, b = ions.win_off[ion], ions.win_off[ion + 1]
+            for k in range(a, b):
+                mzk = float(ions.peak_mz[k])
+                if not (mz_range[0] <= mzk < mz_range[1]):
+                    continue
+                jit = mzk * (1.0 + torch.randn(p.numel(), generator=gp, device=device, dtype=torch.float64) * 0.5e-6)
+                extra_pix.append(p)
+                extra_mz.append(jit.to(torch.float32))
+                extra_int.append((amp * gv * float(ions.peak_int[k]) / 100.0).to(torch.float32))
+            n_planted += 1
+    if extra_pix:
+        pix = torch.cat([pix] + extra_pix)
+        mz = torch.cat([mz] + extra_mz)
+        ints = torch.cat([ints] + extra_int)
+    hits = (pix & 0xFFFFFFFF) | (ints.view(torch.int32).to(torch.int64) << 32)
+    del pix, ints
+    info = {"n_points": int(mz.numel()), "n_spectra": n_sp, "n_planted_ions": n_planted,
+            "n_planted_points": int(sum(t.numel() for t in extra_mz))}
+    return mz, hits, (nrows, ncols), info
