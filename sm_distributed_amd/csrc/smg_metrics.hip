@@ -30,12 +30,16 @@ namespace smg {
 
 constexpr int BLOCK = 256;
 constexpr int NW = BLOCK / WAVE;
-constexpr int CAP = 4096;            // max points in the principal window on the LDS path
-constexpr int R0 = CAP / BLOCK;      // principal-window points held per thread
+constexpr int RMAX = 16;             // principal-window points held per thread
+constexpr int CAP_MAX = BLOCK * RMAX; // max points in the principal window on the LDS path
+constexpr int RC = 16;               // points per thread per chunk of the other windows
+constexpr int RT = 8;                // points per thread per chunk for windows > BLOCK*RC points
 constexpr int MAXK = 8;              // windows per ion on the LDS path
 constexpr int MAXK_DENSE = 32;       // windows per ion supported at all
-constexpr int FILT_WORDS = 2048;     // 65536-bit duplicate filter, two of them
-constexpr int FILT_BITS = FILT_WORDS * 32;
+constexpr int FILT_LOG2 = 15;        // 32768-bit duplicate filter, two of them
+constexpr int FILT_BITS = 1 << FILT_LOG2;
+constexpr int FILT_WORDS = FILT_BITS / 32;
+constexpr size_t LDS_BUDGET = 80 * 1024;  // per workgroup: two workgroups per CU
 constexpr int SUSP_CAP = 512;
 constexpr int NPX_LDS_MAX = 1 << 18; // images up to 262144 pixels use the LDS path
 
@@ -56,6 +60,10 @@ template <>
 struct Hits<SMG_HITS_PACKED_F32> {
   const uint64_t* h;
   const double* unused;
+  using Reg = uint64_t;
+  __device__ __forceinline__ Reg load(int64_t i) const { return h[i]; }
+  static __device__ __forceinline__ uint32_t pix(Reg r) { return (uint32_t)r; }
+  static __device__ __forceinline__ double val(Reg r) { return (double)__uint_as_float((uint32_t)(r >> 32)); }
   __device__ __forceinline__ void get(int64_t i, uint32_t& p, double& v) const {
     const uint64_t x = h[i];
     p = (uint32_t)x;
@@ -63,13 +71,22 @@ struct Hits<SMG_HITS_PACKED_F32> {
   }
 };
 
+struct PixVal {
+  uint32_t p;
+  double v;
+};
+
 template <>
 struct Hits<SMG_HITS_SPLIT_F64> {
-  const uint32_t* pix;
-  const double* val;
+  const uint32_t* pa;
+  const double* va;
+  using Reg = PixVal;
+  __device__ __forceinline__ Reg load(int64_t i) const { return PixVal{pa[i], va[i]}; }
+  static __device__ __forceinline__ uint32_t pix(Reg r) { return r.p; }
+  static __device__ __forceinline__ double val(Reg r) { return r.v; }
   __device__ __forceinline__ void get(int64_t i, uint32_t& p, double& v) const {
-    p = pix[i];
-    v = val[i];
+    p = pa[i];
+    v = va[i];
   }
 };
 
@@ -241,22 +258,37 @@ __device__ __forceinline__ bool uf_unite(uint32_t* par, uint32_t a, uint32_t b) 
 
 struct LdsLayout {
   int w32;        // bitmap words incl. padding (multiple of 4)
+  int cap;        // max principal-window points on the LDS path (runtime, <= CAP_MAX)
   size_t o_pf, o_vals, o_L, o_filt, o_susp_pix, o_susp_val, o_red, o_stats, o_ctr, o_wsc, bytes;
 };
 
 static inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+// LDS carve for an image of npx pixels: the principal-image capacity is whatever fits the per-workgroup
+// budget (LDS_BUDGET -> two workgroups per CU), capped by CAP_MAX and by the rank-order E-pixel array
+// that reuses the filter + suspect region in the chaos phase (4 * cap bytes).
 static LdsLayout lds_layout(int npx) {
   LdsLayout L;
   const int words = (npx + 31) / 32 + 2;
   L.w32 = (words + 3) & ~3;
+  size_t fixed = al16((size_t)L.w32 * 4) + al16((size_t)(L.w32 / 2) * 2) + al16((size_t)2 * FILT_WORDS * 4) +
+                 al16((size_t)SUSP_CAP * 4) + al16((size_t)SUSP_CAP * 8) + al16((size_t)8 * NW * 8) +
+                 al16((size_t)4 * MAXK * 8) + al16((size_t)C_NCTR * 4) + al16((size_t)NW * 4) + 64;
+  long avail = (long)LDS_BUDGET - (long)fixed;
+  int cap = avail > 0 ? (int)(avail / 9) : 0;
+  const int cap_e = (int)((al16((size_t)2 * FILT_WORDS * 4) + al16((size_t)SUSP_CAP * 4) +
+                           al16((size_t)SUSP_CAP * 8)) / 4);
+  cap = cap < CAP_MAX ? cap : CAP_MAX;
+  cap = cap < cap_e ? cap : cap_e;
+  cap &= ~63;
+  L.cap = cap;
   size_t o = al16((size_t)L.w32 * 4);
   L.o_pf = o;
   o = al16(o + (size_t)(L.w32 / 2) * 2);
   L.o_vals = o;
-  o = al16(o + (size_t)CAP * 8);
+  o = al16(o + (size_t)cap * 8);
   L.o_L = o;
-  o = al16(o + (size_t)CAP);
+  o = al16(o + (size_t)cap);
   L.o_filt = o;
   o = al16(o + (size_t)2 * FILT_WORDS * 4);
   L.o_susp_pix = o;
@@ -276,16 +308,31 @@ static LdsLayout lds_layout(int npx) {
 }
 
 __device__ __forceinline__ uint32_t filt_hash(uint32_t p, int npx) {
-  return npx <= FILT_BITS ? p : ((p * 2654435761u) >> 16);
+  return npx <= FILT_BITS ? p : ((p * 2654435761u) >> (32 - FILT_LOG2));
 }
 
+// ---------------------------------------------------------------------------------------------
+// LDS path kernel.  Phases (all on one workgroup, barriers between):
+//   0  issue the loads of the principal window (<= cap points, RMAX per thread) and of the first
+//      chunk of window 1 into registers; zero the LDS structures meanwhile
+//   1  principal bitmap (atomicOr; the thread that sets a bit owns that pixel), rank prefix,
+//      f64 values in rank order (ds_add_f64 sums duplicate pixels)
+//   2  sum x, sum x^2, sum x[x>0], #(x>0), max
+//   3  level index L per principal pixel
+//   5  for k >= 1: stream window k (registers, next window prefetched), join against the principal
+//      image, duplicate-pixel filter for sum y^2
+//   4a chaos candidates from owned principal pixels (7x7 bit windows, isolation pre-filter)
+//   4b Kruskal over eL with an LDS union-find
+//   6  finalize (thread 0)
+// ---------------------------------------------------------------------------------------------
 template <int FMT>
-__global__ void __launch_bounds__(BLOCK) ion_lds_kernel(
+__global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
     Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
     const int64_t* __restrict__ ion_off, const double* __restrict__ theor, const int64_t* __restrict__ ion_order,
     int64_t n_ions, Params P, LdsLayout LL, double* __restrict__ oc, double* __restrict__ osp,
     double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags,
     uint32_t* __restrict__ dense_list, uint32_t* __restrict__ dense_count) {
+  using Reg = typename Hits<FMT>::Reg;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* Hbm = reinterpret_cast<uint32_t*>(smem);
   uint16_t* pf = reinterpret_cast<uint16_t*>(smem + LL.o_pf);
@@ -299,10 +346,11 @@ __global__ void __launch_bounds__(BLOCK) ion_lds_kernel(
   double* stats = reinterpret_cast<double*>(smem + LL.o_stats);  // s, sy, syy, sxy  x MAXK
   int* ctr = reinterpret_cast<int*>(smem + LL.o_ctr);
   int* wsc = reinterpret_cast<int*>(smem + LL.o_wsc);
-  // E-phase aliases
+  const int cap = LL.cap;
+  // chaos-phase aliases
   uint32_t* epix = reinterpret_cast<uint32_t*>(vals);                 // append order
-  uint8_t* eL8 = reinterpret_cast<uint8_t*>(vals) + (size_t)CAP * 4;  // append order
-  uint32_t* epix_r = filtA;                                           // rank order (needs 4*CAP bytes)
+  uint8_t* eL8 = reinterpret_cast<uint8_t*>(vals) + (size_t)cap * 4;  // append order
+  uint32_t* epix_r = filtA;                                           // rank order (4*cap bytes)
   uint8_t* eLr = Lv;                                                  // rank order
   uint32_t* par = reinterpret_cast<uint32_t*>(vals);                  // rank order (after epix consumed)
 
@@ -323,13 +371,31 @@ __global__ void __launch_bounds__(BLOCK) ion_lds_kernel(
     return;
   }
   const int64_t lo0 = lo[w0];
-  const int n0 = (int)min<int64_t>(hi[w0] - lo0, (int64_t)CAP + 1);
-  if (K > MAXK || n0 > CAP) {
+  const int n0 = (int)min<int64_t>(hi[w0] - lo0, (int64_t)CAP_MAX + 1);
+  if (K > MAXK || n0 > cap) {
     if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
     return;
   }
 
-  // ---- phase 1: principal image -> bitmap, rank prefix, f64 values -------------------------
+  // ---- phase 0: loads in flight, LDS zeroing meanwhile --------------------------------------
+  Reg h0[RMAX];
+#pragma unroll
+  for (int j = 0; j < RMAX; ++j) {
+    const int i = tid + j * BLOCK;
+    if (i < n0) h0[j] = hits.load(lo0 + i);
+  }
+  Reg ra[RC], rb[RC];
+  if (K > 1) {
+    const int64_t a1 = lo[w0 + 1];
+    const int64_t n1 = hi[w0 + 1] - a1;
+    if (n1 <= (int64_t)BLOCK * RC) {
+#pragma unroll
+      for (int j = 0; j < RC; ++j) {
+        const int i = tid + j * BLOCK;
+        if (i < n1) ra[j] = hits.load(a1 + i);
+      }
+    }
+  }
   {
     uint4* z = reinterpret_cast<uint4*>(Hbm);
     for (int i = tid; i < LL.w32 / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
@@ -337,18 +403,22 @@ __global__ void __launch_bounds__(BLOCK) ion_lds_kernel(
     for (int i = tid; i < FILT_WORDS / 2; i += BLOCK) zf[i] = make_uint4(0, 0, 0, 0);
     if (tid < C_NCTR) ctr[tid] = 0;
   }
-  uint32_t hp[R0];
-  double hv[R0];
-#pragma unroll
-  for (int j = 0; j < R0; ++j) {
-    const int i = tid + j * BLOCK;
-    if (i < n0) hits.get(lo0 + i, hp[j], hv[j]);
-  }
   __syncthreads();
+
+  // ---- phase 1: principal image -> bitmap (+ ownership), rank prefix, f64 values ----------------
+  uint32_t own = 0;
+  uint32_t hp[RMAX];
 #pragma unroll
-  for (int j = 0; j < R0; ++j) {
+  for (int j = 0; j < RMAX; ++j) {
     const int i = tid + j * BLOCK;
-    if (i < n0) atomicOr(&Hbm[hp[j] >> 5], 1u << (hp[j] & 31));
+    hp[j] = 0;
+    if (i < n0) {
+      const uint32_t p = Hits<FMT>::pix(h0[j]);
+      hp[j] = p;
+      const uint32_t bit = 1u << (p & 31);
+      const uint32_t old = atomicOr(&Hbm[p >> 5], bit);
+      if (!(old & bit)) own |= 1u << j;
+    }
   }
   __syncthreads();
   const int n64 = (P.npx + 63) / 64;
@@ -356,9 +426,9 @@ __global__ void __launch_bounds__(BLOCK) ion_lds_kernel(
   for (int r = tid; r < nnz; r += BLOCK) vals[r] = 0.0;
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < R0; ++j) {
+  for (int j = 0; j < RMAX; ++j) {
     const int i = tid + j * BLOCK;
-    if (i < n0) atomicAdd(&vals[bm_rank(Hbm, pf, (int)hp[j])], hv[j]);
+    if (i < n0) atomicAdd(&vals[bm_rank(Hbm, pf, (int)hp[j])], Hits<FMT>::val(h0[j]));
   }
   __syncthreads();
 
@@ -391,14 +461,26 @@ __global__ void __launch_bounds__(BLOCK) ion_lds_kernel(
     for (int r = tid; r < nnz; r += BLOCK) Lv[r] = (uint8_t)level_of(vals[r], vmax, P);
   }
 
-  // ---- phase 5: stream the other isotope windows, join against the principal image ------------
-  for (int k = 1; k < K; ++k) {
+  // ---- phase 5: other isotope windows, joined against the principal image ------------------------
+  bool overflow = false;
+  auto window_pass = [&](int k, Reg (&cur)[RC], Reg (&nxt)[RC]) {
     const int64_t a = lo[w0 + k], b = hi[w0 + k];
+    const int64_t n = b - a;
+    const bool single = n <= (int64_t)BLOCK * RC;
+    // prefetch the next window's first chunk
+    if (k + 1 < K) {
+      const int64_t a2 = lo[w0 + k + 1];
+      const int64_t n2 = hi[w0 + k + 1] - a2;
+      if (n2 <= (int64_t)BLOCK * RC) {
+#pragma unroll
+        for (int j = 0; j < RC; ++j) {
+          const int i = tid + j * BLOCK;
+          if (i < n2) nxt[j] = hits.load(a2 + i);
+        }
+      }
+    }
     double psy = 0.0, psyy = 0.0, psxy = 0.0, psk = 0.0;
-    for (int64_t i = a + tid; i < b; i += BLOCK) {
-      uint32_t p;
-      double v;
-      hits.get(i, p, v);
+    auto pass1 = [&](uint32_t p, double v) {
       double x = 0.0;
       if (bm_test(Hbm, (int)p)) x = vals[bm_rank(Hbm, pf, (int)p)];
       psy += v;
@@ -408,12 +490,8 @@ __global__ void __launch_bounds__(BLOCK) ion_lds_kernel(
       const uint32_t bit = 1u << (h & 31);
       const uint32_t old = atomicOr(&filtA[h >> 5], bit);
       if (old & bit) atomicOr(&filtD[h >> 5], bit);
-    }
-    __syncthreads();
-    for (int64_t i = a + tid; i < b; i += BLOCK) {
-      uint32_t p;
-      double v;
-      hits.get(i, p, v);
+    };
+    auto pass2 = [&](uint32_t p, double v) {
       const uint32_t h = filt_hash(p, P.npx);
       if ((filtD[h >> 5] >> (h & 31)) & 1u) {
         const int s = atomicAdd(&ctr[C_NSUSP], 1);
@@ -423,6 +501,47 @@ __global__ void __launch_bounds__(BLOCK) ion_lds_kernel(
         }
       } else {
         psyy += v * v;
+      }
+    };
+    if (single) {
+#pragma unroll
+      for (int j = 0; j < RC; ++j) {
+        const int i = tid + j * BLOCK;
+        if (i < n) pass1(Hits<FMT>::pix(cur[j]), Hits<FMT>::val(cur[j]));
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < RC; ++j) {
+        const int i = tid + j * BLOCK;
+        if (i < n) pass2(Hits<FMT>::pix(cur[j]), Hits<FMT>::val(cur[j]));
+      }
+    } else {
+      for (int64_t c = 0; c < n; c += (int64_t)BLOCK * RT) {
+        Reg t[RT];
+#pragma unroll
+        for (int j = 0; j < RT; ++j) {
+          const int64_t i = c + tid + j * BLOCK;
+          if (i < n) t[j] = hits.load(a + i);
+        }
+#pragma unroll
+        for (int j = 0; j < RT; ++j) {
+          const int64_t i = c + tid + j * BLOCK;
+          if (i < n) pass1(Hits<FMT>::pix(t[j]), Hits<FMT>::val(t[j]));
+        }
+      }
+      __syncthreads();
+      for (int64_t c = 0; c < n; c += (int64_t)BLOCK * RT) {
+        Reg t[RT];
+#pragma unroll
+        for (int j = 0; j < RT; ++j) {
+          const int64_t i = c + tid + j * BLOCK;
+          if (i < n) t[j] = hits.load(a + i);
+        }
+#pragma unroll
+        for (int j = 0; j < RT; ++j) {
+          const int64_t i = c + tid + j * BLOCK;
+          if (i < n) pass2(Hits<FMT>::pix(t[j]), Hits<FMT>::val(t[j]));
+        }
       }
     }
     __syncthreads();
@@ -450,10 +569,7 @@ __global__ void __launch_bounds__(BLOCK) ion_lds_kernel(
     }
     double acc[4] = {psy, psyy, psxy, psk};
     block_sum<BLOCK, 4>(acc, red);  // contains barriers: every thread has read ctr[C_NSUSP]
-    if (ns > SUSP_CAP) {
-      if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
-      return;
-    }
+    if (ns > SUSP_CAP) overflow = true;
     if (tid == 0) {
       stats[0 * MAXK + k] = acc[3];
       stats[1 * MAXK + k] = acc[0];
@@ -461,117 +577,122 @@ __global__ void __launch_bounds__(BLOCK) ion_lds_kernel(
       stats[3 * MAXK + k] = acc[2];
       ctr[C_NSUSP] = 0;
     }
+  };
+  for (int k = 1; k < K && !overflow; k += 2) {
+    window_pass(k, ra, rb);
+    if (k + 1 < K && !overflow) window_pass(k + 1, rb, ra);
+  }
+  if (overflow) {
+    if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
+    return;
   }
   __syncthreads();
 
-  // ---- phase 4a: chaos candidates (pixels with eL >= 1) -----------------------------------------
+  // ---- phase 4a: chaos candidates (pixels with eL >= 1) from owned principal pixels --------------
+  // (i) bit-level screen: a candidate p in cross(s) survives if its 3x3 box is covered by the
+  //     dilated bitmap (superset of the exact condition) and s is its owner (smallest principal pixel
+  //     of cross(p)); survivors go to an LDS list (the vals region is free: L is computed).
+  // (ii) exact eL for the survivors from the level indices.
   double chaos_raw = NAN;
   if (chaos_ok) {
-    const int w32u = (P.npx + 31) / 32;
-    for (int w = tid; w < w32u; w += BLOCK) {
-      uint32_t bits = Hbm[w];
-      while (bits) {
-        const int bpos = __ffs(bits) - 1;
-        bits &= bits - 1u;
-        const int s = w * 32 + bpos;
-        const int rs = s / P.ncols, cs = s - rs * P.ncols;
-        uint32_t H[7];
+#pragma unroll 1
+    for (int j = 0; j < RMAX; ++j) {
+      if (!((own >> j) & 1u)) continue;
+      const int s = (int)hp[j];
+      const int rs = s / P.ncols, cs = s - rs * P.ncols;
+      uint32_t H[7];
 #pragma unroll
-        for (int d = 0; d < 7; ++d) H[d] = bits7(Hbm, rs - 3 + d, cs - 3, P);
-        uint32_t cv = 0;
+      for (int d = 0; d < 7; ++d) H[d] = bits7(Hbm, rs - 3 + d, cs - 3, P);
+      // isolation pre-filter (erosion border = background only): an eL>0 pixel in the cross of s needs
+      // another principal pixel in s's 7x7, since the 4-cross of s alone cannot cover a 3x3 box
+      if (!P.erosion_border && (H[0] | H[1] | H[2] | (H[3] & ~8u) | H[4] | H[5] | H[6]) == 0u) continue;
+      uint32_t cv = 0;
 #pragma unroll
-        for (int j = 0; j < 7; ++j) {
-          const int c = cs - 3 + j;
-          if (c >= 0 && c < P.ncols) cv |= 1u << j;
-        }
-        uint32_t D[7];
-        D[0] = D[6] = 0;
+      for (int jj = 0; jj < 7; ++jj) {
+        const int c = cs - 3 + jj;
+        if (c >= 0 && c < P.ncols) cv |= 1u << jj;
+      }
+      uint32_t D[7];
+      D[0] = D[6] = 0;
 #pragma unroll
-        for (int d = 1; d <= 5; ++d) {
-          const int row = rs - 3 + d;
-          const bool rv = row >= 0 && row < P.nrows;
-          uint32_t x = (H[d] | (H[d] << 1) | (H[d] >> 1) | H[d - 1] | H[d + 1]) & cv;
-          if (!rv) x = 0;
-          if (P.erosion_border) x |= rv ? (~cv & 0x7Fu) : 0x7Fu;
-          D[d] = x & 0x7Fu;
-        }
-        auto hb = [&](int dr, int dc) -> uint32_t { return (H[3 + dr] >> (3 + dc)) & 1u; };
-        const int cand_dr[5] = {0, 0, 0, -1, 1};
-        const int cand_dc[5] = {0, 1, -1, 0, 0};
-#pragma unroll
-        for (int ci = 0; ci < 5; ++ci) {
-          const int dr = cand_dr[ci], dc = cand_dc[ci];
-          const int rp = rs + dr, cp = cs + dc;
-          if (rp < 0 || rp >= P.nrows || cp < 0 || cp >= P.ncols) continue;
-          bool owner;
-          if (ci == 0) owner = !hb(-1, 0) && !hb(0, -1);
-          else if (ci == 1) owner = !hb(-1, 1);
-          else if (ci == 2) owner = !hb(-1, -1) && !hb(0, -2) && !hb(0, -1);
-          else if (ci == 3) owner = !hb(-2, 0) && !hb(-1, -1) && !hb(-1, 0) && !hb(-1, 1);
-          else owner = true;
-          if (!owner) continue;
-          bool pass = true;
-#pragma unroll
-          for (int e = -1; e <= 1; ++e) pass = pass && (((D[3 + dr + e] >> (3 + dc - 1)) & 7u) == 7u);
-          if (!pass) continue;
-          // exact eL(p) = min_{q in N9(p)} max_{q' in N4[q]} L(q')
-          int lv[5][5];
-#pragma unroll
-          for (int a = -2; a <= 2; ++a)
-#pragma unroll
-            for (int b = -2; b <= 2; ++b) {
-              lv[a + 2][b + 2] = 0;
-              if ((a == -2 || a == 2) && (b == -2 || b == 2)) continue;
-              if (hb(dr + a, dc + b)) {
-                const int q = (rp + a) * P.ncols + (cp + b);
-                lv[a + 2][b + 2] = Lv[bm_rank(Hbm, pf, q)];
-              }
-            }
-          int mn = 1 << 20;
-#pragma unroll
-          for (int qa = -1; qa <= 1; ++qa)
-#pragma unroll
-            for (int qb = -1; qb <= 1; ++qb) {
-              const int rq = rp + qa, cq = cp + qb;
-              if (rq < 0 || rq >= P.nrows || cq < 0 || cq >= P.ncols) {
-                if (!P.erosion_border) mn = 0;
-                continue;
-              }
-              int dl = lv[qa + 2][qb + 2];
-              dl = max(dl, lv[qa + 1][qb + 2]);
-              dl = max(dl, lv[qa + 3][qb + 2]);
-              dl = max(dl, lv[qa + 2][qb + 1]);
-              dl = max(dl, lv[qa + 2][qb + 3]);
-              mn = min(mn, dl);
-            }
-          if (mn >= 1 && mn < (1 << 20)) {
-            const int idx = atomicAdd(&ctr[C_NE], 1);
-            if (idx < CAP) {
-              epix[idx] = (uint32_t)(rp * P.ncols + cp);
-              eL8[idx] = (uint8_t)mn;
-            }
-            atomicMax(&ctr[C_EMAX], mn);
-          }
-        }
+      for (int d = 1; d <= 5; ++d) {
+        const int row = rs - 3 + d;
+        const bool rv = row >= 0 && row < P.nrows;
+        uint32_t x = (H[d] | (H[d] << 1) | (H[d] >> 1) | H[d - 1] | H[d + 1]) & cv;
+        if (!rv) x = 0;
+        if (P.erosion_border) x |= rv ? (~cv & 0x7Fu) : 0x7Fu;
+        D[d] = x & 0x7Fu;
+      }
+#define SMG_HB(dr, dc) ((H[3 + (dr)] >> (3 + (dc))) & 1u)
+#define SMG_BOX(dr, dc) ((((D[2 + (dr)] >> (2 + (dc))) & 7u) == 7u) && (((D[3 + (dr)] >> (2 + (dc))) & 7u) == 7u) && \
+                         (((D[4 + (dr)] >> (2 + (dc))) & 7u) == 7u))
+      const bool in_l = cs > 0, in_r = cs + 1 < P.ncols, in_u = rs > 0, in_d = rs + 1 < P.nrows;
+      uint32_t pass = 0;
+      if (SMG_BOX(0, 0) && !SMG_HB(-1, 0) && !SMG_HB(0, -1)) pass |= 1u;
+      if (in_r && SMG_BOX(0, 1) && !SMG_HB(-1, 1)) pass |= 2u;
+      if (in_l && SMG_BOX(0, -1) && !SMG_HB(-1, -1) && !SMG_HB(0, -2) && !SMG_HB(0, -1)) pass |= 4u;
+      if (in_u && SMG_BOX(-1, 0) && !SMG_HB(-2, 0) && !SMG_HB(-1, -1) && !SMG_HB(-1, 0) && !SMG_HB(-1, 1))
+        pass |= 8u;
+      if (in_d && SMG_BOX(1, 0)) pass |= 16u;
+#undef SMG_BOX
+#undef SMG_HB
+      while (pass) {
+        const int ci = __ffs(pass) - 1;
+        pass &= pass - 1;
+        const int p = s + (ci == 1 ? 1 : ci == 2 ? -1 : ci == 3 ? -P.ncols : ci == 4 ? P.ncols : 0);
+        const int idx = atomicAdd(&ctr[C_NE], 1);
+        if (idx < cap) epix[idx] = (uint32_t)p;
       }
     }
     __syncthreads();
-
-    // ---- phase 4b: Kruskal over eL (levels descending) with an LDS union-find -------------------
-    const int m = ctr[C_NE];
-    if (m > CAP) {
+    const int ncand = ctr[C_NE];
+    if (ncand > cap) {
       if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
       return;
     }
+    // (ii) exact eL(p) = min_{q in N9(p)} max_{q' in N4[q] in image} L(q')
+    int emax_local = 0;
+    for (int c = tid; c < ncand; c += BLOCK) {
+      const int p = (int)epix[c];
+      const int rp = p / P.ncols, cp = p - rp * P.ncols;
+      int mn = 1 << 20;
+      for (int qa = -1; qa <= 1; ++qa) {
+        for (int qb = -1; qb <= 1; ++qb) {
+          const int rq = rp + qa, cq = cp + qb;
+          if (rq < 0 || rq >= P.nrows || cq < 0 || cq >= P.ncols) {
+            if (!P.erosion_border) mn = 0;
+            continue;
+          }
+          int dl = 0;
+          for (int t = 0; t < 5; ++t) {
+            const int ra = rq + (t == 1 ? -1 : t == 2 ? 1 : 0);
+            const int ca = cq + (t == 3 ? -1 : t == 4 ? 1 : 0);
+            if (ra < 0 || ra >= P.nrows || ca < 0 || ca >= P.ncols) continue;
+            const int q = ra * P.ncols + ca;
+            if (bm_test(Hbm, q)) dl = max(dl, (int)Lv[bm_rank(Hbm, pf, q)]);
+          }
+          mn = min(mn, dl);
+        }
+      }
+      if (mn >= (1 << 20)) mn = 0;
+      eL8[c] = (uint8_t)mn;
+      emax_local = max(emax_local, mn);
+    }
+    if (emax_local > 0) atomicMax(&ctr[C_EMAX], emax_local);
+    __syncthreads();
+
+    // ---- phase 4b: Kruskal over eL (levels descending) with an LDS union-find -------------------
     double sum_c = 0.0;
-    if (m > 0) {
+    if (ctr[C_EMAX] > 0) {
       uint4* z = reinterpret_cast<uint4*>(Hbm);
       for (int i = tid; i < LL.w32 / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
       __syncthreads();
-      for (int i = tid; i < m; i += BLOCK) atomicOr(&Hbm[epix[i] >> 5], 1u << (epix[i] & 31));
+      for (int i = tid; i < ncand; i += BLOCK)
+        if (eL8[i]) atomicOr(&Hbm[epix[i] >> 5], 1u << (epix[i] & 31));
       __syncthreads();
-      bm_build_prefix(Hbm, pf, n64, wsc);
-      for (int i = tid; i < m; i += BLOCK) {
+      const int m = bm_build_prefix(Hbm, pf, n64, wsc);
+      for (int i = tid; i < ncand; i += BLOCK) {
+        if (!eL8[i]) continue;
         const uint32_t p = epix[i];
         const int r = bm_rank(Hbm, pf, (int)p);
         epix_r[r] = p;
@@ -621,21 +742,10 @@ __global__ void __launch_bounds__(BLOCK) ion_lds_kernel(
   }
 
   if (tid == 0) {
-    double t[MAXK], s[MAXK], sy[MAXK], syy[MAXK], sxy[MAXK];
-    for (int k = 0; k < K; ++k) {
-      t[k] = theor[w0 + k];
-      if (k == 0) {
-        s[k] = s0;
-        sy[k] = syy[k] = sxy[k] = 0.0;
-      } else {
-        s[k] = stats[0 * MAXK + k];
-        sy[k] = stats[1 * MAXK + k];
-        syy[k] = stats[2 * MAXK + k];
-        sxy[k] = stats[3 * MAXK + k];
-      }
-    }
-    finalize_ion(K, t, s, sx, sxx, sy, syy, sxy, (double)P.npx, chaos_raw, ion, flags, oc, osp, osc, omsm,
-                 oflags);
+    stats[0] = s0;
+    stats[MAXK] = stats[2 * MAXK] = stats[3 * MAXK] = 0.0;
+    finalize_ion(K, theor + w0, stats, sx, sxx, stats + MAXK, stats + 2 * MAXK, stats + 3 * MAXK, (double)P.npx,
+                 chaos_raw, ion, flags, oc, osp, osc, omsm, oflags);
   }
 }
 
@@ -927,8 +1037,8 @@ static int launch_metrics(Hits<FMT> hits, const int64_t* lo, const int64_t* hi, 
   unsigned char* slots = ws + WS_HEADER + al16((size_t)n_ions * 4);
   const size_t slot_bytes = dense_slot_bytes(P.npx);
   SMG_HIP(hipMemsetAsync(ws, 0, WS_HEADER, st));
-  if (P.npx <= NPX_LDS_MAX) {
-    LdsLayout LL = lds_layout(P.npx);
+  LdsLayout LL = lds_layout(P.npx);
+  if (P.npx <= NPX_LDS_MAX && LL.cap >= 256) {
     SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ion_lds_kernel<FMT>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LL.bytes));
     hipLaunchKernelGGL(ion_lds_kernel<FMT>, dim3((unsigned)n_ions), dim3(BLOCK), LL.bytes, st, hits, lo, hi,
