@@ -40,10 +40,30 @@ constexpr int FILT_LOG2 = 15;        // 32768-bit duplicate filter, two of them
 constexpr int FILT_BITS = 1 << FILT_LOG2;
 constexpr int FILT_WORDS = FILT_BITS / 32;
 constexpr size_t LDS_BUDGET = 80 * 1024;  // per workgroup: two workgroups per CU
-constexpr int SUSP_CAP = 512;
+constexpr int SUSP_CAP = 512;         // duplicate-filter suspects per window on the LDS path
+constexpr int TBL = 1024;             // suspect table slots (pixel-keyed f64 sums)
+constexpr int SIDE = 256;             // principal duplicate-pixel table slots (rank-keyed f64 sums)
 constexpr int NPX_LDS_MAX = 1 << 18; // images up to 262144 pixels use the LDS path
 
 enum { C_NSUSP = 0, C_NE, C_EMAX, C_ABORT, C_NCTR = 8 };
+
+// Diagnostic build only (-DSMG_STAMPS): per-phase wall cycles of the LDS kernel, summed over workgroups
+// into a buffer of their own (read back by smg_debug_stamps); the shipped build executes no stamp.
+#ifdef SMG_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define STAMP_INIT() unsigned long long _st0 = __builtin_amdgcn_s_memtime(), _st1
+#define STAMP(i)                                                                   \
+  do {                                                                             \
+    if (threadIdx.x == 0) {                                                        \
+      _st1 = __builtin_amdgcn_s_memtime();                                         \
+      atomicAdd(&g_stamps[i], _st1 - _st0);                                        \
+      _st0 = _st1;                                                                 \
+    }                                                                              \
+  } while (0)
+#else
+#define STAMP_INIT()
+#define STAMP(i)
+#endif
 
 struct Params {
   int32_t nrows, ncols, npx;
@@ -259,46 +279,55 @@ __device__ __forceinline__ bool uf_unite(uint32_t* par, uint32_t a, uint32_t b) 
 struct LdsLayout {
   int w32;        // bitmap words incl. padding (multiple of 4)
   int cap;        // max principal-window points on the LDS path (runtime, <= CAP_MAX)
-  size_t o_pf, o_vals, o_L, o_filt, o_susp_pix, o_susp_val, o_red, o_stats, o_ctr, o_wsc, bytes;
+  size_t o_pf, o_vals, o_L, o_dupb, o_side_k, o_side_v, o_filt, o_tkey, o_tval, o_part, o_red, o_ctr, o_wsc,
+      bytes;
 };
 
 static inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-// LDS carve for an image of npx pixels: the principal-image capacity is whatever fits the per-workgroup
-// budget (LDS_BUDGET -> two workgroups per CU), capped by CAP_MAX and by the rank-order E-pixel array
-// that reuses the filter + suspect region in the chaos phase (4 * cap bytes).
-static LdsLayout lds_layout(int npx) {
+// LDS carve for an image of npx pixels and principal values of val_bytes each.  The principal-image
+// capacity is whatever fits the per-workgroup budget (LDS_BUDGET -> two workgroups per CU), capped by
+// CAP_MAX and by the chaos phase's reuse of the filter + table region (rank-ordered E pixels: 5 B each).
+static LdsLayout lds_layout(int npx, int val_bytes) {
   LdsLayout L;
   const int words = (npx + 31) / 32 + 2;
   L.w32 = (words + 3) & ~3;
-  size_t fixed = al16((size_t)L.w32 * 4) + al16((size_t)(L.w32 / 2) * 2) + al16((size_t)2 * FILT_WORDS * 4) +
-                 al16((size_t)SUSP_CAP * 4) + al16((size_t)SUSP_CAP * 8) + al16((size_t)8 * NW * 8) +
-                 al16((size_t)4 * MAXK * 8) + al16((size_t)C_NCTR * 4) + al16((size_t)NW * 4) + 64;
-  long avail = (long)LDS_BUDGET - (long)fixed;
-  int cap = avail > 0 ? (int)(avail / 9) : 0;
-  const int cap_e = (int)((al16((size_t)2 * FILT_WORDS * 4) + al16((size_t)SUSP_CAP * 4) +
-                           al16((size_t)SUSP_CAP * 8)) / 4);
+  const size_t region_ft = al16((size_t)2 * FILT_WORDS * 4) + al16((size_t)TBL * 4) + al16((size_t)TBL * 8);
+  const size_t fixed = al16((size_t)L.w32 * 4) + al16((size_t)(L.w32 / 2) * 2) + al16((size_t)SIDE * 4) +
+                       al16((size_t)SIDE * 8) + region_ft + al16((size_t)MAXK * NW * 4 * 8) +
+                       al16((size_t)8 * NW * 8) + al16((size_t)C_NCTR * 4) + al16((size_t)NW * 4) + 128;
+  const long avail = (long)LDS_BUDGET - (long)fixed;
+  // per principal point: value + level byte + dup bit
+  int cap = avail > 0 ? (int)((avail * 8) / (8 * val_bytes + 8 + 1)) : 0;
   cap = cap < CAP_MAX ? cap : CAP_MAX;
+  const int cap_e = (int)(region_ft / 5);
   cap = cap < cap_e ? cap : cap_e;
+  cap = cap < (int)(((size_t)cap * val_bytes) / 4) ? cap : cap;  // epix (4 B) fits the value region
   cap &= ~63;
   L.cap = cap;
   size_t o = al16((size_t)L.w32 * 4);
   L.o_pf = o;
   o = al16(o + (size_t)(L.w32 / 2) * 2);
   L.o_vals = o;
-  o = al16(o + (size_t)cap * 8);
+  o = al16(o + (size_t)cap * (val_bytes < 4 ? 4 : val_bytes));
   L.o_L = o;
   o = al16(o + (size_t)cap);
+  L.o_dupb = o;
+  o = al16(o + (size_t)((cap + 31) / 32) * 4);
+  L.o_side_k = o;
+  o = al16(o + (size_t)SIDE * 4);
+  L.o_side_v = o;
+  o = al16(o + (size_t)SIDE * 8);
   L.o_filt = o;
   o = al16(o + (size_t)2 * FILT_WORDS * 4);
-  L.o_susp_pix = o;
-  o = al16(o + (size_t)SUSP_CAP * 4);
-  L.o_susp_val = o;
-  o = al16(o + (size_t)SUSP_CAP * 8);
+  L.o_tkey = o;
+  o = al16(o + (size_t)TBL * 4);
+  L.o_tval = o;
+  o = al16(o + (size_t)TBL * 8);
+  L.o_part = o;
+  o = al16(o + (size_t)MAXK * NW * 4 * 8);
   L.o_red = o;
   o = al16(o + (size_t)8 * NW * 8);
-  L.o_stats = o;
-  o = al16(o + (size_t)4 * MAXK * 8);
   L.o_ctr = o;
   o = al16(o + (size_t)C_NCTR * 4);
   L.o_wsc = o;
@@ -311,17 +340,68 @@ __device__ __forceinline__ uint32_t filt_hash(uint32_t p, int npx) {
   return npx <= FILT_BITS ? p : ((p * 2654435761u) >> (32 - FILT_LOG2));
 }
 
+// open-addressing f64 accumulators keyed by u32 (EMPTY = 0xFFFFFFFF); returns false when full
+template <int NSLOT>
+__device__ __forceinline__ bool tbl_add(uint32_t* keys, double* vals, uint32_t key, double v) {
+  uint32_t h = (key * 2654435761u) >> (32 - __builtin_ctz(NSLOT));
+  for (int probe = 0; probe < NSLOT; ++probe) {
+    const uint32_t old = atomicCAS(&keys[h], 0xFFFFFFFFu, key);
+    if (old == 0xFFFFFFFFu || old == key) {
+      atomicAdd(&vals[h], v);
+      return true;
+    }
+    h = (h + 1) & (NSLOT - 1);
+  }
+  return false;
+}
+
+template <int NSLOT>
+__device__ __forceinline__ int tbl_find(const uint32_t* keys, uint32_t key) {
+  uint32_t h = (key * 2654435761u) >> (32 - __builtin_ctz(NSLOT));
+  for (int probe = 0; probe < NSLOT; ++probe) {
+    const uint32_t k = keys[h];
+    if (k == key) return (int)h;
+    if (k == 0xFFFFFFFFu) return -1;
+    h = (h + 1) & (NSLOT - 1);
+  }
+  return -1;
+}
+
+// level index via the closed form of np.linspace(0, 1, n): lev_i = i*step (i < n-1), lev_{n-1} = 1.0;
+// L = #{i : lev_i < norm}; the estimate is corrected with exact comparisons so it equals the loop.
+__device__ __forceinline__ int level_fast(double v, double vmax, const Params& P) {
+  const double norm = v / vmax;
+  const int n = P.nlevels;
+  if (n == 1) return (0.0 < norm) ? 1 : 0;
+  if (!(norm > 0.0)) return 0;
+  int j = (int)(norm * (double)(n - 1));  // candidate count of i*step < norm among i < n-1
+  j = j < 0 ? 0 : (j > n - 1 ? n - 1 : j);
+  while (j > 0 && !((double)(j - 1) * P.step < norm)) --j;
+  while (j < n - 1 && (double)j * P.step < norm) ++j;
+  return j + ((1.0 < norm) ? 1 : 0);
+}
+
+template <int FMT>
+struct ValStore;
+template <>
+struct ValStore<SMG_HITS_PACKED_F32> {
+  using T = float;  // a single f32 hit is exact in f32; duplicate pixels use the f64 side table
+};
+template <>
+struct ValStore<SMG_HITS_SPLIT_F64> {
+  using T = double;
+};
+
 // ---------------------------------------------------------------------------------------------
-// LDS path kernel.  Phases (all on one workgroup, barriers between):
+// LDS path kernel (one workgroup per ion; two workgroups per CU).  Phases, barriers between:
 //   0  issue the loads of the principal window (<= cap points, RMAX per thread) and of the first
-//      chunk of window 1 into registers; zero the LDS structures meanwhile
-//   1  principal bitmap (atomicOr; the thread that sets a bit owns that pixel), rank prefix,
-//      f64 values in rank order (ds_add_f64 sums duplicate pixels)
-//   2  sum x, sum x^2, sum x[x>0], #(x>0), max
-//   3  level index L per principal pixel
+//      chunk of window 1 into registers; initialise the LDS structures meanwhile
+//   1  principal bitmap (atomicOr; the thread that sets a bit owns the pixel), rank prefix, values in
+//      rank order (f32 for single hits, exact f64 side table for duplicate pixels)
+//   2  one fused reduction: sum x, sum x^2, sum x[x>0], #(x>0), max; then level index per pixel
 //   5  for k >= 1: stream window k (registers, next window prefetched), join against the principal
-//      image, duplicate-pixel filter for sum y^2
-//   4a chaos candidates from owned principal pixels (7x7 bit windows, isolation pre-filter)
+//      image; duplicate pixels of window k found by a hashed 2-bit filter and summed in an LDS table
+//   4a chaos candidates from owned principal pixels (7x7 bit windows, isolation pre-filter), exact eL
 //   4b Kruskal over eL with an LDS union-find
 //   6  finalize (thread 0)
 // ---------------------------------------------------------------------------------------------
@@ -333,28 +413,34 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
     double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags,
     uint32_t* __restrict__ dense_list, uint32_t* __restrict__ dense_count) {
   using Reg = typename Hits<FMT>::Reg;
+  using VT = typename ValStore<FMT>::T;
+  constexpr bool SIDE_TABLE = (FMT == SMG_HITS_PACKED_F32);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* Hbm = reinterpret_cast<uint32_t*>(smem);
   uint16_t* pf = reinterpret_cast<uint16_t*>(smem + LL.o_pf);
-  double* vals = reinterpret_cast<double*>(smem + LL.o_vals);
+  VT* vals = reinterpret_cast<VT*>(smem + LL.o_vals);
   uint8_t* Lv = reinterpret_cast<uint8_t*>(smem + LL.o_L);
+  uint32_t* dupb = reinterpret_cast<uint32_t*>(smem + LL.o_dupb);
+  uint32_t* side_k = reinterpret_cast<uint32_t*>(smem + LL.o_side_k);
+  double* side_v = reinterpret_cast<double*>(smem + LL.o_side_v);
   uint32_t* filtA = reinterpret_cast<uint32_t*>(smem + LL.o_filt);
   uint32_t* filtD = filtA + FILT_WORDS;
-  uint32_t* susp_pix = reinterpret_cast<uint32_t*>(smem + LL.o_susp_pix);
-  double* susp_val = reinterpret_cast<double*>(smem + LL.o_susp_val);
+  uint32_t* tkey = reinterpret_cast<uint32_t*>(smem + LL.o_tkey);
+  double* tval = reinterpret_cast<double*>(smem + LL.o_tval);
+  double* part = reinterpret_cast<double*>(smem + LL.o_part);  // [MAXK][NW][4]: s_k, sy, syy, sxy
   double* red = reinterpret_cast<double*>(smem + LL.o_red);
-  double* stats = reinterpret_cast<double*>(smem + LL.o_stats);  // s, sy, syy, sxy  x MAXK
   int* ctr = reinterpret_cast<int*>(smem + LL.o_ctr);
   int* wsc = reinterpret_cast<int*>(smem + LL.o_wsc);
   const int cap = LL.cap;
-  // chaos-phase aliases
-  uint32_t* epix = reinterpret_cast<uint32_t*>(vals);                 // append order
-  uint8_t* eL8 = reinterpret_cast<uint8_t*>(vals) + (size_t)cap * 4;  // append order
-  uint32_t* epix_r = filtA;                                           // rank order (4*cap bytes)
-  uint8_t* eLr = Lv;                                                  // rank order
-  uint32_t* par = reinterpret_cast<uint32_t*>(vals);                  // rank order (after epix consumed)
+  // chaos-phase aliases (the value, filter and table regions are dead by then)
+  uint32_t* epix = reinterpret_cast<uint32_t*>(vals);                  // candidates, append order
+  uint32_t* epix_r = filtA;                                            // E pixels, rank order (4*cap)
+  uint8_t* eL8 = reinterpret_cast<uint8_t*>(filtA) + (size_t)cap * 4;  // candidates' eL, append order
+  uint8_t* eLr = Lv;                                                   // rank order
+  uint32_t* par = reinterpret_cast<uint32_t*>(vals);                   // rank order (after epix consumed)
 
   const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
   const int64_t ion = ion_order ? ion_order[blockIdx.x] : (int64_t)blockIdx.x;
   if (ion >= n_ions) return;
   const int64_t w0 = ion_off[ion];
@@ -377,7 +463,8 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
     return;
   }
 
-  // ---- phase 0: loads in flight, LDS zeroing meanwhile --------------------------------------
+  // ---- phase 0: loads in flight, LDS initialisation meanwhile -----------------------------------
+  STAMP_INIT();
   Reg h0[RMAX];
 #pragma unroll
   for (int j = 0; j < RMAX; ++j) {
@@ -401,11 +488,21 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
     for (int i = tid; i < LL.w32 / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
     uint4* zf = reinterpret_cast<uint4*>(filtA);
     for (int i = tid; i < FILT_WORDS / 2; i += BLOCK) zf[i] = make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < TBL; i += BLOCK) {
+      tkey[i] = 0xFFFFFFFFu;
+      tval[i] = 0.0;
+    }
+    for (int i = tid; i < SIDE; i += BLOCK) {
+      side_k[i] = 0xFFFFFFFFu;
+      side_v[i] = 0.0;
+    }
+    for (int i = tid; i < (cap + 31) / 32; i += BLOCK) dupb[i] = 0u;
     if (tid < C_NCTR) ctr[tid] = 0;
   }
   __syncthreads();
+  STAMP(0);
 
-  // ---- phase 1: principal image -> bitmap (+ ownership), rank prefix, f64 values ----------------
+  // ---- phase 1: principal image -> bitmap (+ ownership), rank prefix, values --------------------
   uint32_t own = 0;
   uint32_t hp[RMAX];
 #pragma unroll
@@ -423,43 +520,94 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
   __syncthreads();
   const int n64 = (P.npx + 63) / 64;
   const int nnz = bm_build_prefix(Hbm, pf, n64, wsc);
-  for (int r = tid; r < nnz; r += BLOCK) vals[r] = 0.0;
-  __syncthreads();
+  if constexpr (SIDE_TABLE) {
+    // owners store their f32 value; every other hit of an owned pixel is a duplicate -> f64 side table
 #pragma unroll
-  for (int j = 0; j < RMAX; ++j) {
-    const int i = tid + j * BLOCK;
-    if (i < n0) atomicAdd(&vals[bm_rank(Hbm, pf, (int)hp[j])], Hits<FMT>::val(h0[j]));
+    for (int j = 0; j < RMAX; ++j) {
+      const int i = tid + j * BLOCK;
+      if (i < n0) {
+        const int r = bm_rank(Hbm, pf, (int)hp[j]);
+        if ((own >> j) & 1u) {
+          vals[r] = (VT)Hits<FMT>::val(h0[j]);
+        } else {
+          atomicOr(&dupb[r >> 5], 1u << (r & 31));
+          if (!tbl_add<SIDE>(side_k, side_v, (uint32_t)r, Hits<FMT>::val(h0[j]))) ctr[C_ABORT] = 1;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RMAX; ++j) {
+      const int i = tid + j * BLOCK;
+      if (i < n0 && ((own >> j) & 1u)) {
+        const int r = bm_rank(Hbm, pf, (int)hp[j]);
+        if ((dupb[r >> 5] >> (r & 31)) & 1u) {
+          if (!tbl_add<SIDE>(side_k, side_v, (uint32_t)r, Hits<FMT>::val(h0[j]))) ctr[C_ABORT] = 1;
+        }
+      }
+    }
+  } else {
+    for (int r = tid; r < nnz; r += BLOCK) vals[r] = (VT)0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RMAX; ++j) {
+      const int i = tid + j * BLOCK;
+      if (i < n0) atomicAdd(&vals[bm_rank(Hbm, pf, (int)hp[j])], Hits<FMT>::val(h0[j]));
+    }
   }
   __syncthreads();
+  if (ctr[C_ABORT]) {  // more duplicate pixels than the side table holds
+    if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
+    return;
+  }
+  auto value_at = [&](int r) -> double {
+    if constexpr (SIDE_TABLE) {
+      if ((dupb[r >> 5] >> (r & 31)) & 1u) return side_v[tbl_find<SIDE>(side_k, (uint32_t)r)];
+    }
+    return (double)vals[r];
+  };
+  STAMP(1);
 
-  // ---- phase 2: principal-image statistics ---------------------------------------------------
+  // ---- phase 2: fused principal-image statistics, then level index per pixel -------------------
   double sx, sxx, s0, npos, vmax;
   {
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    double mx = -INFINITY;
+    double acc[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
     for (int r = tid; r < nnz; r += BLOCK) {
-      const double v = vals[r];
+      const double v = value_at(r);
       acc[0] += v;
       acc[1] += v * v;
       if (v > 0.0) {
         acc[2] += v;
         acc[3] += 1.0;
       }
-      mx = v > mx ? v : mx;
+      acc[4] = v > acc[4] ? v : acc[4];
     }
-    block_sum<BLOCK, 4>(acc, red);
-    sx = acc[0];
-    sxx = acc[1];
-    s0 = acc[2];
-    npos = acc[3];
-    vmax = block_max(mx, red);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = wave_sum(acc[q]);
+    acc[4] = wave_max(acc[4]);
+    if (lane == 0) {
+#pragma unroll
+      for (int q = 0; q < 5; ++q) red[q * NW + wid] = acc[q];
+    }
+    __syncthreads();
+    double t[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[q] += red[q * NW + w];
+      t[4] = red[4 * NW + w] > t[4] ? red[4 * NW + w] : t[4];
+    }
+    sx = t[0];
+    sxx = t[1];
+    s0 = t[2];
+    npos = t[3];
+    vmax = t[4];
   }
   const bool chaos_ok = (sx > 0.0) && (npos >= 4.0);
-
-  // ---- phase 3: level index per principal pixel ------------------------------------------------
   if (chaos_ok) {
-    for (int r = tid; r < nnz; r += BLOCK) Lv[r] = (uint8_t)level_of(vals[r], vmax, P);
+    for (int r = tid; r < nnz; r += BLOCK) Lv[r] = (uint8_t)level_fast(value_at(r), vmax, P);
   }
+  STAMP(2);
 
   // ---- phase 5: other isotope windows, joined against the principal image ------------------------
   bool overflow = false;
@@ -467,8 +615,7 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
     const int64_t a = lo[w0 + k], b = hi[w0 + k];
     const int64_t n = b - a;
     const bool single = n <= (int64_t)BLOCK * RC;
-    // prefetch the next window's first chunk
-    if (k + 1 < K) {
+    if (k + 1 < K) {  // prefetch the next window's first chunk
       const int64_t a2 = lo[w0 + k + 1];
       const int64_t n2 = hi[w0 + k + 1] - a2;
       if (n2 <= (int64_t)BLOCK * RC) {
@@ -482,7 +629,7 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
     double psy = 0.0, psyy = 0.0, psxy = 0.0, psk = 0.0;
     auto pass1 = [&](uint32_t p, double v) {
       double x = 0.0;
-      if (bm_test(Hbm, (int)p)) x = vals[bm_rank(Hbm, pf, (int)p)];
+      if (bm_test(Hbm, (int)p)) x = value_at(bm_rank(Hbm, pf, (int)p));
       psy += v;
       psxy += x * v;
       if (x > 0.0) psk += v;
@@ -494,11 +641,7 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
     auto pass2 = [&](uint32_t p, double v) {
       const uint32_t h = filt_hash(p, P.npx);
       if ((filtD[h >> 5] >> (h & 31)) & 1u) {
-        const int s = atomicAdd(&ctr[C_NSUSP], 1);
-        if (s < SUSP_CAP) {
-          susp_pix[s] = p;
-          susp_val[s] = v;
-        }
+        if (atomicAdd(&ctr[C_NSUSP], 1) >= SUSP_CAP || !tbl_add<TBL>(tkey, tval, p, v)) ctr[C_ABORT] = 1;
       } else {
         psyy += v * v;
       }
@@ -545,38 +688,33 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
       }
     }
     __syncthreads();
-    const int ns = ctr[C_NSUSP];
+    // drain the duplicate table (exact per-pixel sums), clear the filter, per-wave partials
+    for (int sl = tid; sl < TBL; sl += BLOCK) {
+      if (tkey[sl] != 0xFFFFFFFFu) {
+        const double y = tval[sl];
+        psyy += y * y;
+        tkey[sl] = 0xFFFFFFFFu;
+        tval[sl] = 0.0;
+      }
+    }
     {
       uint4* zf = reinterpret_cast<uint4*>(filtA);
       for (int i = tid; i < FILT_WORDS / 2; i += BLOCK) zf[i] = make_uint4(0, 0, 0, 0);
     }
-    if (ns <= SUSP_CAP) {
-      for (int s = tid; s < ns; s += BLOCK) {
-        const uint32_t ps = susp_pix[s];
-        bool first = true;
-        double sum = 0.0;
-        for (int u = 0; u < ns; ++u) {
-          if (susp_pix[u] == ps) {
-            if (u < s) {
-              first = false;
-              break;
-            }
-            sum += susp_val[u];
-          }
-        }
-        if (first) psyy += sum * sum;
-      }
+    psk = wave_sum(psk);
+    psy = wave_sum(psy);
+    psyy = wave_sum(psyy);
+    psxy = wave_sum(psxy);
+    if (lane == 0) {
+      double* pk = part + ((size_t)k * NW + wid) * 4;
+      pk[0] = psk;
+      pk[1] = psy;
+      pk[2] = psyy;
+      pk[3] = psxy;
     }
-    double acc[4] = {psy, psyy, psxy, psk};
-    block_sum<BLOCK, 4>(acc, red);  // contains barriers: every thread has read ctr[C_NSUSP]
-    if (ns > SUSP_CAP) overflow = true;
-    if (tid == 0) {
-      stats[0 * MAXK + k] = acc[3];
-      stats[1 * MAXK + k] = acc[0];
-      stats[2 * MAXK + k] = acc[1];
-      stats[3 * MAXK + k] = acc[2];
-      ctr[C_NSUSP] = 0;
-    }
+    __syncthreads();
+    if (ctr[C_ABORT]) overflow = true;
+    if (tid == 0) ctr[C_NSUSP] = 0;  // read by nobody until after the next window's first barrier
   };
   for (int k = 1; k < K && !overflow; k += 2) {
     window_pass(k, ra, rb);
@@ -586,16 +724,17 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
     if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
     return;
   }
-  __syncthreads();
+  STAMP(3);
 
   // ---- phase 4a: chaos candidates (pixels with eL >= 1) from owned principal pixels --------------
   // (i) bit-level screen: a candidate p in cross(s) survives if its 3x3 box is covered by the
   //     dilated bitmap (superset of the exact condition) and s is its owner (smallest principal pixel
-  //     of cross(p)); survivors go to an LDS list (the vals region is free: L is computed).
+  //     of cross(p)); survivors go to an LDS list (the value region is free once L is computed).
   // (ii) exact eL for the survivors from the level indices.
   double chaos_raw = NAN;
   if (chaos_ok) {
-#pragma unroll 1
+    __syncthreads();  // everyone is done reading values before the candidate list overwrites them
+#pragma unroll
     for (int j = 0; j < RMAX; ++j) {
       if (!((own >> j) & 1u)) continue;
       const int s = (int)hp[j];
@@ -645,6 +784,7 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
       }
     }
     __syncthreads();
+    STAMP(4);
     const int ncand = ctr[C_NE];
     if (ncand > cap) {
       if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
@@ -665,10 +805,10 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
           }
           int dl = 0;
           for (int t = 0; t < 5; ++t) {
-            const int ra = rq + (t == 1 ? -1 : t == 2 ? 1 : 0);
-            const int ca = cq + (t == 3 ? -1 : t == 4 ? 1 : 0);
-            if (ra < 0 || ra >= P.nrows || ca < 0 || ca >= P.ncols) continue;
-            const int q = ra * P.ncols + ca;
+            const int r2 = rq + (t == 1 ? -1 : t == 2 ? 1 : 0);
+            const int c2 = cq + (t == 3 ? -1 : t == 4 ? 1 : 0);
+            if (r2 < 0 || r2 >= P.nrows || c2 < 0 || c2 >= P.ncols) continue;
+            const int q = r2 * P.ncols + c2;
             if (bm_test(Hbm, q)) dl = max(dl, (int)Lv[bm_rank(Hbm, pf, q)]);
           }
           mn = min(mn, dl);
@@ -680,6 +820,7 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
     }
     if (emax_local > 0) atomicMax(&ctr[C_EMAX], emax_local);
     __syncthreads();
+    STAMP(5);
 
     // ---- phase 4b: Kruskal over eL (levels descending) with an LDS union-find -------------------
     double sum_c = 0.0;
@@ -737,15 +878,26 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
       sum_c = acc[0] - acc[1];
     }
     chaos_raw = 1.0 - sum_c / (double)P.nlevels / npos;
+    STAMP(6);
   } else {
     flags |= SMG_ION_CHAOS_NAN;
   }
 
   if (tid == 0) {
-    stats[0] = s0;
-    stats[MAXK] = stats[2 * MAXK] = stats[3 * MAXK] = 0.0;
-    finalize_ion(K, theor + w0, stats, sx, sxx, stats + MAXK, stats + 2 * MAXK, stats + 3 * MAXK, (double)P.npx,
-                 chaos_raw, ion, flags, oc, osp, osc, omsm, oflags);
+    // s, sy, syy, sxy per window from the per-wave partials (wave order: deterministic)
+    double* st = red;  // reuse: [4][MAXK]
+    for (int k = 0; k < K; ++k) {
+      double a4[4] = {0.0, 0.0, 0.0, 0.0};
+      if (k > 0) {
+        for (int w = 0; w < NW; ++w)
+          for (int q = 0; q < 4; ++q) a4[q] += part[((size_t)k * NW + w) * 4 + q];
+      } else {
+        a4[0] = s0;
+      }
+      for (int q = 0; q < 4; ++q) st[q * MAXK + k] = a4[q];
+    }
+    finalize_ion(K, theor + w0, st, sx, sxx, st + MAXK, st + 2 * MAXK, st + 3 * MAXK, (double)P.npx, chaos_raw,
+                 ion, flags, oc, osp, osc, omsm, oflags);
   }
 }
 
@@ -1037,7 +1189,7 @@ static int launch_metrics(Hits<FMT> hits, const int64_t* lo, const int64_t* hi, 
   unsigned char* slots = ws + WS_HEADER + al16((size_t)n_ions * 4);
   const size_t slot_bytes = dense_slot_bytes(P.npx);
   SMG_HIP(hipMemsetAsync(ws, 0, WS_HEADER, st));
-  LdsLayout LL = lds_layout(P.npx);
+  LdsLayout LL = lds_layout(P.npx, FMT == SMG_HITS_PACKED_F32 ? 4 : 8);
   if (P.npx <= NPX_LDS_MAX && LL.cap >= 256) {
     SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ion_lds_kernel<FMT>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LL.bytes));
@@ -1063,6 +1215,20 @@ static int launch_metrics(Hits<FMT> hits, const int64_t* lo, const int64_t* hi, 
 using namespace smg;
 
 extern "C" {
+
+int smg_debug_stamps(unsigned long long* host_out, int n) {
+#ifdef SMG_STAMPS
+  SMG_HIP(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * (n < 16 ? n : 16)));
+  unsigned long long z[16] = {0};
+  SMG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)));
+  return SMG_OK;
+#else
+  (void)host_out;
+  (void)n;
+  set_error("library built without -DSMG_STAMPS");
+  return SMG_ERR_UNSUPPORTED;
+#endif
+}
 
 int smg_ion_metrics_workspace_size(int64_t n_ions, int32_t nrows, int32_t ncols, size_t* bytes) {
   SMG_CHECK_ARG(bytes && n_ions >= 0 && nrows > 0 && ncols > 0, "bad arguments");
