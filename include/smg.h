@@ -35,6 +35,7 @@ extern "C" {
 #define SMG_ION_HAS_HITS 0x1u    /* >= 1 window with >= 1 point: the ion gets a row (formula_img_validator.py:115-118) */
 #define SMG_ION_DENSE 0x2u       /* scored by the dense (global-scratch) path instead of the LDS path */
 #define SMG_ION_CHAOS_NAN 0x4u   /* raw measure_of_chaos was NaN (empty / < 4 positive pixels) */
+#define SMG_ION_BIG 0x8u         /* scored by the big-ion LDS pass (1024-thread workgroup, whole LDS) */
 
 /* hit formats accepted by smg_ion_metrics */
 #define SMG_HITS_PACKED_F32 0    /* uint64: low 32 bits pixel index, high 32 bits float32 intensity */

@@ -14,6 +14,7 @@ SMG_OK = 0
 SMG_ION_HAS_HITS = 0x1
 SMG_ION_DENSE = 0x2
 SMG_ION_CHAOS_NAN = 0x4
+SMG_ION_BIG = 0x8
 SMG_HITS_PACKED_F32 = 0
 SMG_HITS_SPLIT_F64 = 1
 

@@ -33,7 +33,7 @@ constexpr int NW = BLOCK / WAVE;
 constexpr int RMAX = 16;             // principal-window points held per thread
 constexpr int CAP_MAX = BLOCK * RMAX; // max points in the principal window on the LDS path
 constexpr int RC = 16;               // points per thread per chunk of the other windows
-constexpr int RT = 8;                // points per thread per chunk for windows > BLOCK*RC points
+constexpr int RT = 4;                // points per thread per chunk for windows > BLOCK*RC points
 constexpr int MAXK = 8;              // windows per ion on the LDS path
 constexpr int MAXK_DENSE = 32;       // windows per ion supported at all
 constexpr int FILT_LOG2 = 15;        // 32768-bit duplicate filter, two of them
@@ -174,7 +174,9 @@ __device__ void finalize_ion(int K, const double* __restrict__ t, const double* 
   oflags[ion] = flags;
 }
 
+template <int NW_ = NW>
 __device__ __forceinline__ double block_max(double v, double* scratch) {
+  constexpr int NW = NW_;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   v = wave_max(v);
   if (lane == 0) scratch[wid] = v;
@@ -198,7 +200,9 @@ __device__ __forceinline__ int bm_rank(const uint32_t* bm, const uint16_t* pf, i
 
 // exclusive popcount prefix over the first n64 64-bit words: each wave scans a contiguous range
 // 64 words at a time (lane-parallel), then wave offsets are added.  Returns the total.
+template <int NW_>
 __device__ int bm_build_prefix(const uint32_t* bm, uint16_t* pf, int n64, int* wscratch) {
+  constexpr int NW = NW_;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(bm);
   const int span = ((n64 + NW - 1) / NW + 63) & ~63;
@@ -288,22 +292,25 @@ static inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 // LDS carve for an image of npx pixels and principal values of val_bytes each.  The principal-image
 // capacity is whatever fits the per-workgroup budget (LDS_BUDGET -> two workgroups per CU), capped by
 // CAP_MAX and by the chaos phase's reuse of the filter + table region (rank-ordered E pixels: 5 B each).
-static LdsLayout lds_layout(int npx, int val_bytes) {
+static LdsLayout lds_layout(int npx, int val_bytes, int NW, int CAP_MAX, size_t LDS_BUDGET) {
   LdsLayout L;
   const int words = (npx + 31) / 32 + 2;
   L.w32 = (words + 3) & ~3;
-  const size_t region_ft = al16((size_t)2 * FILT_WORDS * 4) + al16((size_t)TBL * 4) + al16((size_t)TBL * 8);
+  const size_t region_ft0 = al16((size_t)2 * FILT_WORDS * 4) + al16((size_t)TBL * 4) + al16((size_t)TBL * 8);
   const size_t fixed = al16((size_t)L.w32 * 4) + al16((size_t)(L.w32 / 2) * 2) + al16((size_t)SIDE * 4) +
-                       al16((size_t)SIDE * 8) + region_ft + al16((size_t)MAXK * NW * 4 * 8) +
-                       al16((size_t)8 * NW * 8) + al16((size_t)C_NCTR * 4) + al16((size_t)NW * 4) + 128;
-  const long avail = (long)LDS_BUDGET - (long)fixed;
-  // per principal point: value + level byte + dup bit
-  int cap = avail > 0 ? (int)((avail * 8) / (8 * val_bytes + 8 + 1)) : 0;
-  cap = cap < CAP_MAX ? cap : CAP_MAX;
-  const int cap_e = (int)(region_ft / 5);
-  cap = cap < cap_e ? cap : cap_e;
-  cap = cap < (int)(((size_t)cap * val_bytes) / 4) ? cap : cap;  // epix (4 B) fits the value region
-  cap &= ~63;
+                       al16((size_t)SIDE * 8) + al16((size_t)MAXK * NW * 4 * 8) + al16((size_t)8 * NW * 8) +
+                       al16((size_t)C_NCTR * 4) + al16((size_t)NW * 4) + 256;
+  // largest cap (multiple of 64, <= CAP_MAX) whose carve fits the budget; the filter + table region
+  // doubles as the chaos phase's E-pixel storage (5 B per point) and grows with cap when needed
+  int cap = CAP_MAX & ~63;
+  size_t region_ft = region_ft0;
+  for (; cap >= 64; cap -= 64) {
+    region_ft = region_ft0 > al16((size_t)5 * cap) ? region_ft0 : al16((size_t)5 * cap);
+    const size_t need = fixed + region_ft + al16((size_t)cap * (val_bytes < 4 ? 4 : val_bytes)) + al16((size_t)cap) +
+                        al16((size_t)((cap + 31) / 32) * 4);
+    if (need <= LDS_BUDGET) break;
+  }
+  if (cap < 64) cap = 0;
   L.cap = cap;
   size_t o = al16((size_t)L.w32 * 4);
   L.o_pf = o;
@@ -324,6 +331,7 @@ static LdsLayout lds_layout(int npx, int val_bytes) {
   o = al16(o + (size_t)TBL * 4);
   L.o_tval = o;
   o = al16(o + (size_t)TBL * 8);
+  if (o - L.o_filt < region_ft) o = L.o_filt + region_ft;
   L.o_part = o;
   o = al16(o + (size_t)MAXK * NW * 4 * 8);
   L.o_red = o;
@@ -405,13 +413,17 @@ struct ValStore<SMG_HITS_SPLIT_F64> {
 //   4b Kruskal over eL with an LDS union-find
 //   6  finalize (thread 0)
 // ---------------------------------------------------------------------------------------------
-template <int FMT>
-__global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
-    Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
-    const int64_t* __restrict__ ion_off, const double* __restrict__ theor, const int64_t* __restrict__ ion_order,
-    int64_t n_ions, Params P, LdsLayout LL, double* __restrict__ oc, double* __restrict__ osp,
-    double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags,
-    uint32_t* __restrict__ dense_list, uint32_t* __restrict__ dense_count) {
+template <int FMT, int LB, int LRMAX, int LRC>
+__device__ __forceinline__ void process_ion_lds(
+    int64_t ion, const Hits<FMT>& hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
+    const int64_t* __restrict__ ion_off, const double* __restrict__ theor, const Params& P, const LdsLayout& LL,
+    double* __restrict__ oc, double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm,
+    uint32_t* __restrict__ oflags, uint32_t* __restrict__ dense_list, uint32_t* __restrict__ dense_count) {
+  constexpr int BLOCK = LB;
+  constexpr int NW = LB / WAVE;
+  constexpr int RMAX = LRMAX;
+  constexpr int RC = LRC;
+  constexpr int CAP_MAX = BLOCK * RMAX;
   using Reg = typename Hits<FMT>::Reg;
   using VT = typename ValStore<FMT>::T;
   constexpr bool SIDE_TABLE = (FMT == SMG_HITS_PACKED_F32);
@@ -441,12 +453,10 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
-  const int64_t ion = ion_order ? ion_order[blockIdx.x] : (int64_t)blockIdx.x;
-  if (ion >= n_ions) return;
   const int64_t w0 = ion_off[ion];
   const int K = (int)(ion_off[ion + 1] - w0);
 
-  uint32_t flags = 0;
+  uint32_t flags = (LB >= 1024) ? SMG_ION_BIG : 0u;
   for (int k = 0; k < K && k < MAXK_DENSE; ++k)
     if (hi[w0 + k] > lo[w0 + k]) flags |= SMG_ION_HAS_HITS;
   if (K == 0) {
@@ -519,7 +529,7 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
   }
   __syncthreads();
   const int n64 = (P.npx + 63) / 64;
-  const int nnz = bm_build_prefix(Hbm, pf, n64, wsc);
+  const int nnz = bm_build_prefix<NW>(Hbm, pf, n64, wsc);
   if constexpr (SIDE_TABLE) {
     // owners store their f32 value; every other hit of an owned pixel is a duplicate -> f64 side table
 #pragma unroll
@@ -734,10 +744,24 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
   double chaos_raw = NAN;
   if (chaos_ok) {
     __syncthreads();  // everyone is done reading values before the candidate list overwrites them
-#pragma unroll
-    for (int j = 0; j < RMAX; ++j) {
-      if (!((own >> j) & 1u)) continue;
-      const int s = (int)hp[j];
+    // principal pixels in rank order into the (now free) filter region
+    uint32_t* opix = filtA;
+    {
+      const int w32u = (P.npx + 31) / 32;
+      for (int w = tid; w < w32u; w += BLOCK) {
+        uint32_t bits = Hbm[w];
+        if (!bits) continue;
+        int r = bm_rank(Hbm, pf, w * 32 + (__ffs(bits) - 1));
+        while (bits) {
+          const int b = __ffs(bits) - 1;
+          bits &= bits - 1u;
+          opix[r++] = (uint32_t)(w * 32 + b);
+        }
+      }
+    }
+    __syncthreads();
+    for (int rr = tid; rr < nnz; rr += BLOCK) {
+      const int s = (int)opix[rr];
       const int rs = s / P.ncols, cs = s - rs * P.ncols;
       uint32_t H[7];
 #pragma unroll
@@ -831,7 +855,7 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
       for (int i = tid; i < ncand; i += BLOCK)
         if (eL8[i]) atomicOr(&Hbm[epix[i] >> 5], 1u << (epix[i] & 31));
       __syncthreads();
-      const int m = bm_build_prefix(Hbm, pf, n64, wsc);
+      const int m = bm_build_prefix<NW>(Hbm, pf, n64, wsc);
       for (int i = tid; i < ncand; i += BLOCK) {
         if (!eL8[i]) continue;
         const uint32_t p = epix[i];
@@ -851,23 +875,20 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
           if (e < t) continue;
           const int p = (int)epix_r[r];
           const int rp = p / P.ncols, cp = p - rp * P.ncols;
-          int nb[4];
-          int nn = 0;
-          if (cp + 1 < P.ncols) nb[nn++] = p + 1;
-          if (rp + 1 < P.nrows) {
-            nb[nn++] = p + P.ncols;
-            if (P.connectivity == 8) {
-              if (cp > 0) nb[nn++] = p + P.ncols - 1;
-              if (cp + 1 < P.ncols) nb[nn++] = p + P.ncols + 1;
-            }
-          }
-          for (int j = 0; j < nn; ++j) {
-            const int q = nb[j];
-            if (!bm_test(Hbm, q)) continue;
+          auto edge = [&](int q) {
+            if (!bm_test(Hbm, q)) return;
             const int rq = bm_rank(Hbm, pf, q);
             const int eq = eLr[rq];
             if ((e < eq ? e : eq) == t) {
               if (uf_unite(par, (uint32_t)r, (uint32_t)rq)) wsum += (double)t;
+            }
+          };
+          if (cp + 1 < P.ncols) edge(p + 1);
+          if (rp + 1 < P.nrows) {
+            edge(p + P.ncols);
+            if (P.connectivity == 8) {
+              if (cp > 0) edge(p + P.ncols - 1);
+              if (cp + 1 < P.ncols) edge(p + P.ncols + 1);
             }
           }
         }
@@ -898,6 +919,44 @@ __global__ void __launch_bounds__(BLOCK, 2) ion_lds_kernel(
     }
     finalize_ion(K, theor + w0, st, sx, sxx, st + MAXK, st + 2 * MAXK, st + 3 * MAXK, (double)P.npx, chaos_raw,
                  ion, flags, oc, osp, osc, omsm, oflags);
+  }
+}
+
+
+template <int FMT, int LB, int LRMAX, int LRC>
+__global__ void __launch_bounds__(LB, 4) ion_lds_kernel(
+    Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
+    const int64_t* __restrict__ ion_off, const double* __restrict__ theor, const int64_t* __restrict__ ion_order,
+    int64_t n_ions, Params P, LdsLayout LL, double* __restrict__ oc, double* __restrict__ osp,
+    double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags,
+    uint32_t* __restrict__ next_list, uint32_t* __restrict__ next_count) {
+  const int64_t ion = ion_order ? ion_order[blockIdx.x] : (int64_t)blockIdx.x;
+  if (ion >= n_ions) return;
+  process_ion_lds<FMT, LB, LRMAX, LRC>(ion, hits, lo, hi, ion_off, theor, P, LL, oc, osp, osc, omsm, oflags,
+                                       next_list, next_count);
+}
+
+// persistent variant over a device list of ions (the rejects of a smaller-geometry pass)
+template <int FMT, int LB, int LRMAX, int LRC>
+__global__ void __launch_bounds__(LB, 4) ion_lds_list_kernel(
+    Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
+    const int64_t* __restrict__ ion_off, const double* __restrict__ theor, const uint32_t* __restrict__ list,
+    const uint32_t* __restrict__ count, uint32_t* __restrict__ cursor, Params P, LdsLayout LL,
+    double* __restrict__ oc, double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm,
+    uint32_t* __restrict__ oflags, uint32_t* __restrict__ next_list, uint32_t* __restrict__ next_count) {
+  __shared__ int sh_ion;
+  const uint32_t total = *count;
+  while (true) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t k = atomicAdd(cursor, 1u);
+      sh_ion = (k < total) ? (int)list[k] : -1;
+    }
+    __syncthreads();
+    const int ion = sh_ion;
+    if (ion < 0) break;
+    process_ion_lds<FMT, LB, LRMAX, LRC>(ion, hits, lo, hi, ion_off, theor, P, LL, oc, osp, osc, omsm, oflags,
+                                         next_list, next_count);
   }
 }
 
@@ -1117,21 +1176,18 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
           const int e = S.E8[p];
           if (e < t) continue;
           const int r = p / nc, c = p - r * nc;
-          int nb[4];
-          int nn = 0;
-          if (c + 1 < nc) nb[nn++] = p + 1;
-          if (r + 1 < nr) {
-            nb[nn++] = p + nc;
-            if (P.connectivity == 8) {
-              if (c > 0) nb[nn++] = p + nc - 1;
-              if (c + 1 < nc) nb[nn++] = p + nc + 1;
-            }
-          }
-          for (int j = 0; j < nn; ++j) {
-            const int q = nb[j];
+          auto edge = [&](int q) {
             const int eq = S.E8[q];
             if (eq >= 1 && (e < eq ? e : eq) == t) {
               if (guf_unite(S.par, (uint32_t)p, (uint32_t)q)) wsum += (double)t;
+            }
+          };
+          if (c + 1 < nc) edge(p + 1);
+          if (r + 1 < nr) {
+            edge(p + nc);
+            if (P.connectivity == 8) {
+              if (c > 0) edge(p + nc - 1);
+              if (c + 1 < nc) edge(p + nc + 1);
             }
           }
         }
@@ -1173,39 +1229,62 @@ __global__ void list_all_kernel(uint32_t* list, uint32_t* count, const int64_t* 
 
 static constexpr int DENSE_SLOTS = 256;
 static constexpr size_t WS_HEADER = 256;
+// LDS-path geometries: the main pass (two 512-thread workgroups per CU) and the big-ion pass over its
+// rejects (one 1024-thread workgroup per CU with the whole LDS)
+static constexpr int MAIN_BLOCK = 512, MAIN_RMAX = 8, MAIN_RC = 4;
+static constexpr int BIG_BLOCK = 1024, BIG_RMAX = 8, BIG_RC = 4;
+static constexpr size_t MAIN_LDS = 80 * 1024, BIG_LDS = 160 * 1024 - 512;
 
 static size_t ws_bytes_for(int64_t n_ions, int npx) {
-  return WS_HEADER + al16((size_t)n_ions * 4) + (size_t)DENSE_SLOTS * dense_slot_bytes(npx);
+  return WS_HEADER + 2 * al16((size_t)n_ions * 4) + (size_t)DENSE_SLOTS * dense_slot_bytes(npx);
 }
+
+static LdsLayout main_layout(int npx, int vb) { return lds_layout(npx, vb, MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX, MAIN_LDS); }
+static LdsLayout big_layout(int npx, int vb) { return lds_layout(npx, vb, BIG_BLOCK / WAVE, BIG_BLOCK * BIG_RMAX, BIG_LDS); }
 
 template <int FMT>
 static int launch_metrics(Hits<FMT> hits, const int64_t* lo, const int64_t* hi, const int64_t* ion_off,
                           const double* theor, const int64_t* ion_order, int64_t n_ions, const Params& P,
                           double* oc, double* osp, double* osc, double* omsm, uint32_t* oflags,
                           unsigned char* ws, hipStream_t st) {
-  uint32_t* dense_count = reinterpret_cast<uint32_t*>(ws);
-  uint32_t* next = dense_count + 1;
-  uint32_t* dense_list = reinterpret_cast<uint32_t*>(ws + WS_HEADER);
-  unsigned char* slots = ws + WS_HEADER + al16((size_t)n_ions * 4);
+  // header: [0] count A, [1] cursor A, [2] count B, [3] cursor B
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(ws);
+  uint32_t* list_a = reinterpret_cast<uint32_t*>(ws + WS_HEADER);
+  uint32_t* list_b = reinterpret_cast<uint32_t*>(ws + WS_HEADER + al16((size_t)n_ions * 4));
+  unsigned char* slots = ws + WS_HEADER + 2 * al16((size_t)n_ions * 4);
   const size_t slot_bytes = dense_slot_bytes(P.npx);
   SMG_HIP(hipMemsetAsync(ws, 0, WS_HEADER, st));
-  LdsLayout LL = lds_layout(P.npx, FMT == SMG_HITS_PACKED_F32 ? 4 : 8);
-  if (P.npx <= NPX_LDS_MAX && LL.cap >= 256) {
-    SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ion_lds_kernel<FMT>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)LL.bytes));
-    hipLaunchKernelGGL(ion_lds_kernel<FMT>, dim3((unsigned)n_ions), dim3(BLOCK), LL.bytes, st, hits, lo, hi,
-                       ion_off, theor, ion_order, n_ions, P, LL, oc, osp, osc, omsm, oflags, dense_list,
-                       dense_count);
+  const int vb = FMT == SMG_HITS_PACKED_F32 ? 4 : 8;
+  LdsLayout LM = main_layout(P.npx, vb);
+  LdsLayout LB = big_layout(P.npx, vb);
+  const bool lds_ok = P.npx <= NPX_LDS_MAX && LM.cap >= 256;
+  if (lds_ok) {
+    auto k1 = &ion_lds_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC>;
+    SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k1), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)LM.bytes));
+    hipLaunchKernelGGL(k1, dim3((unsigned)n_ions), dim3(MAIN_BLOCK), LM.bytes, st, hits, lo, hi, ion_off, theor,
+                       ion_order, n_ions, P, LM, oc, osp, osc, omsm, oflags, list_a, hdr + 0);
     SMG_LAUNCH_CHECK();
+    if (LB.cap > LM.cap) {
+      auto k2 = &ion_lds_list_kernel<FMT, BIG_BLOCK, BIG_RMAX, BIG_RC>;
+      SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k2), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)LB.bytes));
+      const int nwg = (int)(n_ions < 256 ? n_ions : 256);
+      hipLaunchKernelGGL(k2, dim3((unsigned)nwg), dim3(BIG_BLOCK), LB.bytes, st, hits, lo, hi, ion_off, theor,
+                         list_a, hdr + 0, hdr + 1, P, LB, oc, osp, osc, omsm, oflags, list_b, hdr + 2);
+      SMG_LAUNCH_CHECK();
+    } else {
+      SMG_HIP(hipMemcpyAsync(list_b, list_a, (size_t)n_ions * 4, hipMemcpyDeviceToDevice, st));
+      SMG_HIP(hipMemcpyAsync(hdr + 2, hdr + 0, 4, hipMemcpyDeviceToDevice, st));
+    }
   } else {
-    hipLaunchKernelGGL(list_all_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, dense_list,
-                       dense_count, ion_order, n_ions);
+    hipLaunchKernelGGL(list_all_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, list_b, hdr + 2,
+                       ion_order, n_ions);
     SMG_LAUNCH_CHECK();
   }
   const int nslots = (int)(n_ions < DENSE_SLOTS ? n_ions : DENSE_SLOTS);
   hipLaunchKernelGGL(ion_dense_kernel<FMT>, dim3((unsigned)nslots), dim3(BLOCK), 0, st, hits, lo, hi, ion_off,
-                     theor, n_ions, P, dense_list, dense_count, next, slots, slot_bytes, oc, osp, osc, omsm,
-                     oflags);
+                     theor, n_ions, P, list_b, hdr + 2, hdr + 3, slots, slot_bytes, oc, osp, osc, omsm, oflags);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

@@ -118,6 +118,11 @@ def make_case(name: str):
         ds = syn.make_dataset_np(80, 80, 60, seed=53, ions=ions, plant_fraction=1.0, plant_seed=54,
                                  blob_sigma=(150.0, 200.0))
         return ds, ions, 10.0, {}
+    if name == "huge_window":  # principal window > big-ion LDS capacity (8192 points) -> dense path
+        ions = syn.make_ion_table(4, seed=81, decoy_seed=82)
+        ds = syn.make_dataset_np(105, 105, 20, seed=83, ions=ions, plant_fraction=1.0, plant_seed=84,
+                                 blob_sigma=(300.0, 400.0))
+        return add_duplicates(ds, 0.02, 85), ions, 10.0, {}
     if name == "large_image":  # > 2^18 pixels -> dense path for every ion
         full = syn.make_ion_table(2, seed=61, decoy_seed=62)
         tgt = np.nonzero(np.isin(full.adducts, list(full.target_adducts)))[0][:4]
@@ -131,7 +136,7 @@ def make_case(name: str):
     raise KeyError(name)
 
 
-CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels", "nlevels1", "big_window",
+CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels", "nlevels1", "big_window", "huge_window",
          "large_image", "boundary"]
 
 

@@ -94,7 +94,9 @@ def test_images_match_oracle(name):
 
 def test_dense_path_used_when_needed():
     _, _, _, _, _, _, _, m, _, _ = _run_case("big_window")
-    assert ((m["flags"] & 2) != 0).any()
+    assert ((m["flags"] & 8) != 0).any()      # big-ion LDS pass
+    _, _, _, _, _, _, _, m, _, _ = _run_case("huge_window")
+    assert ((m["flags"] & 2) != 0).any()      # dense global-scratch pass
     _, _, _, _, _, _, _, m, _, _ = _run_case("large_image")
     has = (m["flags"] & 1) != 0
     assert ((m["flags"][has] & 2) != 0).all()
