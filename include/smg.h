@@ -51,6 +51,16 @@ const char* smg_last_error(void);
 int smg_pack_hits(const int64_t* sp_off, const int32_t* pixel_map, int64_t n_spectra,
                   const float* ints, int64_t n_points, uint64_t* hits, void* stream);
 
+/* Duplicate-candidate flags (bit 31 of the packed pixel field).  Two points of one theoretical window can
+ * only fall on the same pixel (and must then be summed, coo.toarray() in formula_img_validator.py:73-75) if
+ * they come from the same spectrum and lie within one window width of each other, i.e. they are neighbours
+ * in the m/z-sorted spectrum with gap <= 2*ppm*1e-6*mz/(1-ppm*1e-6).  This pass sets the flag on exactly
+ * those points (and on every point of a spectrum that is not m/z-sorted, or whose pixel is shared with
+ * another spectrum: force[s] != 0), clears it elsewhere, and writes only hits whose flag changes.
+ * Run it on the dataset-order hits before smg_sort_points; consumers mask pixels with 0x7FFFFFFF. */
+int smg_flag_duplicates(const int64_t* sp_off, int64_t n_spectra, const float* mz, uint64_t* hits,
+                        int64_t n_points, double ppm, const uint8_t* force, void* stream);
+
 /* Global m/z sort of the packed points (the pandas sort_values('mz') of formula_imager_segm.py:73-74,
  * done once over the whole dataset instead of per m/z segment).  Keys are positive float32 m/z. */
 int smg_sort_points_workspace_size(int64_t n_points, size_t* bytes);

@@ -9,12 +9,13 @@ from sm_distributed_amd import engine as E, synthetic as syn
 n_sf = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 ions = syn.make_ion_table(n_sf, seed=43, decoy_seed=44)
 mz, hits, dims, info = syn.make_dataset_torch(500, 500, 2000, seed=42, device="cuda", ions=ions)
-peaks = E.DevicePeaks.from_device(mz, hits, dims)
+peaks = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
 dions = E.DeviceIons.from_arrays(ions.win_off, ions.peak_mz, ions.peak_int)
 L = _lib.lib()
 L.smg_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 buf = (ctypes.c_ulonglong * 16)()
 m, lo, hi = E.run_hot_path(peaks, dions, 2.0, 30)
+print("flagged fraction", float(((peaks.hits >> 31) & 1).float().mean()))
 torch.cuda.synchronize()
 L.smg_debug_stamps(buf, 16)
 t0 = time.perf_counter()

@@ -16,6 +16,7 @@ SMG_ION_DENSE = 0x2
 SMG_ION_CHAOS_NAN = 0x4
 SMG_ION_BIG = 0x8
 SMG_HITS_PACKED_F32 = 0
+PIXEL_MASK = 0x7FFFFFFF   # bit 31 of the pixel field = duplicate-candidate flag
 SMG_HITS_SPLIT_F64 = 1
 
 # every symbol include/smg.h declares, with its ctypes prototype
@@ -28,6 +29,7 @@ PROTOTYPES = {
     "smg_version": (ctypes.c_char_p, []),
     "smg_last_error": (ctypes.c_char_p, []),
     "smg_pack_hits": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _P, _P]),
+    "smg_flag_duplicates": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _D, _P, _P]),
     "smg_sort_points_workspace_size": (ctypes.c_int, [_I64, ctypes.POINTER(_SZ)]),
     "smg_sort_points": (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _SZ, _P]),
     "smg_window_bounds": (ctypes.c_int, [_P, _P, _I64, _D, _P, _I64, _P, _P, _P]),

@@ -36,16 +36,12 @@ constexpr int RC = 16;               // points per thread per chunk of the other
 constexpr int RT = 4;                // points per thread per chunk for windows > BLOCK*RC points
 constexpr int MAXK = 8;              // windows per ion on the LDS path
 constexpr int MAXK_DENSE = 32;       // windows per ion supported at all
-constexpr int FILT_LOG2 = 15;        // 32768-bit duplicate filter, two of them
-constexpr int FILT_BITS = 1 << FILT_LOG2;
-constexpr int FILT_WORDS = FILT_BITS / 32;
 constexpr size_t LDS_BUDGET = 80 * 1024;  // per workgroup: two workgroups per CU
-constexpr int SUSP_CAP = 512;         // duplicate-filter suspects per window on the LDS path
-constexpr int TBL = 1024;             // suspect table slots (pixel-keyed f64 sums)
+constexpr int TBL = 1024;             // duplicate-candidate table slots ((pixel, window)-keyed f64 sums)
 constexpr int SIDE = 256;             // principal duplicate-pixel table slots (rank-keyed f64 sums)
 constexpr int NPX_LDS_MAX = 1 << 18; // images up to 262144 pixels use the LDS path
 
-enum { C_NSUSP = 0, C_NE, C_EMAX, C_ABORT, C_NCTR = 8 };
+enum { C_NE = 0, C_EMAX, C_ABORT, C_NCTR = 8 };
 
 // Diagnostic build only (-DSMG_STAMPS): per-phase wall cycles of the LDS kernel, summed over workgroups
 // into a buffer of their own (read back by smg_debug_stamps); the shipped build executes no stamp.
@@ -82,11 +78,12 @@ struct Hits<SMG_HITS_PACKED_F32> {
   const double* unused;
   using Reg = uint64_t;
   __device__ __forceinline__ Reg load(int64_t i) const { return h[i]; }
-  static __device__ __forceinline__ uint32_t pix(Reg r) { return (uint32_t)r; }
+  static __device__ __forceinline__ uint32_t pix(Reg r) { return (uint32_t)r & 0x7FFFFFFFu; }
+  static __device__ __forceinline__ bool dup(Reg r) { return ((uint32_t)r >> 31) != 0u; }
   static __device__ __forceinline__ double val(Reg r) { return (double)__uint_as_float((uint32_t)(r >> 32)); }
   __device__ __forceinline__ void get(int64_t i, uint32_t& p, double& v) const {
     const uint64_t x = h[i];
-    p = (uint32_t)x;
+    p = (uint32_t)x & 0x7FFFFFFFu;
     v = (double)__uint_as_float((uint32_t)(x >> 32));
   }
 };
@@ -102,10 +99,11 @@ struct Hits<SMG_HITS_SPLIT_F64> {
   const double* va;
   using Reg = PixVal;
   __device__ __forceinline__ Reg load(int64_t i) const { return PixVal{pa[i], va[i]}; }
-  static __device__ __forceinline__ uint32_t pix(Reg r) { return r.p; }
+  static __device__ __forceinline__ uint32_t pix(Reg r) { return r.p & 0x7FFFFFFFu; }
+  static __device__ __forceinline__ bool dup(Reg r) { return (r.p >> 31) != 0u; }
   static __device__ __forceinline__ double val(Reg r) { return r.v; }
   __device__ __forceinline__ void get(int64_t i, uint32_t& p, double& v) const {
-    p = pa[i];
+    p = pa[i] & 0x7FFFFFFFu;
     v = va[i];
   }
 };
@@ -296,7 +294,7 @@ static LdsLayout lds_layout(int npx, int val_bytes, int NW, int CAP_MAX, size_t 
   LdsLayout L;
   const int words = (npx + 31) / 32 + 2;
   L.w32 = (words + 3) & ~3;
-  const size_t region_ft0 = al16((size_t)2 * FILT_WORDS * 4) + al16((size_t)TBL * 4) + al16((size_t)TBL * 8);
+  const size_t region_ft0 = al16((size_t)TBL * 4) + al16((size_t)TBL * 8);
   const size_t fixed = al16((size_t)L.w32 * 4) + al16((size_t)(L.w32 / 2) * 2) + al16((size_t)SIDE * 4) +
                        al16((size_t)SIDE * 8) + al16((size_t)MAXK * NW * 4 * 8) + al16((size_t)8 * NW * 8) +
                        al16((size_t)C_NCTR * 4) + al16((size_t)NW * 4) + 256;
@@ -325,8 +323,7 @@ static LdsLayout lds_layout(int npx, int val_bytes, int NW, int CAP_MAX, size_t 
   o = al16(o + (size_t)SIDE * 4);
   L.o_side_v = o;
   o = al16(o + (size_t)SIDE * 8);
-  L.o_filt = o;
-  o = al16(o + (size_t)2 * FILT_WORDS * 4);
+  L.o_filt = o;  // region shared by the duplicate table and (later) the chaos phase's E arrays
   L.o_tkey = o;
   o = al16(o + (size_t)TBL * 4);
   L.o_tval = o;
@@ -344,9 +341,6 @@ static LdsLayout lds_layout(int npx, int val_bytes, int NW, int CAP_MAX, size_t 
   return L;
 }
 
-__device__ __forceinline__ uint32_t filt_hash(uint32_t p, int npx) {
-  return npx <= FILT_BITS ? p : ((p * 2654435761u) >> (32 - FILT_LOG2));
-}
 
 // open-addressing f64 accumulators keyed by u32 (EMPTY = 0xFFFFFFFF); returns false when full
 template <int NSLOT>
@@ -435,8 +429,7 @@ __device__ __forceinline__ void process_ion_lds(
   uint32_t* dupb = reinterpret_cast<uint32_t*>(smem + LL.o_dupb);
   uint32_t* side_k = reinterpret_cast<uint32_t*>(smem + LL.o_side_k);
   double* side_v = reinterpret_cast<double*>(smem + LL.o_side_v);
-  uint32_t* filtA = reinterpret_cast<uint32_t*>(smem + LL.o_filt);
-  uint32_t* filtD = filtA + FILT_WORDS;
+  uint32_t* filtA = reinterpret_cast<uint32_t*>(smem + LL.o_filt);  // base of the table / E region
   uint32_t* tkey = reinterpret_cast<uint32_t*>(smem + LL.o_tkey);
   double* tval = reinterpret_cast<double*>(smem + LL.o_tval);
   double* part = reinterpret_cast<double*>(smem + LL.o_part);  // [MAXK][NW][4]: s_k, sy, syy, sxy
@@ -496,8 +489,6 @@ __device__ __forceinline__ void process_ion_lds(
   {
     uint4* z = reinterpret_cast<uint4*>(Hbm);
     for (int i = tid; i < LL.w32 / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
-    uint4* zf = reinterpret_cast<uint4*>(filtA);
-    for (int i = tid; i < FILT_WORDS / 2; i += BLOCK) zf[i] = make_uint4(0, 0, 0, 0);
     for (int i = tid; i < TBL; i += BLOCK) {
       tkey[i] = 0xFFFFFFFFu;
       tval[i] = 0.0;
@@ -619,120 +610,118 @@ __device__ __forceinline__ void process_ion_lds(
   }
   STAMP(2);
 
-  // ---- phase 5: other isotope windows, joined against the principal image ------------------------
-  bool overflow = false;
-  auto window_pass = [&](int k, Reg (&cur)[RC], Reg (&nxt)[RC]) {
-    const int64_t a = lo[w0 + k], b = hi[w0 + k];
-    const int64_t n = b - a;
-    const bool single = n <= (int64_t)BLOCK * RC;
-    if (k + 1 < K) {  // prefetch the next window's first chunk
-      const int64_t a2 = lo[w0 + k + 1];
-      const int64_t n2 = hi[w0 + k + 1] - a2;
-      if (n2 <= (int64_t)BLOCK * RC) {
-#pragma unroll
-        for (int j = 0; j < RC; ++j) {
-          const int i = tid + j * BLOCK;
-          if (i < n2) nxt[j] = hits.load(a2 + i);
-        }
-      }
-    }
-    double psy = 0.0, psyy = 0.0, psxy = 0.0, psk = 0.0;
-    auto pass1 = [&](uint32_t p, double v) {
-      double x = 0.0;
-      if (bm_test(Hbm, (int)p)) x = value_at(bm_rank(Hbm, pf, (int)p));
-      psy += v;
-      psxy += x * v;
-      if (x > 0.0) psk += v;
-      const uint32_t h = filt_hash(p, P.npx);
-      const uint32_t bit = 1u << (h & 31);
-      const uint32_t old = atomicOr(&filtA[h >> 5], bit);
-      if (old & bit) atomicOr(&filtD[h >> 5], bit);
-    };
-    auto pass2 = [&](uint32_t p, double v) {
-      const uint32_t h = filt_hash(p, P.npx);
-      if ((filtD[h >> 5] >> (h & 31)) & 1u) {
-        if (atomicAdd(&ctr[C_NSUSP], 1) >= SUSP_CAP || !tbl_add<TBL>(tkey, tval, p, v)) ctr[C_ABORT] = 1;
-      } else {
-        psyy += v * v;
+  // ---- phase 5: other isotope windows in one streaming pass, joined against the principal image -----
+  // Chunks of BLOCK*RC points walk windows 1..K-1 in order with the next chunk prefetched into the other
+  // register buffer; there is no barrier between windows.  Per-window partial sums are reduced per wave at
+  // the window's last chunk.  A point whose duplicate-candidate flag is set (smg_flag_duplicates: it has a
+  // same-spectrum neighbour within a window width) goes to the pixel-keyed f64 table so that duplicate
+  // pixels are summed before squaring (sum y^2 over pixels); every other point contributes v^2 directly.
+  {
+    int ck = 1;        // window of the current chunk
+    int64_t cbase = 0; // offset of the current chunk in its window
+    auto skip_empty = [&](int& k, int64_t& base) {
+      while (k < K && base >= hi[w0 + k] - lo[w0 + k]) {
+        ++k;
+        base = 0;
       }
     };
-    if (single) {
+    auto load_chunk = [&](int k, int64_t base, Reg (&buf)[RC]) {
+      const int64_t a = lo[w0 + k];
+      const int64_t n = hi[w0 + k] - a;
 #pragma unroll
       for (int j = 0; j < RC; ++j) {
-        const int i = tid + j * BLOCK;
-        if (i < n) pass1(Hits<FMT>::pix(cur[j]), Hits<FMT>::val(cur[j]));
+        const int64_t i = base + tid + j * BLOCK;
+        if (i < n) buf[j] = hits.load(a + i);
       }
-      __syncthreads();
+    };
+    double psk = 0.0, psy = 0.0, psyy = 0.0, psxy = 0.0;
+    auto flush = [&](int k) {
+      const double a0 = wave_sum(psk), a1 = wave_sum(psy), a2 = wave_sum(psyy), a3 = wave_sum(psxy);
+      if (lane == 0) {
+        double* pk = part + ((size_t)k * NW + wid) * 4;
+        pk[0] = a0;
+        pk[1] = a1;
+        pk[2] = a2;
+        pk[3] = a3;
+      }
+      psk = psy = psyy = psxy = 0.0;
+    };
+    auto process = [&](int k, int64_t base, Reg (&buf)[RC]) {
+      const int64_t n = hi[w0 + k] - lo[w0 + k];
 #pragma unroll
       for (int j = 0; j < RC; ++j) {
-        const int i = tid + j * BLOCK;
-        if (i < n) pass2(Hits<FMT>::pix(cur[j]), Hits<FMT>::val(cur[j]));
-      }
-    } else {
-      for (int64_t c = 0; c < n; c += (int64_t)BLOCK * RT) {
-        Reg t[RT];
-#pragma unroll
-        for (int j = 0; j < RT; ++j) {
-          const int64_t i = c + tid + j * BLOCK;
-          if (i < n) t[j] = hits.load(a + i);
-        }
-#pragma unroll
-        for (int j = 0; j < RT; ++j) {
-          const int64_t i = c + tid + j * BLOCK;
-          if (i < n) pass1(Hits<FMT>::pix(t[j]), Hits<FMT>::val(t[j]));
-        }
-      }
-      __syncthreads();
-      for (int64_t c = 0; c < n; c += (int64_t)BLOCK * RT) {
-        Reg t[RT];
-#pragma unroll
-        for (int j = 0; j < RT; ++j) {
-          const int64_t i = c + tid + j * BLOCK;
-          if (i < n) t[j] = hits.load(a + i);
-        }
-#pragma unroll
-        for (int j = 0; j < RT; ++j) {
-          const int64_t i = c + tid + j * BLOCK;
-          if (i < n) pass2(Hits<FMT>::pix(t[j]), Hits<FMT>::val(t[j]));
+        const int64_t i = base + tid + j * BLOCK;
+        if (i < n) {
+          const uint32_t p = Hits<FMT>::pix(buf[j]);
+          const double v = Hits<FMT>::val(buf[j]);
+          double x = 0.0;
+          if (bm_test(Hbm, (int)p)) x = value_at(bm_rank(Hbm, pf, (int)p));
+          psy += v;
+          psxy += x * v;
+          if (x > 0.0) psk += v;
+          if (!Hits<FMT>::dup(buf[j])) {
+            psyy += v * v;
+          } else if (!tbl_add<TBL>(tkey, tval, (p << 3) | (uint32_t)k, v)) {
+            ctr[C_ABORT] = 1;
+          }
         }
       }
-    }
-    __syncthreads();
-    // drain the duplicate table (exact per-pixel sums), clear the filter, per-wave partials
-    for (int sl = tid; sl < TBL; sl += BLOCK) {
-      if (tkey[sl] != 0xFFFFFFFFu) {
-        const double y = tval[sl];
-        psyy += y * y;
-        tkey[sl] = 0xFFFFFFFFu;
-        tval[sl] = 0.0;
+      if (base + (int64_t)BLOCK * RC >= n) flush(k);  // last chunk of window k
+    };
+    // windows 1..K-1 with zero points still need their (zero) partials
+    for (int k = 1; k < K; ++k)
+      if (hi[w0 + k] <= lo[w0 + k] && lane == 0) {
+        double* pk = part + ((size_t)k * NW + wid) * 4;
+        pk[0] = pk[1] = pk[2] = pk[3] = 0.0;
       }
+    skip_empty(ck, cbase);
+    // ra already holds window 1's first chunk when it fits (issued in phase 0); otherwise load it now
+    if (ck < K && !(ck == 1 && cbase == 0 && hi[w0 + 1] - lo[w0 + 1] <= (int64_t)BLOCK * RC)) load_chunk(ck, cbase, ra);
+    while (ck < K) {
+      int nk = ck;
+      int64_t nbase = cbase + (int64_t)BLOCK * RC;
+      skip_empty(nk, nbase);
+      if (nk < K) load_chunk(nk, nbase, rb);
+      process(ck, cbase, ra);
+      ck = nk;
+      cbase = nbase;
+      if (ck >= K) break;
+      nk = ck;
+      nbase = cbase + (int64_t)BLOCK * RC;
+      skip_empty(nk, nbase);
+      if (nk < K) load_chunk(nk, nbase, ra);
+      process(ck, cbase, rb);
+      ck = nk;
+      cbase = nbase;
     }
-    {
-      uint4* zf = reinterpret_cast<uint4*>(filtA);
-      for (int i = tid; i < FILT_WORDS / 2; i += BLOCK) zf[i] = make_uint4(0, 0, 0, 0);
-    }
-    psk = wave_sum(psk);
-    psy = wave_sum(psy);
-    psyy = wave_sum(psyy);
-    psxy = wave_sum(psxy);
-    if (lane == 0) {
-      double* pk = part + ((size_t)k * NW + wid) * 4;
-      pk[0] = psk;
-      pk[1] = psy;
-      pk[2] = psyy;
-      pk[3] = psxy;
-    }
-    __syncthreads();
-    if (ctr[C_ABORT]) overflow = true;
-    if (tid == 0) ctr[C_NSUSP] = 0;  // read by nobody until after the next window's first barrier
-  };
-  for (int k = 1; k < K && !overflow; k += 2) {
-    window_pass(k, ra, rb);
-    if (k + 1 < K && !overflow) window_pass(k + 1, rb, ra);
   }
-  if (overflow) {
+  __syncthreads();
+  if (ctr[C_ABORT]) {  // duplicate-candidate table full
     if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
     return;
+  }
+  // drain the duplicate-candidate table: exact per-(pixel, window) sums, squared, into per-wave partials
+  {
+    double dq[MAXK];
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k) dq[k] = 0.0;
+    for (int sl = tid; sl < TBL; sl += BLOCK) {
+      const uint32_t key = tkey[sl];
+      if (key != 0xFFFFFFFFu) {
+        const double y = tval[sl];
+        const int k = (int)(key & 7u);
+#pragma unroll
+        for (int kk = 1; kk < MAXK; ++kk)
+          if (kk == k) dq[kk] += y * y;
+      }
+    }
+#pragma unroll
+    for (int kk = 1; kk < MAXK; ++kk) {
+      if (kk < K) {
+        const double t = wave_sum(dq[kk]);
+        if (lane == 0) part[((size_t)kk * NW + wid) * 4 + 2] += t;
+      }
+    }
   }
   STAMP(3);
 

@@ -137,6 +137,34 @@ __global__ void __launch_bounds__(256) sample_spectra_kernel(
   }
 }
 
+// duplicate-candidate flags: one workgroup per spectrum (grid-stride)
+__global__ void __launch_bounds__(256) flag_duplicates_kernel(const int64_t* __restrict__ sp_off, int64_t n_spectra,
+                                                              const float* __restrict__ mz,
+                                                              uint64_t* __restrict__ hits, double ppm,
+                                                              const uint8_t* __restrict__ force) {
+  const double slack = 2.0 * ppm * 1e-6 / (1.0 - ppm * 1e-6) * (1.0 + 1e-9);
+  for (int64_t s = blockIdx.x; s < n_spectra; s += gridDim.x) {
+    const int64_t a = sp_off[s], b = sp_off[s + 1];
+    int unsorted = 0;
+    for (int64_t i = a + 1 + threadIdx.x; i < b; i += blockDim.x) unsorted |= (mz[i] < mz[i - 1]);
+    const bool all = __syncthreads_or(unsorted) || (force && force[s]);
+    for (int64_t i = a + threadIdx.x; i < b; i += blockDim.x) {
+      bool f = all;
+      if (!f) {
+        const double m = (double)mz[i];
+        if (i > a) f = f || (m - (double)mz[i - 1] <= slack * m);
+        if (i + 1 < b) {
+          const double m2 = (double)mz[i + 1];
+          f = f || (m2 - m <= slack * m2);
+        }
+      }
+      const uint64_t h = hits[i];
+      const uint64_t nh = f ? (h | 0x80000000ull) : (h & ~0x80000000ull);
+      if (nh != h) hits[i] = nh;
+    }
+  }
+}
+
 }  // namespace smg
 
 using namespace smg;
@@ -155,6 +183,18 @@ int smg_pack_hits(const int64_t* sp_off, const int32_t* pixel_map, int64_t n_spe
   const int64_t grid = n_spectra < (1 << 20) ? n_spectra : (1 << 20);
   hipLaunchKernelGGL(pack_hits_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream), sp_off,
                      pixel_map, n_spectra, ints, hits);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_flag_duplicates(const int64_t* sp_off, int64_t n_spectra, const float* mz, uint64_t* hits,
+                        int64_t n_points, double ppm, const uint8_t* force, void* stream) {
+  SMG_CHECK_ARG(n_spectra >= 0 && n_points >= 0 && ppm >= 0 && ppm < 1e6, "bad arguments");
+  if (n_spectra == 0 || n_points == 0) return SMG_OK;
+  SMG_CHECK_ARG(sp_off && mz && hits, "null pointer");
+  const int64_t grid = n_spectra < (1 << 20) ? n_spectra : (1 << 20);
+  hipLaunchKernelGGL(flag_duplicates_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream), sp_off,
+                     n_spectra, mz, hits, ppm, force);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

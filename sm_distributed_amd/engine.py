@@ -55,8 +55,11 @@ class DevicePeaks:
     hits: torch.Tensor
     nrows: int
     ncols: int
+    sp_off: torch.Tensor | None = None     # int64[n_spectra+1] (dataset order), for duplicate flags
+    force: torch.Tensor | None = None      # uint8[n_spectra]: spectra whose pixel is shared (non-injective map)
     mz_sorted: torch.Tensor | None = None
     hits_sorted: torch.Tensor | None = None
+    flag_ppm: float | None = None
 
     @property
     def n_points(self) -> int:
@@ -79,11 +82,24 @@ class DevicePeaks:
         hits = torch.empty(mz.shape[0], dtype=torch.int64, device=device)
         check(lib().smg_pack_hits(_p(d_off), _p(d_pix), len(pixel_map), _p(d_ints), mz.shape[0], _p(hits),
                                   _stream(stream)), "smg_pack_hits")
-        return cls(mz=d_mz, hits=hits, nrows=int(dims[0]), ncols=int(dims[1]))
+        return cls(mz=d_mz, hits=hits, nrows=int(dims[0]), ncols=int(dims[1]), sp_off=d_off,
+                   force=_force_flags(pixel_map, device))
 
     @classmethod
-    def from_device(cls, mz: torch.Tensor, hits: torch.Tensor, dims) -> "DevicePeaks":
-        return cls(mz=mz, hits=hits, nrows=int(dims[0]), ncols=int(dims[1]))
+    def from_device(cls, mz: torch.Tensor, hits: torch.Tensor, dims, sp_off: torch.Tensor,
+                    pixel_map=None) -> "DevicePeaks":
+        force = _force_flags(pixel_map, mz.device) if pixel_map is not None else None
+        return cls(mz=mz, hits=hits, nrows=int(dims[0]), ncols=int(dims[1]), sp_off=sp_off, force=force)
+
+    def flag_duplicates(self, ppm: float, stream=None) -> "DevicePeaks":
+        """Duplicate-candidate flags for this ppm (smg_flag_duplicates); idempotent, writes only changes."""
+        if self.sp_off is None:
+            raise ValueError("DevicePeaks needs sp_off (spectrum offsets) for duplicate flags")
+        n_sp = int(self.sp_off.numel()) - 1
+        check(lib().smg_flag_duplicates(_p(self.sp_off), n_sp, _p(self.mz), _p(self.hits), self.n_points,
+                                        float(ppm), _p(self.force), _stream(stream)), "smg_flag_duplicates")
+        self.flag_ppm = float(ppm)
+        return self
 
     def sort(self, stream=None) -> "DevicePeaks":
         n = self.n_points
@@ -189,8 +205,20 @@ def ion_metrics(peaks: DevicePeaks, ions: DeviceIons, lo, hi, nlevels=30, q=99.0
                            connectivity, erosion_border, out, stream)
 
 
+def _force_flags(pixel_map, device):
+    """uint8 per spectrum: 1 where the pixel is shared by several spectra (reference tolerates duplicate
+    coordinates with a warning, imzml_txt_converter.py:95-100); None when the map is injective."""
+    pm = np.asarray(pixel_map)
+    uniq, inv, cnt = np.unique(pm, return_inverse=True, return_counts=True)
+    shared = cnt[inv] > 1
+    if not shared.any():
+        return None
+    return torch.from_numpy(shared.astype(np.uint8)).to(device)
+
+
 def run_hot_path(peaks: DevicePeaks, ions: DeviceIons, ppm: float, nlevels: int = 30, **kw):
-    """One full pass: sort -> window search -> fused metrics (all on the current stream)."""
+    """One full pass: duplicate flags -> sort -> window search -> fused metrics (all on the current stream)."""
+    peaks.flag_duplicates(ppm)
     peaks.sort()
     lo, hi = window_bounds(peaks, ions, ppm)
     return ion_metrics(peaks, ions, lo, hi, nlevels=nlevels, **kw), lo, hi
@@ -214,6 +242,9 @@ def metrics_from_images(ion_images, nrows, ncols, nlevels=30, q=99.0, do_preproc
             if img is not None:
                 c = img.tocoo()
                 p = (c.row.astype(np.int64) * ncols + c.col.astype(np.int64))
+                # duplicate pixels of this image carry the duplicate-candidate flag (bit 31)
+                _, inv, cnt = np.unique(p, return_inverse=True, return_counts=True)
+                p = np.where(cnt[inv] > 1, p | 0x80000000, p)
                 pix_l.append(p.astype(np.uint32))
                 val_l.append(c.data.astype(np.float64))
                 pos += p.shape[0]

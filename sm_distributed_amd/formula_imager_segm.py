@@ -88,7 +88,7 @@ class IonImageSet:
             offs = torch.repeat_interleave(torch.cumsum(ct, 0) - ct, ct)
             idx = base + (torch.arange(total, device=dev) - offs)
             out_hits = self.peaks.hits_sorted[idx].cpu().numpy().view(np.uint64)
-        pix = (out_hits & np.uint64(0xFFFFFFFF)).astype(np.int64)
+        pix = (out_hits & np.uint64(0x7FFFFFFF)).astype(np.int64)
         val = (out_hits >> np.uint64(32)).astype(np.uint32).view(np.float32).astype(np.float64)
         res = []
         pos = 0
@@ -189,6 +189,7 @@ def compute_sf_images(sc, ds, sf_peak_df, ppm):
     else:
         off, mz, it = spectra_from_duck(ds)
         peaks = DevicePeaks.from_arrays(off, mz, it, np.asarray(ds.norm_img_pixel_inds), ds.get_dims())
+    peaks.flag_duplicates(ppm)
     peaks.sort()
     keys, win_off, peak_mz, _ = ion_layout(sf_peak_df)
     # padding windows (NaN m/z) must stay empty: give them an m/z no point can match

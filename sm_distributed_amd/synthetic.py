@@ -304,8 +304,17 @@ def make_dataset_torch(nrows: int, ncols: int, peaks_per_spectrum: float, seed: 
         pix = torch.cat([pix] + extra_pix)
         mz = torch.cat([mz] + extra_mz)
         ints = torch.cat([ints] + extra_int)
+    # dataset order: spectrum-major, each spectrum m/z-sorted (as a centroided imzML spectrum is)
+    key = (pix << 32) | mz.view(torch.int32).to(torch.int64)
+    order = torch.sort(key).indices
+    del key
+    pix, mz, ints = pix[order], mz[order], ints[order]
+    del order
+    counts = torch.bincount(pix, minlength=n_sp)
+    sp_off = torch.zeros(n_sp + 1, dtype=torch.int64, device=device)
+    sp_off[1:] = torch.cumsum(counts, 0)
     hits = (pix & 0xFFFFFFFF) | (ints.view(torch.int32).to(torch.int64) << 32)
     del pix, ints
     info = {"n_points": int(mz.numel()), "n_spectra": n_sp, "n_planted_ions": n_planted,
-            "n_planted_points": int(sum(t.numel() for t in extra_mz))}
+            "n_planted_points": int(sum(t.numel() for t in extra_mz)), "sp_off": sp_off}
     return mz, hits, (nrows, ncols), info

@@ -69,7 +69,7 @@ def test_images_match_oracle(name):
     """Per (ion, peak): device image = sorted hits[lo:hi] summed per pixel == oracle coo.toarray()."""
     ds, ions, ppm, kw, imgs, df, peaks, m, lo, hi = _run_case(name)
     hits = peaks.hits_sorted.cpu().numpy().view(np.uint64)
-    pix = (hits & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    pix = (hits & np.uint64(0x7FFFFFFF)).astype(np.int64)
     val = (hits >> np.uint64(32)).astype(np.uint32).view(np.float32).astype(np.float64)
     nrows, ncols = peaks.nrows, peaks.ncols
     checked = 0
@@ -104,6 +104,27 @@ def test_dense_path_used_when_needed():
 
 def test_sort_is_a_permutation():
     ds, ions, ppm, kw, imgs, df, peaks, m, lo, hi = _run_case("basic")
-    a = np.sort(peaks.hits.cpu().numpy())
+    a = np.sort(peaks.hits.cpu().numpy())  # flags are set before the sort, so both sides carry them
     b = np.sort(peaks.hits_sorted.cpu().numpy())
     np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("name", ["dups", "basic"])
+def test_duplicate_flags_cover_every_window_duplicate(name):
+    """Every pair of points sharing a pixel inside one window carries the duplicate-candidate flag."""
+    ds, ions, ppm, kw, imgs, df, peaks, m, lo, hi = _run_case(name)
+    hits = peaks.hits_sorted.cpu().numpy().view(np.uint64)
+    pix = (hits & np.uint64(0x7FFFFFFF)).astype(np.int64)
+    flag = ((hits >> np.uint64(31)) & np.uint64(1)).astype(bool)
+    n_dup = 0
+    for w in range(len(lo)):
+        p = pix[lo[w]:hi[w]]
+        if p.size < 2:
+            continue
+        _, inv, cnt = np.unique(p, return_inverse=True, return_counts=True)
+        d = cnt[inv] > 1
+        n_dup += int(d.sum())
+        assert flag[lo[w]:hi[w]][d].all()
+    assert n_dup > 0 or name == "basic"
+    if name == "basic":
+        assert flag.mean() < 0.2  # flags stay a small minority on ordinary data
