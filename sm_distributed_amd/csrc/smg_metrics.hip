@@ -522,27 +522,18 @@ __device__ __forceinline__ void process_ion_lds(
   const int n64 = (P.npx + 63) / 64;
   const int nnz = bm_build_prefix<NW>(Hbm, pf, n64, wsc);
   if constexpr (SIDE_TABLE) {
-    // owners store their f32 value; every other hit of an owned pixel is a duplicate -> f64 side table
+    // A point without the duplicate-candidate flag is the only point of its pixel in this window
+    // (smg_flag_duplicates), so its f32 value is the pixel value exactly.  Flagged points (true duplicates
+    // and a few false positives) are summed per rank in the f64 side table, marked in dupb.
 #pragma unroll
     for (int j = 0; j < RMAX; ++j) {
       const int i = tid + j * BLOCK;
       if (i < n0) {
         const int r = bm_rank(Hbm, pf, (int)hp[j]);
-        if ((own >> j) & 1u) {
+        if (!Hits<FMT>::dup(h0[j])) {
           vals[r] = (VT)Hits<FMT>::val(h0[j]);
         } else {
           atomicOr(&dupb[r >> 5], 1u << (r & 31));
-          if (!tbl_add<SIDE>(side_k, side_v, (uint32_t)r, Hits<FMT>::val(h0[j]))) ctr[C_ABORT] = 1;
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < RMAX; ++j) {
-      const int i = tid + j * BLOCK;
-      if (i < n0 && ((own >> j) & 1u)) {
-        const int r = bm_rank(Hbm, pf, (int)hp[j]);
-        if ((dupb[r >> 5] >> (r & 31)) & 1u) {
           if (!tbl_add<SIDE>(side_k, side_v, (uint32_t)r, Hits<FMT>::val(h0[j]))) ctr[C_ABORT] = 1;
         }
       }
@@ -733,24 +724,10 @@ __device__ __forceinline__ void process_ion_lds(
   double chaos_raw = NAN;
   if (chaos_ok) {
     __syncthreads();  // everyone is done reading values before the candidate list overwrites them
-    // principal pixels in rank order into the (now free) filter region
-    uint32_t* opix = filtA;
-    {
-      const int w32u = (P.npx + 31) / 32;
-      for (int w = tid; w < w32u; w += BLOCK) {
-        uint32_t bits = Hbm[w];
-        if (!bits) continue;
-        int r = bm_rank(Hbm, pf, w * 32 + (__ffs(bits) - 1));
-        while (bits) {
-          const int b = __ffs(bits) - 1;
-          bits &= bits - 1u;
-          opix[r++] = (uint32_t)(w * 32 + b);
-        }
-      }
-    }
-    __syncthreads();
-    for (int rr = tid; rr < nnz; rr += BLOCK) {
-      const int s = (int)opix[rr];
+#pragma unroll
+    for (int j = 0; j < RMAX; ++j) {
+      if (!((own >> j) & 1u)) continue;
+      const int s = (int)hp[j];
       const int rs = s / P.ncols, cs = s - rs * P.ncols;
       uint32_t H[7];
 #pragma unroll
