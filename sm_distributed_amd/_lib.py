@@ -8,7 +8,8 @@ from __future__ import annotations
 import ctypes
 import os
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsmg.so")
+# SMG_LIB overrides the path (diagnostic builds of the same C-ABI, e.g. scripts/variants.sh)
+LIB_PATH = os.environ.get("SMG_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsmg.so")
 
 SMG_OK = 0
 SMG_ION_HAS_HITS = 0x1

@@ -61,13 +61,59 @@ __device__ __forceinline__ T wave_max(T v) {
   return v;
 }
 
+// ---- DPP cross-lane primitives (VALU latency instead of ds_bpermute round trips).  They require the
+// whole wave to be active (uniform control flow); results of the reductions are wave-uniform.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xF, true);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = dpp_i<CTRL>((int)b), hi = dpp_i<CTRL>((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+enum : int { DPP_QP_1032 = 0xB1, DPP_QP_2301 = 0x4E, DPP_ROR4 = 0x124, DPP_ROR8 = 0x128, DPP_SHR1 = 0x111,
+             DPP_SHR2 = 0x112, DPP_SHR4 = 0x114, DPP_SHR8 = 0x118, DPP_BCAST15 = 0x142, DPP_BCAST31 = 0x143 };
+
+// sum over the 64 lanes, combined in a fixed order (row sums, then rows 0..3): deterministic
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_d<DPP_QP_1032>(v);
+  v += dpp_d<DPP_QP_2301>(v);
+  v += dpp_d<DPP_ROR4>(v);
+  v += dpp_d<DPP_ROR8>(v);
+  return ((readlane_d(v, 0) + readlane_d(v, 16)) + readlane_d(v, 32)) + readlane_d(v, 48);
+}
+__device__ __forceinline__ double wave_max_dpp(double v) {
+  v = fmax(v, dpp_d<DPP_QP_1032>(v));
+  v = fmax(v, dpp_d<DPP_QP_2301>(v));
+  v = fmax(v, dpp_d<DPP_ROR4>(v));
+  v = fmax(v, dpp_d<DPP_ROR8>(v));
+  return fmax(fmax(readlane_d(v, 0), readlane_d(v, 16)), fmax(readlane_d(v, 32), readlane_d(v, 48)));
+}
+// inclusive prefix sum over the 64 lanes
+__device__ __forceinline__ int wave_incl_scan_dpp(int x) {
+  x += dpp_i<DPP_SHR1>(x);
+  x += dpp_i<DPP_SHR2>(x);
+  x += dpp_i<DPP_SHR4>(x);
+  x += dpp_i<DPP_SHR8>(x);
+  x += dpp_i<DPP_BCAST15, 0xA>(x);
+  x += dpp_i<DPP_BCAST31, 0xC>(x);
+  return x;
+}
+
 // Block-wide sum of NV doubles; `scratch` holds NV * (BLOCK/64) doubles of LDS.  Result broadcast.
-template <int BLOCK, int NV>
+template <int BLOCK, int NV, bool DPP = false>
 __device__ __forceinline__ void block_sum(double (&v)[NV], double* scratch) {
   constexpr int NW = BLOCK / WAVE;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-  for (int j = 0; j < NV; ++j) v[j] = wave_sum(v[j]);
+  for (int j = 0; j < NV; ++j) v[j] = DPP ? wave_sum_dpp(v[j]) : wave_sum(v[j]);
   if (lane == 0) {
 #pragma unroll
     for (int j = 0; j < NV; ++j) scratch[j * NW + wid] = v[j];

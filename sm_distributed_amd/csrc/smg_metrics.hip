@@ -28,20 +28,15 @@
 
 namespace smg {
 
-constexpr int BLOCK = 256;
+constexpr int BLOCK = 256;           // dense (global-scratch) kernel
 constexpr int NW = BLOCK / WAVE;
-constexpr int RMAX = 16;             // principal-window points held per thread
-constexpr int CAP_MAX = BLOCK * RMAX; // max points in the principal window on the LDS path
-constexpr int RC = 16;               // points per thread per chunk of the other windows
-constexpr int RT = 4;                // points per thread per chunk for windows > BLOCK*RC points
 constexpr int MAXK = 8;              // windows per ion on the LDS path
 constexpr int MAXK_DENSE = 32;       // windows per ion supported at all
-constexpr size_t LDS_BUDGET = 80 * 1024;  // per workgroup: two workgroups per CU
 constexpr int TBL = 1024;             // duplicate-candidate table slots ((pixel, window)-keyed f64 sums)
 constexpr int SIDE = 256;             // principal duplicate-pixel table slots (rank-keyed f64 sums)
 constexpr int NPX_LDS_MAX = 1 << 18; // images up to 262144 pixels use the LDS path
 
-enum { C_NE = 0, C_EMAX, C_ABORT, C_NCTR = 8 };
+enum { C_NE = 0, C_EMAX, C_ABORT, C_NOWN, C_NCTR = 8 };
 
 // Diagnostic build only (-DSMG_STAMPS): per-phase wall cycles of the LDS kernel, summed over workgroups
 // into a buffer of their own (read back by smg_debug_stamps); the shipped build executes no stamp.
@@ -66,8 +61,22 @@ struct Params {
   int32_t nlevels;
   int32_t connectivity;
   int32_t erosion_border;
-  double step;  // np.linspace(0, 1, nlevels) step
+  double step;      // np.linspace(0, 1, nlevels) step
+  float inv_ncols;  // 1/ncols for the LDS path's row/column split (npx < 2^24)
 };
+
+// row and column of pixel p < 2^24 from a float reciprocal: the estimate is off by at most one row
+__device__ __forceinline__ void rowcol(int p, const Params& P, int& r, int& c) {
+  r = (int)((float)p * P.inv_ncols);
+  c = p - r * P.ncols;
+  if (c < 0) {
+    --r;
+    c += P.ncols;
+  } else if (c >= P.ncols) {
+    ++r;
+    c -= P.ncols;
+  }
+}
 
 template <int FMT>
 struct Hits;
@@ -78,6 +87,8 @@ struct Hits<SMG_HITS_PACKED_F32> {
   const double* unused;
   using Reg = uint64_t;
   __device__ __forceinline__ Reg load(int64_t i) const { return h[i]; }
+  // scalar base + 32-bit lane offset (saddr addressing)
+  __device__ __forceinline__ Reg load(int64_t base, int i) const { return (h + base)[i]; }
   static __device__ __forceinline__ uint32_t pix(Reg r) { return (uint32_t)r & 0x7FFFFFFFu; }
   static __device__ __forceinline__ bool dup(Reg r) { return ((uint32_t)r >> 31) != 0u; }
   static __device__ __forceinline__ double val(Reg r) { return (double)__uint_as_float((uint32_t)(r >> 32)); }
@@ -99,6 +110,7 @@ struct Hits<SMG_HITS_SPLIT_F64> {
   const double* va;
   using Reg = PixVal;
   __device__ __forceinline__ Reg load(int64_t i) const { return PixVal{pa[i], va[i]}; }
+  __device__ __forceinline__ Reg load(int64_t base, int i) const { return PixVal{(pa + base)[i], (va + base)[i]}; }
   static __device__ __forceinline__ uint32_t pix(Reg r) { return r.p & 0x7FFFFFFFu; }
   static __device__ __forceinline__ bool dup(Reg r) { return (r.p >> 31) != 0u; }
   static __device__ __forceinline__ double val(Reg r) { return r.v; }
@@ -210,14 +222,9 @@ __device__ int bm_build_prefix(const uint32_t* bm, uint16_t* pf, int n64, int* w
   for (int base = a; base < b; base += 64) {
     const int j = base + lane;
     const int c = (j < b) ? __popcll(bm64[j]) : 0;
-    int inc = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int u = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += u;
-    }
+    const int inc = wave_incl_scan_dpp(c);
     if (j < b) pf[j] = (uint16_t)(carry + inc - c);
-    carry += __shfl(inc, 63, 64);
+    carry += __builtin_amdgcn_readlane(inc, 63);
   }
   if (lane == 0) wscratch[wid] = carry;
   __syncthreads();
@@ -234,18 +241,14 @@ __device__ int bm_build_prefix(const uint32_t* bm, uint16_t* pf, int n64, int* w
   return tot;
 }
 
-// bits of image row `row`, columns c0..c0+6 (bit j <-> column c0+j); 0 outside the image
-__device__ __forceinline__ uint32_t bits7(const uint32_t* bm, int row, int c0, const Params& P) {
-  if (row < 0 || row >= P.nrows) return 0u;
-  const int lc = c0 < 0 ? 0 : c0;
-  const int hc = (c0 + 6) < (P.ncols - 1) ? (c0 + 6) : (P.ncols - 1);
-  if (lc > hc) return 0u;
-  const int start = row * P.ncols + lc;
-  const int n = hc - lc + 1;
-  const int w = start >> 5, off = start & 31;
-  const uint64_t v = (uint64_t)bm[w] | ((uint64_t)bm[w + 1] << 32);
-  const uint32_t bits = (uint32_t)(v >> off) & ((1u << n) - 1u);
-  return bits << (lc - c0);
+// bits of image row `row`, columns c0..c0+6 (bit j <-> column c0+j), masked by the valid-column mask cv;
+// 0 outside the image.  c0 >= -3: the bitmap has a zero guard word in front (LdsLayout::o_hbm).
+__device__ __forceinline__ uint32_t bits7(const uint32_t* bm, int row, int c0, uint32_t cv, const Params& P) {
+  const bool rv = (unsigned)row < (unsigned)P.nrows;
+  const int st = (rv ? row : 0) * P.ncols + c0;
+  const int w = st >> 5;
+  const uint32_t v = __builtin_amdgcn_alignbit(bm[w + 1], bm[w], (uint32_t)(st & 31)) & cv;
+  return rv ? v : 0u;
 }
 
 __device__ __forceinline__ uint32_t uf_load(const uint32_t* p) {
@@ -295,7 +298,7 @@ static LdsLayout lds_layout(int npx, int val_bytes, int NW, int CAP_MAX, size_t 
   const int words = (npx + 31) / 32 + 2;
   L.w32 = (words + 3) & ~3;
   const size_t region_ft0 = al16((size_t)TBL * 4) + al16((size_t)TBL * 8);
-  const size_t fixed = al16((size_t)L.w32 * 4) + al16((size_t)(L.w32 / 2) * 2) + al16((size_t)SIDE * 4) +
+  const size_t fixed = 16 + al16((size_t)L.w32 * 4) + al16((size_t)(L.w32 / 2) * 2) + al16((size_t)SIDE * 4) +
                        al16((size_t)SIDE * 8) + al16((size_t)MAXK * NW * 4 * 8) + al16((size_t)8 * NW * 8) +
                        al16((size_t)C_NCTR * 4) + al16((size_t)NW * 4) + 256;
   // largest cap (multiple of 64, <= CAP_MAX) whose carve fits the budget; the filter + table region
@@ -310,7 +313,7 @@ static LdsLayout lds_layout(int npx, int val_bytes, int NW, int CAP_MAX, size_t 
   }
   if (cap < 64) cap = 0;
   L.cap = cap;
-  size_t o = al16((size_t)L.w32 * 4);
+  size_t o = 16 + al16((size_t)L.w32 * 4);  // zero guard word(s), then the bitmap at offset 16
   L.o_pf = o;
   o = al16(o + (size_t)(L.w32 / 2) * 2);
   L.o_vals = o;
@@ -422,7 +425,7 @@ __device__ __forceinline__ void process_ion_lds(
   using VT = typename ValStore<FMT>::T;
   constexpr bool SIDE_TABLE = (FMT == SMG_HITS_PACKED_F32);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t* Hbm = reinterpret_cast<uint32_t*>(smem);
+  uint32_t* Hbm = reinterpret_cast<uint32_t*>(smem + 16);  // smem[0..16): zero guard for bits7
   uint16_t* pf = reinterpret_cast<uint16_t*>(smem + LL.o_pf);
   VT* vals = reinterpret_cast<VT*>(smem + LL.o_vals);
   uint8_t* Lv = reinterpret_cast<uint8_t*>(smem + LL.o_L);
@@ -472,23 +475,36 @@ __device__ __forceinline__ void process_ion_lds(
 #pragma unroll
   for (int j = 0; j < RMAX; ++j) {
     const int i = tid + j * BLOCK;
-    if (i < n0) h0[j] = hits.load(lo0 + i);
+    if (i < n0) h0[j] = hits.load(lo0, i);
   }
-  Reg ra[RC], rb[RC];
-  if (K > 1) {
-    const int64_t a1 = lo[w0 + 1];
-    const int64_t n1 = hi[w0 + 1] - a1;
-    if (n1 <= (int64_t)BLOCK * RC) {
-#pragma unroll
-      for (int j = 0; j < RC; ++j) {
-        const int i = tid + j * BLOCK;
-        if (i < n1) ra[j] = hits.load(a1 + i);
-      }
+  // windows 1..K-1 are streamed in chunks of BLOCK*RC points that never span two windows; a chunk is
+  // (window k, offset base).  The first chunk (A) is issued here with the principal window, the second (B)
+  // right after phase 1, so both are in flight during phases 1-3.
+  constexpr int CH = BLOCK * RC;
+  auto skip_empty = [&](int& k, int64_t& base) {
+    while (k < K && base >= hi[w0 + k] - lo[w0 + k]) {
+      ++k;
+      base = 0;
     }
-  }
+  };
+  auto load_chunk = [&](int k, int64_t base, Reg (&buf)[RC]) {
+    const int64_t a = lo[w0 + k];
+    const int64_t n = hi[w0 + k] - a;
+    const int rem = (int)min<int64_t>(n - base, (int64_t)CH);
+#pragma unroll
+    for (int j = 0; j < RC; ++j) {
+      const int i = tid + j * BLOCK;
+      if (i < rem) buf[j] = hits.load(a + base, i);
+    }
+  };
+  Reg ra[RC], rb[RC];
+  int ka = 1, kb = K;
+  int64_t ba = 0, bb = 0;
+  skip_empty(ka, ba);
+  if (ka < K) load_chunk(ka, ba, ra);
   {
-    uint4* z = reinterpret_cast<uint4*>(Hbm);
-    for (int i = tid; i < LL.w32 / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
+    uint4* z = reinterpret_cast<uint4*>(smem);
+    for (int i = tid; i < LL.w32 / 4 + 1; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
     for (int i = tid; i < TBL; i += BLOCK) {
       tkey[i] = 0xFFFFFFFFu;
       tval[i] = 0.0;
@@ -547,6 +563,12 @@ __device__ __forceinline__ void process_ion_lds(
       if (i < n0) atomicAdd(&vals[bm_rank(Hbm, pf, (int)hp[j])], Hits<FMT>::val(h0[j]));
     }
   }
+  if (ka < K) {
+    kb = ka;
+    bb = ba + CH;
+    skip_empty(kb, bb);
+    if (kb < K) load_chunk(kb, bb, rb);
+  }
   __syncthreads();
   if (ctr[C_ABORT]) {  // more duplicate pixels than the side table holds
     if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
@@ -575,8 +597,8 @@ __device__ __forceinline__ void process_ion_lds(
       acc[4] = v > acc[4] ? v : acc[4];
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = wave_sum(acc[q]);
-    acc[4] = wave_max(acc[4]);
+    for (int q = 0; q < 4; ++q) acc[q] = wave_sum_dpp(acc[q]);
+    acc[4] = wave_max_dpp(acc[4]);
     if (lane == 0) {
 #pragma unroll
       for (int q = 0; q < 5; ++q) red[q * NW + wid] = acc[q];
@@ -595,7 +617,10 @@ __device__ __forceinline__ void process_ion_lds(
     npos = t[3];
     vmax = t[4];
   }
-  const bool chaos_ok = (sx > 0.0) && (npos >= 4.0);
+#ifndef SMG_ABL
+#define SMG_ABL 0  // diagnostic ablations (timing only, wrong results): 1 = no chaos, 2 = no windows k >= 1
+#endif
+  const bool chaos_ok = (sx > 0.0) && (npos >= 4.0) && !(SMG_ABL & 1);
   if (chaos_ok) {
     for (int r = tid; r < nnz; r += BLOCK) Lv[r] = (uint8_t)level_fast(value_at(r), vmax, P);
   }
@@ -608,26 +633,9 @@ __device__ __forceinline__ void process_ion_lds(
   // same-spectrum neighbour within a window width) goes to the pixel-keyed f64 table so that duplicate
   // pixels are summed before squaring (sum y^2 over pixels); every other point contributes v^2 directly.
   {
-    int ck = 1;        // window of the current chunk
-    int64_t cbase = 0; // offset of the current chunk in its window
-    auto skip_empty = [&](int& k, int64_t& base) {
-      while (k < K && base >= hi[w0 + k] - lo[w0 + k]) {
-        ++k;
-        base = 0;
-      }
-    };
-    auto load_chunk = [&](int k, int64_t base, Reg (&buf)[RC]) {
-      const int64_t a = lo[w0 + k];
-      const int64_t n = hi[w0 + k] - a;
-#pragma unroll
-      for (int j = 0; j < RC; ++j) {
-        const int64_t i = base + tid + j * BLOCK;
-        if (i < n) buf[j] = hits.load(a + i);
-      }
-    };
     double psk = 0.0, psy = 0.0, psyy = 0.0, psxy = 0.0;
     auto flush = [&](int k) {
-      const double a0 = wave_sum(psk), a1 = wave_sum(psy), a2 = wave_sum(psyy), a3 = wave_sum(psxy);
+      const double a0 = wave_sum_dpp(psk), a1 = wave_sum_dpp(psy), a2 = wave_sum_dpp(psyy), a3 = wave_sum_dpp(psxy);
       if (lane == 0) {
         double* pk = part + ((size_t)k * NW + wid) * 4;
         pk[0] = a0;
@@ -639,10 +647,10 @@ __device__ __forceinline__ void process_ion_lds(
     };
     auto process = [&](int k, int64_t base, Reg (&buf)[RC]) {
       const int64_t n = hi[w0 + k] - lo[w0 + k];
+      const int rem = (int)min<int64_t>(n - base, (int64_t)BLOCK * RC);
 #pragma unroll
       for (int j = 0; j < RC; ++j) {
-        const int64_t i = base + tid + j * BLOCK;
-        if (i < n) {
+        if (tid + j * BLOCK < rem) {
           const uint32_t p = Hits<FMT>::pix(buf[j]);
           const double v = Hits<FMT>::val(buf[j]);
           double x = 0.0;
@@ -665,25 +673,20 @@ __device__ __forceinline__ void process_ion_lds(
         double* pk = part + ((size_t)k * NW + wid) * 4;
         pk[0] = pk[1] = pk[2] = pk[3] = 0.0;
       }
-    skip_empty(ck, cbase);
-    // ra already holds window 1's first chunk when it fits (issued in phase 0); otherwise load it now
-    if (ck < K && !(ck == 1 && cbase == 0 && hi[w0 + 1] - lo[w0 + 1] <= (int64_t)BLOCK * RC)) load_chunk(ck, cbase, ra);
-    while (ck < K) {
-      int nk = ck;
-      int64_t nbase = cbase + (int64_t)BLOCK * RC;
-      skip_empty(nk, nbase);
-      if (nk < K) load_chunk(nk, nbase, rb);
-      process(ck, cbase, ra);
-      ck = nk;
-      cbase = nbase;
-      if (ck >= K) break;
-      nk = ck;
-      nbase = cbase + (int64_t)BLOCK * RC;
-      skip_empty(nk, nbase);
-      if (nk < K) load_chunk(nk, nbase, ra);
-      process(ck, cbase, rb);
-      ck = nk;
-      cbase = nbase;
+    // ra holds chunk A, rb chunk B (when they exist); each buffer is refilled as soon as it is consumed
+    while (ka < K && !(SMG_ABL & 2)) {
+      process(ka, ba, ra);
+      if (kb >= K) break;
+      ka = kb;
+      ba = bb + CH;
+      skip_empty(ka, ba);
+      if (ka < K) load_chunk(ka, ba, ra);
+      process(kb, bb, rb);
+      if (ka >= K) break;
+      kb = ka;
+      bb = ba + CH;
+      skip_empty(kb, bb);
+      if (kb < K) load_chunk(kb, bb, rb);
     }
   }
   __syncthreads();
@@ -709,7 +712,7 @@ __device__ __forceinline__ void process_ion_lds(
 #pragma unroll
     for (int kk = 1; kk < MAXK; ++kk) {
       if (kk < K) {
-        const double t = wave_sum(dq[kk]);
+        const double t = wave_sum_dpp(dq[kk]);
         if (lane == 0) part[((size_t)kk * NW + wid) * 4 + 2] += t;
       }
     }
@@ -723,24 +726,34 @@ __device__ __forceinline__ void process_ion_lds(
   // (ii) exact eL for the survivors from the level indices.
   double chaos_raw = NAN;
   if (chaos_ok) {
-    __syncthreads();  // everyone is done reading values before the candidate list overwrites them
+    __syncthreads();  // values and the duplicate table are dead: the table region takes the owned list
+    // compact the owned principal pixels (one per distinct pixel) into a dense list so that every lane of
+    // the screen below has a pixel: the register slots are only ~half owned
+    uint32_t* olist = filtA;
+    {
+      const int cnt = __popc(own);
+      const int inc = wave_incl_scan_dpp(cnt);
+      int wbase = 0;
+      if (lane == 63) wbase = atomicAdd(&ctr[C_NOWN], inc);
+      int pos = __builtin_amdgcn_readlane(wbase, 63) + inc - cnt;
 #pragma unroll
-    for (int j = 0; j < RMAX; ++j) {
-      if (!((own >> j) & 1u)) continue;
-      const int s = (int)hp[j];
-      const int rs = s / P.ncols, cs = s - rs * P.ncols;
+      for (int j = 0; j < RMAX; ++j)
+        if ((own >> j) & 1u) olist[pos++] = hp[j];
+    }
+    __syncthreads();
+    for (int oc_i = tid; oc_i < nnz; oc_i += BLOCK) {
+      const int s = (int)olist[oc_i];
+      int rs, cs;
+      rowcol(s, P, rs, cs);
+      // valid-column mask of columns cs-3..cs+3
+      const int clo = 3 - cs > 0 ? 3 - cs : 0, chi = P.ncols - cs + 3 < 7 ? P.ncols - cs + 3 : 7;
+      const uint32_t cv = ((1u << chi) - 1u) & ~((1u << clo) - 1u);
       uint32_t H[7];
 #pragma unroll
-      for (int d = 0; d < 7; ++d) H[d] = bits7(Hbm, rs - 3 + d, cs - 3, P);
+      for (int d = 0; d < 7; ++d) H[d] = bits7(Hbm, rs - 3 + d, cs - 3, cv, P);
       // isolation pre-filter (erosion border = background only): an eL>0 pixel in the cross of s needs
       // another principal pixel in s's 7x7, since the 4-cross of s alone cannot cover a 3x3 box
       if (!P.erosion_border && (H[0] | H[1] | H[2] | (H[3] & ~8u) | H[4] | H[5] | H[6]) == 0u) continue;
-      uint32_t cv = 0;
-#pragma unroll
-      for (int jj = 0; jj < 7; ++jj) {
-        const int c = cs - 3 + jj;
-        if (c >= 0 && c < P.ncols) cv |= 1u << jj;
-      }
       uint32_t D[7];
       D[0] = D[6] = 0;
 #pragma unroll
@@ -784,7 +797,8 @@ __device__ __forceinline__ void process_ion_lds(
     int emax_local = 0;
     for (int c = tid; c < ncand; c += BLOCK) {
       const int p = (int)epix[c];
-      const int rp = p / P.ncols, cp = p - rp * P.ncols;
+      int rp, cp;
+      rowcol(p, P, rp, cp);
       int mn = 1 << 20;
       for (int qa = -1; qa <= 1; ++qa) {
         for (int qb = -1; qb <= 1; ++qb) {
@@ -816,7 +830,7 @@ __device__ __forceinline__ void process_ion_lds(
     double sum_c = 0.0;
     if (ctr[C_EMAX] > 0) {
       uint4* z = reinterpret_cast<uint4*>(Hbm);
-      for (int i = tid; i < LL.w32 / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
+      for (int i = tid; i < LL.w32 / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);  // guard stays zero
       __syncthreads();
       for (int i = tid; i < ncand; i += BLOCK)
         if (eL8[i]) atomicOr(&Hbm[epix[i] >> 5], 1u << (epix[i] & 31));
@@ -840,7 +854,8 @@ __device__ __forceinline__ void process_ion_lds(
           const int e = eLr[r];
           if (e < t) continue;
           const int p = (int)epix_r[r];
-          const int rp = p / P.ncols, cp = p - rp * P.ncols;
+          int rp, cp;
+          rowcol(p, P, rp, cp);
           auto edge = [&](int q) {
             if (!bm_test(Hbm, q)) return;
             const int rq = bm_rank(Hbm, pf, q);
@@ -861,7 +876,7 @@ __device__ __forceinline__ void process_ion_lds(
         __syncthreads();
       }
       double acc[2] = {esum, wsum};
-      block_sum<BLOCK, 2>(acc, red);
+      block_sum<BLOCK, 2, true>(acc, red);
       sum_c = acc[0] - acc[1];
     }
     chaos_raw = 1.0 - sum_c / (double)P.nlevels / npos;
@@ -889,8 +904,8 @@ __device__ __forceinline__ void process_ion_lds(
 }
 
 
-template <int FMT, int LB, int LRMAX, int LRC>
-__global__ void __launch_bounds__(LB, 4) ion_lds_kernel(
+template <int FMT, int LB, int LRMAX, int LRC, int WPE>
+__global__ void __launch_bounds__(LB, WPE) ion_lds_kernel(
     Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
     const int64_t* __restrict__ ion_off, const double* __restrict__ theor, const int64_t* __restrict__ ion_order,
     int64_t n_ions, Params P, LdsLayout LL, double* __restrict__ oc, double* __restrict__ osp,
@@ -1197,7 +1212,13 @@ static constexpr int DENSE_SLOTS = 256;
 static constexpr size_t WS_HEADER = 256;
 // LDS-path geometries: the main pass (two 512-thread workgroups per CU) and the big-ion pass over its
 // rejects (one 1024-thread workgroup per CU with the whole LDS)
-static constexpr int MAIN_BLOCK = 512, MAIN_RMAX = 8, MAIN_RC = 4;
+#ifndef SMG_MAIN_CFG
+#define SMG_MAIN_CFG 512, 8, 4, 4
+#endif
+// main LDS pass: threads, principal points per thread, chunk points per thread, min waves per SIMD
+static constexpr int MAIN_CFG[4] = {SMG_MAIN_CFG};
+static constexpr int MAIN_BLOCK = MAIN_CFG[0], MAIN_RMAX = MAIN_CFG[1], MAIN_RC = MAIN_CFG[2],
+                     MAIN_WPE = MAIN_CFG[3];
 static constexpr int BIG_BLOCK = 1024, BIG_RMAX = 8, BIG_RC = 4;
 static constexpr size_t MAIN_LDS = 80 * 1024, BIG_LDS = 160 * 1024 - 512;
 
@@ -1225,7 +1246,7 @@ static int launch_metrics(Hits<FMT> hits, const int64_t* lo, const int64_t* hi, 
   LdsLayout LB = big_layout(P.npx, vb);
   const bool lds_ok = P.npx <= NPX_LDS_MAX && LM.cap >= 256;
   if (lds_ok) {
-    auto k1 = &ion_lds_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC>;
+    auto k1 = &ion_lds_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE>;
     SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k1), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)LM.bytes));
     hipLaunchKernelGGL(k1, dim3((unsigned)n_ions), dim3(MAIN_BLOCK), LM.bytes, st, hits, lo, hi, ion_off, theor,
@@ -1316,6 +1337,7 @@ int smg_ion_metrics(int32_t hit_format, const void* hits, const double* hit_vals
   P.connectivity = connectivity;
   P.erosion_border = erosion_border;
   P.step = nlevels > 1 ? 1.0 / (double)(nlevels - 1) : 0.0;
+  P.inv_ncols = 1.0f / (float)ncols;
   unsigned char* ws = reinterpret_cast<unsigned char*>(workspace);
   hipStream_t st = as_stream(stream);
   if (hit_format == SMG_HITS_PACKED_F32) {
