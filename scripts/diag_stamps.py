@@ -2,7 +2,8 @@
 import ctypes, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from sm_distributed_amd import _lib
-_lib.LIB_PATH = _lib.LIB_PATH.replace("libsmg.so", "libsmg_stamps.so")
+if not os.environ.get("SMG_LIB"):
+    _lib.LIB_PATH = _lib.LIB_PATH.replace("libsmg.so", "libsmg_stamps.so")
 import torch
 from sm_distributed_amd import engine as E, synthetic as syn
 
@@ -24,9 +25,10 @@ torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 L.smg_debug_stamps(buf, 16)
 names = ["p0 load+zero", "p1 bitmap/prefix/vals", "p2-3 stats+levels", "p5 windows k>=1", "p4a screen",
-         "p4a exact eL", "p4b kruskal"]
+         "p4a exact eL", "p4b kruskal", "finalize+loop"]
 n = dions.n_ions
-tot = sum(buf[i] for i in range(7))
+tot = sum(buf[i] for i in range(8))
+print(os.path.basename(_lib.LIB_PATH))
 print(f"metrics launch {dt*1e3:.1f} ms for {n} ions; sum cycles/ion {tot/n:.0f}")
 for i, nm in enumerate(names):
     print(f"  {nm:24s} {buf[i]/n:10.0f} cycles/ion  {100*buf[i]/max(tot,1):5.1f}%")

@@ -1,6 +1,11 @@
-"""Diagnostic: time the fused ion-metrics launch of whatever libsmg the SMG_LIB env var names (config 3)."""
+"""Diagnostic: time the fused ion-metrics launch of whatever libsmg the SMG_LIB env var names (config 3).
+
+The first variant run in a GPU session saves its outputs (gpurun_out/ab_ref.npz); later variants report their
+max |difference| from it, so an A/B session checks that a faster variant still computes the same table.
+"""
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
 import torch
 from sm_distributed_amd import engine as E, synthetic as syn, _lib
 
@@ -10,7 +15,6 @@ peaks = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
 dions = E.DeviceIons.from_arrays(ions.win_off, ions.peak_mz, ions.peak_int)
 m, lo, hi = E.run_hot_path(peaks, dions, 2.0, 30)
 torch.cuda.synchronize()
-ref = m.to_numpy()
 ts = []
 for _ in range(5):
     t0 = time.perf_counter()
@@ -18,7 +22,17 @@ for _ in range(5):
     torch.cuda.synchronize()
     ts.append(time.perf_counter() - t0)
 got = m.to_numpy()
-import numpy as np
-err = max(float(np.nanmax(np.abs(got[c] - ref[c]))) for c in ("chaos", "spatial", "spectral", "msm"))
+cols = ("chaos", "spatial", "spectral", "msm")
+ref_path = os.path.join("gpurun_out", "ab_ref.npz")
+if os.path.exists(ref_path):
+    ref = np.load(ref_path)
+    err = max(float(np.nanmax(np.abs(got[c] - ref[c]))) for c in cols)
+    hits_same = bool(np.array_equal(got["flags"] & 1, ref["flags"] & 1))
+    note = f"max|d| vs first variant {err:.1e}, scored set same {hits_same}"
+else:
+    os.makedirs("gpurun_out", exist_ok=True)
+    np.savez(ref_path, **{c: got[c] for c in cols + ("flags",)})
+    note = "reference variant"
+fl = got["flags"]
 print(f"{os.path.basename(_lib.LIB_PATH)}: ion_metrics min {min(ts)*1e3:.2f} ms median {sorted(ts)[2]*1e3:.2f} ms "
-      f"(self-consistency {err:.1e}, dense {int(((got['flags'] & 2) != 0).sum())})", flush=True)
+      f"({note}; big {int(((fl & 8) != 0).sum())} dense {int(((fl & 2) != 0).sum())})", flush=True)

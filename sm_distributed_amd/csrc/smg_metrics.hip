@@ -32,11 +32,9 @@ constexpr int BLOCK = 256;           // dense (global-scratch) kernel
 constexpr int NW = BLOCK / WAVE;
 constexpr int MAXK = 8;              // windows per ion on the LDS path
 constexpr int MAXK_DENSE = 32;       // windows per ion supported at all
-constexpr int TBL = 1024;             // duplicate-candidate table slots ((pixel, window)-keyed f64 sums)
-constexpr int SIDE = 256;             // principal duplicate-pixel table slots (rank-keyed f64 sums)
 constexpr int NPX_LDS_MAX = 1 << 18; // images up to 262144 pixels use the LDS path
 
-enum { C_NE = 0, C_EMAX, C_ABORT, C_NOWN, C_NCTR = 8 };
+enum { C_NE = 0, C_EMAX, C_ABORT, C_PDUP, C_NEXT, C_NCTR = 8 };
 
 // Diagnostic build only (-DSMG_STAMPS): per-phase wall cycles of the LDS kernel, summed over workgroups
 // into a buffer of their own (read back by smg_debug_stamps); the shipped build executes no stamp.
@@ -63,6 +61,8 @@ struct Params {
   int32_t erosion_border;
   double step;      // np.linspace(0, 1, nlevels) step
   float inv_ncols;  // 1/ncols for the LDS path's row/column split (npx < 2^24)
+  int32_t w32;      // LDS path: bitmap words (Lay::w32)
+  uint32_t o_pf;    // LDS path: byte offset of the rank prefix (Lay::o_pf)
 };
 
 // row and column of pixel p < 2^24 from a float reciprocal: the estimate is off by at most one row
@@ -242,7 +242,7 @@ __device__ int bm_build_prefix(const uint32_t* bm, uint16_t* pf, int n64, int* w
 }
 
 // bits of image row `row`, columns c0..c0+6 (bit j <-> column c0+j), masked by the valid-column mask cv;
-// 0 outside the image.  c0 >= -3: the bitmap has a zero guard word in front (LdsLayout::o_hbm).
+// 0 outside the image.  c0 >= -3: the bitmap has a zero guard word in front (Lay::o_guard).
 __device__ __forceinline__ uint32_t bits7(const uint32_t* bm, int row, int c0, uint32_t cv, const Params& P) {
   const bool rv = (unsigned)row < (unsigned)P.nrows;
   const int st = (rv ? row : 0) * P.ncols + c0;
@@ -281,69 +281,36 @@ __device__ __forceinline__ bool uf_unite(uint32_t* par, uint32_t a, uint32_t b) 
   }
 }
 
-struct LdsLayout {
-  int w32;        // bitmap words incl. padding (multiple of 4)
-  int cap;        // max principal-window points on the LDS path (runtime, <= CAP_MAX)
-  size_t o_pf, o_vals, o_L, o_dupb, o_side_k, o_side_v, o_filt, o_tkey, o_tval, o_part, o_red, o_ctr, o_wsc,
-      bytes;
-};
-
+// LDS carve of the persistent kernel.  Everything but the pixel bitmap and its rank prefix has a
+// compile-time offset (immediate ds_* offsets, no offset SGPRs); the bitmap (npx bits, a zero guard word in
+// front) and the prefix (one u16 per 64-bit word) come last and are sized at run time (Params::w32, o_pf).
 static inline size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
-
-// LDS carve for an image of npx pixels and principal values of val_bytes each.  The principal-image
-// capacity is whatever fits the per-workgroup budget (LDS_BUDGET -> two workgroups per CU), capped by
-// CAP_MAX and by the chaos phase's reuse of the filter + table region (rank-ordered E pixels: 5 B each).
-static LdsLayout lds_layout(int npx, int val_bytes, int NW, int CAP_MAX, size_t LDS_BUDGET) {
-  LdsLayout L;
-  const int words = (npx + 31) / 32 + 2;
-  L.w32 = (words + 3) & ~3;
-  const size_t region_ft0 = al16((size_t)TBL * 4) + al16((size_t)TBL * 8);
-  const size_t fixed = 16 + al16((size_t)L.w32 * 4) + al16((size_t)(L.w32 / 2) * 2) + al16((size_t)SIDE * 4) +
-                       al16((size_t)SIDE * 8) + al16((size_t)MAXK * NW * 4 * 8) + al16((size_t)8 * NW * 8) +
-                       al16((size_t)C_NCTR * 4) + al16((size_t)NW * 4) + 256;
-  // largest cap (multiple of 64, <= CAP_MAX) whose carve fits the budget; the filter + table region
-  // doubles as the chaos phase's E-pixel storage (5 B per point) and grows with cap when needed
-  int cap = CAP_MAX & ~63;
-  size_t region_ft = region_ft0;
-  for (; cap >= 64; cap -= 64) {
-    region_ft = region_ft0 > al16((size_t)5 * cap) ? region_ft0 : al16((size_t)5 * cap);
-    const size_t need = fixed + region_ft + al16((size_t)cap * (val_bytes < 4 ? 4 : val_bytes)) + al16((size_t)cap) +
-                        al16((size_t)((cap + 31) / 32) * 4);
-    if (need <= LDS_BUDGET) break;
-  }
-  if (cap < 64) cap = 0;
-  L.cap = cap;
-  size_t o = 16 + al16((size_t)L.w32 * 4);  // zero guard word(s), then the bitmap at offset 16
-  L.o_pf = o;
-  o = al16(o + (size_t)(L.w32 / 2) * 2);
-  L.o_vals = o;
-  o = al16(o + (size_t)cap * (val_bytes < 4 ? 4 : val_bytes));
-  L.o_L = o;
-  o = al16(o + (size_t)cap);
-  L.o_dupb = o;
-  o = al16(o + (size_t)((cap + 31) / 32) * 4);
-  L.o_side_k = o;
-  o = al16(o + (size_t)SIDE * 4);
-  L.o_side_v = o;
-  o = al16(o + (size_t)SIDE * 8);
-  L.o_filt = o;  // region shared by the duplicate table and (later) the chaos phase's E arrays
-  L.o_tkey = o;
-  o = al16(o + (size_t)TBL * 4);
-  L.o_tval = o;
-  o = al16(o + (size_t)TBL * 8);
-  if (o - L.o_filt < region_ft) o = L.o_filt + region_ft;
-  L.o_part = o;
-  o = al16(o + (size_t)MAXK * NW * 4 * 8);
-  L.o_red = o;
-  o = al16(o + (size_t)8 * NW * 8);
-  L.o_ctr = o;
-  o = al16(o + (size_t)C_NCTR * 4);
-  L.o_wsc = o;
-  o = al16(o + (size_t)NW * 4);
-  L.bytes = o;
-  return L;
-}
-
+static constexpr uint32_t cal16(uint32_t x) { return (x + 15u) & ~15u; }
+constexpr int DSEG = 64;   // deferred duplicate-candidate tail points per wave and ion (NW * DSEG = block)
+constexpr int DTBL = 512;  // their (pixel, window)-keyed sum table
+template <int NW, int CAPC>
+struct Lay {
+  static constexpr uint32_t o_vals = 0;                                // principal f64 values, rank order
+  static constexpr uint32_t o_L = cal16(o_vals + (uint32_t)CAPC * 8);  // level index, rank order
+  static constexpr uint32_t o_filt = cal16(o_L + CAPC);  // tail duplicate lists, later the chaos E arrays
+  static constexpr uint32_t o_dkey = o_filt;                             // [NW][DSEG] (pixel << 3 | window)
+  static constexpr uint32_t o_dval = cal16(o_dkey + NW * DSEG * 4);      // [NW][DSEG] values
+  static constexpr uint32_t o_dcnt = cal16(o_dval + NW * DSEG * 8);      // [NW] entries per wave
+  static constexpr uint32_t o_tkey = cal16(o_dcnt + NW * 4);              // (pixel, window)-keyed f64 sums
+  static constexpr uint32_t o_tval = cal16(o_tkey + DTBL * 4);
+  static constexpr uint32_t filt_bytes = (o_tval + DTBL * 8 - o_filt) > 5u * CAPC ? (o_tval + DTBL * 8 - o_filt)
+                                                                                 : 5u * CAPC;
+  static constexpr uint32_t o_part = cal16(o_filt + filt_bytes);  // [MAXK][NW][4] per-wave window partials
+  static constexpr uint32_t o_red = cal16(o_part + MAXK * NW * 4 * 8);
+  static constexpr uint32_t o_ctr = cal16(o_red + 8 * NW * 8);
+  static constexpr uint32_t o_wsc = cal16(o_ctr + C_NCTR * 4);
+  static constexpr uint32_t o_desc = cal16(o_wsc + NW * 4);  // two ion descriptors (current, next)
+  static constexpr uint32_t o_guard = cal16(o_desc + 2 * 256);
+  static constexpr uint32_t o_bm = o_guard + 16;
+  static int w32(int npx) { return (((npx + 31) / 32 + 2) + 3) & ~3; }
+  static uint32_t o_pf(int npx) { return cal16(o_bm + (uint32_t)w32(npx) * 4); }
+  static size_t bytes(int npx) { return cal16(o_pf(npx) + (uint32_t)(w32(npx) / 2) * 2); }
+};
 
 // open-addressing f64 accumulators keyed by u32 (EMPTY = 0xFFFFFFFF); returns false when full
 template <int NSLOT>
@@ -360,18 +327,6 @@ __device__ __forceinline__ bool tbl_add(uint32_t* keys, double* vals, uint32_t k
   return false;
 }
 
-template <int NSLOT>
-__device__ __forceinline__ int tbl_find(const uint32_t* keys, uint32_t key) {
-  uint32_t h = (key * 2654435761u) >> (32 - __builtin_ctz(NSLOT));
-  for (int probe = 0; probe < NSLOT; ++probe) {
-    const uint32_t k = keys[h];
-    if (k == key) return (int)h;
-    if (k == 0xFFFFFFFFu) return -1;
-    h = (h + 1) & (NSLOT - 1);
-  }
-  return -1;
-}
-
 // level index via the closed form of np.linspace(0, 1, n): lev_i = i*step (i < n-1), lev_{n-1} = 1.0;
 // L = #{i : lev_i < norm}; the estimate is corrected with exact comparisons so it equals the loop.
 __device__ __forceinline__ int level_fast(double v, double vmax, const Params& P) {
@@ -386,560 +341,724 @@ __device__ __forceinline__ int level_fast(double v, double vmax, const Params& P
   return j + ((1.0 < norm) ? 1 : 0);
 }
 
-template <int FMT>
-struct ValStore;
-template <>
-struct ValStore<SMG_HITS_PACKED_F32> {
-  using T = float;  // a single f32 hit is exact in f32; duplicate pixels use the f64 side table
+// ---------------------------------------------------------------------------------------------
+// Ion descriptors: one 256-B record per position of the processing order (ion_desc_kernel), so that a
+// workgroup reaches an ion's windows with one coalesced read instead of the ion_order -> ion_off -> lo/hi
+// chain.  The tail windows 1..K-1 form one stream of 64-point groups, each window padded to whole groups,
+// so that every group (one wave's share of a chunk slot) lies in a single window.
+// ---------------------------------------------------------------------------------------------
+struct IonDesc {
+  int64_t base[MAXK];  // [0]: lo of the principal window; [k>=1]: lo[k] - 64*gs[k] (padded tail position -> hit)
+  int32_t end[MAXK];   // [0]: principal points; [k>=1]: 64*gs[k] + n[k] (end of window k in the padded tail)
+  int32_t gs[MAXK];    // [k>=1]: first group of window k; INT_MAX for k >= K
+  double theor[MAXK];  // theoretical intensities
+  int32_t ion, K, ngroups, hits;  // ngroups < 0: tail too long for 32-bit positions (dense path)
+  int32_t pad[12];
 };
-template <>
-struct ValStore<SMG_HITS_SPLIT_F64> {
-  using T = double;
+static_assert(sizeof(IonDesc) == 256, "IonDesc is 256 B");
+constexpr int DESC_WORDS = (int)(sizeof(IonDesc) / 4);
+
+__global__ void ion_desc_kernel(const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
+                                const int64_t* __restrict__ ion_off, const double* __restrict__ theor,
+                                const int64_t* __restrict__ ion_order, int64_t n_ions, IonDesc* __restrict__ out) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n_ions) return;
+  const int64_t ion = ion_order ? ion_order[b] : b;
+  const int64_t w0 = ion_off[ion];
+  const int K = (int)(ion_off[ion + 1] - w0);
+  IonDesc* d = out + b;
+  int64_t g = 0;
+  uint32_t has = 0;
+  int64_t wb[MAXK];
+  int32_t we[MAXK], wg[MAXK];
+  double wt[MAXK];
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) {
+    wb[k] = 0;
+    we[k] = 0;
+    wg[k] = 0x7FFFFFFF;
+    wt[k] = 0.0;
+    if (k < K) {
+      const int64_t a = lo[w0 + k], n = hi[w0 + k] - a;
+      wt[k] = theor[w0 + k];
+      if (n > 0) has = SMG_ION_HAS_HITS;
+      if (k == 0) {
+        wb[k] = a;
+        we[k] = (int32_t)(n < 0x7FFFFFFF ? n : 0x7FFFFFFF);
+        wg[k] = 0;
+      } else {
+        wb[k] = a - 64 * g;
+        we[k] = (int32_t)(64 * g + n < 0x7FFFFFFF ? 64 * g + n : 0x7FFFFFFF);
+        wg[k] = (int32_t)(g < 0x7FFFFFFF ? g : 0x7FFFFFFF);
+        g += (n + 63) / 64;
+      }
+    }
+  }
+  for (int k = MAXK; k < K && k < MAXK_DENSE; ++k)
+    if (hi[w0 + k] > lo[w0 + k]) has = SMG_ION_HAS_HITS;
+#pragma unroll
+  for (int k = 0; k < MAXK; k += 2) {
+    reinterpret_cast<longlong2*>(d->base)[k / 2] = make_longlong2(wb[k], wb[k + 1]);
+    reinterpret_cast<double2*>(d->theor)[k / 2] = make_double2(wt[k], wt[k + 1]);
+  }
+#pragma unroll
+  for (int k = 0; k < MAXK; k += 4) {
+    reinterpret_cast<int4*>(d->end)[k / 4] = make_int4(we[k], we[k + 1], we[k + 2], we[k + 3]);
+    reinterpret_cast<int4*>(d->gs)[k / 4] = make_int4(wg[k], wg[k + 1], wg[k + 2], wg[k + 3]);
+  }
+  const int32_t ng = 64 * g < (1ll << 30) ? (int32_t)g : -1;
+  reinterpret_cast<int4*>(&d->ion)[0] = make_int4((int32_t)ion, K, ng, (int)has);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) reinterpret_cast<int4*>(d->pad)[i] = make_int4(0, 0, 0, 0);
+}
+
+// Work sources of the persistent LDS kernel.
+//  SRC_RANGES: positions [0, n) split into 8 contiguous ranges, one per XCD (workgroup w runs on XCD w % 8),
+//    so concurrently scored ions of one XCD are m/z neighbours and share windows in that XCD's L2; a
+//    workgroup whose range is exhausted steals from the other ranges.
+//  SRC_LIST: a device list of positions (the rejects of the previous pass) with a global cursor.
+enum { SRC_RANGES = 0, SRC_LIST = 1 };
+constexpr int XCDS = 8;
+constexpr int CTR_STRIDE = 32;  // u32 words between counters (one 128-B line each)
+
+struct Sched {
+  int64_t n;              // SRC_RANGES: positions
+  uint32_t* ctr;          // SRC_RANGES: XCDS counters; SRC_LIST: cursor
+  const uint32_t* list;   // SRC_LIST
+  const uint32_t* count;  // SRC_LIST
 };
 
+template <int SRC>
+__device__ __forceinline__ uint32_t sched_issue(const Sched& S) {
+  if constexpr (SRC == SRC_RANGES) return atomicAdd(&S.ctr[(blockIdx.x % XCDS) * CTR_STRIDE], 1u);
+  else return atomicAdd(S.ctr, 1u);
+}
+
+// resolves a ticket of sched_issue into a position (-1: no work left)
+template <int SRC>
+__device__ __forceinline__ int64_t sched_resolve(const Sched& S, uint32_t t) {
+  if constexpr (SRC == SRC_RANGES) {
+    const int home = blockIdx.x % XCDS;
+    for (int i = 0; i < XCDS; ++i) {
+      const int x = (home + i) % XCDS;
+      const int64_t a = S.n * x / XCDS, b = S.n * (x + 1) / XCDS;
+      if (i > 0) t = atomicAdd(&S.ctr[x * CTR_STRIDE], 1u);
+      if ((int64_t)t < b - a) return a + (int64_t)t;
+    }
+    return -1;
+  } else {
+    const uint32_t c = *S.count;
+    return t < c ? (int64_t)S.list[t] : -1;
+  }
+}
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+  const int lo = __builtin_amdgcn_readfirstlane((int)v), hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+  return ((int64_t)hi << 32) | (uint32_t)lo;
+}
+
+__device__ __forceinline__ bool desc_lds_ok(const IonDesc* D, int capc) {
+  const int K = D->K;
+  return K >= 1 && K <= MAXK && D->end[0] <= capc && D->ngroups >= 0;
+}
+
 // ---------------------------------------------------------------------------------------------
-// LDS path kernel (one workgroup per ion; two workgroups per CU).  Phases, barriers between:
-//   0  issue the loads of the principal window (<= cap points, RMAX per thread) and of the first
-//      chunk of window 1 into registers; initialise the LDS structures meanwhile
-//   1  principal bitmap (atomicOr; the thread that sets a bit owns the pixel), rank prefix, values in
-//      rank order (f32 for single hits, exact f64 side table for duplicate pixels)
-//   2  one fused reduction: sum x, sum x^2, sum x[x>0], #(x>0), max; then level index per pixel
-//   5  for k >= 1: stream window k (registers, next window prefetched), join against the principal
-//      image; duplicate pixels of window k found by a hashed 2-bit filter and summed in an LDS table
-//   4a chaos candidates from owned principal pixels (7x7 bit windows, isolation pre-filter), exact eL
+// LDS path: persistent, software-pipelined kernel.  Each workgroup scores a sequence of ions.  Iteration b
+// scores ion b (phases 0-5), then issues the loads of ion b+1 (principal window, first two tail chunks)
+// into the registers ion b no longer needs, then finishes ion b (duplicates, chaos, finalize) while those
+// loads are in flight.  Barriers between phases:
+//   0  initialise the LDS structures; thread 0 takes a ticket for ion b+1
+//   1  principal bitmap (atomicOr), rank prefix, f64 values in rank order (duplicate-candidate points
+//      zero their slot, then add atomically); ion b+1 resolved and its descriptor fetched
+//   2  one fused reduction: sum x, sum x^2, sum x[x>0], #(x>0), max; level index per pixel
+//   5  tail windows as one stream of 64-point groups (each group in one window; a wave sees windows in
+//      increasing order, keeps running sums for its current window and flushes them when it moves on),
+//      chunks of BLOCK*RC points, two register buffers, next chunk in flight; duplicate-candidate points
+//      deferred to an LDS list.  Then the loads of ion b+1 are issued
+//   d  deferred duplicates summed per (pixel, window) in an LDS table, squared into the partials
+//   4a chaos candidates from the principal pixels (7x7 bit windows, isolation pre-filter), exact eL
 //   4b Kruskal over eL with an LDS union-find
-//   6  finalize (thread 0)
+//   6  finalize (wave 0, one lane per window)
+// measure_of_chaos by threshold decomposition: per-level dilate(cross)/erode(box) equals thresholding
+// eL = erode_box(dilate_cross(L)), so sum_levels #components = sum_p eL(p) - weight(maximum spanning
+// forest with edge weight min(eL)).
+// Ions that do not fit (K > MAXK, principal window > CAPC, list/table overflows) go to `rej_list`: positions
+// (SRC_RANGES pass, read by the big-ion pass) or ion indices (SRC_LIST pass, read by the dense kernel).
 // ---------------------------------------------------------------------------------------------
-template <int FMT, int LB, int LRMAX, int LRC>
-__device__ __forceinline__ void process_ion_lds(
-    int64_t ion, const Hits<FMT>& hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
-    const int64_t* __restrict__ ion_off, const double* __restrict__ theor, const Params& P, const LdsLayout& LL,
-    double* __restrict__ oc, double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm,
-    uint32_t* __restrict__ oflags, uint32_t* __restrict__ dense_list, uint32_t* __restrict__ dense_count) {
+template <int FMT, int LB, int LRMAX, int LRC, int WPE, int SRC>
+__global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
+    Hits<FMT> hits, const IonDesc* __restrict__ desc, Sched S, Params P, double* __restrict__ oc,
+    double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags,
+    uint32_t* __restrict__ rej_list, uint32_t* __restrict__ rej_count) {
   constexpr int BLOCK = LB;
   constexpr int NW = LB / WAVE;
   constexpr int RMAX = LRMAX;
   constexpr int RC = LRC;
-  constexpr int CAP_MAX = BLOCK * RMAX;
+  constexpr int GPC = BLOCK * RC / 64;  // 64-point groups per chunk
+  constexpr int CAPC = BLOCK * RMAX;
   using Reg = typename Hits<FMT>::Reg;
-  using VT = typename ValStore<FMT>::T;
-  constexpr bool SIDE_TABLE = (FMT == SMG_HITS_PACKED_F32);
+  using LY = Lay<NW, CAPC>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t* Hbm = reinterpret_cast<uint32_t*>(smem + 16);  // smem[0..16): zero guard for bits7
-  uint16_t* pf = reinterpret_cast<uint16_t*>(smem + LL.o_pf);
-  VT* vals = reinterpret_cast<VT*>(smem + LL.o_vals);
-  uint8_t* Lv = reinterpret_cast<uint8_t*>(smem + LL.o_L);
-  uint32_t* dupb = reinterpret_cast<uint32_t*>(smem + LL.o_dupb);
-  uint32_t* side_k = reinterpret_cast<uint32_t*>(smem + LL.o_side_k);
-  double* side_v = reinterpret_cast<double*>(smem + LL.o_side_v);
-  uint32_t* filtA = reinterpret_cast<uint32_t*>(smem + LL.o_filt);  // base of the table / E region
-  uint32_t* tkey = reinterpret_cast<uint32_t*>(smem + LL.o_tkey);
-  double* tval = reinterpret_cast<double*>(smem + LL.o_tval);
-  double* part = reinterpret_cast<double*>(smem + LL.o_part);  // [MAXK][NW][4]: s_k, sy, syy, sxy
-  double* red = reinterpret_cast<double*>(smem + LL.o_red);
-  int* ctr = reinterpret_cast<int*>(smem + LL.o_ctr);
-  int* wsc = reinterpret_cast<int*>(smem + LL.o_wsc);
-  const int cap = LL.cap;
+  uint32_t* Hbm = reinterpret_cast<uint32_t*>(smem + LY::o_bm);  // a zero guard word in front, for bits7
+  uint16_t* pf = reinterpret_cast<uint16_t*>(smem + P.o_pf);
+  double* vals = reinterpret_cast<double*>(smem + LY::o_vals);
+  uint8_t* Lv = reinterpret_cast<uint8_t*>(smem + LY::o_L);
+  uint32_t* filtA = reinterpret_cast<uint32_t*>(smem + LY::o_filt);
+  uint32_t* dkey = reinterpret_cast<uint32_t*>(smem + LY::o_dkey);
+  double* dval = reinterpret_cast<double*>(smem + LY::o_dval);
+  int* dcnt = reinterpret_cast<int*>(smem + LY::o_dcnt);
+  uint32_t* tkey = reinterpret_cast<uint32_t*>(smem + LY::o_tkey);
+  double* tval = reinterpret_cast<double*>(smem + LY::o_tval);
+  double* part = reinterpret_cast<double*>(smem + LY::o_part);  // [MAXK][NW][4]: s_k, sy, syy, sxy
+  double* red = reinterpret_cast<double*>(smem + LY::o_red);
+  int* ctr = reinterpret_cast<int*>(smem + LY::o_ctr);
+  int* wsc = reinterpret_cast<int*>(smem + LY::o_wsc);
+  IonDesc* dsl = reinterpret_cast<IonDesc*>(smem + LY::o_desc);  // [2]: current / next
   // chaos-phase aliases (the value, filter and table regions are dead by then)
-  uint32_t* epix = reinterpret_cast<uint32_t*>(vals);                  // candidates, append order
-  uint32_t* epix_r = filtA;                                            // E pixels, rank order (4*cap)
-  uint8_t* eL8 = reinterpret_cast<uint8_t*>(filtA) + (size_t)cap * 4;  // candidates' eL, append order
-  uint8_t* eLr = Lv;                                                   // rank order
-  uint32_t* par = reinterpret_cast<uint32_t*>(vals);                   // rank order (after epix consumed)
+  uint32_t* epix = reinterpret_cast<uint32_t*>(vals);                   // candidates, append order
+  uint32_t* epix_r = filtA;                                             // E pixels, rank order (4*CAPC)
+  uint8_t* eL8 = reinterpret_cast<uint8_t*>(filtA) + (size_t)CAPC * 4;  // candidates' eL, append order
+  uint8_t* eLr = Lv;                                                    // rank order
+  uint32_t* par = reinterpret_cast<uint32_t*>(vals);                    // rank order (after epix consumed)
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wid = tid >> 6;
-  const int64_t w0 = ion_off[ion];
-  const int K = (int)(ion_off[ion + 1] - w0);
+  const int lane = tid & 63;
+  const int wid = uni(tid >> 6);
+  const int n64 = (P.npx + 63) / 64;
+  const uint32_t big_flag = (SRC == SRC_LIST) ? SMG_ION_BIG : 0u;
 
-  uint32_t flags = (LB >= 1024) ? SMG_ION_BIG : 0u;
-  for (int k = 0; k < K && k < MAXK_DENSE; ++k)
-    if (hi[w0 + k] > lo[w0 + k]) flags |= SMG_ION_HAS_HITS;
-  if (K == 0) {
-    if (tid == 0) {
-      oc[ion] = osp[ion] = osc[ion] = omsm[ion] = 0.0;
-      oflags[ion] = 0;
-    }
-    return;
-  }
-  const int64_t lo0 = lo[w0];
-  const int n0 = (int)min<int64_t>(hi[w0] - lo0, (int64_t)CAP_MAX + 1);
-  if (K > MAXK || n0 > cap) {
-    if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
-    return;
-  }
-
-  // ---- phase 0: loads in flight, LDS initialisation meanwhile -----------------------------------
-  STAMP_INIT();
-  Reg h0[RMAX];
+  auto issue_principal = [&](const IonDesc* D, Reg (&buf)[RMAX]) {
+    const int n0 = uni(D->end[0]);
+    const int64_t a = uni64(D->base[0]);
 #pragma unroll
-  for (int j = 0; j < RMAX; ++j) {
-    const int i = tid + j * BLOCK;
-    if (i < n0) h0[j] = hits.load(lo0, i);
-  }
-  // windows 1..K-1 are streamed in chunks of BLOCK*RC points that never span two windows; a chunk is
-  // (window k, offset base).  The first chunk (A) is issued here with the principal window, the second (B)
-  // right after phase 1, so both are in flight during phases 1-3.
-  constexpr int CH = BLOCK * RC;
-  auto skip_empty = [&](int& k, int64_t& base) {
-    while (k < K && base >= hi[w0 + k] - lo[w0 + k]) {
-      ++k;
-      base = 0;
+    for (int j = 0; j < RMAX; ++j) {
+      const int i = tid + j * BLOCK;
+      if (i < n0) buf[j] = hits.load(a, i);
     }
   };
-  auto load_chunk = [&](int k, int64_t base, Reg (&buf)[RC]) {
-    const int64_t a = lo[w0 + k];
-    const int64_t n = hi[w0 + k] - a;
-    const int rem = (int)min<int64_t>(n - base, (int64_t)CH);
+  // tail chunk c: groups [c*GPC, (c+1)*GPC); slot j of wave w holds group c*GPC + j*NW + w
+  auto issue_chunk = [&](const IonDesc* D, int c, Reg (&buf)[RC]) {
+    const int ng = uni(D->ngroups);
 #pragma unroll
     for (int j = 0; j < RC; ++j) {
-      const int i = tid + j * BLOCK;
-      if (i < rem) buf[j] = hits.load(a + base, i);
+      const int G = c * GPC + j * NW + wid;
+      if (G < ng) {
+        int k = 1;
+#pragma unroll
+        for (int kk = 2; kk < MAXK; ++kk) k += (G >= uni(D->gs[kk])) ? 1 : 0;
+        const int i = G * 64 + lane;
+        if (i < uni(D->end[k])) buf[j] = hits.load(uni64(D->base[k]) + i);
+      }
     }
   };
-  Reg ra[RC], rb[RC];
-  int ka = 1, kb = K;
-  int64_t ba = 0, bb = 0;
-  skip_empty(ka, ba);
-  if (ka < K) load_chunk(ka, ba, ra);
-  {
-    uint4* z = reinterpret_cast<uint4*>(smem);
-    for (int i = tid; i < LL.w32 / 4 + 1; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
-    for (int i = tid; i < TBL; i += BLOCK) {
-      tkey[i] = 0xFFFFFFFFu;
-      tval[i] = 0.0;
-    }
-    for (int i = tid; i < SIDE; i += BLOCK) {
-      side_k[i] = 0xFFFFFFFFu;
-      side_v[i] = 0.0;
-    }
-    for (int i = tid; i < (cap + 31) / 32; i += BLOCK) dupb[i] = 0u;
-    if (tid < C_NCTR) ctr[tid] = 0;
-  }
-  __syncthreads();
-  STAMP(0);
 
-  // ---- phase 1: principal image -> bitmap (+ ownership), rank prefix, values --------------------
-  uint32_t own = 0;
-  uint32_t hp[RMAX];
-#pragma unroll
-  for (int j = 0; j < RMAX; ++j) {
-    const int i = tid + j * BLOCK;
-    hp[j] = 0;
-    if (i < n0) {
-      const uint32_t p = Hits<FMT>::pix(h0[j]);
-      hp[j] = p;
-      const uint32_t bit = 1u << (p & 31);
-      const uint32_t old = atomicOr(&Hbm[p >> 5], bit);
-      if (!(old & bit)) own |= 1u << j;
+  Reg h0[RMAX], ra[RC], rb[RC];
+  int64_t pos = -1;  // ion scored in this iteration (-1: none; the first iteration only issues loads)
+  int cur = 0;
+  while (true) {
+    const IonDesc* D = &dsl[cur];
+    IonDesc* DN = &dsl[cur ^ 1];
+    uint32_t ticket = 0;
+    if (tid == 0) ticket = sched_issue<SRC>(S);
+    STAMP_INIT();
+    bool skip = pos < 0;
+    int K = 0, ion = 0, n0 = 0;
+    auto reject = [&]() {
+      if (tid == 0) rej_list[atomicAdd(rej_count, 1u)] = (SRC == SRC_RANGES) ? (uint32_t)pos : (uint32_t)ion;
+    };
+    if (!skip) {
+      K = uni(D->K);
+      ion = uni(D->ion);
+      n0 = uni(D->end[0]);
+      if (K == 0) {
+        if (tid == 0) {
+          oc[ion] = osp[ion] = osc[ion] = omsm[ion] = 0.0;
+          oflags[ion] = 0;
+        }
+        skip = true;
+      } else if (!desc_lds_ok(D, CAPC)) {
+        reject();
+        skip = true;
+      }
     }
-  }
-  __syncthreads();
-  const int n64 = (P.npx + 63) / 64;
-  const int nnz = bm_build_prefix<NW>(Hbm, pf, n64, wsc);
-  if constexpr (SIDE_TABLE) {
-    // A point without the duplicate-candidate flag is the only point of its pixel in this window
-    // (smg_flag_duplicates), so its f32 value is the pixel value exactly.  Flagged points (true duplicates
-    // and a few false positives) are summed per rank in the f64 side table, marked in dupb.
+
+    // ---- phase 0: LDS initialisation -------------------------------------------------------------
+    if (!skip) {
+      uint4* z = reinterpret_cast<uint4*>(smem + LY::o_guard);
+      for (int i = tid; i < P.w32 / 4 + 1; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
+      for (int i = tid; i < MAXK * NW * 4; i += BLOCK) part[i] = 0.0;
+      if (tid < C_NEXT) ctr[tid] = 0;
+    }
+    __syncthreads();
+    STAMP(0);
+
+    // ---- phase 1: principal image -> bitmap, rank prefix, f64 values -----------------------------
+    int nnz = 0;
+    if (!skip) {
 #pragma unroll
-    for (int j = 0; j < RMAX; ++j) {
-      const int i = tid + j * BLOCK;
-      if (i < n0) {
-        const int r = bm_rank(Hbm, pf, (int)hp[j]);
-        if (!Hits<FMT>::dup(h0[j])) {
-          vals[r] = (VT)Hits<FMT>::val(h0[j]);
-        } else {
-          atomicOr(&dupb[r >> 5], 1u << (r & 31));
-          if (!tbl_add<SIDE>(side_k, side_v, (uint32_t)r, Hits<FMT>::val(h0[j]))) ctr[C_ABORT] = 1;
+      for (int j = 0; j < RMAX; ++j) {
+        const int i = tid + j * BLOCK;
+        if (i < n0) {
+          const uint32_t p = Hits<FMT>::pix(h0[j]);
+          atomicOr(&Hbm[p >> 5], 1u << (p & 31));
+        }
+      }
+      __syncthreads();
+      nnz = bm_build_prefix<NW>(Hbm, pf, n64, wsc);
+      // A point without the duplicate-candidate flag is the only point of its pixel in this window
+      // (smg_flag_duplicates), so it stores its value; flagged points (true duplicates and a few false
+      // positives) zero the slot here and add atomically after a barrier (coo.toarray() sums duplicates).
+      bool any_dup = false;
+#pragma unroll
+      for (int j = 0; j < RMAX; ++j) {
+        const int i = tid + j * BLOCK;
+        if (i < n0) {
+          const int r = bm_rank(Hbm, pf, (int)Hits<FMT>::pix(h0[j]));
+          const bool d = Hits<FMT>::dup(h0[j]);
+          vals[r] = d ? 0.0 : Hits<FMT>::val(h0[j]);
+          any_dup |= d;
+        }
+      }
+      if (any_dup) ctr[C_PDUP] = 1;
+      __syncthreads();
+      if (ctr[C_PDUP]) {
+#pragma unroll
+        for (int j = 0; j < RMAX; ++j) {
+          const int i = tid + j * BLOCK;
+          if (i < n0 && Hits<FMT>::dup(h0[j]))
+            atomicAdd(&vals[bm_rank(Hbm, pf, (int)Hits<FMT>::pix(h0[j]))], Hits<FMT>::val(h0[j]));
         }
       }
     }
-  } else {
-    for (int r = tid; r < nnz; r += BLOCK) vals[r] = (VT)0;
+    if (tid == 0) ctr[C_NEXT] = (int)sched_resolve<SRC>(S, ticket);
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < RMAX; ++j) {
-      const int i = tid + j * BLOCK;
-      if (i < n0) atomicAdd(&vals[bm_rank(Hbm, pf, (int)hp[j])], Hits<FMT>::val(h0[j]));
-    }
-  }
-  if (ka < K) {
-    kb = ka;
-    bb = ba + CH;
-    skip_empty(kb, bb);
-    if (kb < K) load_chunk(kb, bb, rb);
-  }
-  __syncthreads();
-  if (ctr[C_ABORT]) {  // more duplicate pixels than the side table holds
-    if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
-    return;
-  }
-  auto value_at = [&](int r) -> double {
-    if constexpr (SIDE_TABLE) {
-      if ((dupb[r >> 5] >> (r & 31)) & 1u) return side_v[tbl_find<SIDE>(side_k, (uint32_t)r)];
-    }
-    return (double)vals[r];
-  };
-  STAMP(1);
+    const int64_t npos = uni(ctr[C_NEXT]);
+    uint32_t dword = 0;
+    if (npos >= 0 && tid < DESC_WORDS) dword = reinterpret_cast<const uint32_t*>(desc + npos)[tid];
+    STAMP(1);
 
-  // ---- phase 2: fused principal-image statistics, then level index per pixel -------------------
-  double sx, sxx, s0, npos, vmax;
-  {
-    double acc[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
-    for (int r = tid; r < nnz; r += BLOCK) {
-      const double v = value_at(r);
-      acc[0] += v;
-      acc[1] += v * v;
-      if (v > 0.0) {
-        acc[2] += v;
-        acc[3] += 1.0;
-      }
-      acc[4] = v > acc[4] ? v : acc[4];
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = wave_sum_dpp(acc[q]);
-    acc[4] = wave_max_dpp(acc[4]);
-    if (lane == 0) {
-#pragma unroll
-      for (int q = 0; q < 5; ++q) red[q * NW + wid] = acc[q];
-    }
-    __syncthreads();
-    double t[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) t[q] += red[q * NW + w];
-      t[4] = red[4 * NW + w] > t[4] ? red[4 * NW + w] : t[4];
-    }
-    sx = t[0];
-    sxx = t[1];
-    s0 = t[2];
-    npos = t[3];
-    vmax = t[4];
-  }
-#ifndef SMG_ABL
-#define SMG_ABL 0  // diagnostic ablations (timing only, wrong results): 1 = no chaos, 2 = no windows k >= 1
-#endif
-  const bool chaos_ok = (sx > 0.0) && (npos >= 4.0) && !(SMG_ABL & 1);
-  if (chaos_ok) {
-    for (int r = tid; r < nnz; r += BLOCK) Lv[r] = (uint8_t)level_fast(value_at(r), vmax, P);
-  }
-  STAMP(2);
-
-  // ---- phase 5: other isotope windows in one streaming pass, joined against the principal image -----
-  // Chunks of BLOCK*RC points walk windows 1..K-1 in order with the next chunk prefetched into the other
-  // register buffer; there is no barrier between windows.  Per-window partial sums are reduced per wave at
-  // the window's last chunk.  A point whose duplicate-candidate flag is set (smg_flag_duplicates: it has a
-  // same-spectrum neighbour within a window width) goes to the pixel-keyed f64 table so that duplicate
-  // pixels are summed before squaring (sum y^2 over pixels); every other point contributes v^2 directly.
-  {
-    double psk = 0.0, psy = 0.0, psyy = 0.0, psxy = 0.0;
-    auto flush = [&](int k) {
-      const double a0 = wave_sum_dpp(psk), a1 = wave_sum_dpp(psy), a2 = wave_sum_dpp(psyy), a3 = wave_sum_dpp(psxy);
-      if (lane == 0) {
-        double* pk = part + ((size_t)k * NW + wid) * 4;
-        pk[0] = a0;
-        pk[1] = a1;
-        pk[2] = a2;
-        pk[3] = a3;
-      }
-      psk = psy = psyy = psxy = 0.0;
-    };
-    auto process = [&](int k, int64_t base, Reg (&buf)[RC]) {
-      const int64_t n = hi[w0 + k] - lo[w0 + k];
-      const int rem = (int)min<int64_t>(n - base, (int64_t)BLOCK * RC);
-#pragma unroll
-      for (int j = 0; j < RC; ++j) {
-        if (tid + j * BLOCK < rem) {
-          const uint32_t p = Hits<FMT>::pix(buf[j]);
-          const double v = Hits<FMT>::val(buf[j]);
-          double x = 0.0;
-          if (bm_test(Hbm, (int)p)) x = value_at(bm_rank(Hbm, pf, (int)p));
-          psy += v;
-          psxy += x * v;
-          if (x > 0.0) psk += v;
-          if (!Hits<FMT>::dup(buf[j])) {
-            psyy += v * v;
-          } else if (!tbl_add<TBL>(tkey, tval, (p << 3) | (uint32_t)k, v)) {
-            ctr[C_ABORT] = 1;
-          }
-        }
-      }
-      if (base + (int64_t)BLOCK * RC >= n) flush(k);  // last chunk of window k
-    };
-    // windows 1..K-1 with zero points still need their (zero) partials
-    for (int k = 1; k < K; ++k)
-      if (hi[w0 + k] <= lo[w0 + k] && lane == 0) {
-        double* pk = part + ((size_t)k * NW + wid) * 4;
-        pk[0] = pk[1] = pk[2] = pk[3] = 0.0;
-      }
-    // ra holds chunk A, rb chunk B (when they exist); each buffer is refilled as soon as it is consumed
-    while (ka < K && !(SMG_ABL & 2)) {
-      process(ka, ba, ra);
-      if (kb >= K) break;
-      ka = kb;
-      ba = bb + CH;
-      skip_empty(ka, ba);
-      if (ka < K) load_chunk(ka, ba, ra);
-      process(kb, bb, rb);
-      if (ka >= K) break;
-      kb = ka;
-      bb = ba + CH;
-      skip_empty(kb, bb);
-      if (kb < K) load_chunk(kb, bb, rb);
-    }
-  }
-  __syncthreads();
-  if (ctr[C_ABORT]) {  // duplicate-candidate table full
-    if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
-    return;
-  }
-  // drain the duplicate-candidate table: exact per-(pixel, window) sums, squared, into per-wave partials
-  {
-    double dq[MAXK];
-#pragma unroll
-    for (int k = 0; k < MAXK; ++k) dq[k] = 0.0;
-    for (int sl = tid; sl < TBL; sl += BLOCK) {
-      const uint32_t key = tkey[sl];
-      if (key != 0xFFFFFFFFu) {
-        const double y = tval[sl];
-        const int k = (int)(key & 7u);
-#pragma unroll
-        for (int kk = 1; kk < MAXK; ++kk)
-          if (kk == k) dq[kk] += y * y;
-      }
-    }
-#pragma unroll
-    for (int kk = 1; kk < MAXK; ++kk) {
-      if (kk < K) {
-        const double t = wave_sum_dpp(dq[kk]);
-        if (lane == 0) part[((size_t)kk * NW + wid) * 4 + 2] += t;
-      }
-    }
-  }
-  STAMP(3);
-
-  // ---- phase 4a: chaos candidates (pixels with eL >= 1) from owned principal pixels --------------
-  // (i) bit-level screen: a candidate p in cross(s) survives if its 3x3 box is covered by the
-  //     dilated bitmap (superset of the exact condition) and s is its owner (smallest principal pixel
-  //     of cross(p)); survivors go to an LDS list (the value region is free once L is computed).
-  // (ii) exact eL for the survivors from the level indices.
-  double chaos_raw = NAN;
-  if (chaos_ok) {
-    __syncthreads();  // values and the duplicate table are dead: the table region takes the owned list
-    // compact the owned principal pixels (one per distinct pixel) into a dense list so that every lane of
-    // the screen below has a pixel: the register slots are only ~half owned
-    uint32_t* olist = filtA;
+    // ---- phase 2: fused principal-image statistics, then level index per pixel -------------------
+    double sx = 0.0, sxx = 0.0, s0 = 0.0, npx_pos = 0.0, vmax = 0.0;
     {
-      const int cnt = __popc(own);
-      const int inc = wave_incl_scan_dpp(cnt);
-      int wbase = 0;
-      if (lane == 63) wbase = atomicAdd(&ctr[C_NOWN], inc);
-      int pos = __builtin_amdgcn_readlane(wbase, 63) + inc - cnt;
-#pragma unroll
-      for (int j = 0; j < RMAX; ++j)
-        if ((own >> j) & 1u) olist[pos++] = hp[j];
-    }
-    __syncthreads();
-    for (int oc_i = tid; oc_i < nnz; oc_i += BLOCK) {
-      const int s = (int)olist[oc_i];
-      int rs, cs;
-      rowcol(s, P, rs, cs);
-      // valid-column mask of columns cs-3..cs+3
-      const int clo = 3 - cs > 0 ? 3 - cs : 0, chi = P.ncols - cs + 3 < 7 ? P.ncols - cs + 3 : 7;
-      const uint32_t cv = ((1u << chi) - 1u) & ~((1u << clo) - 1u);
-      uint32_t H[7];
-#pragma unroll
-      for (int d = 0; d < 7; ++d) H[d] = bits7(Hbm, rs - 3 + d, cs - 3, cv, P);
-      // isolation pre-filter (erosion border = background only): an eL>0 pixel in the cross of s needs
-      // another principal pixel in s's 7x7, since the 4-cross of s alone cannot cover a 3x3 box
-      if (!P.erosion_border && (H[0] | H[1] | H[2] | (H[3] & ~8u) | H[4] | H[5] | H[6]) == 0u) continue;
-      uint32_t D[7];
-      D[0] = D[6] = 0;
-#pragma unroll
-      for (int d = 1; d <= 5; ++d) {
-        const int row = rs - 3 + d;
-        const bool rv = row >= 0 && row < P.nrows;
-        uint32_t x = (H[d] | (H[d] << 1) | (H[d] >> 1) | H[d - 1] | H[d + 1]) & cv;
-        if (!rv) x = 0;
-        if (P.erosion_border) x |= rv ? (~cv & 0x7Fu) : 0x7Fu;
-        D[d] = x & 0x7Fu;
-      }
-#define SMG_HB(dr, dc) ((H[3 + (dr)] >> (3 + (dc))) & 1u)
-#define SMG_BOX(dr, dc) ((((D[2 + (dr)] >> (2 + (dc))) & 7u) == 7u) && (((D[3 + (dr)] >> (2 + (dc))) & 7u) == 7u) && \
-                         (((D[4 + (dr)] >> (2 + (dc))) & 7u) == 7u))
-      const bool in_l = cs > 0, in_r = cs + 1 < P.ncols, in_u = rs > 0, in_d = rs + 1 < P.nrows;
-      uint32_t pass = 0;
-      if (SMG_BOX(0, 0) && !SMG_HB(-1, 0) && !SMG_HB(0, -1)) pass |= 1u;
-      if (in_r && SMG_BOX(0, 1) && !SMG_HB(-1, 1)) pass |= 2u;
-      if (in_l && SMG_BOX(0, -1) && !SMG_HB(-1, -1) && !SMG_HB(0, -2) && !SMG_HB(0, -1)) pass |= 4u;
-      if (in_u && SMG_BOX(-1, 0) && !SMG_HB(-2, 0) && !SMG_HB(-1, -1) && !SMG_HB(-1, 0) && !SMG_HB(-1, 1))
-        pass |= 8u;
-      if (in_d && SMG_BOX(1, 0)) pass |= 16u;
-#undef SMG_BOX
-#undef SMG_HB
-      while (pass) {
-        const int ci = __ffs(pass) - 1;
-        pass &= pass - 1;
-        const int p = s + (ci == 1 ? 1 : ci == 2 ? -1 : ci == 3 ? -P.ncols : ci == 4 ? P.ncols : 0);
-        const int idx = atomicAdd(&ctr[C_NE], 1);
-        if (idx < cap) epix[idx] = (uint32_t)p;
-      }
-    }
-    __syncthreads();
-    STAMP(4);
-    const int ncand = ctr[C_NE];
-    if (ncand > cap) {
-      if (tid == 0) dense_list[atomicAdd(dense_count, 1u)] = (uint32_t)ion;
-      return;
-    }
-    // (ii) exact eL(p) = min_{q in N9(p)} max_{q' in N4[q] in image} L(q')
-    int emax_local = 0;
-    for (int c = tid; c < ncand; c += BLOCK) {
-      const int p = (int)epix[c];
-      int rp, cp;
-      rowcol(p, P, rp, cp);
-      int mn = 1 << 20;
-      for (int qa = -1; qa <= 1; ++qa) {
-        for (int qb = -1; qb <= 1; ++qb) {
-          const int rq = rp + qa, cq = cp + qb;
-          if (rq < 0 || rq >= P.nrows || cq < 0 || cq >= P.ncols) {
-            if (!P.erosion_border) mn = 0;
-            continue;
+      double acc[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
+      if (!skip) {
+        for (int r = tid; r < nnz; r += BLOCK) {
+          const double v = vals[r];
+          acc[0] += v;
+          acc[1] += v * v;
+          if (v > 0.0) {
+            acc[2] += v;
+            acc[3] += 1.0;
           }
-          int dl = 0;
-          for (int t = 0; t < 5; ++t) {
-            const int r2 = rq + (t == 1 ? -1 : t == 2 ? 1 : 0);
-            const int c2 = cq + (t == 3 ? -1 : t == 4 ? 1 : 0);
-            if (r2 < 0 || r2 >= P.nrows || c2 < 0 || c2 >= P.ncols) continue;
-            const int q = r2 * P.ncols + c2;
-            if (bm_test(Hbm, q)) dl = max(dl, (int)Lv[bm_rank(Hbm, pf, q)]);
-          }
-          mn = min(mn, dl);
+          acc[4] = v > acc[4] ? v : acc[4];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = wave_sum_dpp(acc[q]);
+        acc[4] = wave_max_dpp(acc[4]);
+        if (lane == 0) {
+#pragma unroll
+          for (int q = 0; q < 5; ++q) red[q * NW + wid] = acc[q];
         }
       }
-      if (mn >= (1 << 20)) mn = 0;
-      eL8[c] = (uint8_t)mn;
-      emax_local = max(emax_local, mn);
-    }
-    if (emax_local > 0) atomicMax(&ctr[C_EMAX], emax_local);
-    __syncthreads();
-    STAMP(5);
-
-    // ---- phase 4b: Kruskal over eL (levels descending) with an LDS union-find -------------------
-    double sum_c = 0.0;
-    if (ctr[C_EMAX] > 0) {
-      uint4* z = reinterpret_cast<uint4*>(Hbm);
-      for (int i = tid; i < LL.w32 / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);  // guard stays zero
+      if (npos >= 0 && tid < DESC_WORDS) reinterpret_cast<uint32_t*>(DN)[tid] = dword;
       __syncthreads();
-      for (int i = tid; i < ncand; i += BLOCK)
-        if (eL8[i]) atomicOr(&Hbm[epix[i] >> 5], 1u << (epix[i] & 31));
-      __syncthreads();
-      const int m = bm_build_prefix<NW>(Hbm, pf, n64, wsc);
-      for (int i = tid; i < ncand; i += BLOCK) {
-        if (!eL8[i]) continue;
-        const uint32_t p = epix[i];
-        const int r = bm_rank(Hbm, pf, (int)p);
-        epix_r[r] = p;
-        eLr[r] = eL8[i];
+      if (!skip) {
+        double t[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) t[q] += red[q * NW + w];
+          t[4] = red[4 * NW + w] > t[4] ? red[4 * NW + w] : t[4];
+        }
+        sx = t[0];
+        sxx = t[1];
+        s0 = t[2];
+        npx_pos = t[3];
+        vmax = t[4];
       }
-      __syncthreads();
-      for (int r = tid; r < m; r += BLOCK) par[r] = (uint32_t)r;
-      __syncthreads();
-      const int emax = ctr[C_EMAX];
-      double wsum = 0.0, esum = 0.0;
-      for (int r = tid; r < m; r += BLOCK) esum += (double)eLr[r];
-      for (int t = emax; t >= 1; --t) {
-        for (int r = tid; r < m; r += BLOCK) {
-          const int e = eLr[r];
-          if (e < t) continue;
-          const int p = (int)epix_r[r];
-          int rp, cp;
-          rowcol(p, P, rp, cp);
-          auto edge = [&](int q) {
-            if (!bm_test(Hbm, q)) return;
-            const int rq = bm_rank(Hbm, pf, q);
-            const int eq = eLr[rq];
-            if ((e < eq ? e : eq) == t) {
-              if (uf_unite(par, (uint32_t)r, (uint32_t)rq)) wsum += (double)t;
+    }
+#ifndef SMG_ABL
+#define SMG_ABL 0  // diagnostic ablations (timing only, wrong results): 1 = no chaos, 2 = no tail windows,
+                   // 4 = tail chunk 0 only, 8 = no duplicate deferral, 16 = no principal lookups in the tail
+#endif
+    const bool chaos_ok = !skip && (sx > 0.0) && (npx_pos >= 4.0) && !(SMG_ABL & 1);
+    if (chaos_ok) {
+      for (int r = tid; r < nnz; r += BLOCK) Lv[r] = (uint8_t)level_fast(vals[r], vmax, P);
+    }
+    STAMP(2);
+
+    // ---- phase 5: tail windows, one stream of window-aligned 64-point groups -------------------------
+    if (!skip && !(SMG_ABL & 2)) {
+      const int ng = uni(D->ngroups);
+      double psk = 0.0, psy = 0.0, psyy = 0.0, psxy = 0.0;
+      int curk = 1;
+      int nd = 0;  // this wave's deferred duplicate candidates (uniform)
+      uint32_t* wdkey = dkey + wid * DSEG;
+      double* wdval = dval + wid * DSEG;
+      int gnext = uni(D->gs[2]);
+      int wend = uni(D->end[1]);
+      auto flush = [&]() {
+        const double a0 = wave_sum_dpp(psk), a1 = wave_sum_dpp(psy), a2 = wave_sum_dpp(psyy),
+                     a3 = wave_sum_dpp(psxy);
+        if (lane == 0) {
+          double* pk = part + ((size_t)curk * NW + wid) * 4;
+          pk[0] = a0;
+          pk[1] = a1;
+          pk[2] = a2;
+          pk[3] = a3;
+        }
+        psk = psy = psyy = psxy = 0.0;
+      };
+      auto process = [&](int c, Reg (&buf)[RC]) {
+#pragma unroll
+        for (int j = 0; j < RC; ++j) {
+          const int G = c * GPC + j * NW + wid;
+          if (G < ng) {
+            while (G >= gnext) {  // this wave moves on to a later window (uniform)
+              flush();
+              ++curk;
+              gnext = curk + 1 < MAXK ? uni(D->gs[curk + 1]) : 0x7FFFFFFF;
+              wend = uni(D->end[curk]);
             }
-          };
-          if (cp + 1 < P.ncols) edge(p + 1);
-          if (rp + 1 < P.nrows) {
-            edge(p + P.ncols);
-            if (P.connectivity == 8) {
-              if (cp > 0) edge(p + P.ncols - 1);
-              if (cp + 1 < P.ncols) edge(p + P.ncols + 1);
+            const bool valid = G * 64 + lane < wend;
+            const uint32_t p = Hits<FMT>::pix(buf[j]);
+            const double v = valid ? Hits<FMT>::val(buf[j]) : 0.0;
+            const bool dup = valid && Hits<FMT>::dup(buf[j]) && !(SMG_ABL & 8);
+            if (valid) {
+              const double x = (SMG_ABL & 16) ? 0.0 : bm_test(Hbm, (int)p) ? vals[bm_rank(Hbm, pf, (int)p)] : 0.0;
+              psy += v;
+              psxy += x * v;
+              if (x > 0.0) psk += v;
+              if (!dup) psyy += v * v;
+            }
+            // duplicate candidates are summed per (pixel, window) before squaring: appended to this wave's
+            // list segment (ballot compaction, no atomics)
+            const uint64_t dm = __ballot(dup);
+            if (dm) {
+              const int e = nd + (int)__popcll(dm & ((1ull << lane) - 1ull));
+              if (dup && e < DSEG) {
+                wdkey[e] = (p << 3) | (uint32_t)curk;
+                wdval[e] = v;
+              }
+              nd += (int)__popcll(dm);
             }
           }
+        }
+      };
+      // chunks 0 and 1 are in flight (issued during the previous iteration); later chunks one ahead
+      for (int c = 0; c * GPC < ng; c += 2) {
+        process(c, ra);
+        if ((SMG_ABL & 4) && c >= 0) break;
+        if ((c + 2) * GPC < ng) issue_chunk(D, c + 2, ra);
+        if ((c + 1) * GPC >= ng) break;
+        process(c + 1, rb);
+        if ((c + 3) * GPC < ng) issue_chunk(D, c + 3, rb);
+      }
+      flush();
+      if (lane == 0) dcnt[wid] = nd;
+    } else if (!skip && tid < NW) {
+      dcnt[tid] = 0;
+    }
+    // ---- the registers of ion b are dead: ion b+1's principal window and first two chunks go in flight
+    if (npos >= 0 && desc_lds_ok(DN, CAPC)) {
+      issue_principal(DN, h0);
+      issue_chunk(DN, 0, ra);
+      issue_chunk(DN, 1, rb);
+    }
+    __syncthreads();
+    // ---- deferred duplicate candidates: exact per-(pixel, window) sums, squared into the partials --------
+    // Thread t owns list slot t (segment t / DSEG, entry t % DSEG); the entries are summed per key in an LDS
+    // table and each key's square goes to its window's partial (LDS f64 atomics: the few keys per ion make
+    // the order of these additions immaterial at f64 precision).
+    if (!skip) {
+      int nd_tot = 0, nd_max = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        nd_tot += dcnt[w];
+        nd_max = max(nd_max, dcnt[w]);
+      }
+      if (nd_max > DSEG) {
+        reject();
+        skip = true;
+      } else if (nd_tot > 0) {
+        static_assert(NW * DSEG == BLOCK, "one list slot per thread");
+        for (int i = tid; i < DTBL; i += BLOCK) {
+          tkey[i] = 0xFFFFFFFFu;
+          tval[i] = 0.0;
         }
         __syncthreads();
+        if ((tid % DSEG) < dcnt[tid / DSEG] && !tbl_add<DTBL>(tkey, tval, dkey[tid], dval[tid])) ctr[C_ABORT] = 1;
+        __syncthreads();
+        if (ctr[C_ABORT]) {
+          reject();
+          skip = true;
+        } else {
+          for (int i = tid; i < DTBL; i += BLOCK) {
+            const uint32_t key = tkey[i];
+            if (key != 0xFFFFFFFFu) {
+              const double y = tval[i];
+              atomicAdd(&part[(size_t)(key & 7u) * NW * 4 + 2], y * y);
+            }
+          }
+          __syncthreads();
+        }
       }
-      double acc[2] = {esum, wsum};
-      block_sum<BLOCK, 2, true>(acc, red);
-      sum_c = acc[0] - acc[1];
     }
-    chaos_raw = 1.0 - sum_c / (double)P.nlevels / npos;
-    STAMP(6);
-  } else {
-    flags |= SMG_ION_CHAOS_NAN;
-  }
+    STAMP(3);
 
-  if (tid == 0) {
-    // s, sy, syy, sxy per window from the per-wave partials (wave order: deterministic)
-    double* st = red;  // reuse: [4][MAXK]
-    for (int k = 0; k < K; ++k) {
-      double a4[4] = {0.0, 0.0, 0.0, 0.0};
-      if (k > 0) {
-        for (int w = 0; w < NW; ++w)
-          for (int q = 0; q < 4; ++q) a4[q] += part[((size_t)k * NW + w) * 4 + q];
-      } else {
-        a4[0] = s0;
+    // ---- phase 4a: chaos candidates (pixels with eL >= 1) from the principal pixels -----------------
+    // (i) bit-level screen: a candidate p in cross(s) survives if its 3x3 box is covered by the
+    //     dilated bitmap (superset of the exact condition) and s is its owner (smallest principal pixel
+    //     of cross(p)); survivors go to an LDS list (the value region is free once L is computed).
+    // (ii) exact eL for the survivors from the level indices.
+    double chaos_raw = NAN;
+    uint32_t flags = 0;
+    if (!skip && chaos_ok) {
+      // the distinct principal pixels in rank order (olist[pf[w] + i] = i-th set bit of word w)
+      uint32_t* olist = filtA;
+      {
+        const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(Hbm);
+        for (int w = tid; w < n64; w += BLOCK) {
+          uint64_t bits = bm64[w];
+          if (!bits) continue;
+          int r = pf[w];
+          while (bits) {
+            olist[r++] = (uint32_t)(w * 64 + __builtin_ctzll(bits));
+            bits &= bits - 1;
+          }
+        }
       }
-      for (int q = 0; q < 4; ++q) st[q * MAXK + k] = a4[q];
+      __syncthreads();
+      for (int oc_i = tid; oc_i < nnz; oc_i += BLOCK) {
+        const int s = (int)olist[oc_i];
+        int rs, cs;
+        rowcol(s, P, rs, cs);
+        // valid-column mask of columns cs-3..cs+3
+        const int clo = 3 - cs > 0 ? 3 - cs : 0, chi = P.ncols - cs + 3 < 7 ? P.ncols - cs + 3 : 7;
+        const uint32_t cv = ((1u << chi) - 1u) & ~((1u << clo) - 1u);
+        uint32_t H[7];
+#pragma unroll
+        for (int d = 0; d < 7; ++d) H[d] = bits7(Hbm, rs - 3 + d, cs - 3, cv, P);
+        // isolation pre-filter (erosion border = background only): an eL>0 pixel in the cross of s needs
+        // another principal pixel in s's 7x7, since the 4-cross of s alone cannot cover a 3x3 box
+        if (!P.erosion_border && (H[0] | H[1] | H[2] | (H[3] & ~8u) | H[4] | H[5] | H[6]) == 0u) continue;
+        uint32_t Dl[7];
+        Dl[0] = Dl[6] = 0;
+#pragma unroll
+        for (int d = 1; d <= 5; ++d) {
+          const int row = rs - 3 + d;
+          const bool rv = row >= 0 && row < P.nrows;
+          uint32_t x = (H[d] | (H[d] << 1) | (H[d] >> 1) | H[d - 1] | H[d + 1]) & cv;
+          if (!rv) x = 0;
+          if (P.erosion_border) x |= rv ? (~cv & 0x7Fu) : 0x7Fu;
+          Dl[d] = x & 0x7Fu;
+        }
+#define SMG_HB(dr, dc) ((H[3 + (dr)] >> (3 + (dc))) & 1u)
+#define SMG_BOX(dr, dc) ((((Dl[2 + (dr)] >> (2 + (dc))) & 7u) == 7u) && (((Dl[3 + (dr)] >> (2 + (dc))) & 7u) == 7u) && \
+                         (((Dl[4 + (dr)] >> (2 + (dc))) & 7u) == 7u))
+        const bool in_l = cs > 0, in_r = cs + 1 < P.ncols, in_u = rs > 0, in_d = rs + 1 < P.nrows;
+        uint32_t pass = 0;
+        if (SMG_BOX(0, 0) && !SMG_HB(-1, 0) && !SMG_HB(0, -1)) pass |= 1u;
+        if (in_r && SMG_BOX(0, 1) && !SMG_HB(-1, 1)) pass |= 2u;
+        if (in_l && SMG_BOX(0, -1) && !SMG_HB(-1, -1) && !SMG_HB(0, -2) && !SMG_HB(0, -1)) pass |= 4u;
+        if (in_u && SMG_BOX(-1, 0) && !SMG_HB(-2, 0) && !SMG_HB(-1, -1) && !SMG_HB(-1, 0) && !SMG_HB(-1, 1))
+          pass |= 8u;
+        if (in_d && SMG_BOX(1, 0)) pass |= 16u;
+#undef SMG_BOX
+#undef SMG_HB
+        while (pass) {
+          const int ci = __ffs(pass) - 1;
+          pass &= pass - 1;
+          const int p = s + (ci == 1 ? 1 : ci == 2 ? -1 : ci == 3 ? -P.ncols : ci == 4 ? P.ncols : 0);
+          const int idx = atomicAdd(&ctr[C_NE], 1);
+          if (idx < CAPC) epix[idx] = (uint32_t)p;
+        }
+      }
+      __syncthreads();
+      STAMP(4);
+      const int ncand = ctr[C_NE];
+      if (ncand > CAPC) {
+        reject();
+        skip = true;
+      }
+      if (!skip) {
+        // (ii) exact eL(p) = min_{q in N9(p)} max_{q' in N4[q] in image} L(q')
+        int emax_local = 0;
+        for (int c = tid; c < ncand; c += BLOCK) {
+          const int p = (int)epix[c];
+          int rp, cp;
+          rowcol(p, P, rp, cp);
+          int mn = 1 << 20;
+#pragma unroll 1
+          for (int qa = -1; qa <= 1; ++qa) {
+#pragma unroll 1
+            for (int qb = -1; qb <= 1; ++qb) {
+              const int rq = rp + qa, cq = cp + qb;
+              if (rq < 0 || rq >= P.nrows || cq < 0 || cq >= P.ncols) {
+                if (!P.erosion_border) mn = 0;
+                continue;
+              }
+              int dl = 0;
+#pragma unroll
+              for (int t = 0; t < 5; ++t) {
+                const int r2 = rq + (t == 1 ? -1 : t == 2 ? 1 : 0);
+                const int c2 = cq + (t == 3 ? -1 : t == 4 ? 1 : 0);
+                if (r2 < 0 || r2 >= P.nrows || c2 < 0 || c2 >= P.ncols) continue;
+                const int q = r2 * P.ncols + c2;
+                if (bm_test(Hbm, q)) dl = max(dl, (int)Lv[bm_rank(Hbm, pf, q)]);
+              }
+              mn = min(mn, dl);
+            }
+          }
+          if (mn >= (1 << 20)) mn = 0;
+          eL8[c] = (uint8_t)mn;
+          emax_local = max(emax_local, mn);
+        }
+        if (emax_local > 0) atomicMax(&ctr[C_EMAX], emax_local);
+        __syncthreads();
+        STAMP(5);
+
+        // ---- phase 4b: Kruskal over eL (levels descending) with an LDS union-find -------------------
+        double sum_c = 0.0;
+        if (ctr[C_EMAX] > 0) {
+          uint4* z = reinterpret_cast<uint4*>(Hbm);
+          for (int i = tid; i < P.w32 / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);  // guard stays zero
+          __syncthreads();
+          for (int i = tid; i < ncand; i += BLOCK)
+            if (eL8[i]) atomicOr(&Hbm[epix[i] >> 5], 1u << (epix[i] & 31));
+          __syncthreads();
+          const int m = bm_build_prefix<NW>(Hbm, pf, n64, wsc);
+          for (int i = tid; i < ncand; i += BLOCK) {
+            if (!eL8[i]) continue;
+            const uint32_t p = epix[i];
+            const int r = bm_rank(Hbm, pf, (int)p);
+            epix_r[r] = p;
+            eLr[r] = eL8[i];
+          }
+          __syncthreads();
+          for (int r = tid; r < m; r += BLOCK) par[r] = (uint32_t)r;
+          __syncthreads();
+          const int emax = ctr[C_EMAX];
+          double wsum = 0.0, esum = 0.0;
+          for (int r = tid; r < m; r += BLOCK) esum += (double)eLr[r];
+          for (int t = emax; t >= 1; --t) {
+            for (int r = tid; r < m; r += BLOCK) {
+              const int e = eLr[r];
+              if (e < t) continue;
+              const int p = (int)epix_r[r];
+              int rp, cp;
+              rowcol(p, P, rp, cp);
+              auto edge = [&](int q) {
+                if (!bm_test(Hbm, q)) return;
+                const int rq = bm_rank(Hbm, pf, q);
+                const int eq = eLr[rq];
+                if ((e < eq ? e : eq) == t) {
+                  if (uf_unite(par, (uint32_t)r, (uint32_t)rq)) wsum += (double)t;
+                }
+              };
+              if (cp + 1 < P.ncols) edge(p + 1);
+              if (rp + 1 < P.nrows) {
+                edge(p + P.ncols);
+                if (P.connectivity == 8) {
+                  if (cp > 0) edge(p + P.ncols - 1);
+                  if (cp + 1 < P.ncols) edge(p + P.ncols + 1);
+                }
+              }
+            }
+            __syncthreads();
+          }
+          double acc[2] = {esum, wsum};
+          block_sum<BLOCK, 2, true>(acc, red);
+          sum_c = acc[0] - acc[1];
+        }
+        chaos_raw = 1.0 - sum_c / (double)P.nlevels / npx_pos;
+        STAMP(6);
+      }
+    } else if (!skip) {
+      flags |= SMG_ION_CHAOS_NAN;
     }
-    finalize_ion(K, theor + w0, st, sx, sxx, st + MAXK, st + 2 * MAXK, st + 3 * MAXK, (double)P.npx, chaos_raw,
-                 ion, flags, oc, osp, osc, omsm, oflags);
+
+    // ---- finalize (formula_img_validator.py:78-84 + the restated pyImagingMSpec functions): wave 0,
+    // lane k = window k; sums over lanes in a fixed order
+    if (!skip && wid == 0) {
+      const int k = lane;
+      double s = 0.0, sy = 0.0, syy = 0.0, sxy = 0.0, t = 0.0;
+      if (k < K) {
+        t = D->theor[k];
+        if (k == 0) {
+          s = s0;
+        } else {
+#pragma unroll
+          for (int w = 0; w < NW; ++w) {
+            const double* pk = part + ((size_t)k * NW + w) * 4;
+            s += pk[0];
+            sy += pk[1];
+            syy += pk[2];
+            sxy += pk[3];
+          }
+        }
+      }
+      // isotope_pattern_match
+      const double nt = sqrt(wave_sum_dpp(t * t)), ns = sqrt(wave_sum_dpp(s * s));
+      double spectral = 1.0 - wave_sum_dpp(k < K ? fabs(t / nt - s / ns) : 0.0) / (double)K;
+      if (spectral == 1.0) spectral = 0.0;
+      // isotope_image_correlation: np.corrcoef rows, weights = theor[1:]
+      double spatial = 0.0;
+      if (K >= 2) {
+        const double npx = (double)P.npx, n1 = npx - 1.0;
+        const double sd0 = sqrt((sxx - sx * sx / npx) / n1);
+        double rt = 0.0, tw = 0.0;
+        if (k >= 1 && k < K) {
+          const double syy_c = (syy - sy * sy / npx) / n1;
+          const double sxy_c = (sxy - sx * sy / npx) / n1;
+          double r = sxy_c / sqrt(syy_c) / sd0;
+          if (!isnan(r)) r = r > 1.0 ? 1.0 : (r < -1.0 ? -1.0 : r);
+          if (isinf(r)) r = 0.0;
+          rt = r * t;
+          tw = t;
+        }
+        spatial = wave_sum_dpp(rt) / wave_sum_dpp(tw);
+      }
+      if (lane == 0) {
+        double chaos = chaos_raw;
+        if (!isnan(chaos) && fabs(chaos - 1.0) <= 1e-8 + 1e-5) chaos = 0.0;  // np.isclose(moc, 1.0)
+        chaos = clean(chaos);
+        spatial = clean(spatial);
+        spectral = clean(spectral);
+        oc[ion] = chaos;
+        osp[ion] = spatial;
+        osc[ion] = spectral;
+        omsm[ion] = chaos * spatial * spectral;
+        oflags[ion] = flags | big_flag | (uint32_t)D->hits;
+      }
+    }
+    if (npos < 0) break;
+    pos = npos;
+    cur ^= 1;
+    __syncthreads();  // the next ion re-initialises the LDS structures
+    STAMP(7);
   }
 }
 
-
-template <int FMT, int LB, int LRMAX, int LRC, int WPE>
-__global__ void __launch_bounds__(LB, WPE) ion_lds_kernel(
-    Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
-    const int64_t* __restrict__ ion_off, const double* __restrict__ theor, const int64_t* __restrict__ ion_order,
-    int64_t n_ions, Params P, LdsLayout LL, double* __restrict__ oc, double* __restrict__ osp,
-    double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags,
-    uint32_t* __restrict__ next_list, uint32_t* __restrict__ next_count) {
-  const int64_t ion = ion_order ? ion_order[blockIdx.x] : (int64_t)blockIdx.x;
-  if (ion >= n_ions) return;
-  process_ion_lds<FMT, LB, LRMAX, LRC>(ion, hits, lo, hi, ion_off, theor, P, LL, oc, osp, osc, omsm, oflags,
-                                       next_list, next_count);
+// position list -> ion list (when the big-ion pass is skipped, the dense kernel reads ion indices)
+__global__ void pos_to_ion_kernel(const IonDesc* __restrict__ desc, const uint32_t* __restrict__ in,
+                                  const uint32_t* __restrict__ count, uint32_t* __restrict__ out,
+                                  uint32_t* __restrict__ out_count) {
+  const uint32_t n = *count;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    out[i] = (uint32_t)desc[in[i]].ion;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *out_count = n;
 }
 
-// persistent variant over a device list of ions (the rejects of a smaller-geometry pass)
-template <int FMT, int LB, int LRMAX, int LRC>
-__global__ void __launch_bounds__(LB, 4) ion_lds_list_kernel(
-    Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
-    const int64_t* __restrict__ ion_off, const double* __restrict__ theor, const uint32_t* __restrict__ list,
-    const uint32_t* __restrict__ count, uint32_t* __restrict__ cursor, Params P, LdsLayout LL,
-    double* __restrict__ oc, double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm,
-    uint32_t* __restrict__ oflags, uint32_t* __restrict__ next_list, uint32_t* __restrict__ next_count) {
-  __shared__ int sh_ion;
-  const uint32_t total = *count;
-  while (true) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint32_t k = atomicAdd(cursor, 1u);
-      sh_ion = (k < total) ? (int)list[k] : -1;
-    }
-    __syncthreads();
-    const int ion = sh_ion;
-    if (ion < 0) break;
-    process_ion_lds<FMT, LB, LRMAX, LRC>(ion, hits, lo, hi, ion_off, theor, P, LL, oc, osp, osc, omsm, oflags,
-                                         next_list, next_count);
-  }
+// every position into the list (images too large for the main pass but not for the big-ion pass)
+__global__ void list_positions_kernel(uint32_t* list, uint32_t* count, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) list[i] = (uint32_t)i;
+  if (i == 0) *count = (uint32_t)n;
 }
+
+
 
 // ---------------------------------------------------------------------------------------------
 // dense path: persistent workgroups, one global scratch slot each
@@ -1209,11 +1328,14 @@ __global__ void list_all_kernel(uint32_t* list, uint32_t* count, const int64_t* 
 }
 
 static constexpr int DENSE_SLOTS = 256;
-static constexpr size_t WS_HEADER = 256;
+// workspace: header (pass counters at word 0.., per-XCD range counters at word 64..), two ion lists,
+// the ion descriptors, dense scratch slots
+static constexpr size_t WS_HEADER = 2048;
+static constexpr int HDR_XCD = 64;
 // LDS-path geometries: the main pass (two 512-thread workgroups per CU) and the big-ion pass over its
 // rejects (one 1024-thread workgroup per CU with the whole LDS)
 #ifndef SMG_MAIN_CFG
-#define SMG_MAIN_CFG 512, 8, 4, 4
+#define SMG_MAIN_CFG 512, 5, 3, 4
 #endif
 // main LDS pass: threads, principal points per thread, chunk points per thread, min waves per SIMD
 static constexpr int MAIN_CFG[4] = {SMG_MAIN_CFG};
@@ -1223,47 +1345,76 @@ static constexpr int BIG_BLOCK = 1024, BIG_RMAX = 8, BIG_RC = 4;
 static constexpr size_t MAIN_LDS = 80 * 1024, BIG_LDS = 160 * 1024 - 512;
 
 static size_t ws_bytes_for(int64_t n_ions, int npx) {
-  return WS_HEADER + 2 * al16((size_t)n_ions * 4) + (size_t)DENSE_SLOTS * dense_slot_bytes(npx);
+  return WS_HEADER + 2 * al16((size_t)n_ions * 4) + (size_t)n_ions * sizeof(IonDesc) +
+         (size_t)DENSE_SLOTS * dense_slot_bytes(npx);
 }
 
-static LdsLayout main_layout(int npx, int vb) { return lds_layout(npx, vb, MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX, MAIN_LDS); }
-static LdsLayout big_layout(int npx, int vb) { return lds_layout(npx, vb, BIG_BLOCK / WAVE, BIG_BLOCK * BIG_RMAX, BIG_LDS); }
+using MainLay = Lay<MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX>;
+using BigLay = Lay<BIG_BLOCK / WAVE, BIG_BLOCK * BIG_RMAX>;
+
+static int device_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                              hipSuccess || cus <= 0)
+    cus = 256;
+  return cus;
+}
 
 template <int FMT>
 static int launch_metrics(Hits<FMT> hits, const int64_t* lo, const int64_t* hi, const int64_t* ion_off,
                           const double* theor, const int64_t* ion_order, int64_t n_ions, const Params& P,
                           double* oc, double* osp, double* osc, double* omsm, uint32_t* oflags,
                           unsigned char* ws, hipStream_t st) {
-  // header: [0] count A, [1] cursor A, [2] count B, [3] cursor B
+  // header words: [0] count A, [1] cursor A, [2] count B, [3] cursor B, [HDR_XCD + x*CTR_STRIDE] range x
   uint32_t* hdr = reinterpret_cast<uint32_t*>(ws);
   uint32_t* list_a = reinterpret_cast<uint32_t*>(ws + WS_HEADER);
   uint32_t* list_b = reinterpret_cast<uint32_t*>(ws + WS_HEADER + al16((size_t)n_ions * 4));
-  unsigned char* slots = ws + WS_HEADER + 2 * al16((size_t)n_ions * 4);
+  IonDesc* desc = reinterpret_cast<IonDesc*>(ws + WS_HEADER + 2 * al16((size_t)n_ions * 4));
+  unsigned char* slots = reinterpret_cast<unsigned char*>(desc) + (size_t)n_ions * sizeof(IonDesc);
   const size_t slot_bytes = dense_slot_bytes(P.npx);
   SMG_HIP(hipMemsetAsync(ws, 0, WS_HEADER, st));
-  const int vb = FMT == SMG_HITS_PACKED_F32 ? 4 : 8;
-  LdsLayout LM = main_layout(P.npx, vb);
-  LdsLayout LB = big_layout(P.npx, vb);
-  const bool lds_ok = P.npx <= NPX_LDS_MAX && LM.cap >= 256;
-  if (lds_ok) {
-    auto k1 = &ion_lds_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE>;
-    SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k1), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)LM.bytes));
-    hipLaunchKernelGGL(k1, dim3((unsigned)n_ions), dim3(MAIN_BLOCK), LM.bytes, st, hits, lo, hi, ion_off, theor,
-                       ion_order, n_ions, P, LM, oc, osp, osc, omsm, oflags, list_a, hdr + 0);
+  Params PM = P, PB = P;
+  PM.w32 = MainLay::w32(P.npx);
+  PM.o_pf = MainLay::o_pf(P.npx);
+  PB.w32 = BigLay::w32(P.npx);
+  PB.o_pf = BigLay::o_pf(P.npx);
+  const size_t lds_main = MainLay::bytes(P.npx), lds_big = BigLay::bytes(P.npx);
+  const bool main_ok = P.npx <= NPX_LDS_MAX && lds_main <= MAIN_LDS;
+  const bool big_ok = P.npx <= NPX_LDS_MAX && lds_big <= BIG_LDS;
+  const int cus = device_cus();
+  if (main_ok || big_ok) {
+    hipLaunchKernelGGL(ion_desc_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, lo, hi, ion_off,
+                       theor, ion_order, n_ions, desc);
     SMG_LAUNCH_CHECK();
-    if (LB.cap > LM.cap) {
-      auto k2 = &ion_lds_list_kernel<FMT, BIG_BLOCK, BIG_RMAX, BIG_RC>;
-      SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k2), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)LB.bytes));
-      const int nwg = (int)(n_ions < 256 ? n_ions : 256);
-      hipLaunchKernelGGL(k2, dim3((unsigned)nwg), dim3(BIG_BLOCK), LB.bytes, st, hits, lo, hi, ion_off, theor,
-                         list_a, hdr + 0, hdr + 1, P, LB, oc, osp, osc, omsm, oflags, list_b, hdr + 2);
-      SMG_LAUNCH_CHECK();
-    } else {
-      SMG_HIP(hipMemcpyAsync(list_b, list_a, (size_t)n_ions * 4, hipMemcpyDeviceToDevice, st));
-      SMG_HIP(hipMemcpyAsync(hdr + 2, hdr + 0, 4, hipMemcpyDeviceToDevice, st));
-    }
+  }
+  if (main_ok) {
+    Sched SA{n_ions, hdr + HDR_XCD, nullptr, nullptr};
+    auto k1 = &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES>;
+    SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k1), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds_main));
+    // two resident workgroups per CU, a multiple of the XCD count
+    int64_t nwg = (int64_t)cus * 2;
+    if (nwg > n_ions) nwg = ((n_ions + XCDS - 1) / XCDS) * XCDS;
+    hipLaunchKernelGGL(k1, dim3((unsigned)nwg), dim3(MAIN_BLOCK), lds_main, st, hits, desc, SA, PM, oc, osp, osc,
+                       omsm, oflags, list_a, hdr + 0);
+    SMG_LAUNCH_CHECK();
+  } else if (big_ok) {
+    hipLaunchKernelGGL(list_positions_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, list_a,
+                       hdr + 0, n_ions);
+    SMG_LAUNCH_CHECK();
+  }
+  if (big_ok) {
+    Sched SB{0, hdr + 1, list_a, hdr + 0};
+    auto k2 = &ion_pipe_kernel<FMT, BIG_BLOCK, BIG_RMAX, BIG_RC, 1, SRC_LIST>;
+    SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k2), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds_big));
+    const int nwg2 = (int)(n_ions < cus ? n_ions : cus);
+    hipLaunchKernelGGL(k2, dim3((unsigned)nwg2), dim3(BIG_BLOCK), lds_big, st, hits, desc, SB, PB, oc, osp, osc,
+                       omsm, oflags, list_b, hdr + 2);
+    SMG_LAUNCH_CHECK();
+  } else if (main_ok) {
+    hipLaunchKernelGGL(pos_to_ion_kernel, dim3(64), dim3(256), 0, st, desc, list_a, hdr + 0, list_b, hdr + 2);
+    SMG_LAUNCH_CHECK();
   } else {
     hipLaunchKernelGGL(list_all_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, list_b, hdr + 2,
                        ion_order, n_ions);
@@ -1275,6 +1426,7 @@ static int launch_metrics(Hits<FMT> hits, const int64_t* lo, const int64_t* hi, 
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }
+
 
 }  // namespace smg
 
@@ -1338,6 +1490,8 @@ int smg_ion_metrics(int32_t hit_format, const void* hits, const double* hit_vals
   P.erosion_border = erosion_border;
   P.step = nlevels > 1 ? 1.0 / (double)(nlevels - 1) : 0.0;
   P.inv_ncols = 1.0f / (float)ncols;
+  P.w32 = 0;
+  P.o_pf = 0;
   unsigned char* ws = reinterpret_cast<unsigned char*>(workspace);
   hipStream_t st = as_stream(stream);
   if (hit_format == SMG_HITS_PACKED_F32) {
