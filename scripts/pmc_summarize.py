@@ -7,6 +7,9 @@ for r in rows:
     name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
     short = re.sub(r"\(.*", "", name)
     short = re.sub(r"<.*>", "<..>", short)
+    m = re.search(r"ion_pipe_kernel<[^,]*, (\d+)", name)
+    if m:
+        short = "smg::ion_pipe_kernel[" + m.group(1) + "]"
     if not any(k in name for k in ("smg::", "copy", "rocprim")):
         continue
     acc[(short[:60], r["Counter_Name"])].append(float(r["Counter_Value"]))

@@ -92,6 +92,7 @@ struct Hits<SMG_HITS_PACKED_F32> {
   static __device__ __forceinline__ uint32_t pix(Reg r) { return (uint32_t)r & 0x7FFFFFFFu; }
   static __device__ __forceinline__ bool dup(Reg r) { return ((uint32_t)r >> 31) != 0u; }
   static __device__ __forceinline__ double val(Reg r) { return (double)__uint_as_float((uint32_t)(r >> 32)); }
+  static __device__ __forceinline__ Reg zero() { return 0ull; }  // pixel 0, value 0, no flag
   __device__ __forceinline__ void get(int64_t i, uint32_t& p, double& v) const {
     const uint64_t x = h[i];
     p = (uint32_t)x & 0x7FFFFFFFu;
@@ -104,6 +105,27 @@ struct PixVal {
   double v;
 };
 
+// Asynchronous 8-byte loads for the software pipeline of the LDS kernel.  The compiler's wait-count pass
+// serialises any use of a register loaded before a loop or a branch behind s_waitcnt vmcnt(0), i.e. behind
+// every load issued since, which would expose the latency of each prefetched chunk; these loads are
+// invisible to it and are waited for with counted waits (vm_wait<N>: all but the N youngest vector-memory
+// operations of this wave done).  Vector-memory operations complete in issue order, so operations the
+// compiler issues in between only make a counted wait stricter.  The destination registers are neither
+// read nor copied between issue and wait (the wait takes them as in/out operands).
+__device__ __forceinline__ uint64_t ld8_async(const void* sbase, uint32_t voff) {
+  uint64_t r;
+  asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(r) : "v"(voff), "s"(sbase) : "memory");
+  return r;
+}
+template <int N, int M>
+__device__ __forceinline__ void vm_wait(uint64_t (&r)[M]) {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#pragma unroll
+  for (int j = 0; j < M; ++j) asm volatile("" : "+v"(r[j]));
+}
+template <int N, int M>
+__device__ __forceinline__ void vm_wait(PixVal (&)[M]) {}  // split-format hits use compiler-tracked loads
+
 template <>
 struct Hits<SMG_HITS_SPLIT_F64> {
   const uint32_t* pa;
@@ -114,6 +136,7 @@ struct Hits<SMG_HITS_SPLIT_F64> {
   static __device__ __forceinline__ uint32_t pix(Reg r) { return r.p & 0x7FFFFFFFu; }
   static __device__ __forceinline__ bool dup(Reg r) { return (r.p >> 31) != 0u; }
   static __device__ __forceinline__ double val(Reg r) { return r.v; }
+  static __device__ __forceinline__ Reg zero() { return PixVal{0u, 0.0}; }
   __device__ __forceinline__ void get(int64_t i, uint32_t& p, double& v) const {
     p = pa[i] & 0x7FFFFFFFu;
     v = va[i];
@@ -208,37 +231,40 @@ __device__ __forceinline__ int bm_rank(const uint32_t* bm, const uint16_t* pf, i
   return (int)pf[p >> 6] + __popcll(m);
 }
 
-// exclusive popcount prefix over the first n64 64-bit words: each wave scans a contiguous range
-// 64 words at a time (lane-parallel), then wave offsets are added.  Returns the total.
+// exclusive popcount prefix over the first n64 <= NPX_LDS_MAX/64 64-bit words: thread t scans WPT consecutive
+// words serially, thread totals are scanned across the wave (DPP) and the waves.  Returns the total.
 template <int NW_>
 __device__ int bm_build_prefix(const uint32_t* bm, uint16_t* pf, int n64, int* wscratch) {
   constexpr int NW = NW_;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int WPT = (NPX_LDS_MAX / 64) / (NW * WAVE);
+  static_assert(WPT >= 1 && WPT * NW * WAVE * 64 == NPX_LDS_MAX, "prefix geometry");
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(bm);
-  const int span = ((n64 + NW - 1) / NW + 63) & ~63;
-  const int a = wid * span;
-  const int b = min(n64, a + span);
-  int carry = 0;
-  for (int base = a; base < b; base += 64) {
-    const int j = base + lane;
-    const int c = (j < b) ? __popcll(bm64[j]) : 0;
-    const int inc = wave_incl_scan_dpp(c);
-    if (j < b) pf[j] = (uint16_t)(carry + inc - c);
-    carry += __builtin_amdgcn_readlane(inc, 63);
+  const int a = tid * WPT;
+  int c[WPT];
+  int tot = 0;
+#pragma unroll
+  for (int i = 0; i < WPT; ++i) {
+    c[i] = (a + i < n64) ? __popcll(bm64[a + i]) : 0;
+    tot += c[i];
   }
-  if (lane == 0) wscratch[wid] = carry;
+  const int inc = wave_incl_scan_dpp(tot);
+  if (lane == 63) wscratch[wid] = inc;
   __syncthreads();
-  int off = 0, tot = 0;
+  int off = inc - tot, all = 0;
+#pragma unroll
   for (int w = 0; w < NW; ++w) {
-    const int c = wscratch[w];
-    if (w < wid) off += c;
-    tot += c;
+    const int x = wscratch[w];
+    off += (w < wid) ? x : 0;
+    all += x;
   }
-  if (off) {
-    for (int j = a + lane; j < b; j += 64) pf[j] = (uint16_t)(pf[j] + off);
+#pragma unroll
+  for (int i = 0; i < WPT; ++i) {
+    if (a + i < n64) pf[a + i] = (uint16_t)off;
+    off += c[i];
   }
   __syncthreads();
-  return tot;
+  return all;
 }
 
 // bits of image row `row`, columns c0..c0+6 (bit j <-> column c0+j), masked by the valid-column mask cv;
@@ -528,27 +554,52 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   const int n64 = (P.npx + 63) / 64;
   const uint32_t big_flag = (SRC == SRC_LIST) ? SMG_ION_BIG : 0u;
 
+  constexpr bool ASYNC = (FMT == SMG_HITS_PACKED_F32);
+  // principal window (<= CAPC points, RMAX per thread).  Async form: every slot issues exactly one load
+  // (clamped to the window's last point, or to hit 0 for an empty window) so that the counted waits hold.
   auto issue_principal = [&](const IonDesc* D, Reg (&buf)[RMAX]) {
     const int n0 = uni(D->end[0]);
     const int64_t a = uni64(D->base[0]);
+    if constexpr (ASYNC) {
+      const uint64_t* sb = n0 > 0 ? hits.h + a : hits.h;
 #pragma unroll
-    for (int j = 0; j < RMAX; ++j) {
-      const int i = tid + j * BLOCK;
-      if (i < n0) buf[j] = hits.load(a, i);
+      for (int j = 0; j < RMAX; ++j) {
+        const int i = tid + j * BLOCK;
+        buf[j] = ld8_async(sb, (uint32_t)(n0 > 0 ? min(i, n0 - 1) : 0) * 8u);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < RMAX; ++j) {
+        const int i = tid + j * BLOCK;
+        if (i < n0) buf[j] = hits.load(a, i);
+      }
     }
   };
-  // tail chunk c: groups [c*GPC, (c+1)*GPC); slot j of wave w holds group c*GPC + j*NW + w
+  // tail chunk c: groups [c*GPC, (c+1)*GPC); slot j of wave w holds group c*GPC + j*NW + w.  Async form:
+  // exactly RC loads per chunk; lanes past their window's end load its last point, groups past the tail
+  // load hit 0 (consumers mask both).  Compiler form: such lanes hold a zero hit.
   auto issue_chunk = [&](const IonDesc* D, int c, Reg (&buf)[RC]) {
     const int ng = uni(D->ngroups);
 #pragma unroll
     for (int j = 0; j < RC; ++j) {
       const int G = c * GPC + j * NW + wid;
-      if (G < ng) {
-        int k = 1;
+      int k = 1;
 #pragma unroll
-        for (int kk = 2; kk < MAXK; ++kk) k += (G >= uni(D->gs[kk])) ? 1 : 0;
-        const int i = G * 64 + lane;
-        if (i < uni(D->end[k])) buf[j] = hits.load(uni64(D->base[k]) + i);
+      for (int kk = 2; kk < MAXK; ++kk) k += (G >= uni(D->gs[kk])) ? 1 : 0;
+      if constexpr (ASYNC) {
+        const uint64_t* sb = hits.h;
+        uint32_t off = 0;
+        if (G < ng) {
+          sb = hits.h + (uni64(D->base[k]) + (int64_t)G * 64);
+          off = (uint32_t)min(lane, uni(D->end[k]) - G * 64 - 1) * 8u;
+        }
+        buf[j] = ld8_async(sb, off);
+      } else {
+        buf[j] = Hits<FMT>::zero();
+        if (G < ng) {
+          const int i = G * 64 + lane;
+          if (i < uni(D->end[k])) buf[j] = hits.load(uni64(D->base[k]) + i);
+        }
       }
     }
   };
@@ -596,6 +647,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     // ---- phase 1: principal image -> bitmap, rank prefix, f64 values -----------------------------
     int nnz = 0;
     if (!skip) {
+      vm_wait<2 * RC>(h0);  // issued before this ion's two prefetched tail chunks
 #pragma unroll
       for (int j = 0; j < RMAX; ++j) {
         const int i = tid + j * BLOCK;
@@ -710,7 +762,28 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         }
         psk = psy = psyy = psxy = 0.0;
       };
+      // Lanes past the end of their window hold a zero hit (issue_chunk), which contributes nothing, so
+      // only whole groups past the tail need skipping.  Stage 1 does the principal-image lookups of every
+      // slot (LDS reads only, so the slots' lookups overlap); stage 2 accumulates slot by slot, flushing
+      // at window changes.
       auto process = [&](int c, Reg (&buf)[RC]) {
+        double xs[RC];
+        uint64_t bw[RC];
+        int rk[RC];
+#pragma unroll
+        for (int j = 0; j < RC; ++j) {
+          const uint32_t p = Hits<FMT>::pix(buf[j]);
+          bw[j] = reinterpret_cast<const uint64_t*>(Hbm)[p >> 6];
+          rk[j] = (int)pf[p >> 6];
+        }
+#pragma unroll
+        for (int j = 0; j < RC; ++j) {
+          const uint32_t p = Hits<FMT>::pix(buf[j]);
+          const uint64_t bit = 1ull << (p & 63);
+          const bool in = (bw[j] & bit) != 0ull;
+          const double x = vals[in ? rk[j] + __popcll(bw[j] & (bit - 1ull)) : 0];
+          xs[j] = (in && !(SMG_ABL & 16)) ? x : 0.0;
+        }
 #pragma unroll
         for (int j = 0; j < RC; ++j) {
           const int G = c * GPC + j * NW + wid;
@@ -721,17 +794,15 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
               gnext = curk + 1 < MAXK ? uni(D->gs[curk + 1]) : 0x7FFFFFFF;
               wend = uni(D->end[curk]);
             }
-            const bool valid = G * 64 + lane < wend;
+            const bool valid = lane < wend - G * 64;
             const uint32_t p = Hits<FMT>::pix(buf[j]);
             const double v = valid ? Hits<FMT>::val(buf[j]) : 0.0;
             const bool dup = valid && Hits<FMT>::dup(buf[j]) && !(SMG_ABL & 8);
-            if (valid) {
-              const double x = (SMG_ABL & 16) ? 0.0 : bm_test(Hbm, (int)p) ? vals[bm_rank(Hbm, pf, (int)p)] : 0.0;
-              psy += v;
-              psxy += x * v;
-              if (x > 0.0) psk += v;
-              if (!dup) psyy += v * v;
-            }
+            const double x = xs[j];
+            psy += v;
+            psxy += x * v;
+            if (x > 0.0) psk += v;
+            if (!dup) psyy += v * v;
             // duplicate candidates are summed per (pixel, window) before squaring: appended to this wave's
             // list segment (ballot compaction, no atomics)
             const uint64_t dm = __ballot(dup);
@@ -747,13 +818,16 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         }
       };
       // chunks 0 and 1 are in flight (issued during the previous iteration); later chunks one ahead
+      // (refills are issued unconditionally so that exactly RC loads follow each buffer's)
       for (int c = 0; c * GPC < ng; c += 2) {
+        vm_wait<RC>(ra);
         process(c, ra);
         if ((SMG_ABL & 4) && c >= 0) break;
-        if ((c + 2) * GPC < ng) issue_chunk(D, c + 2, ra);
+        issue_chunk(D, c + 2, ra);
         if ((c + 1) * GPC >= ng) break;
+        vm_wait<RC>(rb);
         process(c + 1, rb);
-        if ((c + 3) * GPC < ng) issue_chunk(D, c + 3, rb);
+        issue_chunk(D, c + 3, rb);
       }
       flush();
       if (lane == 0) dcnt[wid] = nd;
@@ -819,9 +893,15 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       uint32_t* olist = filtA;
       {
         const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(Hbm);
-        for (int w = tid; w < n64; w += BLOCK) {
-          uint64_t bits = bm64[w];
+        constexpr int WPT = (NPX_LDS_MAX / 64) / BLOCK;
+        uint64_t wb[WPT];
+#pragma unroll
+        for (int i = 0; i < WPT; ++i) wb[i] = (tid * WPT + i < n64) ? bm64[tid * WPT + i] : 0ull;
+#pragma unroll
+        for (int i = 0; i < WPT; ++i) {
+          uint64_t bits = wb[i];
           if (!bits) continue;
+          const int w = tid * WPT + i;
           int r = pf[w];
           while (bits) {
             olist[r++] = (uint32_t)(w * 64 + __builtin_ctzll(bits));
@@ -830,8 +910,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         }
       }
       __syncthreads();
-      for (int oc_i = tid; oc_i < nnz; oc_i += BLOCK) {
-        const int s = (int)olist[oc_i];
+      for (int ob = 0; ob < nnz; ob += BLOCK) {  // uniform trip count: the candidates are wave-compacted
+        const int oc_i = ob + tid;
+        const int s = oc_i < nnz ? (int)olist[oc_i] : 0;
         int rs, cs;
         rowcol(s, P, rs, cs);
         // valid-column mask of columns cs-3..cs+3
@@ -842,7 +923,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         for (int d = 0; d < 7; ++d) H[d] = bits7(Hbm, rs - 3 + d, cs - 3, cv, P);
         // isolation pre-filter (erosion border = background only): an eL>0 pixel in the cross of s needs
         // another principal pixel in s's 7x7, since the 4-cross of s alone cannot cover a 3x3 box
-        if (!P.erosion_border && (H[0] | H[1] | H[2] | (H[3] & ~8u) | H[4] | H[5] | H[6]) == 0u) continue;
+        const bool isolated = !P.erosion_border && (H[0] | H[1] | H[2] | (H[3] & ~8u) | H[4] | H[5] | H[6]) == 0u;
+        uint32_t pass = 0;
+        if (oc_i < nnz && !isolated) {
         uint32_t Dl[7];
         Dl[0] = Dl[6] = 0;
 #pragma unroll
@@ -858,7 +941,6 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
 #define SMG_BOX(dr, dc) ((((Dl[2 + (dr)] >> (2 + (dc))) & 7u) == 7u) && (((Dl[3 + (dr)] >> (2 + (dc))) & 7u) == 7u) && \
                          (((Dl[4 + (dr)] >> (2 + (dc))) & 7u) == 7u))
         const bool in_l = cs > 0, in_r = cs + 1 < P.ncols, in_u = rs > 0, in_d = rs + 1 < P.nrows;
-        uint32_t pass = 0;
         if (SMG_BOX(0, 0) && !SMG_HB(-1, 0) && !SMG_HB(0, -1)) pass |= 1u;
         if (in_r && SMG_BOX(0, 1) && !SMG_HB(-1, 1)) pass |= 2u;
         if (in_l && SMG_BOX(0, -1) && !SMG_HB(-1, -1) && !SMG_HB(0, -2) && !SMG_HB(0, -1)) pass |= 4u;
@@ -867,12 +949,22 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         if (in_d && SMG_BOX(1, 0)) pass |= 16u;
 #undef SMG_BOX
 #undef SMG_HB
-        while (pass) {
-          const int ci = __ffs(pass) - 1;
-          pass &= pass - 1;
-          const int p = s + (ci == 1 ? 1 : ci == 2 ? -1 : ci == 3 ? -P.ncols : ci == 4 ? P.ncols : 0);
-          const int idx = atomicAdd(&ctr[C_NE], 1);
-          if (idx < CAPC) epix[idx] = (uint32_t)p;
+        }
+        // wave-compacted append: one LDS atomic per wave
+        const int cnt = __popc(pass);
+        const int inc = wave_incl_scan_dpp(cnt);
+        const int wtot = __builtin_amdgcn_readlane(inc, 63);
+        if (wtot > 0) {
+          int wbase = 0;
+          if (lane == 63) wbase = atomicAdd(&ctr[C_NE], wtot);
+          int idx = __builtin_amdgcn_readlane(wbase, 63) + inc - cnt;
+          while (pass) {
+            const int ci = __ffs(pass) - 1;
+            pass &= pass - 1;
+            const int p = s + (ci == 1 ? 1 : ci == 2 ? -1 : ci == 3 ? -P.ncols : ci == 4 ? P.ncols : 0);
+            if (idx < CAPC) epix[idx] = (uint32_t)p;
+            ++idx;
+          }
         }
       }
       __syncthreads();
