@@ -172,8 +172,9 @@ def main():
                        "achieved_GBs": (alg[n] / (stages[n] * 1e-3) / 1e9) if stages[n] > 0 else None}
                    for n in ("flag+sort", "window_search", "ion_metrics")}
     ach = kernel_rows[dominant]["achieved_GBs"]
+    traffic, traffic_src = measured_traffic(dominant)
     roofline = {"bound": "hbm", "kernel": dominant, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": (ach / HBM_PEAK_GBS) if ach else None, "traffic": None,
+                "frac": (ach / HBM_PEAK_GBS) if ach else None, "traffic": traffic, "traffic_source": traffic_src,
                 "imaging_kernel": {"kernel": "ion_metrics", "achieved": kernel_rows["ion_metrics"]["achieved_GBs"],
                                    "frac": (kernel_rows["ion_metrics"]["achieved_GBs"] or 0) / HBM_PEAK_GBS}}
 
@@ -211,6 +212,20 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def measured_traffic(stage):
+    """HBM bytes per launch of the ion kernel from the newest committed PMC summary (profiles/*/traffic_*.json,
+    written by scripts/gpu_traffic.sh: FETCH_SIZE calibrated for 8-B-per-lane loads, + WRITE_SIZE).  The
+    counters cannot be read from inside this process; None for other stages or when no summary exists."""
+    import glob
+    if stage != "ion_metrics":
+        return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic_*.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return float(d["traffic_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(args, ions, mz, hits, dims, out):

@@ -105,6 +105,11 @@ int smg_sample_spectra(const int64_t* sp_off, const double* mzs, const double* c
                        int64_t* out_window, int64_t* out_spectrum, double* out_value, int64_t capacity,
                        int64_t* count, void* stream);
 
+/* Diagnostics.  Calibration stream for the rocprofv3 HBM-traffic counters: reads n_words 8-byte words with
+ * the ion kernel's access width (one coalesced 8-byte load per lane) and XOR-folds them into out[n_blocks]
+ * (device), so that FETCH_SIZE can be converted to bytes for this access pattern (bench.py `traffic`). */
+int smg_debug_stream_read(const uint64_t* data, int64_t n_words, uint64_t* out, int32_t n_blocks, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -14,3 +14,13 @@ for _ in range(2):
     m = E.ion_metrics(peaks, dions, lo, hi, nlevels=30)
 torch.cuda.synchronize()
 print("ok")
+# calibration dispatch for the HBM-traffic counters: one read of the sorted hits (known byte count) with the
+# ion kernel's access width; scripts/traffic_summary.py converts FETCH_SIZE with it
+import ctypes
+from sm_distributed_amd import _lib
+out = torch.zeros(4096, dtype=torch.int64, device="cuda")
+rc = _lib.lib().smg_debug_stream_read(ctypes.c_void_p(peaks.hits_sorted.data_ptr()), peaks.n_points,
+                                      ctypes.c_void_p(out.data_ptr()), 4096, None)
+assert rc == 0
+torch.cuda.synchronize()
+print("calibration bytes", peaks.n_points * 8)

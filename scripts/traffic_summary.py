@@ -1,0 +1,37 @@
+"""HBM traffic per launch of the ion kernel from two rocprofv3 --pmc runs (FETCH_SIZE, WRITE_SIZE) of
+scripts/pmc_ion.py, calibrated on its smg_debug_stream_read dispatch (n_points x 8 B read once with the same
+8-byte-per-lane access width: MI355X_MICROARCH.md says FETCH_SIZE is exact only for 16-B-per-lane reads and
+must be calibrated otherwise).  FETCH_SIZE counts L2 -> fabric requests (Infinity-Cache hits included).
+
+usage: traffic_summary.py FETCH.csv WRITE.csv n_points out.json
+"""
+import csv, json, re, sys
+from collections import defaultdict
+
+
+def per_kernel(path, counter):
+    acc = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        name = r.get("Kernel_Name") or ""
+        m = re.search(r"ion_pipe_kernel<[^,]*, (\d+)", name)
+        key = f"ion_pipe_kernel[{m.group(1)}]" if m else ("stream_read" if "stream_read_kernel" in name else None)
+        if key:
+            acc[key].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
+write = per_kernel(sys.argv[2], "WRITE_SIZE")
+n_points = int(sys.argv[3])
+calib_bytes = n_points * 8
+scale = calib_bytes / fetch["stream_read"]  # bytes per FETCH_SIZE unit for 8-B-per-lane loads
+res = {"kernel": "ion_pipe_kernel[512]", "calibration": {"bytes": calib_bytes, "fetch_size": fetch["stream_read"],
+                                                          "bytes_per_unit": scale},
+       "fetch_size_raw": fetch, "write_size_raw": write,
+       "read_bytes": {k: v * scale for k, v in fetch.items()},
+       "write_bytes_kb_units": write}
+res["traffic_bytes_per_launch"] = res["read_bytes"]["ion_pipe_kernel[512]"] + 1024.0 * write.get("ion_pipe_kernel[512]", 0.0)
+json.dump(res, open(sys.argv[4], "w"), indent=1)
+print(json.dumps(res, indent=1))

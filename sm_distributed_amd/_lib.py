@@ -38,6 +38,7 @@ PROTOTYPES = {
     "smg_ion_metrics": (ctypes.c_int, [_I32, _P, _P, _P, _P, _P, _P, _P, _I64, _I32, _I32, _I32, _D, _I32,
                                        _I32, _I32, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "smg_sample_spectra": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _I64, _P, _P, _P, _I64, _P, _P]),
+    "smg_debug_stream_read": (ctypes.c_int, [_P, _I64, _P, _I32, _P]),
 }
 
 

@@ -444,7 +444,10 @@ __global__ void ion_desc_kernel(const int64_t* __restrict__ lo, const int64_t* _
 //    workgroup whose range is exhausted steals from the other ranges.
 //  SRC_LIST: a device list of positions (the rejects of the previous pass) with a global cursor.
 enum { SRC_RANGES = 0, SRC_LIST = 1 };
-constexpr int XCDS = 8;
+#ifndef SMG_XCDS
+#define SMG_XCDS 8  // diagnostic: 1 = one global range (no XCD locality)
+#endif
+constexpr int XCDS = SMG_XCDS;
 constexpr int CTR_STRIDE = 32;  // u32 words between counters (one 128-B line each)
 
 struct Sched {
@@ -1427,7 +1430,7 @@ static constexpr int HDR_XCD = 64;
 // LDS-path geometries: the main pass (two 512-thread workgroups per CU) and the big-ion pass over its
 // rejects (one 1024-thread workgroup per CU with the whole LDS)
 #ifndef SMG_MAIN_CFG
-#define SMG_MAIN_CFG 512, 5, 3, 4
+#define SMG_MAIN_CFG 512, 5, 2, 4
 #endif
 // main LDS pass: threads, principal points per thread, chunk points per thread, min waves per SIMD
 static constexpr int MAIN_CFG[4] = {SMG_MAIN_CFG};

@@ -165,6 +165,17 @@ __global__ void __launch_bounds__(256) flag_duplicates_kernel(const int64_t* __r
   }
 }
 
+// calibration stream: every lane reads 8-byte words, grid-stride, coalesced (the access width of the ion
+// kernel's hit loads); XOR-folded per block so nothing is elided
+__global__ void stream_read_kernel(const uint64_t* __restrict__ p, int64_t n, uint64_t* __restrict__ out) {
+  uint64_t acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    acc ^= p[i];
+  acc = wave_sum(acc);  // any fold will do
+  if ((threadIdx.x & 63) == 0) atomicXor(reinterpret_cast<unsigned long long*>(out + blockIdx.x),
+                                          (unsigned long long)acc);
+}
+
 }  // namespace smg
 
 using namespace smg;
@@ -261,6 +272,15 @@ int smg_sample_spectra(const int64_t* sp_off, const double* mzs, const double* c
   hipLaunchKernelGGL(sample_spectra_kernel, grid, dim3(256), 0, as_stream(stream), sp_off, mzs, cum_ints,
                      n_spectra, lower, upper, n_windows, out_window, out_spectrum, out_value, capacity,
                      reinterpret_cast<unsigned long long*>(count));
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int smg_debug_stream_read(const uint64_t* data, int64_t n_words, uint64_t* out, int32_t n_blocks, void* stream) {
+  SMG_CHECK_ARG(data && out && n_words >= 0 && n_blocks > 0, "bad arguments");
+  hipStream_t st = as_stream(stream);
+  SMG_HIP(hipMemsetAsync(out, 0, (size_t)n_blocks * 8, st));
+  hipLaunchKernelGGL(stream_read_kernel, dim3((unsigned)n_blocks), dim3(256), 0, st, data, n_words, out);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

@@ -130,6 +130,18 @@ def make_case(name: str):
         ds = syn.make_dataset_np(520, 520, 3, seed=63, ions=ions, plant_fraction=1.0, plant_seed=64,
                                  blob_sigma=(3.0, 8.0))
         return ds, ions, 50.0, {}
+    if name == "long_tail":    # tails of several register chunks (chunk refills, window changes inside chunks)
+        full = syn.make_ion_table(12, seed=91, decoy_seed=92)
+        ions = subset_ions(full, np.arange(0, full.n_ions, 6))
+        ds = syn.make_dataset_np(64, 64, 2000, seed=93, ions=ions, plant_fraction=0.5, plant_seed=94)
+        return ds, ions, 100.0, {}
+    if name == "dups_heavy":   # duplicate lists overflow the main pass (-> big-ion pass -> dense path)
+        ds, ions, ppm, _ = make_case("long_tail")
+        return add_duplicates(ds, 0.3, 95), ions, ppm, {}
+    if name == "kmix":         # 1..10 isotope peaks per ion: K = 1 (no tail) and K > 8 (dense path)
+        ions = syn.make_ion_table(25, seed=101, decoy_seed=102, k_range=(1, 10))
+        ds = syn.make_dataset_np(40, 40, 500, seed=103, ions=ions, plant_fraction=0.4, plant_seed=104)
+        return ds, ions, 30.0, {}
     if name == "boundary":
         ds = syn.make_dataset_np(16, 16, 300, seed=71)
         return ds, boundary_ions(ds, 5.0, 40, 72), 5.0, {}
@@ -137,7 +149,7 @@ def make_case(name: str):
 
 
 CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels", "nlevels1", "big_window", "huge_window",
-         "large_image", "boundary"]
+         "large_image", "boundary", "long_tail", "dups_heavy", "kmix"]
 
 
 def oracle_run(ds, ions, ppm, nlevels=30, connectivity=4, erosion_border=0):

@@ -128,3 +128,21 @@ def test_duplicate_flags_cover_every_window_duplicate(name):
     assert n_dup > 0 or name == "basic"
     if name == "basic":
         assert flag.mean() < 0.2  # flags stay a small minority on ordinary data
+
+
+def test_lds_pipeline_paths_exercised():
+    """The new cases reach the code they are meant for: multi-chunk tails on the main pass, duplicate-list
+    overflow handed to the big-ion / dense passes, K = 1 and K > 8 ions."""
+    ds, ions, ppm, kw, imgs, df, peaks, m, lo, hi = _run_case("long_tail")
+    has = (m["flags"] & 1) != 0
+    main = has & ((m["flags"] & (2 | 8)) == 0)
+    tail = np.array([hi[ions.win_off[i] + 1:ions.win_off[i + 1]].sum() - lo[ions.win_off[i] + 1:ions.win_off[i + 1]].sum()
+                     for i in range(ions.n_ions)])
+    assert (main & (tail > 4 * 1024)).sum() >= 10  # > 4 register chunks of 1024 points
+    _, _, _, _, _, _, _, m, _, _ = _run_case("dups_heavy")
+    assert ((m["flags"] & (2 | 8)) != 0).any()
+    ds, ions, ppm, kw, imgs, df, peaks, m, lo, hi = _run_case("kmix")
+    K = np.diff(ions.win_off)
+    has = (m["flags"] & 1) != 0
+    assert (has & (K == 1)).any() and (has & (K > 8)).any()
+    assert ((m["flags"][has & (K > 8)] & 2) != 0).all()
