@@ -133,7 +133,7 @@ def make_case(name: str):
     if name == "long_tail":    # tails of several register chunks (chunk refills, window changes inside chunks)
         full = syn.make_ion_table(12, seed=91, decoy_seed=92)
         ions = subset_ions(full, np.arange(0, full.n_ions, 6))
-        ds = syn.make_dataset_np(64, 64, 2000, seed=93, ions=ions, plant_fraction=0.5, plant_seed=94)
+        ds = syn.make_dataset_np(128, 256, 250, seed=93, ions=ions, plant_fraction=0.5, plant_seed=94)
         return ds, ions, 100.0, {}
     if name == "dups_heavy":   # duplicate lists overflow the main pass (-> big-ion pass -> dense path)
         ds, ions, ppm, _ = make_case("long_tail")
