@@ -62,9 +62,11 @@ int smg_flag_duplicates(const int64_t* sp_off, int64_t n_spectra, const float* m
                         int64_t n_points, double ppm, const uint8_t* force, void* stream);
 
 /* Global m/z sort of the packed points (the pandas sort_values('mz') of formula_imager_segm.py:73-74,
- * done once over the whole dataset instead of per m/z segment).  Keys are positive float32 m/z. */
+ * done once over the whole dataset instead of per m/z segment).  Keys are positive float32 m/z; only their
+ * low key_bits bits are sorted on (all keys must agree above them: key_bits = 32 - clz(bits(min) ^ bits(max));
+ * 0 = all 31 bits). */
 int smg_sort_points_workspace_size(int64_t n_points, size_t* bytes);
-int smg_sort_points(const float* mz, const uint64_t* hits, int64_t n_points,
+int smg_sort_points(const float* mz, const uint64_t* hits, int64_t n_points, int32_t key_bits,
                     float* mz_sorted, uint64_t* hits_sorted, void* workspace, size_t workspace_bytes,
                     void* stream);
 

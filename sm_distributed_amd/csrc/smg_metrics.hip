@@ -112,10 +112,11 @@ struct PixVal {
 // operations of this wave done).  Vector-memory operations complete in issue order, so operations the
 // compiler issues in between only make a counted wait stricter.  The destination registers are neither
 // read nor copied between issue and wait (the wait takes them as in/out operands).
-__device__ __forceinline__ uint64_t ld8_async(const void* sbase, uint32_t voff) {
-  uint64_t r;
-  asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(r) : "v"(voff), "s"(sbase) : "memory");
-  return r;
+// The destination is an in/out operand: its previous value counts as used by the next load into it, so
+// a register with a load in flight is never reallocated to another value, even when that load's data end
+// up unused (a refill past the tail, or an ion that is handed to another pass).
+__device__ __forceinline__ void ld8_async(uint64_t& r, const void* sbase, uint32_t voff) {
+  asm volatile("global_load_dwordx2 %0, %1, %2" : "+v"(r) : "v"(voff), "s"(sbase) : "memory");
 }
 template <int N, int M>
 __device__ __forceinline__ void vm_wait(uint64_t (&r)[M]) {
@@ -544,12 +545,15 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   int* ctr = reinterpret_cast<int*>(smem + LY::o_ctr);
   int* wsc = reinterpret_cast<int*>(smem + LY::o_wsc);
   IonDesc* dsl = reinterpret_cast<IonDesc*>(smem + LY::o_desc);  // [2]: current / next
-  // chaos-phase aliases (the value, filter and table regions are dead by then)
-  uint32_t* epix = reinterpret_cast<uint32_t*>(vals);                   // candidates, append order
-  uint32_t* epix_r = filtA;                                             // E pixels, rank order (4*CAPC)
+  // chaos-phase aliases.  The distinct principal pixels in rank order (olist) sit in the value region: right
+  // behind the nnz values when 12*nnz <= 8*CAPC (written by their owners in phase 1), else at its start
+  // (bitmap scan once the values are dead).  Candidates go to the (then dead) duplicate-list region.
+  constexpr int OL_MAX = (2 * CAPC) / 3;
+  uint32_t* epix = filtA;                                               // candidates, append order (4*CAPC)
   uint8_t* eL8 = reinterpret_cast<uint8_t*>(filtA) + (size_t)CAPC * 4;  // candidates' eL, append order
+  uint32_t* epix_r = reinterpret_cast<uint32_t*>(vals);                 // E pixels, rank order
   uint8_t* eLr = Lv;                                                    // rank order
-  uint32_t* par = reinterpret_cast<uint32_t*>(vals);                    // rank order (after epix consumed)
+  uint32_t* par = reinterpret_cast<uint32_t*>(vals) + CAPC;             // rank order
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -568,7 +572,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
 #pragma unroll
       for (int j = 0; j < RMAX; ++j) {
         const int i = tid + j * BLOCK;
-        buf[j] = ld8_async(sb, (uint32_t)(n0 > 0 ? min(i, n0 - 1) : 0) * 8u);
+        ld8_async(buf[j], sb, (uint32_t)(n0 > 0 ? min(i, n0 - 1) : 0) * 8u);
       }
     } else {
 #pragma unroll
@@ -596,7 +600,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
           sb = hits.h + (uni64(D->base[k]) + (int64_t)G * 64);
           off = (uint32_t)min(lane, uni(D->end[k]) - G * 64 - 1) * 8u;
         }
-        buf[j] = ld8_async(sb, off);
+        ld8_async(buf[j], sb, off);
       } else {
         buf[j] = Hits<FMT>::zero();
         if (G < ng) {
@@ -608,6 +612,10 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   };
 
   Reg h0[RMAX], ra[RC], rb[RC];
+#pragma unroll
+  for (int j = 0; j < RMAX; ++j) h0[j] = Hits<FMT>::zero();
+#pragma unroll
+  for (int j = 0; j < RC; ++j) ra[j] = rb[j] = Hits<FMT>::zero();
   int64_t pos = -1;  // ion scored in this iteration (-1: none; the first iteration only issues loads)
   int cur = 0;
   while (true) {
@@ -649,18 +657,22 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
 
     // ---- phase 1: principal image -> bitmap, rank prefix, f64 values -----------------------------
     int nnz = 0;
+    uint32_t* olist = nullptr;
     if (!skip) {
       vm_wait<2 * RC>(h0);  // issued before this ion's two prefetched tail chunks
+      uint32_t own = 0;     // slots whose atomicOr set the pixel's bit (one owner per distinct pixel)
 #pragma unroll
       for (int j = 0; j < RMAX; ++j) {
         const int i = tid + j * BLOCK;
         if (i < n0) {
           const uint32_t p = Hits<FMT>::pix(h0[j]);
-          atomicOr(&Hbm[p >> 5], 1u << (p & 31));
+          const uint32_t bit = 1u << (p & 31);
+          if (!(atomicOr(&Hbm[p >> 5], bit) & bit)) own |= 1u << j;
         }
       }
       __syncthreads();
       nnz = bm_build_prefix<NW>(Hbm, pf, n64, wsc);
+      olist = reinterpret_cast<uint32_t*>(vals) + (nnz <= OL_MAX ? ((2 * nnz + 3) & ~3) : 0);
       // A point without the duplicate-candidate flag is the only point of its pixel in this window
       // (smg_flag_duplicates), so it stores its value; flagged points (true duplicates and a few false
       // positives) zero the slot here and add atomically after a barrier (coo.toarray() sums duplicates).
@@ -673,6 +685,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
           const bool d = Hits<FMT>::dup(h0[j]);
           vals[r] = d ? 0.0 : Hits<FMT>::val(h0[j]);
           any_dup |= d;
+          if (nnz <= OL_MAX && ((own >> j) & 1u)) olist[r] = Hits<FMT>::pix(h0[j]);
         }
       }
       if (any_dup) ctr[C_PDUP] = 1;
@@ -735,10 +748,11 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     }
 #ifndef SMG_ABL
 #define SMG_ABL 0  // diagnostic ablations (timing only, wrong results): 1 = no chaos, 2 = no tail windows,
-                   // 4 = tail chunk 0 only, 8 = no duplicate deferral, 16 = no principal lookups in the tail
+                   // 4 = tail chunk 0 only, 8 = no duplicate deferral, 16 = no principal lookups in the tail,
+                   // 32 = no exact eL / Kruskal, 64 = no screen, 128 = no levels
 #endif
     const bool chaos_ok = !skip && (sx > 0.0) && (npx_pos >= 4.0) && !(SMG_ABL & 1);
-    if (chaos_ok) {
+    if (chaos_ok && nnz > OL_MAX && !(SMG_ABL & 128)) {  // else after the screen, if it finds candidates
       for (int r = tid; r < nnz; r += BLOCK) Lv[r] = (uint8_t)level_fast(vals[r], vmax, P);
     }
     STAMP(2);
@@ -892,9 +906,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     double chaos_raw = NAN;
     uint32_t flags = 0;
     if (!skip && chaos_ok) {
-      // the distinct principal pixels in rank order (olist[pf[w] + i] = i-th set bit of word w)
-      uint32_t* olist = filtA;
-      {
+      if (nnz > OL_MAX) {
+        // olist did not fit behind the values: the distinct principal pixels from the bitmap, rank order
+        // (olist[pf[w] + i] = i-th set bit of word w); the values are dead
         const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(Hbm);
         constexpr int WPT = (NPX_LDS_MAX / 64) / BLOCK;
         uint64_t wb[WPT];
@@ -911,9 +925,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
             bits &= bits - 1;
           }
         }
+        __syncthreads();
       }
-      __syncthreads();
-      for (int ob = 0; ob < nnz; ob += BLOCK) {  // uniform trip count: the candidates are wave-compacted
+      for (int ob = 0; ob < ((SMG_ABL & 64) ? 0 : nnz); ob += BLOCK) {  // uniform trip count: wave-compacted
         const int oc_i = ob + tid;
         const int s = oc_i < nnz ? (int)olist[oc_i] : 0;
         int rs, cs;
@@ -972,10 +986,16 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       }
       __syncthreads();
       STAMP(4);
-      const int ncand = ctr[C_NE];
+      const int ncand = (SMG_ABL & 32) ? 0 : ctr[C_NE];
       if (ncand > CAPC) {
         reject();
         skip = true;
+      }
+      if (!skip && ncand > 0 && nnz <= OL_MAX) {
+        // level index per principal pixel, only for images with candidates (the values are intact: olist
+        // sits behind them, candidates elsewhere)
+        for (int r = tid; r < nnz; r += BLOCK) Lv[r] = (uint8_t)level_fast(vals[r], vmax, P);
+        __syncthreads();
       }
       if (!skip) {
         // (ii) exact eL(p) = min_{q in N9(p)} max_{q' in N4[q] in image} L(q')
@@ -1134,6 +1154,10 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     __syncthreads();  // the next ion re-initialises the LDS structures
     STAMP(7);
   }
+  // no load of this wave outlives it
+  vm_wait<0>(h0);
+  vm_wait<0>(ra);
+  vm_wait<0>(rb);
 }
 
 // position list -> ion list (when the big-ion pass is skipped, the dense kernel reads ion indices)

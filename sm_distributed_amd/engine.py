@@ -60,6 +60,7 @@ class DevicePeaks:
     mz_sorted: torch.Tensor | None = None
     hits_sorted: torch.Tensor | None = None
     flag_ppm: float | None = None
+    sort_key_bits: int | None = None
 
     @property
     def n_points(self) -> int:
@@ -111,9 +112,19 @@ class DevicePeaks:
         sz = ctypes.c_size_t(0)
         check(lib().smg_sort_points_workspace_size(n, ctypes.byref(sz)), "smg_sort_points_workspace_size")
         ws = workspace(sz.value, self.device, "sort")
-        check(lib().smg_sort_points(_p(self.mz), _p(self.hits), n, _p(self.mz_sorted), _p(self.hits_sorted),
-                                    _p(ws), ws.numel(), _stream(stream)), "smg_sort_points")
+        check(lib().smg_sort_points(_p(self.mz), _p(self.hits), n, self.key_bits(), _p(self.mz_sorted),
+                                    _p(self.hits_sorted), _p(ws), ws.numel(), _stream(stream)), "smg_sort_points")
         return self
+
+    def key_bits(self) -> int:
+        """Low bits in which the dataset's f32 m/z bit patterns differ (the sort ignores the common prefix);
+        computed once, the m/z array does not change."""
+        if self.sort_key_bits is None:
+            lo, hi = torch.aminmax(self.mz)
+            a = int(lo.view(torch.int32).item())
+            b = int(hi.view(torch.int32).item())
+            self.sort_key_bits = max(1, (a ^ b).bit_length())
+        return self.sort_key_bits
 
 
 @dataclass
