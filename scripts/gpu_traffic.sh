@@ -14,5 +14,5 @@ done
 n=$(grep "calibration bytes" gpurun_out/$TAG/FETCH_SIZE.log | awk '{print $3/8}')
 python3 scripts/traffic_summary.py gpurun_out/$TAG/FETCH_SIZE.csv gpurun_out/$TAG/WRITE_SIZE.csv $n gpurun_out/$TAG/traffic.json
 rc=$?
-rm -f gpurun_out/$TAG/*.csv  # large; the summary keeps what is used
+rm -f gpurun_out/$TAG/FETCH_SIZE.csv gpurun_out/$TAG/WRITE_SIZE.csv  # large; the summary keeps what is used
 exit $rc

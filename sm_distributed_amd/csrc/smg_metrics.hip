@@ -9,19 +9,15 @@
 //   pyImagingMSpec 0.1.1 isotope_pattern_match / isotope_image_correlation,
 //   cpyImagingMSpec 0.0.4 measure_of_chaos   (restated, see oracle/msm_oracle.py)
 //
-// Two paths:
-//  * LDS path (ion_lds_kernel): one 256-thread workgroup per ion.  The principal image lives in LDS
-//    as a pixel bitmap + per-64-bit-word popcount prefix (rank) + f64 values in rank order.  The
-//    other isotope windows are streamed once and joined against it (spectral sums, Pearson sums);
-//    their own duplicate pixels are found with a hashed two-bit filter.  measure_of_chaos uses the
-//    threshold decomposition of flat morphology: the per-level dilate(cross)/erode(box) equals
-//    thresholding eL = erode_box(dilate_cross(L)) of the per-pixel level index L, so
-//    sum_levels #components = sum_p eL(p) - weight(maximum spanning forest), computed with one
-//    Kruskal pass (levels descending) over an LDS union-find.  Candidates for eL > 0 are found from
-//    7x7 bit windows of the bitmap, so isolated pixels cost ~14 LDS reads.
-//  * dense path (ion_dense_kernel): persistent workgroups with a global-memory scratch slot of
-//    N_px-sized images, for ions that do not fit the LDS path (principal window > CAP points, too
-//    many E pixels / suspects, images larger than 2^18 pixels).
+// Three passes (launch_metrics):
+//  * main LDS pass (ion_pipe_kernel<512>): persistent, software-pipelined; two 512-thread workgroups per CU,
+//    one ion at a time per workgroup with the principal image in LDS (pixel bitmap + rank prefix + f64 values),
+//    the other isotope windows streamed once and joined against it, measure_of_chaos by the threshold
+//    decomposition of flat morphology (Kruskal over eL with an LDS union-find).  See the kernel's comment.
+//  * big-ion LDS pass (ion_pipe_kernel<1024>): the same code with one 1024-thread workgroup per CU and the
+//    whole LDS, over the main pass's rejects (principal window > 2560 points, duplicate-list overflow).
+//  * dense path (ion_dense_kernel): persistent workgroups with a global-memory scratch slot of N_px-sized
+//    images, for what the LDS passes cannot take (K > 8, principal window > 8192 points, images > 2^18 px).
 #include <stdarg.h>
 
 #include "smg_common.hpp"
