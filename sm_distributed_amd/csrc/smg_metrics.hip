@@ -987,41 +987,70 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         reject();
         skip = true;
       }
-      if (!skip && ncand > 0 && nnz <= OL_MAX) {
-        // level index per principal pixel, only for images with candidates (the values are intact: olist
-        // sits behind them, candidates elsewhere)
+      // level index L: precomputed for every principal pixel when there are many candidates, else computed
+      // on demand from the values (intact: olist sits behind them, candidates elsewhere) for the few principal
+      // pixels around the candidates
+      const bool lazyL = (nnz <= OL_MAX) && (ncand * 16 < nnz);
+      if (!skip && ncand > 0 && nnz <= OL_MAX && !lazyL) {
         for (int r = tid; r < nnz; r += BLOCK) Lv[r] = (uint8_t)level_fast(vals[r], vmax, P);
         __syncthreads();
       }
       if (!skip) {
-        // (ii) exact eL(p) = min_{q in N9(p)} max_{q' in N4[q] in image} L(q')
+        // (ii) exact eL(p) = min_{q in box(p)} max_{q' in cross[q], in image} L(q').  The 21 pixels involved
+        // (p's 5x5 neighbourhood without corners) come from five bitmap rows read at once; L is fetched only
+        // for the principal pixels among them and packed six bits per column.
         int emax_local = 0;
+        const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(Hbm);
         for (int c = tid; c < ncand; c += BLOCK) {
           const int p = (int)epix[c];
           int rp, cp;
           rowcol(p, P, rp, cp);
+          const int clo = 2 - cp > 0 ? 2 - cp : 0, chi = P.ncols - cp + 2 < 5 ? P.ncols - cp + 2 : 5;
+          const uint32_t cv5 = ((1u << chi) - 1u) & ~((1u << clo) - 1u);  // columns cp-2..cp+2 in the image
+          uint32_t Lrow[5];
+#pragma unroll
+          for (int d = 0; d < 5; ++d) {
+            const int row = rp - 2 + d;
+            const bool rv = (unsigned)row < (unsigned)P.nrows;
+            const int st = (rv ? row : 0) * P.ncols + cp - 2;  // >= -2: the guard word in front reads as zero
+            const int w = st >> 6, b = st & 63;
+            const uint64_t w0 = bm64[w], w1 = bm64[w + 1];
+            const int r0 = pf[w], r1 = pf[w + 1];
+            const uint32_t bits = rv ? (uint32_t)((b ? ((w0 >> b) | (w1 << (64 - b))) : w0) & 31u) & cv5 : 0u;
+            uint32_t packed = 0;
+            for (uint32_t rest = bits; rest; rest &= rest - 1u) {
+              const int j = __builtin_ctz(rest);
+              const int bj = b + j;  // bit of column cp-2+j in w0 (bj < 64) or w1
+              const int r = bj < 64 ? r0 + __popcll(w0 & ((1ull << bj) - 1ull))
+                                    : r1 + __popcll(w1 & ((1ull << (bj - 64)) - 1ull));
+              const uint32_t L = lazyL ? (uint32_t)level_fast(vals[r], vmax, P) : (uint32_t)Lv[r];
+              packed |= L << (6 * j);
+            }
+            Lrow[d] = packed;
+          }
+#define SMG_L(r, cc) ((Lrow[r] >> (6 * (cc))) & 63u)
           int mn = 1 << 20;
-#pragma unroll 1
-          for (int qa = -1; qa <= 1; ++qa) {
-#pragma unroll 1
-            for (int qb = -1; qb <= 1; ++qb) {
-              const int rq = rp + qa, cq = cp + qb;
+          bool outside = false;
+#pragma unroll
+          for (int a2 = -1; a2 <= 1; ++a2) {
+#pragma unroll
+            for (int b2 = -1; b2 <= 1; ++b2) {
+              const int rq = rp + a2, cq = cp + b2;
               if (rq < 0 || rq >= P.nrows || cq < 0 || cq >= P.ncols) {
-                if (!P.erosion_border) mn = 0;
+                outside = true;
                 continue;
               }
-              int dl = 0;
-#pragma unroll
-              for (int t = 0; t < 5; ++t) {
-                const int r2 = rq + (t == 1 ? -1 : t == 2 ? 1 : 0);
-                const int c2 = cq + (t == 3 ? -1 : t == 4 ? 1 : 0);
-                if (r2 < 0 || r2 >= P.nrows || c2 < 0 || c2 >= P.ncols) continue;
-                const int q = r2 * P.ncols + c2;
-                if (bm_test(Hbm, q)) dl = max(dl, (int)Lv[bm_rank(Hbm, pf, q)]);
-              }
-              mn = min(mn, dl);
+              const int R = 2 + a2, C = 2 + b2;
+              uint32_t dl = SMG_L(R, C);
+              dl = max(dl, SMG_L(R - 1, C));
+              dl = max(dl, SMG_L(R + 1, C));
+              dl = max(dl, SMG_L(R, C - 1));
+              dl = max(dl, SMG_L(R, C + 1));
+              mn = min(mn, (int)dl);
             }
           }
+#undef SMG_L
+          if (outside && !P.erosion_border) mn = 0;
           if (mn >= (1 << 20)) mn = 0;
           eL8[c] = (uint8_t)mn;
           emax_local = max(emax_local, mn);
