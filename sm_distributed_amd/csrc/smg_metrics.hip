@@ -1061,7 +1061,46 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
 
         // ---- phase 4b: Kruskal over eL (levels descending) with an LDS union-find -------------------
         double sum_c = 0.0;
-        if (ctr[C_EMAX] > 0) {
+        const int emax_all = ctr[C_EMAX];
+        if (emax_all > 0 && ncand <= WAVE) {
+          // few candidates (most noise images): wave 0 alone, one candidate per lane; forward neighbours
+          // found by comparing pixel indices across lanes, union-find over candidate indices in LDS; no
+          // bitmap rebuild and no barrier.  Only wave 0 needs the result (finalize).
+          if (wid == 0) {
+            uint32_t* upar = reinterpret_cast<uint32_t*>(red);  // 64 entries (red is free until finalize)
+            const bool act = lane < ncand;
+            const int p = act ? (int)epix[lane] : -1;
+            const int e = act ? (int)eL8[lane] : 0;
+            int rp = 0, cp = 0;
+            rowcol(p < 0 ? 0 : p, P, rp, cp);
+            int nb[4] = {-1, -1, -1, -1};
+            for (int j = 0; j < ncand; ++j) {
+              const int pj = __shfl(p, j, WAVE), ej = __shfl(e, j, WAVE);
+              if (e >= 1 && ej >= 1) {
+                if (cp + 1 < P.ncols && pj == p + 1) nb[0] = j;
+                if (rp + 1 < P.nrows) {
+                  if (pj == p + P.ncols) nb[1] = j;
+                  if (P.connectivity == 8 && cp > 0 && pj == p + P.ncols - 1) nb[2] = j;
+                  if (P.connectivity == 8 && cp + 1 < P.ncols && pj == p + P.ncols + 1) nb[3] = j;
+                }
+              }
+            }
+            int eq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int v = __shfl(e, nb[q] < 0 ? 0 : nb[q], WAVE);
+              eq[q] = nb[q] < 0 ? 0 : (e < v ? e : v);  // edge weight min(eL)
+            }
+            upar[lane] = (uint32_t)lane;
+            double wsum = 0.0;
+            for (int t = emax_all; t >= 1; --t) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                if (eq[q] == t && uf_unite(upar, (uint32_t)lane, (uint32_t)nb[q])) wsum += (double)t;
+            }
+            sum_c = wave_sum_dpp(e >= 1 ? (double)e : 0.0) - wave_sum_dpp(wsum);
+          }
+        } else if (emax_all > 0) {
           uint4* z = reinterpret_cast<uint4*>(Hbm);
           for (int i = tid; i < P.w32 / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);  // guard stays zero
           __syncthreads();
@@ -1079,7 +1118,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
           __syncthreads();
           for (int r = tid; r < m; r += BLOCK) par[r] = (uint32_t)r;
           __syncthreads();
-          const int emax = ctr[C_EMAX];
+          const int emax = emax_all;
           double wsum = 0.0, esum = 0.0;
           for (int r = tid; r < m; r += BLOCK) esum += (double)eLr[r];
           for (int t = emax; t >= 1; --t) {
