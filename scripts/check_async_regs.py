@@ -1,49 +1,84 @@
-"""Static check of the async-load discipline in the LDS kernel's ISA: between an inline-asm global_load into
-v[a:b] and the next inline-asm s_waitcnt vmcnt (linear order), no other instruction may read or write
-v[a..b] except another inline-asm load into the same registers.  usage: check_async_regs.py file.s [kernel]"""
-import re, sys
+"""Static check of the async-load discipline in the LDS kernel's ISA (hipcc -S output).
+
+For every inline-asm global_load into v[a:b], every control-flow path from the load (following s_branch /
+s_cbranch_* targets and fall-through) must reach a counted wait (inline-asm s_waitcnt) or a full vmcnt(0)
+drain before any other instruction reads or writes v[a..b]; the only exception is another inline-asm load
+into the same registers (its "+v" operand keeps them allocated).  Also fails on a spill of any async-load
+destination register (a spill could copy a load still in flight).
+
+usage: check_async_regs.py file.s [kernel-symbol-prefix]
+"""
+import re
+import sys
 
 src = open(sys.argv[1]).read().split("\n")
 kern = sys.argv[2] if len(sys.argv) > 2 else "_ZN3smg15ion_pipe_kernelILi0E"
 bad = total = 0
-starts = [i for i, l in enumerate(src) if l.startswith(kern)]
-for st in starts:
-    en = next(i for i in range(st, len(src)) if src[i].strip().startswith(".size") and kern in src[i])
+
+
+def regs(tok):
+    m = re.match(r"v\[(\d+):(\d+)\]", tok)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.match(r"v(\d+)$", tok)
+    return {int(m.group(1))} if m else set()
+
+
+for st in [i for i, l in enumerate(src) if l.startswith(kern)]:
+    name = src[st].split(":")[0]
+    en = next(i for i in range(st, len(src)) if src[i].strip().startswith(".size") and name in src[i])
     body = [l.strip() for l in src[st:en]]
-    in_asm = [False] * len(body)
-    f = False
+    in_asm, f = [False] * len(body), False
     for i, l in enumerate(body):
         if l.startswith(";;#ASMSTART"):
             f = True
         elif l.startswith(";;#ASMEND"):
             f = False
         in_asm[i] = f
-
-    def regs(tok):
-        m = re.match(r"v\[(\d+):(\d+)\]", tok)
-        if m:
-            return set(range(int(m.group(1)), int(m.group(2)) + 1))
-        m = re.match(r"v(\d+)$", tok)
-        return {int(m.group(1))} if m else set()
-
+    labels = {l[:-1]: i for i, l in enumerate(body) if re.match(r"^\.LBB\w+:$", l)}
+    dsts = set()
     for i, l in enumerate(body):
-        if not (in_asm[i] and l.startswith("global_load_dwordx2")):
+        if not (in_asm[i] and l.startswith("global_load")):
             continue
         total += 1
         dst = regs(l.split()[1].rstrip(","))
-        for j in range(i + 1, len(body)):
-            t = body[j]
-            if in_asm[j] and t.startswith("s_waitcnt"):
-                break
-            if not t or t.startswith((".", ";")) or t.endswith(":"):
-                continue
-            toks = [x.strip(",") for x in t.split()]
-            touched = set()
-            for x in toks[1:]:
-                touched |= regs(x)
-            if touched & dst and not (in_asm[j] and t.startswith("global_load_dwordx2")):
-                print("VIOLATION", kern, i, l, "->", j, t)
+        dsts |= dst
+        seen, stack, hit = set(), [i + 1], None
+        while stack and hit is None:
+            j = stack.pop()
+            while j < len(body) and j not in seen:
+                seen.add(j)
+                t = body[j]
+                if (in_asm[j] and t.startswith("s_waitcnt")) or (t.startswith("s_waitcnt") and "vmcnt(0)" in t):
+                    break
+                if not t or t.startswith((".", ";")) or t.endswith(":"):
+                    j += 1
+                    continue
+                toks = [x.strip(",") for x in t.split()]
+                touched = set()
+                for x in toks[1:]:
+                    touched |= regs(x)
+                if touched & dst and not (in_asm[j] and t.startswith("global_load")):
+                    hit = (j, t)
+                    break
+                op = toks[0]
+                if op.startswith("s_cbranch") or op == "s_branch":
+                    tgt = toks[1] if len(toks) > 1 else ""
+                    if tgt in labels:
+                        stack.append(labels[tgt])
+                    if op == "s_branch":
+                        break
+                if op in ("s_endpgm", "s_setpc_b64"):
+                    break
+                j += 1
+        if hit:
+            print("VIOLATION", name[:60], i, l, "->", hit[0], hit[1])
+            bad += 1
+    for l in body:
+        if l.startswith("scratch_store") or (l.startswith("buffer_store") and "Spill" in l):
+            src_regs = regs(l.split()[2].rstrip(",")) if len(l.split()) > 2 else set()
+            if src_regs & dsts:
+                print("SPILL of an async-load register", name[:60], l)
                 bad += 1
-                break
 print(f"{total} async loads checked, {bad} violations")
 sys.exit(1 if bad else 0)

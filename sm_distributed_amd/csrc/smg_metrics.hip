@@ -114,6 +114,17 @@ struct PixVal {
 __device__ __forceinline__ void ld8_async(uint64_t& r, const void* sbase, uint32_t voff) {
   asm volatile("global_load_dwordx2 %0, %1, %2" : "+v"(r) : "v"(voff), "s"(sbase) : "memory");
 }
+__device__ __forceinline__ void ld8_async_v(uint64_t& r, const void* addr) {  // 64-bit vector address
+  asm volatile("global_load_dwordx2 %0, %1, off" : "+v"(r) : "v"(addr) : "memory");
+}
+__device__ __forceinline__ void ld4_async_v(uint32_t& r, const void* addr) {
+  asm volatile("global_load_dword %0, %1, off" : "+v"(r) : "v"(addr) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait1(uint32_t& r) {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  asm volatile("" : "+v"(r));
+}
 template <int N, int M>
 __device__ __forceinline__ void vm_wait(uint64_t (&r)[M]) {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -557,24 +568,36 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   const int n64 = (P.npx + 63) / 64;
   const uint32_t big_flag = (SRC == SRC_LIST) ? SMG_ION_BIG : 0u;
 
+  // Register buffers: the tail is streamed through a ring of four chunk buffers (pa, pb, pc, pd); the principal
+  // window of the next ion arrives in pc, pd, pe (RMAX slots), which become tail buffers once phase 1 has
+  // consumed it.  Issue order per ion: [principal, pa <- chunk 0, pb <- chunk 1] at the previous ion's issue
+  // site, then [pc <- chunk 2, pd <- chunk 3] after phase 1, then each buffer is refilled four chunks ahead as
+  // soon as it is processed, so every tail wait has exactly three younger buffers (3*RC loads) behind it.
+  static_assert(RMAX >= 2 * RC, "principal slots double as two tail buffers");
+  constexpr int RE = RMAX - 2 * RC > 0 ? RMAX - 2 * RC : 1;
+  Reg pa[RC], pb[RC], pc[RC], pd[RC], pe[RE];
+#pragma unroll
+  for (int j = 0; j < RC; ++j) pa[j] = pb[j] = pc[j] = pd[j] = Hits<FMT>::zero();
+#pragma unroll
+  for (int j = 0; j < RE; ++j) pe[j] = Hits<FMT>::zero();
+  auto hs = [&](int j) -> Reg& { return j < RC ? pc[j] : (j < 2 * RC ? pd[j - RC] : pe[j - 2 * RC]); };
   constexpr bool ASYNC = (FMT == SMG_HITS_PACKED_F32);
   // principal window (<= CAPC points, RMAX per thread).  Async form: every slot issues exactly one load
   // (clamped to the window's last point, or to hit 0 for an empty window) so that the counted waits hold.
-  auto issue_principal = [&](const IonDesc* D, Reg (&buf)[RMAX]) {
-    const int n0 = uni(D->end[0]);
-    const int64_t a = uni64(D->base[0]);
+  auto issue_principal = [&](const IonDesc* D) {
+    const int n0 = D->end[0];
+    const int64_t a = D->base[0];
     if constexpr (ASYNC) {
-      const uint64_t* sb = n0 > 0 ? hits.h + a : hits.h;
 #pragma unroll
       for (int j = 0; j < RMAX; ++j) {
         const int i = tid + j * BLOCK;
-        ld8_async(buf[j], sb, (uint32_t)(n0 > 0 ? min(i, n0 - 1) : 0) * 8u);
+        ld8_async_v(hs(j), hits.h + (n0 > 0 ? a + min(i, n0 - 1) : 0));
       }
     } else {
 #pragma unroll
       for (int j = 0; j < RMAX; ++j) {
         const int i = tid + j * BLOCK;
-        if (i < n0) buf[j] = hits.load(a, i);
+        if (i < n0) hs(j) = hits.load(a, i);
       }
     }
   };
@@ -582,43 +605,55 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   // exactly RC loads per chunk; lanes past their window's end load its last point, groups past the tail
   // load hit 0 (consumers mask both).  Compiler form: such lanes hold a zero hit.
   auto issue_chunk = [&](const IonDesc* D, int c, Reg (&buf)[RC]) {
-    const int ng = uni(D->ngroups);
+    // descriptor fields are read as broadcast LDS loads into VGPRs (no readfirstlane round trips)
+    const int ng = D->ngroups;
+    int gsv[MAXK];
+#pragma unroll
+    for (int kk = 2; kk < MAXK; ++kk) gsv[kk] = D->gs[kk];
 #pragma unroll
     for (int j = 0; j < RC; ++j) {
       const int G = c * GPC + j * NW + wid;
       int k = 1;
 #pragma unroll
-      for (int kk = 2; kk < MAXK; ++kk) k += (G >= uni(D->gs[kk])) ? 1 : 0;
+      for (int kk = 2; kk < MAXK; ++kk) k += (G >= gsv[kk]) ? 1 : 0;
       if constexpr (ASYNC) {
-        const uint64_t* sb = hits.h;
-        uint32_t off = 0;
-        if (G < ng) {
-          sb = hits.h + (uni64(D->base[k]) + (int64_t)G * 64);
-          off = (uint32_t)min(lane, uni(D->end[k]) - G * 64 - 1) * 8u;
-        }
-        ld8_async(buf[j], sb, off);
+        const int64_t bk = D->base[k];
+        const int ek = D->end[k];
+        const int64_t idx = G < ng ? bk + (int64_t)G * 64 + min(lane, ek - G * 64 - 1) : 0;
+        ld8_async_v(buf[j], hits.h + idx);
       } else {
         buf[j] = Hits<FMT>::zero();
         if (G < ng) {
           const int i = G * 64 + lane;
-          if (i < uni(D->end[k])) buf[j] = hits.load(uni64(D->base[k]) + i);
+          if (i < D->end[k]) buf[j] = hits.load(D->base[k] + i);
         }
       }
     }
   };
 
-  Reg h0[RMAX], ra[RC], rb[RC];
-#pragma unroll
-  for (int j = 0; j < RMAX; ++j) h0[j] = Hits<FMT>::zero();
-#pragma unroll
-  for (int j = 0; j < RC; ++j) ra[j] = rb[j] = Hits<FMT>::zero();
+  // scheduling runs one ion further ahead than the loads: iteration b scores pos, loads npos's descriptor and
+  // data, and takes the ticket of the ion after npos
+  if (tid == 0) ctr[C_NEXT] = (int)sched_resolve<SRC>(S, sched_issue<SRC>(S));
+  __syncthreads();
   int64_t pos = -1;  // ion scored in this iteration (-1: none; the first iteration only issues loads)
+  int64_t npos = uni(ctr[C_NEXT]);
   int cur = 0;
   while (true) {
     const IonDesc* D = &dsl[cur];
     IonDesc* DN = &dsl[cur ^ 1];
     uint32_t ticket = 0;
     if (tid == 0) ticket = sched_issue<SRC>(S);
+    // npos's descriptor: one async word per lane of wave 0 (exactly one load per lane, clamped), waited in
+    // phase 2 behind the 2*RC loads of tail chunks 2 and 3
+    uint32_t dword = 0;
+    if (wid == 0) {
+      if constexpr (ASYNC) {
+        ld4_async_v(dword, reinterpret_cast<const uint32_t*>(desc + (npos >= 0 ? npos : 0)) +
+                               (lane < DESC_WORDS ? lane : 0));
+      } else {
+        if (npos >= 0 && lane < DESC_WORDS) dword = reinterpret_cast<const uint32_t*>(desc + npos)[lane];
+      }
+    }
     STAMP_INIT();
     bool skip = pos < 0;
     int K = 0, ion = 0, n0 = 0;
@@ -655,13 +690,15 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     int nnz = 0;
     uint32_t* olist = nullptr;
     if (!skip) {
-      vm_wait<2 * RC>(h0);  // issued before this ion's two prefetched tail chunks
+      vm_wait<2 * RC>(pc);  // the principal window was issued before this ion's tail chunks 0 and 1
+      vm_wait<2 * RC>(pd);
+      vm_wait<2 * RC>(pe);
       uint32_t own = 0;     // slots whose atomicOr set the pixel's bit (one owner per distinct pixel)
 #pragma unroll
       for (int j = 0; j < RMAX; ++j) {
         const int i = tid + j * BLOCK;
         if (i < n0) {
-          const uint32_t p = Hits<FMT>::pix(h0[j]);
+          const uint32_t p = Hits<FMT>::pix(hs(j));
           const uint32_t bit = 1u << (p & 31);
           if (!(atomicOr(&Hbm[p >> 5], bit) & bit)) own |= 1u << j;
         }
@@ -677,11 +714,11 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       for (int j = 0; j < RMAX; ++j) {
         const int i = tid + j * BLOCK;
         if (i < n0) {
-          const int r = bm_rank(Hbm, pf, (int)Hits<FMT>::pix(h0[j]));
-          const bool d = Hits<FMT>::dup(h0[j]);
-          vals[r] = d ? 0.0 : Hits<FMT>::val(h0[j]);
+          const int r = bm_rank(Hbm, pf, (int)Hits<FMT>::pix(hs(j)));
+          const bool d = Hits<FMT>::dup(hs(j));
+          vals[r] = d ? 0.0 : Hits<FMT>::val(hs(j));
           any_dup |= d;
-          if (nnz <= OL_MAX && ((own >> j) & 1u)) olist[r] = Hits<FMT>::pix(h0[j]);
+          if (nnz <= OL_MAX && ((own >> j) & 1u)) olist[r] = Hits<FMT>::pix(hs(j));
         }
       }
       if (any_dup) ctr[C_PDUP] = 1;
@@ -690,16 +727,18 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
 #pragma unroll
         for (int j = 0; j < RMAX; ++j) {
           const int i = tid + j * BLOCK;
-          if (i < n0 && Hits<FMT>::dup(h0[j]))
-            atomicAdd(&vals[bm_rank(Hbm, pf, (int)Hits<FMT>::pix(h0[j]))], Hits<FMT>::val(h0[j]));
+          if (i < n0 && Hits<FMT>::dup(hs(j)))
+            atomicAdd(&vals[bm_rank(Hbm, pf, (int)Hits<FMT>::pix(hs(j)))], Hits<FMT>::val(hs(j)));
         }
       }
     }
+    if (!skip) {  // the principal registers are consumed: tail chunks 2 and 3 go in flight
+      issue_chunk(D, 2, pc);
+      issue_chunk(D, 3, pd);
+    }
     if (tid == 0) ctr[C_NEXT] = (int)sched_resolve<SRC>(S, ticket);
     __syncthreads();
-    const int64_t npos = uni(ctr[C_NEXT]);
-    uint32_t dword = 0;
-    if (npos >= 0 && tid < DESC_WORDS) dword = reinterpret_cast<const uint32_t*>(desc + npos)[tid];
+    const int64_t n2pos = uni(ctr[C_NEXT]);
     STAMP(1);
 
     // ---- phase 2: fused principal-image statistics, then level index per pixel -------------------
@@ -725,7 +764,10 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
           for (int q = 0; q < 5; ++q) red[q * NW + wid] = acc[q];
         }
       }
-      if (npos >= 0 && tid < DESC_WORDS) reinterpret_cast<uint32_t*>(DN)[tid] = dword;
+      if (wid == 0) {
+        if constexpr (ASYNC) vm_wait1<2 * RC>(dword);
+        if (npos >= 0 && lane < DESC_WORDS) reinterpret_cast<uint32_t*>(DN)[lane] = dword;
+      }
       __syncthreads();
       if (!skip) {
         double t[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
@@ -831,16 +873,23 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         }
       };
       // chunks 0 and 1 are in flight (issued during the previous iteration); later chunks one ahead
-      // (refills are issued unconditionally so that exactly RC loads follow each buffer's)
-      for (int c = 0; c * GPC < ng; c += 2) {
-        vm_wait<RC>(ra);
-        process(c, ra);
-        if ((SMG_ABL & 4) && c >= 0) break;
-        issue_chunk(D, c + 2, ra);
+      // (refills are issued unconditionally so that exactly 3*RC loads follow each buffer's)
+      for (int c = 0; c * GPC < ng; c += 4) {
+        vm_wait<3 * RC>(pa);
+        process(c, pa);
+        issue_chunk(D, c + 4, pa);
         if ((c + 1) * GPC >= ng) break;
-        vm_wait<RC>(rb);
-        process(c + 1, rb);
-        issue_chunk(D, c + 3, rb);
+        vm_wait<3 * RC>(pb);
+        process(c + 1, pb);
+        issue_chunk(D, c + 5, pb);
+        if ((c + 2) * GPC >= ng) break;
+        vm_wait<3 * RC>(pc);
+        process(c + 2, pc);
+        issue_chunk(D, c + 6, pc);
+        if ((c + 3) * GPC >= ng) break;
+        vm_wait<3 * RC>(pd);
+        process(c + 3, pd);
+        issue_chunk(D, c + 7, pd);
       }
       flush();
       if (lane == 0) dcnt[wid] = nd;
@@ -849,9 +898,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     }
     // ---- the registers of ion b are dead: ion b+1's principal window and first two chunks go in flight
     if (npos >= 0 && desc_lds_ok(DN, CAPC)) {
-      issue_principal(DN, h0);
-      issue_chunk(DN, 0, ra);
-      issue_chunk(DN, 1, rb);
+      issue_principal(DN);
+      issue_chunk(DN, 0, pa);
+      issue_chunk(DN, 1, pb);
     }
     __syncthreads();
     // ---- deferred duplicate candidates: exact per-(pixel, window) sums, squared into the partials --------
@@ -1214,14 +1263,17 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     }
     if (npos < 0) break;
     pos = npos;
+    npos = n2pos;
     cur ^= 1;
     __syncthreads();  // the next ion re-initialises the LDS structures
     STAMP(7);
   }
   // no load of this wave outlives it
-  vm_wait<0>(h0);
-  vm_wait<0>(ra);
-  vm_wait<0>(rb);
+  vm_wait<0>(pa);
+  vm_wait<0>(pb);
+  vm_wait<0>(pc);
+  vm_wait<0>(pd);
+  vm_wait<0>(pe);
 }
 
 // position list -> ion list (when the big-ion pass is skipped, the dense kernel reads ion indices)
