@@ -3,8 +3,8 @@
 For every inline-asm global_load into v[a:b], every control-flow path from the load (following s_branch /
 s_cbranch_* targets and fall-through) must reach a counted wait (inline-asm s_waitcnt) or a full vmcnt(0)
 drain before any other instruction reads or writes v[a..b]; the only exception is another inline-asm load
-into the same registers (its "+v" operand keeps them allocated).  Also fails on a spill of any async-load
-destination register (a spill could copy a load still in flight).
+into the same registers (its "+v" operand keeps them allocated).  Spills are covered: a scratch_store of such
+a register on such a path is a read of it.
 
 usage: check_async_regs.py file.s [kernel-symbol-prefix]
 """
@@ -74,11 +74,5 @@ for st in [i for i, l in enumerate(src) if l.startswith(kern)]:
         if hit:
             print("VIOLATION", name[:60], i, l, "->", hit[0], hit[1])
             bad += 1
-    for l in body:
-        if l.startswith("scratch_store") or (l.startswith("buffer_store") and "Spill" in l):
-            src_regs = regs(l.split()[2].rstrip(",")) if len(l.split()) > 2 else set()
-            if src_regs & dsts:
-                print("SPILL of an async-load register", name[:60], l)
-                bad += 1
 print(f"{total} async loads checked, {bad} violations")
 sys.exit(1 if bad else 0)

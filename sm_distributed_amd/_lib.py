@@ -35,7 +35,9 @@ PROTOTYPES = {
     "smg_sort_points": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _SZ, _P]),
     "smg_window_bounds": (ctypes.c_int, [_P, _P, _I64, _D, _P, _I64, _P, _P, _P]),
     "smg_ion_metrics_workspace_size": (ctypes.c_int, [_I64, _I32, _I32, ctypes.POINTER(_SZ)]),
-    "smg_ion_metrics": (ctypes.c_int, [_I32, _P, _P, _P, _P, _P, _P, _P, _I64, _I32, _I32, _I32, _D, _I32,
+    "smg_hit_prefix_sums_workspace_size": (ctypes.c_int, [_I64, ctypes.POINTER(_SZ)]),
+    "smg_hit_prefix_sums": (ctypes.c_int, [_I32, _P, _P, _I64, _P, _P, _SZ, _P]),
+    "smg_ion_metrics": (ctypes.c_int, [_I32, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I32, _I32, _I32, _D, _I32,
                                        _I32, _I32, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "smg_sample_spectra": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _I64, _P, _P, _P, _I64, _P, _P]),
     "smg_debug_stream_read": (ctypes.c_int, [_P, _I64, _P, _I32, _P]),

@@ -121,7 +121,7 @@ __device__ __forceinline__ void ld4_async_v(uint32_t& r, const void* addr) {
   asm volatile("global_load_dword %0, %1, off" : "+v"(r) : "v"(addr) : "memory");
 }
 template <int N>
-__device__ __forceinline__ void vm_wait1(uint32_t& r) {
+__device__ __forceinline__ void vm_wait1(uint64_t& r) {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
   asm volatile("" : "+v"(r));
 }
@@ -339,7 +339,7 @@ struct Lay {
   static constexpr uint32_t o_ctr = cal16(o_red + 8 * NW * 8);
   static constexpr uint32_t o_wsc = cal16(o_ctr + C_NCTR * 4);
   static constexpr uint32_t o_desc = cal16(o_wsc + NW * 4);  // two ion descriptors (current, next)
-  static constexpr uint32_t o_guard = cal16(o_desc + 2 * 256);
+  static constexpr uint32_t o_guard = cal16(o_desc + 2 * 384);
   static constexpr uint32_t o_bm = o_guard + 16;
   static int w32(int npx) { return (((npx + 31) / 32 + 2) + 3) & ~3; }
   static uint32_t o_pf(int npx) { return cal16(o_bm + (uint32_t)w32(npx) * 4); }
@@ -386,15 +386,18 @@ struct IonDesc {
   int32_t end[MAXK];   // [0]: principal points; [k>=1]: 64*gs[k] + n[k] (end of window k in the padded tail)
   int32_t gs[MAXK];    // [k>=1]: first group of window k; INT_MAX for k >= K
   double theor[MAXK];  // theoretical intensities
+  double sy[MAXK];     // window sums of intensities (prefix-sum differences, smg_hit_prefix_sums)
+  double syy[MAXK];    // window sums of squared intensities over points without the duplicate flag
   int32_t ion, K, ngroups, hits;  // ngroups < 0: tail too long for 32-bit positions (dense path)
   int32_t pad[12];
 };
-static_assert(sizeof(IonDesc) == 256, "IonDesc is 256 B");
-constexpr int DESC_WORDS = (int)(sizeof(IonDesc) / 4);
+static_assert(sizeof(IonDesc) == 384, "IonDesc is 384 B");
+constexpr int DESC_QWORDS = (int)(sizeof(IonDesc) / 8);  // 48: one 8-byte load per lane of wave 0
 
 __global__ void ion_desc_kernel(const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
                                 const int64_t* __restrict__ ion_off, const double* __restrict__ theor,
-                                const int64_t* __restrict__ ion_order, int64_t n_ions, IonDesc* __restrict__ out) {
+                                const double2* __restrict__ cum, const int64_t* __restrict__ ion_order,
+                                int64_t n_ions, IonDesc* __restrict__ out) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n_ions) return;
   const int64_t ion = ion_order ? ion_order[b] : b;
@@ -405,16 +408,19 @@ __global__ void ion_desc_kernel(const int64_t* __restrict__ lo, const int64_t* _
   uint32_t has = 0;
   int64_t wb[MAXK];
   int32_t we[MAXK], wg[MAXK];
-  double wt[MAXK];
+  double wt[MAXK], wy[MAXK], wyy[MAXK];
 #pragma unroll
   for (int k = 0; k < MAXK; ++k) {
     wb[k] = 0;
     we[k] = 0;
     wg[k] = 0x7FFFFFFF;
-    wt[k] = 0.0;
+    wt[k] = wy[k] = wyy[k] = 0.0;
     if (k < K) {
       const int64_t a = lo[w0 + k], n = hi[w0 + k] - a;
       wt[k] = theor[w0 + k];
+      const double2 c1 = cum[a + n], c0 = cum[a];
+      wy[k] = c1.x - c0.x;
+      wyy[k] = c1.y - c0.y;
       if (n > 0) has = SMG_ION_HAS_HITS;
       if (k == 0) {
         wb[k] = a;
@@ -434,6 +440,8 @@ __global__ void ion_desc_kernel(const int64_t* __restrict__ lo, const int64_t* _
   for (int k = 0; k < MAXK; k += 2) {
     reinterpret_cast<longlong2*>(d->base)[k / 2] = make_longlong2(wb[k], wb[k + 1]);
     reinterpret_cast<double2*>(d->theor)[k / 2] = make_double2(wt[k], wt[k + 1]);
+    reinterpret_cast<double2*>(d->sy)[k / 2] = make_double2(wy[k], wy[k + 1]);
+    reinterpret_cast<double2*>(d->syy)[k / 2] = make_double2(wyy[k], wyy[k + 1]);
   }
 #pragma unroll
   for (int k = 0; k < MAXK; k += 4) {
@@ -645,13 +653,13 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     if (tid == 0) ticket = sched_issue<SRC>(S);
     // npos's descriptor: one async word per lane of wave 0 (exactly one load per lane, clamped), waited in
     // phase 2 behind the 2*RC loads of tail chunks 2 and 3
-    uint32_t dword = 0;
+    uint64_t dword = 0;
     if (wid == 0) {
       if constexpr (ASYNC) {
-        ld4_async_v(dword, reinterpret_cast<const uint32_t*>(desc + (npos >= 0 ? npos : 0)) +
-                               (lane < DESC_WORDS ? lane : 0));
+        ld8_async_v(dword, reinterpret_cast<const uint64_t*>(desc + (npos >= 0 ? npos : 0)) +
+                               (lane < DESC_QWORDS ? lane : 0));
       } else {
-        if (npos >= 0 && lane < DESC_WORDS) dword = reinterpret_cast<const uint32_t*>(desc + npos)[lane];
+        if (npos >= 0 && lane < DESC_QWORDS) dword = reinterpret_cast<const uint64_t*>(desc + npos)[lane];
       }
     }
     STAMP_INIT();
@@ -765,8 +773,11 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         }
       }
       if (wid == 0) {
-        if constexpr (ASYNC) vm_wait1<2 * RC>(dword);
-        if (npos >= 0 && lane < DESC_WORDS) reinterpret_cast<uint32_t*>(DN)[lane] = dword;
+        if constexpr (ASYNC) {  // chunks 2 and 3 were issued after it only if this ion is being scored
+          if (skip) vm_wait1<0>(dword);
+          else vm_wait1<2 * RC>(dword);
+        }
+        if (npos >= 0 && lane < DESC_QWORDS) reinterpret_cast<uint64_t*>(DN)[lane] = dword;
       }
       __syncthreads();
       if (!skip) {
@@ -798,7 +809,10 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     // ---- phase 5: tail windows, one stream of window-aligned 64-point groups -------------------------
     if (!skip && !(SMG_ABL & 2)) {
       const int ng = uni(D->ngroups);
-      double psk = 0.0, psy = 0.0, psyy = 0.0, psxy = 0.0;
+      // Window sums of y and y^2 come from the prefix sums (descriptor); the stream only joins the tail against
+      // the principal image (sum xy, sum y[x>0]: nonzero for the few points whose pixel is in the principal
+      // image) and collects duplicate-candidate points.
+      double psk = 0.0, psxy = 0.0;
       int curk = 1;
       int nd = 0;  // this wave's deferred duplicate candidates (uniform)
       uint32_t* wdkey = dkey + wid * DSEG;
@@ -806,39 +820,22 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       int gnext = uni(D->gs[2]);
       int wend = uni(D->end[1]);
       auto flush = [&]() {
-        const double a0 = wave_sum_dpp(psk), a1 = wave_sum_dpp(psy), a2 = wave_sum_dpp(psyy),
-                     a3 = wave_sum_dpp(psxy);
+        const double a0 = wave_sum_dpp(psk), a3 = wave_sum_dpp(psxy);
         if (lane == 0) {
           double* pk = part + ((size_t)curk * NW + wid) * 4;
           pk[0] = a0;
-          pk[1] = a1;
-          pk[2] = a2;
           pk[3] = a3;
         }
-        psk = psy = psyy = psxy = 0.0;
+        psk = psxy = 0.0;
       };
-      // Lanes past the end of their window hold a zero hit (issue_chunk), which contributes nothing, so
-      // only whole groups past the tail need skipping.  Stage 1 does the principal-image lookups of every
-      // slot (LDS reads only, so the slots' lookups overlap); stage 2 accumulates slot by slot, flushing
-      // at window changes.
+      // Lanes past the end of their window hold a copy of its last point (masked by `valid`); groups past the
+      // tail are skipped.  Stage 1 reads the bitmap words of every slot at once; stage 2 handles slot by slot:
+      // window changes (flush), principal hits (rank + value lookups only in waves that have one), duplicate
+      // candidates.
       auto process = [&](int c, Reg (&buf)[RC]) {
-        double xs[RC];
         uint64_t bw[RC];
-        int rk[RC];
 #pragma unroll
-        for (int j = 0; j < RC; ++j) {
-          const uint32_t p = Hits<FMT>::pix(buf[j]);
-          bw[j] = reinterpret_cast<const uint64_t*>(Hbm)[p >> 6];
-          rk[j] = (int)pf[p >> 6];
-        }
-#pragma unroll
-        for (int j = 0; j < RC; ++j) {
-          const uint32_t p = Hits<FMT>::pix(buf[j]);
-          const uint64_t bit = 1ull << (p & 63);
-          const bool in = (bw[j] & bit) != 0ull;
-          const double x = vals[in ? rk[j] + __popcll(bw[j] & (bit - 1ull)) : 0];
-          xs[j] = (in && !(SMG_ABL & 16)) ? x : 0.0;
-        }
+        for (int j = 0; j < RC; ++j) bw[j] = reinterpret_cast<const uint64_t*>(Hbm)[Hits<FMT>::pix(buf[j]) >> 6];
 #pragma unroll
         for (int j = 0; j < RC; ++j) {
           const int G = c * GPC + j * NW + wid;
@@ -851,21 +848,23 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
             }
             const bool valid = lane < wend - G * 64;
             const uint32_t p = Hits<FMT>::pix(buf[j]);
-            const double v = valid ? Hits<FMT>::val(buf[j]) : 0.0;
-            const bool dup = valid && Hits<FMT>::dup(buf[j]) && !(SMG_ABL & 8);
-            const double x = xs[j];
-            psy += v;
-            psxy += x * v;
-            if (x > 0.0) psk += v;
-            if (!dup) psyy += v * v;
+            const uint64_t bit = 1ull << (p & 63);
+            const bool in = valid && (bw[j] & bit) != 0ull && !(SMG_ABL & 16);
+            if (__ballot(in)) {
+              const double x = in ? vals[(int)pf[p >> 6] + __popcll(bw[j] & (bit - 1ull))] : 0.0;
+              const double v = Hits<FMT>::val(buf[j]);
+              psxy += x * v;
+              if (x > 0.0) psk += v;
+            }
             // duplicate candidates are summed per (pixel, window) before squaring: appended to this wave's
             // list segment (ballot compaction, no atomics)
+            const bool dup = valid && Hits<FMT>::dup(buf[j]) && !(SMG_ABL & 8);
             const uint64_t dm = __ballot(dup);
             if (dm) {
               const int e = nd + (int)__popcll(dm & ((1ull << lane) - 1ull));
               if (dup && e < DSEG) {
                 wdkey[e] = (p << 3) | (uint32_t)curk;
-                wdval[e] = v;
+                wdval[e] = Hits<FMT>::val(buf[j]);
               }
               nd += (int)__popcll(dm);
             }
@@ -1217,11 +1216,12 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         if (k == 0) {
           s = s0;
         } else {
+          sy = D->sy[k];
+          syy = D->syy[k];  // + the squared per-pixel sums of duplicate candidates (part[k][*][2])
 #pragma unroll
           for (int w = 0; w < NW; ++w) {
             const double* pk = part + ((size_t)k * NW + w) * 4;
             s += pk[0];
-            sy += pk[1];
             syy += pk[2];
             sxy += pk[3];
           }
@@ -1576,7 +1576,7 @@ static constexpr int HDR_XCD = 64;
 static constexpr int MAIN_CFG[4] = {SMG_MAIN_CFG};
 static constexpr int MAIN_BLOCK = MAIN_CFG[0], MAIN_RMAX = MAIN_CFG[1], MAIN_RC = MAIN_CFG[2],
                      MAIN_WPE = MAIN_CFG[3];
-static constexpr int BIG_BLOCK = 1024, BIG_RMAX = 8, BIG_RC = 4;
+static constexpr int BIG_BLOCK = 1024, BIG_RMAX = 8, BIG_RC = 2;
 static constexpr size_t MAIN_LDS = 80 * 1024, BIG_LDS = 160 * 1024 - 512;
 
 static size_t ws_bytes_for(int64_t n_ions, int npx) {
@@ -1596,7 +1596,8 @@ static int device_cus() {
 }
 
 template <int FMT>
-static int launch_metrics(Hits<FMT> hits, const int64_t* lo, const int64_t* hi, const int64_t* ion_off,
+static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* lo, const int64_t* hi,
+                          const int64_t* ion_off,
                           const double* theor, const int64_t* ion_order, int64_t n_ions, const Params& P,
                           double* oc, double* osp, double* osc, double* omsm, uint32_t* oflags,
                           unsigned char* ws, hipStream_t st) {
@@ -1619,7 +1620,7 @@ static int launch_metrics(Hits<FMT> hits, const int64_t* lo, const int64_t* hi, 
   const int cus = device_cus();
   if (main_ok || big_ok) {
     hipLaunchKernelGGL(ion_desc_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, lo, hi, ion_off,
-                       theor, ion_order, n_ions, desc);
+                       theor, reinterpret_cast<const double2*>(hit_cum), ion_order, n_ions, desc);
     SMG_LAUNCH_CHECK();
   }
   if (main_ok) {
@@ -1690,7 +1691,8 @@ int smg_ion_metrics_workspace_size(int64_t n_ions, int32_t nrows, int32_t ncols,
   return SMG_OK;
 }
 
-int smg_ion_metrics(int32_t hit_format, const void* hits, const double* hit_vals, const int64_t* lo,
+int smg_ion_metrics(int32_t hit_format, const void* hits, const double* hit_vals, const double* hit_cum,
+                    const int64_t* lo,
                     const int64_t* hi, const int64_t* ion_win_off, const double* theor_int,
                     const int64_t* ion_order, int64_t n_ions, int32_t nrows, int32_t ncols, int32_t nlevels,
                     double q, int32_t do_preprocessing, int32_t connectivity, int32_t erosion_border,
@@ -1704,8 +1706,8 @@ int smg_ion_metrics(int32_t hit_format, const void* hits, const double* hit_vals
   SMG_CHECK_ARG(connectivity == 4 || connectivity == 8, "connectivity must be 4 or 8");
   SMG_CHECK_ARG(erosion_border == 0 || erosion_border == 1, "erosion_border must be 0 or 1");
   SMG_CHECK_ARG(hit_format == SMG_HITS_PACKED_F32 || hit_format == SMG_HITS_SPLIT_F64, "bad hit_format");
-  SMG_CHECK_ARG(lo && hi && ion_win_off && theor_int && out_chaos && out_spatial && out_spectral && out_msm &&
-                    out_flags && workspace,
+  SMG_CHECK_ARG(hit_cum && lo && hi && ion_win_off && theor_int && out_chaos && out_spatial && out_spectral &&
+                    out_msm && out_flags && workspace,
                 "null pointer");
   if (do_preprocessing) {
     set_error("do_preprocessing (q-percentile hot-spot clip) is not implemented on the device path yet");
@@ -1732,12 +1734,12 @@ int smg_ion_metrics(int32_t hit_format, const void* hits, const double* hit_vals
   if (hit_format == SMG_HITS_PACKED_F32) {
     SMG_CHECK_ARG(hits != nullptr, "null hits");
     Hits<SMG_HITS_PACKED_F32> h{reinterpret_cast<const uint64_t*>(hits), nullptr};
-    return launch_metrics<SMG_HITS_PACKED_F32>(h, lo, hi, ion_win_off, theor_int, ion_order, n_ions, P, out_chaos,
+    return launch_metrics<SMG_HITS_PACKED_F32>(h, hit_cum, lo, hi, ion_win_off, theor_int, ion_order, n_ions, P, out_chaos,
                                                out_spatial, out_spectral, out_msm, out_flags, ws, st);
   }
   SMG_CHECK_ARG(hits != nullptr && hit_vals != nullptr, "null hits");
   Hits<SMG_HITS_SPLIT_F64> h{reinterpret_cast<const uint32_t*>(hits), hit_vals};
-  return launch_metrics<SMG_HITS_SPLIT_F64>(h, lo, hi, ion_win_off, theor_int, ion_order, n_ions, P, out_chaos,
+  return launch_metrics<SMG_HITS_SPLIT_F64>(h, hit_cum, lo, hi, ion_win_off, theor_int, ion_order, n_ions, P, out_chaos,
                                             out_spatial, out_spectral, out_msm, out_flags, ws, st);
 }
 

@@ -9,6 +9,9 @@
 #include <stdarg.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "smg_common.hpp"
 
@@ -176,6 +179,31 @@ __global__ void stream_read_kernel(const uint64_t* __restrict__ p, int64_t n, ui
                                           (unsigned long long)acc);
 }
 
+// Per-point (v, v^2) prefix sums over the m/z-sorted hits (exclusive, out[0] = 0): window sums of
+// intensities and of squared intensities are then two differences per window.  Squares only for points
+// without the duplicate-candidate flag: a flagged point may share its pixel with another point of the window
+// and is squared after the per-pixel sum (ion kernel).
+struct VV {
+  double a, b;
+};
+struct VVAdd {
+  __host__ __device__ VV operator()(const VV& x, const VV& y) const { return VV{x.a + y.a, x.b + y.b}; }
+};
+struct PackedToVV {
+  __host__ __device__ VV operator()(uint64_t h) const {
+    const double v = (double)__uint_as_float((uint32_t)(h >> 32));
+    return VV{v, ((uint32_t)h >> 31) ? 0.0 : v * v};
+  }
+};
+struct SplitToVV {
+  const uint32_t* pix;
+  const double* val;
+  __host__ __device__ VV operator()(int64_t i) const {
+    const double v = val[i];
+    return VV{v, (pix[i] >> 31) ? 0.0 : v * v};
+  }
+};
+
 }  // namespace smg
 
 using namespace smg;
@@ -296,6 +324,52 @@ int smg_debug_stream_read(const uint64_t* data, int64_t n_words, uint64_t* out, 
   SMG_HIP(hipMemsetAsync(out, 0, (size_t)n_blocks * 8, st));
   hipLaunchKernelGGL(stream_read_kernel, dim3((unsigned)n_blocks), dim3(256), 0, st, data, n_words, out);
   SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+static hipError_t prefix_scan(void* tmp, size_t& bytes, int32_t hit_format, const void* hits, const double* hit_vals,
+                              int64_t n, double* out, hipStream_t st) {
+  VV* o = reinterpret_cast<VV*>(out) + 1;
+  if (hit_format == SMG_HITS_PACKED_F32) {
+    auto it = rocprim::make_transform_iterator(reinterpret_cast<const uint64_t*>(hits), PackedToVV());
+    return rocprim::inclusive_scan(tmp, bytes, it, o, (size_t)n, VVAdd(), st, false);
+  }
+  auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0),
+                                             SplitToVV{reinterpret_cast<const uint32_t*>(hits), hit_vals});
+  return rocprim::inclusive_scan(tmp, bytes, it, o, (size_t)n, VVAdd(), st, false);
+}
+
+int smg_hit_prefix_sums_workspace_size(int64_t n_points, size_t* bytes) {
+  SMG_CHECK_ARG(bytes != nullptr && n_points >= 0, "bad arguments");
+  size_t b0 = 0, b1 = 0;
+  hipError_t e = prefix_scan(nullptr, b0, SMG_HITS_PACKED_F32, nullptr, nullptr, n_points, nullptr, 0);
+  if (e == hipSuccess) e = prefix_scan(nullptr, b1, SMG_HITS_SPLIT_F64, nullptr, nullptr, n_points, nullptr, 0);
+  if (e != hipSuccess) {
+    set_error("rocprim scan workspace query failed: %s", hipGetErrorString(e));
+    return SMG_ERR_HIP;
+  }
+  *bytes = (b0 > b1 ? b0 : b1) + 256;
+  return SMG_OK;
+}
+
+int smg_hit_prefix_sums(int32_t hit_format, const void* hits, const double* hit_vals, int64_t n_points,
+                        double* cum, void* workspace, size_t workspace_bytes, void* stream) {
+  SMG_CHECK_ARG(n_points >= 0, "negative n_points");
+  SMG_CHECK_ARG(hit_format == SMG_HITS_PACKED_F32 || hit_format == SMG_HITS_SPLIT_F64, "bad hit_format");
+  SMG_CHECK_ARG(cum != nullptr, "null pointer");
+  hipStream_t st = as_stream(stream);
+  SMG_HIP(hipMemsetAsync(cum, 0, 2 * sizeof(double), st));
+  if (n_points == 0) return SMG_OK;
+  SMG_CHECK_ARG(hits && workspace && (hit_format == SMG_HITS_PACKED_F32 || hit_vals), "null pointer");
+  size_t need = 0;
+  int rc = smg_hit_prefix_sums_workspace_size(n_points, &need);
+  if (rc) return rc;
+  if (workspace_bytes < need) {
+    set_error("prefix-sum workspace too small: %zu < %zu", workspace_bytes, need);
+    return SMG_ERR_WORKSPACE;
+  }
+  size_t tb = need - 256;
+  SMG_HIP(prefix_scan(workspace, tb, hit_format, hits, hit_vals, n_points, cum, st));
   return SMG_OK;
 }
 

@@ -61,6 +61,8 @@ class DevicePeaks:
     hits_sorted: torch.Tensor | None = None
     flag_ppm: float | None = None
     sort_key_bits: int | None = None
+    cum: torch.Tensor | None = None  # prefix sums of the sorted hits (smg_hit_prefix_sums), float64[n+1, 2]
+    cum_valid: bool = False          # cum describes the current hits_sorted
 
     @property
     def n_points(self) -> int:
@@ -107,6 +109,7 @@ class DevicePeaks:
         if self.mz_sorted is None or self.mz_sorted.numel() != n:
             self.mz_sorted = torch.empty_like(self.mz)
             self.hits_sorted = torch.empty_like(self.hits)
+        self.cum_valid = False
         if n == 0:
             return self
         sz = ctypes.c_size_t(0)
@@ -115,6 +118,19 @@ class DevicePeaks:
         check(lib().smg_sort_points(_p(self.mz), _p(self.hits), n, self.key_bits(), _p(self.mz_sorted),
                                     _p(self.hits_sorted), _p(ws), ws.numel(), _stream(stream)), "smg_sort_points")
         return self
+
+    def prefix_sums(self, stream=None) -> "DevicePeaks":
+        """(sum v, sum v^2 of unflagged points) prefix sums over hits_sorted: window sums for the ion kernel."""
+        self.cum = hit_prefix_sums(_lib.SMG_HITS_PACKED_F32, self.hits_sorted, None, self.n_points, self.cum,
+                                   stream)
+        self.cum_valid = True
+        return self
+
+    def sorted_cum(self, stream=None) -> torch.Tensor:
+        """Prefix sums of the current sorted hits (recomputed after every sort)."""
+        if not self.cum_valid:
+            self.prefix_sums(stream)
+        return self.cum
 
     def key_bits(self) -> int:
         """Low bits in which the dataset's f32 m/z bit patterns differ (the sort ignores the common prefix);
@@ -186,7 +202,19 @@ class IonMetrics:
         return {k: getattr(self, k).cpu().numpy() for k in ("chaos", "spatial", "spectral", "msm", "flags")}
 
 
-def ion_metrics_raw(hit_format: int, hits: torch.Tensor, hit_vals, lo, hi, win_off, theor, ion_order,
+def hit_prefix_sums(hit_format: int, hits: torch.Tensor, hit_vals, n_points: int, out=None, stream=None):
+    device = hits.device
+    if out is None or out.shape[0] != n_points + 1:
+        out = torch.empty(n_points + 1, 2, dtype=torch.float64, device=device)
+    sz = ctypes.c_size_t(0)
+    check(lib().smg_hit_prefix_sums_workspace_size(n_points, ctypes.byref(sz)), "smg_hit_prefix_sums_workspace_size")
+    ws = workspace(sz.value, device, "scan")
+    check(lib().smg_hit_prefix_sums(hit_format, _p(hits), _p(hit_vals), n_points, _p(out), _p(ws), ws.numel(),
+                                    _stream(stream)), "smg_hit_prefix_sums")
+    return out
+
+
+def ion_metrics_raw(hit_format: int, hits: torch.Tensor, hit_vals, hit_cum, lo, hi, win_off, theor, ion_order,
                     n_ions: int, nrows: int, ncols: int, nlevels: int = 30, q: float = 99.0,
                     do_preprocessing: bool = False, connectivity: int = 4, erosion_border: int = 0,
                     out: IonMetrics | None = None, stream=None) -> IonMetrics:
@@ -200,7 +228,8 @@ def ion_metrics_raw(hit_format: int, hits: torch.Tensor, hit_vals, lo, hi, win_o
     check(lib().smg_ion_metrics_workspace_size(n_ions, nrows, ncols, ctypes.byref(sz)),
           "smg_ion_metrics_workspace_size")
     ws = workspace(sz.value, device, "metrics")
-    check(lib().smg_ion_metrics(hit_format, _p(hits), _p(hit_vals), _p(lo), _p(hi), _p(win_off), _p(theor),
+    check(lib().smg_ion_metrics(hit_format, _p(hits), _p(hit_vals), _p(hit_cum), _p(lo), _p(hi), _p(win_off),
+                                _p(theor),
                                 _p(ion_order), n_ions, nrows, ncols, nlevels, float(q), int(bool(do_preprocessing)),
                                 connectivity, erosion_border, _p(out.chaos), _p(out.spatial), _p(out.spectral),
                                 _p(out.msm), _p(out.flags), _p(ws), ws.numel(), _stream(stream)),
@@ -211,7 +240,9 @@ def ion_metrics_raw(hit_format: int, hits: torch.Tensor, hit_vals, lo, hi, win_o
 def ion_metrics(peaks: DevicePeaks, ions: DeviceIons, lo, hi, nlevels=30, q=99.0, do_preprocessing=False,
                 connectivity=4, erosion_border=0, out=None, stream=None) -> IonMetrics:
     """Fused imaging + MSM scoring of every ion (one launch for the LDS path, one for the dense path)."""
-    return ion_metrics_raw(_lib.SMG_HITS_PACKED_F32, peaks.hits_sorted, None, lo, hi, ions.win_off, ions.theor,
+    return ion_metrics_raw(_lib.SMG_HITS_PACKED_F32, peaks.hits_sorted, None, peaks.sorted_cum(stream), lo, hi,
+                           ions.win_off,
+                           ions.theor,
                            ions.ion_order, ions.n_ions, peaks.nrows, peaks.ncols, nlevels, q, do_preprocessing,
                            connectivity, erosion_border, out, stream)
 
@@ -231,6 +262,7 @@ def run_hot_path(peaks: DevicePeaks, ions: DeviceIons, ppm: float, nlevels: int 
     """One full pass: duplicate flags -> sort -> window search -> fused metrics (all on the current stream)."""
     peaks.flag_duplicates(ppm)
     peaks.sort()
+    peaks.prefix_sums()
     lo, hi = window_bounds(peaks, ions, ppm)
     return ion_metrics(peaks, ions, lo, hi, nlevels=nlevels, **kw), lo, hi
 
@@ -270,7 +302,8 @@ def metrics_from_images(ion_images, nrows, ncols, nlevels=30, q=99.0, do_preproc
     t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(device)
     d_pix = t(pix.view(np.int32), np.int32)
     d_val = t(val, np.float64)
-    res = ion_metrics_raw(_lib.SMG_HITS_SPLIT_F64, d_pix, d_val, t(lo_l, np.int64), t(hi_l, np.int64),
+    cum = hit_prefix_sums(_lib.SMG_HITS_SPLIT_F64, d_pix, d_val, pos)
+    res = ion_metrics_raw(_lib.SMG_HITS_SPLIT_F64, d_pix, d_val, cum, t(lo_l, np.int64), t(hi_l, np.int64),
                           t(off, np.int64), t(th_l, np.float64), None, n_ions, nrows, ncols, nlevels, q,
                           do_preprocessing, connectivity, erosion_border)
     torch.cuda.synchronize()

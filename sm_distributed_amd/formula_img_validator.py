@@ -147,7 +147,8 @@ def _metrics_device_batch(ims, sf_ints, img_conf):
     dev = ims.lo.device
     t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)
     nrows, ncols = ims.dims
-    m = E.ion_metrics_raw(SMG_HITS_PACKED_F32, ims.peaks.hits_sorted, None, lo_d, hi_d, t(win_off, np.int64),
+    m = E.ion_metrics_raw(SMG_HITS_PACKED_F32, ims.peaks.hits_sorted, None, ims.peaks.sorted_cum(), lo_d, hi_d,
+                          t(win_off, np.int64),
                           t(theor, np.float64), None, len(keys), nrows, ncols, **opts)
     r = m.to_numpy()
     has = (r["flags"] & 1) != 0

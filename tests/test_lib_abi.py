@@ -40,7 +40,7 @@ def test_version_and_argument_errors_without_gpu():
     assert b"bad arguments" in L.smg_last_error()
     assert L.smg_ion_metrics_workspace_size(10, 500, 500, ctypes.byref(sz)) == 0 and sz.value > 0
     # invalid nlevels is rejected before any device work
-    rc = L.smg_ion_metrics(0, None, None, None, None, None, None, None, 5, 10, 10, 0, 99.0, 0, 4, 0,
+    rc = L.smg_ion_metrics(0, None, None, None, None, None, None, None, None, 5, 10, 10, 0, 99.0, 0, 4, 0,
                            None, None, None, None, None, None, 0, None)
     assert rc == -1 and b"nlevels" in L.smg_last_error()
 
