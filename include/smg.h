@@ -77,19 +77,20 @@ int smg_sort_points(const float* mz, const uint64_t* hits, int64_t n_points, int
 int smg_window_bounds(const double* peak_mz, const int64_t* order, int64_t n_windows, double ppm,
                       const float* mz_sorted, int64_t n_points, int64_t* lo, int64_t* hi, void* stream);
 
-/* Per-point prefix sums over the m/z-sorted hits (exclusive, 2 doubles per entry, n_points+1 entries):
- * cum[i] = (sum of intensities of points < i, sum of squared intensities of those points without the
- * duplicate-candidate flag).  Window sums of the images of formula_imager_segm.py:84-92 become two
- * differences per window (smg_ion_metrics reads them).  hit_format/hits/hit_vals as smg_ion_metrics. */
+/* Prefix sums over the m/z-sorted hits at 64-point granularity (exclusive, 2 doubles per entry,
+ * ceil(n_points/64)+1 entries): cum64[b] = (sum of intensities of points < 64*b, sum of squared intensities
+ * of those points without the duplicate-candidate flag).  Window sums of the images of
+ * formula_imager_segm.py:84-92 become block-prefix differences plus at most 63 points at either end
+ * (smg_ion_metrics reads them).  hit_format/hits/hit_vals as smg_ion_metrics. */
 int smg_hit_prefix_sums_workspace_size(int64_t n_points, size_t* bytes);
 int smg_hit_prefix_sums(int32_t hit_format, const void* hits, const double* hit_vals, int64_t n_points,
-                        double* cum, void* workspace, size_t workspace_bytes, void* stream);
+                        double* cum64, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Fused ion imaging + MSM scoring (replaces formula_imager_segm.py:84-109 _gen_iso_images COO
  * construction + _img_pairs_to_list, and formula_img_validator.py:72-84,93-122 compute/sf_image_metrics).
  * Ion i owns windows [ion_win_off[i], ion_win_off[i+1]) in peak_i order; window w's image is the set
  * of points [lo[w], hi[w]) of the m/z-sorted hit array (duplicate pixels summed, as coo.toarray()).
- * hit_cum: smg_hit_prefix_sums of the same hits.
+ * hit_cum: smg_hit_prefix_sums (cum64) of the same hits.
  * theor_int[w] is the theoretical intensity of window w (FormulasSegm.get_sf_peak_ints).
  * Outputs (device, [n_ion]): cleaned chaos / spatial / spectral (ImgMeasures.to_tuple semantics),
  * msm = chaos*spatial*spectral, and SMG_ION_* flags.

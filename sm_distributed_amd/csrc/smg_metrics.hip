@@ -394,7 +394,23 @@ struct IonDesc {
 static_assert(sizeof(IonDesc) == 384, "IonDesc is 384 B");
 constexpr int DESC_QWORDS = (int)(sizeof(IonDesc) / 8);  // 48: one 8-byte load per lane of wave 0
 
-__global__ void ion_desc_kernel(const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
+// (sum v, sum v^2 of unflagged points) over hits [0, i): 64-point block prefix + the block's first i % 64 points
+template <int FMT>
+__device__ __forceinline__ double2 cum_at(const Hits<FMT>& hits, const double2* __restrict__ cum64, int64_t i) {
+  double2 c = cum64[i >> 6];
+  const int64_t a = i & ~(int64_t)63;
+#pragma unroll 4
+  for (int64_t j = a; j < i; ++j) {
+    const auto h = hits.load(j);
+    const double v = Hits<FMT>::val(h);
+    c.x += v;
+    if (!Hits<FMT>::dup(h)) c.y += v * v;
+  }
+  return c;
+}
+
+template <int FMT>
+__global__ void ion_desc_kernel(Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
                                 const int64_t* __restrict__ ion_off, const double* __restrict__ theor,
                                 const double2* __restrict__ cum, const int64_t* __restrict__ ion_order,
                                 int64_t n_ions, IonDesc* __restrict__ out) {
@@ -418,7 +434,7 @@ __global__ void ion_desc_kernel(const int64_t* __restrict__ lo, const int64_t* _
     if (k < K) {
       const int64_t a = lo[w0 + k], n = hi[w0 + k] - a;
       wt[k] = theor[w0 + k];
-      const double2 c1 = cum[a + n], c0 = cum[a];
+      const double2 c1 = cum_at<FMT>(hits, cum, a + n), c0 = cum_at<FMT>(hits, cum, a);
       wy[k] = c1.x - c0.x;
       wyy[k] = c1.y - c0.y;
       if (n > 0) has = SMG_ION_HAS_HITS;
@@ -1619,8 +1635,8 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   const bool big_ok = P.npx <= NPX_LDS_MAX && lds_big <= BIG_LDS;
   const int cus = device_cus();
   if (main_ok || big_ok) {
-    hipLaunchKernelGGL(ion_desc_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, lo, hi, ion_off,
-                       theor, reinterpret_cast<const double2*>(hit_cum), ion_order, n_ions, desc);
+    hipLaunchKernelGGL(ion_desc_kernel<FMT>, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, hits, lo, hi,
+                       ion_off, theor, reinterpret_cast<const double2*>(hit_cum), ion_order, n_ions, desc);
     SMG_LAUNCH_CHECK();
   }
   if (main_ok) {

@@ -10,8 +10,6 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
-#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "smg_common.hpp"
 
@@ -179,30 +177,42 @@ __global__ void stream_read_kernel(const uint64_t* __restrict__ p, int64_t n, ui
                                           (unsigned long long)acc);
 }
 
-// Per-point (v, v^2) prefix sums over the m/z-sorted hits (exclusive, out[0] = 0): window sums of
-// intensities and of squared intensities are then two differences per window.  Squares only for points
-// without the duplicate-candidate flag: a flagged point may share its pixel with another point of the window
-// and is squared after the per-pixel sum (ion kernel).
+// Prefix sums of (v, v^2) over the m/z-sorted hits at 64-point granularity: cum64[b] = sums over points
+// [0, 64*b) (exclusive, cum64[0] = 0).  A window sum is two block-prefix differences plus the partial sums of
+// at most 63 points at either end (ion_desc_kernel).  Squares only for points without the duplicate-candidate
+// flag: a flagged point may share its pixel with another point of the window and is squared after the
+// per-pixel sum (ion kernel).  One wave per block: a coalesced 512-B read, a fixed-order DPP reduction.
 struct VV {
   double a, b;
 };
 struct VVAdd {
   __host__ __device__ VV operator()(const VV& x, const VV& y) const { return VV{x.a + y.a, x.b + y.b}; }
 };
-struct PackedToVV {
-  __host__ __device__ VV operator()(uint64_t h) const {
-    const double v = (double)__uint_as_float((uint32_t)(h >> 32));
-    return VV{v, ((uint32_t)h >> 31) ? 0.0 : v * v};
+
+template <int FMT>
+__global__ void __launch_bounds__(256) block_sums64_kernel(const void* __restrict__ hits,
+                                                           const double* __restrict__ hit_vals, int64_t n,
+                                                           VV* __restrict__ out) {
+  const int64_t blk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int64_t nblk = (n + 63) >> 6;
+  if (blk >= nblk) return;  // whole waves exit together
+  const int64_t i = blk * 64 + lane;
+  double v = 0.0;
+  bool dup = false;
+  if (i < n) {
+    if constexpr (FMT == SMG_HITS_PACKED_F32) {
+      const uint64_t h = reinterpret_cast<const uint64_t*>(hits)[i];
+      v = (double)__uint_as_float((uint32_t)(h >> 32));
+      dup = ((uint32_t)h >> 31) != 0u;
+    } else {
+      v = hit_vals[i];
+      dup = (reinterpret_cast<const uint32_t*>(hits)[i] >> 31) != 0u;
+    }
   }
-};
-struct SplitToVV {
-  const uint32_t* pix;
-  const double* val;
-  __host__ __device__ VV operator()(int64_t i) const {
-    const double v = val[i];
-    return VV{v, (pix[i] >> 31) ? 0.0 : v * v};
-  }
-};
+  const double a = wave_sum_dpp(v), b = wave_sum_dpp(dup ? 0.0 : v * v);
+  if (lane == 0) out[blk] = VV{a, b};
+}
 
 }  // namespace smg
 
@@ -327,38 +337,30 @@ int smg_debug_stream_read(const uint64_t* data, int64_t n_words, uint64_t* out, 
   return SMG_OK;
 }
 
-static hipError_t prefix_scan(void* tmp, size_t& bytes, int32_t hit_format, const void* hits, const double* hit_vals,
-                              int64_t n, double* out, hipStream_t st) {
-  VV* o = reinterpret_cast<VV*>(out) + 1;
-  if (hit_format == SMG_HITS_PACKED_F32) {
-    auto it = rocprim::make_transform_iterator(reinterpret_cast<const uint64_t*>(hits), PackedToVV());
-    return rocprim::inclusive_scan(tmp, bytes, it, o, (size_t)n, VVAdd(), st, false);
-  }
-  auto it = rocprim::make_transform_iterator(rocprim::counting_iterator<int64_t>(0),
-                                             SplitToVV{reinterpret_cast<const uint32_t*>(hits), hit_vals});
-  return rocprim::inclusive_scan(tmp, bytes, it, o, (size_t)n, VVAdd(), st, false);
+static hipError_t block_scan(void* tmp, size_t& bytes, const VV* in, VV* out, int64_t nblk, hipStream_t st) {
+  return rocprim::inclusive_scan(tmp, bytes, in, out, (size_t)nblk, VVAdd(), st, false);
 }
 
 int smg_hit_prefix_sums_workspace_size(int64_t n_points, size_t* bytes) {
   SMG_CHECK_ARG(bytes != nullptr && n_points >= 0, "bad arguments");
-  size_t b0 = 0, b1 = 0;
-  hipError_t e = prefix_scan(nullptr, b0, SMG_HITS_PACKED_F32, nullptr, nullptr, n_points, nullptr, 0);
-  if (e == hipSuccess) e = prefix_scan(nullptr, b1, SMG_HITS_SPLIT_F64, nullptr, nullptr, n_points, nullptr, 0);
+  const int64_t nblk = (n_points + 63) / 64;
+  size_t b0 = 0;
+  hipError_t e = block_scan(nullptr, b0, nullptr, nullptr, nblk > 0 ? nblk : 1, 0);
   if (e != hipSuccess) {
     set_error("rocprim scan workspace query failed: %s", hipGetErrorString(e));
     return SMG_ERR_HIP;
   }
-  *bytes = (b0 > b1 ? b0 : b1) + 256;
+  *bytes = 256 + ((size_t)(nblk > 0 ? nblk : 1) * sizeof(VV) + 255) / 256 * 256 + b0;
   return SMG_OK;
 }
 
 int smg_hit_prefix_sums(int32_t hit_format, const void* hits, const double* hit_vals, int64_t n_points,
-                        double* cum, void* workspace, size_t workspace_bytes, void* stream) {
+                        double* cum64, void* workspace, size_t workspace_bytes, void* stream) {
   SMG_CHECK_ARG(n_points >= 0, "negative n_points");
   SMG_CHECK_ARG(hit_format == SMG_HITS_PACKED_F32 || hit_format == SMG_HITS_SPLIT_F64, "bad hit_format");
-  SMG_CHECK_ARG(cum != nullptr, "null pointer");
+  SMG_CHECK_ARG(cum64 != nullptr, "null pointer");
   hipStream_t st = as_stream(stream);
-  SMG_HIP(hipMemsetAsync(cum, 0, 2 * sizeof(double), st));
+  SMG_HIP(hipMemsetAsync(cum64, 0, 2 * sizeof(double), st));
   if (n_points == 0) return SMG_OK;
   SMG_CHECK_ARG(hits && workspace && (hit_format == SMG_HITS_PACKED_F32 || hit_vals), "null pointer");
   size_t need = 0;
@@ -368,8 +370,19 @@ int smg_hit_prefix_sums(int32_t hit_format, const void* hits, const double* hit_
     set_error("prefix-sum workspace too small: %zu < %zu", workspace_bytes, need);
     return SMG_ERR_WORKSPACE;
   }
-  size_t tb = need - 256;
-  SMG_HIP(prefix_scan(workspace, tb, hit_format, hits, hit_vals, n_points, cum, st));
+  const int64_t nblk = (n_points + 63) / 64;
+  VV* bs = reinterpret_cast<VV*>(reinterpret_cast<unsigned char*>(workspace) + 256);
+  unsigned char* tmp = reinterpret_cast<unsigned char*>(bs) + ((size_t)nblk * sizeof(VV) + 255) / 256 * 256;
+  size_t tb = need - (size_t)(tmp - reinterpret_cast<unsigned char*>(workspace));
+  const int64_t grid = (nblk * 64 + 255) / 256;
+  if (hit_format == SMG_HITS_PACKED_F32)
+    hipLaunchKernelGGL(block_sums64_kernel<SMG_HITS_PACKED_F32>, dim3((unsigned)grid), dim3(256), 0, st, hits,
+                       hit_vals, n_points, bs);
+  else
+    hipLaunchKernelGGL(block_sums64_kernel<SMG_HITS_SPLIT_F64>, dim3((unsigned)grid), dim3(256), 0, st, hits,
+                       hit_vals, n_points, bs);
+  SMG_LAUNCH_CHECK();
+  SMG_HIP(block_scan(tmp, tb, bs, reinterpret_cast<VV*>(cum64) + 1, nblk, st));
   return SMG_OK;
 }
 

@@ -61,7 +61,7 @@ class DevicePeaks:
     hits_sorted: torch.Tensor | None = None
     flag_ppm: float | None = None
     sort_key_bits: int | None = None
-    cum: torch.Tensor | None = None  # prefix sums of the sorted hits (smg_hit_prefix_sums), float64[n+1, 2]
+    cum: torch.Tensor | None = None  # 64-point block prefix sums of the sorted hits (smg_hit_prefix_sums)
     cum_valid: bool = False          # cum describes the current hits_sorted
 
     @property
@@ -204,8 +204,9 @@ class IonMetrics:
 
 def hit_prefix_sums(hit_format: int, hits: torch.Tensor, hit_vals, n_points: int, out=None, stream=None):
     device = hits.device
-    if out is None or out.shape[0] != n_points + 1:
-        out = torch.empty(n_points + 1, 2, dtype=torch.float64, device=device)
+    nb = (n_points + 63) // 64 + 1
+    if out is None or out.shape[0] != nb:
+        out = torch.empty(nb, 2, dtype=torch.float64, device=device)
     sz = ctypes.c_size_t(0)
     check(lib().smg_hit_prefix_sums_workspace_size(n_points, ctypes.byref(sz)), "smg_hit_prefix_sums_workspace_size")
     ws = workspace(sz.value, device, "scan")
