@@ -57,9 +57,11 @@ int smg_pack_hits(const int64_t* sp_off, const int32_t* pixel_map, int64_t n_spe
  * in the m/z-sorted spectrum with gap <= 2*ppm*1e-6*mz/(1-ppm*1e-6).  This pass sets the flag on exactly
  * those points (and on every point of a spectrum that is not m/z-sorted, or whose pixel is shared with
  * another spectrum: force[s] != 0), clears it elsewhere, and writes only hits whose flag changes.
+ * flag_state (optional, device uint8[n_points]) mirrors the flag each hit carries (initialise it from the hits:
+ * (hit >> 31) & 1); with it, hits are read only where the flag changes.
  * Run it on the dataset-order hits before smg_sort_points; consumers mask pixels with 0x7FFFFFFF. */
 int smg_flag_duplicates(const int64_t* sp_off, int64_t n_spectra, const float* mz, uint64_t* hits,
-                        int64_t n_points, double ppm, const uint8_t* force, void* stream);
+                        int64_t n_points, double ppm, const uint8_t* force, uint8_t* flag_state, void* stream);
 
 /* Global m/z sort of the packed points (the pandas sort_values('mz') of formula_imager_segm.py:73-74,
  * done once over the whole dataset instead of per m/z segment).  Keys are positive float32 m/z; only their
@@ -116,6 +118,22 @@ int smg_sample_spectra(const int64_t* sp_off, const double* mzs, const double* c
                        const double* lower, const double* upper, int64_t n_windows,
                        int64_t* out_window, int64_t* out_spectrum, double* out_value, int64_t capacity,
                        int64_t* count, void* stream);
+
+/* Theoretical isotope centroids (host code, no GPU): replaces the calculator behind
+ * isocalc_wrapper.py:37-70 (complete_isodist(parseSumFormula(sf + adduct), sigma, charge, pts_per_mz,
+ * centroid_kwargs={'weighted_bins': 5}) -> first centroids) as restated in oracle/isocalc_oracle.py: isotopic
+ * fine structure, Gaussian profile of FWHM sigma/2.35482 on the grid j/pts_per_mz, gradient centroids weighted
+ * over +-weighted_bins points, intensities scaled to max 100, ascending m/z.  sf_adduct is a sum formula with
+ * '+'/'-' sub-formulas ("C6H12O6+H"); charge z shifts by z electron masses and divides by |z|.  Writes the first
+ * min(cap, #centroids) centroids and their count; SMG_ERR_INVALID for an invalid formula (pyMSpec
+ * InvalidFormulaError).  The batch form runs n formulas (bytes formulas[offsets[i]:offsets[i+1]]) on n_threads
+ * host threads (<= 0: all cores; theor_peaks_gen.py:113-134's Spark fan-out), writing row i of the [n][cap]
+ * outputs and n_out[i] (-1: invalid formula). */
+int smg_isotope_centroids(const char* sf_adduct, int32_t charge, double sigma, int32_t pts_per_mz,
+                          int32_t weighted_bins, int32_t cap, double* mzs, double* ints, int32_t* n_out);
+int smg_isotope_centroids_batch(const char* formulas, const int64_t* offsets, int64_t n, int32_t charge,
+                                double sigma, int32_t pts_per_mz, int32_t weighted_bins, int32_t cap,
+                                double* mzs, double* ints, int32_t* n_out, int32_t n_threads);
 
 /* Diagnostics.  Calibration stream for the rocprofv3 HBM-traffic counters: reads n_words 8-byte words with
  * the ion kernel's access width (one coalesced 8-byte load per lane) and XOR-folds them into out[n_blocks]

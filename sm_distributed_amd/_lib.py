@@ -30,7 +30,7 @@ PROTOTYPES = {
     "smg_version": (ctypes.c_char_p, []),
     "smg_last_error": (ctypes.c_char_p, []),
     "smg_pack_hits": (ctypes.c_int, [_P, _P, _I64, _P, _I64, _P, _P]),
-    "smg_flag_duplicates": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _D, _P, _P]),
+    "smg_flag_duplicates": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _D, _P, _P, _P]),
     "smg_sort_points_workspace_size": (ctypes.c_int, [_I64, ctypes.POINTER(_SZ)]),
     "smg_sort_points": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _SZ, _P]),
     "smg_window_bounds": (ctypes.c_int, [_P, _P, _I64, _D, _P, _I64, _P, _P, _P]),
@@ -41,6 +41,9 @@ PROTOTYPES = {
                                        _I32, _I32, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "smg_sample_spectra": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _I64, _P, _P, _P, _I64, _P, _P]),
     "smg_debug_stream_read": (ctypes.c_int, [_P, _I64, _P, _I32, _P]),
+    "smg_isotope_centroids": (ctypes.c_int, [ctypes.c_char_p, _I32, _D, _I32, _I32, _I32, _P, _P,
+                                             ctypes.POINTER(_I32)]),
+    "smg_isotope_centroids_batch": (ctypes.c_int, [_P, _P, _I64, _I32, _D, _I32, _I32, _I32, _P, _P, _P, _I32]),
 }
 
 

@@ -138,30 +138,72 @@ __global__ void __launch_bounds__(256) sample_spectra_kernel(
   }
 }
 
-// duplicate-candidate flags: one workgroup per spectrum (grid-stride)
+// duplicate-candidate flags: one workgroup per spectrum (grid-stride).  A spectrum of <= FLAG_TILE points is
+// staged in LDS by one coalesced read, so the sortedness check and the neighbour tests read LDS.  With `state`
+// (one byte per point: the flag the hit currently carries), a hit is read and written only when its flag
+// changes, so a repeated pass reads 5 B per point instead of 12; without it every hit is read.
+constexpr int FLAG_TILE = 4096;
+__device__ __forceinline__ void flag_store(uint64_t* __restrict__ hits, uint8_t* __restrict__ state, int64_t i,
+                                           bool f) {
+  if (state) {
+    if (state[i] != (uint8_t)f) {
+      state[i] = (uint8_t)f;
+      const uint64_t h = hits[i];
+      hits[i] = f ? (h | 0x80000000ull) : (h & ~0x80000000ull);
+    }
+  } else {
+    const uint64_t h = hits[i];
+    const uint64_t nh = f ? (h | 0x80000000ull) : (h & ~0x80000000ull);
+    if (nh != h) hits[i] = nh;
+  }
+}
+
 __global__ void __launch_bounds__(256) flag_duplicates_kernel(const int64_t* __restrict__ sp_off, int64_t n_spectra,
                                                               const float* __restrict__ mz,
                                                               uint64_t* __restrict__ hits, double ppm,
-                                                              const uint8_t* __restrict__ force) {
+                                                              const uint8_t* __restrict__ force,
+                                                              uint8_t* __restrict__ state) {
+  __shared__ float smz[FLAG_TILE];
   const double slack = 2.0 * ppm * 1e-6 / (1.0 - ppm * 1e-6) * (1.0 + 1e-9);
   for (int64_t s = blockIdx.x; s < n_spectra; s += gridDim.x) {
     const int64_t a = sp_off[s], b = sp_off[s + 1];
-    int unsorted = 0;
-    for (int64_t i = a + 1 + threadIdx.x; i < b; i += blockDim.x) unsorted |= (mz[i] < mz[i - 1]);
-    const bool all = __syncthreads_or(unsorted) || (force && force[s]);
-    for (int64_t i = a + threadIdx.x; i < b; i += blockDim.x) {
-      bool f = all;
-      if (!f) {
-        const double m = (double)mz[i];
-        if (i > a) f = f || (m - (double)mz[i - 1] <= slack * m);
-        if (i + 1 < b) {
-          const double m2 = (double)mz[i + 1];
-          f = f || (m2 - m <= slack * m2);
+    if (b - a <= FLAG_TILE) {
+      const int n = (int)(b - a);
+      for (int i = threadIdx.x; i < n; i += blockDim.x) smz[i] = mz[a + i];
+      __syncthreads();
+      int unsorted = 0;
+      for (int i = threadIdx.x + 1; i < n; i += blockDim.x) unsorted |= (smz[i] < smz[i - 1]);
+      const bool all = __syncthreads_or(unsorted) || (force && force[s]);
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        bool f = all;
+        if (!f) {
+          const double m = (double)smz[i];
+          if (i > 0) f = f || (m - (double)smz[i - 1] <= slack * m);
+          if (i + 1 < n) {
+            const double m2 = (double)smz[i + 1];
+            f = f || (m2 - m <= slack * m2);
+          }
         }
+        flag_store(hits, state, a + i, f);
       }
-      const uint64_t h = hits[i];
-      const uint64_t nh = f ? (h | 0x80000000ull) : (h & ~0x80000000ull);
-      if (nh != h) hits[i] = nh;
+      __syncthreads();  // smz is reused by the next spectrum
+    } else {
+      int unsorted = 0;
+      for (int64_t i = a + 1 + threadIdx.x; i < b; i += blockDim.x) unsorted |= (mz[i] < mz[i - 1]);
+      const bool all = __syncthreads_or(unsorted) || (force && force[s]);
+      for (int64_t i = a + threadIdx.x; i < b; i += blockDim.x) {
+        bool f = all;
+        if (!f) {
+          const double m = (double)mz[i];
+          if (i > a) f = f || (m - (double)mz[i - 1] <= slack * m);
+          if (i + 1 < b) {
+            const double m2 = (double)mz[i + 1];
+            f = f || (m2 - m <= slack * m2);
+          }
+        }
+        flag_store(hits, state, i, f);
+      }
+      __syncthreads();
     }
   }
 }
@@ -237,28 +279,40 @@ int smg_pack_hits(const int64_t* sp_off, const int32_t* pixel_map, int64_t n_spe
 }
 
 int smg_flag_duplicates(const int64_t* sp_off, int64_t n_spectra, const float* mz, uint64_t* hits,
-                        int64_t n_points, double ppm, const uint8_t* force, void* stream) {
+                        int64_t n_points, double ppm, const uint8_t* force, uint8_t* flag_state, void* stream) {
   SMG_CHECK_ARG(n_spectra >= 0 && n_points >= 0 && ppm >= 0 && ppm < 1e6, "bad arguments");
   if (n_spectra == 0 || n_points == 0) return SMG_OK;
   SMG_CHECK_ARG(sp_off && mz && hits, "null pointer");
   const int64_t grid = n_spectra < (1 << 20) ? n_spectra : (1 << 20);
   hipLaunchKernelGGL(flag_duplicates_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream), sp_off,
-                     n_spectra, mz, hits, ppm, force);
+                     n_spectra, mz, hits, ppm, force, flag_state);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }
 
 // Onesweep radix sort of the f32 m/z bit patterns.  Only the low `key_bits` bits vary across a dataset whose
 // m/z lie in [lo, hi] (both bit patterns share everything above the highest bit where they differ), so the
-// sort covers [0, key_bits) (27 bits for m/z in [100, 1000)).  8 bits per pass: on MI355X (config 3, 5e8
-// pairs, 27 bits) 9/10/11-bit passes took 16.6/19.1/25.3 ms against 14.5 ms for four 8-bit passes.
+// sort covers [0, key_bits) (27 bits for m/z in [100, 1000)).  Three 9-bit passes, 512 threads x 16 items per
+// tile: on MI355X (config 3, 5e8 pairs, 27 bits; scripts/sort_ab.sh) 14.0 ms, against 14.8 ms for four 8-bit
+// passes at 1024 x 8 and 16.1-21.9 ms for the other tiles tried (8 bits 512x8/512x12/512x16/256x16, 9 bits
+// 1024x8/256x16).
 #ifndef SMG_SORT_RADIX_BITS
-#define SMG_SORT_RADIX_BITS 8
+#define SMG_SORT_RADIX_BITS 9
+#endif
+#ifndef SMG_SORT_BLOCK
+#define SMG_SORT_BLOCK 512
+#endif
+#ifndef SMG_SORT_IPT
+#define SMG_SORT_IPT 16
+#endif
+#ifndef SMG_SORT_RANK
+#define SMG_SORT_RANK match
 #endif
 using SortConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>,
-                                        SMG_SORT_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<SMG_SORT_BLOCK, SMG_SORT_IPT>,
+                                        rocprim::kernel_config<SMG_SORT_BLOCK, SMG_SORT_IPT>, SMG_SORT_RADIX_BITS,
+                                        rocprim::block_radix_rank_algorithm::SMG_SORT_RANK>>;
 
 int smg_sort_points_workspace_size(int64_t n_points, size_t* bytes) {
   SMG_CHECK_ARG(bytes != nullptr && n_points >= 0, "bad arguments");

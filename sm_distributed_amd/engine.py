@@ -57,6 +57,7 @@ class DevicePeaks:
     ncols: int
     sp_off: torch.Tensor | None = None     # int64[n_spectra+1] (dataset order), for duplicate flags
     force: torch.Tensor | None = None      # uint8[n_spectra]: spectra whose pixel is shared (non-injective map)
+    flag_state: torch.Tensor | None = None  # uint8[n_points]: duplicate flag each hit carries (smg_flag_duplicates)
     mz_sorted: torch.Tensor | None = None
     hits_sorted: torch.Tensor | None = None
     flag_ppm: float | None = None
@@ -99,8 +100,12 @@ class DevicePeaks:
         if self.sp_off is None:
             raise ValueError("DevicePeaks needs sp_off (spectrum offsets) for duplicate flags")
         n_sp = int(self.sp_off.numel()) - 1
+        if self.flag_state is None or self.flag_state.numel() != self.n_points:
+            # the flag each hit carries now (one byte per point): later passes touch only hits that change
+            self.flag_state = ((self.hits >> 31) & 1).to(torch.uint8)
         check(lib().smg_flag_duplicates(_p(self.sp_off), n_sp, _p(self.mz), _p(self.hits), self.n_points,
-                                        float(ppm), _p(self.force), _stream(stream)), "smg_flag_duplicates")
+                                        float(ppm), _p(self.force), _p(self.flag_state), _stream(stream)),
+              "smg_flag_duplicates")
         self.flag_ppm = float(ppm)
         return self
 
