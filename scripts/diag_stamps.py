@@ -24,10 +24,10 @@ m = E.ion_metrics(peaks, dions, lo, hi, nlevels=30)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 L.smg_debug_stamps(buf, 16)
-names = ["p0 load+zero", "p1 bitmap/prefix/vals", "p2-3 stats+levels", "p5 windows k>=1", "p4a screen",
-         "p4a exact eL", "p4b kruskal", "finalize+loop"]
+names = ["p0 load+zero", "p1 bitmap/prefix/vals", "p2-3 stats+levels", "d duplicate table", "p4a screen",
+         "p4a exact eL", "p4b kruskal", "finalize+loop", "p5 tail windows", "issue next+barrier"]
 n = dions.n_ions
-tot = sum(buf[i] for i in range(8))
+tot = sum(buf[i] for i in range(len(names)))
 print(os.path.basename(_lib.LIB_PATH))
 print(f"metrics launch {dt*1e3:.1f} ms for {n} ions; sum cycles/ion {tot/n:.0f}")
 for i, nm in enumerate(names):

@@ -36,18 +36,33 @@ enum { C_NE = 0, C_EMAX, C_ABORT, C_PDUP, C_NEXT, C_NCTR = 8 };
 // into a buffer of their own (read back by smg_debug_stamps); the shipped build executes no stamp.
 #ifdef SMG_STAMPS
 __device__ unsigned long long g_stamps[16];
-#define STAMP_INIT() unsigned long long _st0 = __builtin_amdgcn_s_memtime(), _st1
-#define STAMP(i)                                                                   \
-  do {                                                                             \
-    if (threadIdx.x == 0) {                                                        \
-      _st1 = __builtin_amdgcn_s_memtime();                                         \
-      atomicAdd(&g_stamps[i], _st1 - _st0);                                        \
-      _st0 = _st1;                                                                 \
-    }                                                                              \
+// thread 0 of each workgroup accumulates its phase cycles in LDS and adds them to g_stamps once at exit
+#define STAMP_DECL()                                               \
+  __shared__ unsigned long long _sacc[16];                         \
+  unsigned long long _st0 = 0, _st1 = 0;                           \
+  if (threadIdx.x == 0) {                                          \
+    for (int _i = 0; _i < 16; ++_i) _sacc[_i] = 0;                 \
+    _st0 = __builtin_amdgcn_s_memtime();                           \
+  }
+#define STAMP_INIT()
+#define STAMP(i)                                                   \
+  do {                                                             \
+    if (threadIdx.x == 0) {                                        \
+      _st1 = __builtin_amdgcn_s_memtime();                         \
+      _sacc[i] += _st1 - _st0;                                     \
+      _st0 = _st1;                                                 \
+    }                                                              \
+  } while (0)
+#define STAMP_FLUSH()                                              \
+  do {                                                             \
+    if (threadIdx.x == 0)                                          \
+      for (int _i = 0; _i < 16; ++_i) atomicAdd(&g_stamps[_i], _sacc[_i]); \
   } while (0)
 #else
+#define STAMP_DECL()
 #define STAMP_INIT()
 #define STAMP(i)
+#define STAMP_FLUSH()
 #endif
 
 struct Params {
@@ -657,6 +672,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
 
   // scheduling runs one ion further ahead than the loads: iteration b scores pos, loads npos's descriptor and
   // data, and takes the ticket of the ion after npos
+  STAMP_DECL();
   if (tid == 0) ctr[C_NEXT] = (int)sched_resolve<SRC>(S, sched_issue<SRC>(S));
   __syncthreads();
   int64_t pos = -1;  // ion scored in this iteration (-1: none; the first iteration only issues loads)
@@ -911,6 +927,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     } else if (!skip && tid < NW) {
       dcnt[tid] = 0;
     }
+    STAMP(8);
     // ---- the registers of ion b are dead: ion b+1's principal window and first two chunks go in flight
     if (npos >= 0 && desc_lds_ok(DN, CAPC)) {
       issue_principal(DN);
@@ -918,6 +935,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       issue_chunk(DN, 1, pb);
     }
     __syncthreads();
+    STAMP(9);
     // ---- deferred duplicate candidates: exact per-(pixel, window) sums, squared into the partials --------
     // Thread t owns list slot t (segment t / DSEG, entry t % DSEG); the entries are summed per key in an LDS
     // table and each key's square goes to its window's partial (LDS f64 atomics: the few keys per ion make
@@ -1284,6 +1302,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     __syncthreads();  // the next ion re-initialises the LDS structures
     STAMP(7);
   }
+  STAMP_FLUSH();
   // no load of this wave outlives it
   vm_wait<0>(pa);
   vm_wait<0>(pb);
