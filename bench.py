@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--nlevels", type=int, default=30)
     ap.add_argument("--plant-fraction", type=float, default=0.02)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-ions", type=int, default=256)
+    ap.add_argument("--cpu-ions", type=int, default=768)
     ap.add_argument("--cpu-workers", type=int, default=8)
     return ap.parse_args()
 
