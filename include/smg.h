@@ -36,6 +36,7 @@ extern "C" {
 #define SMG_ION_DENSE 0x2u       /* scored by the dense (global-scratch) path instead of the LDS path */
 #define SMG_ION_CHAOS_NAN 0x4u   /* raw measure_of_chaos was NaN (empty / < 4 positive pixels) */
 #define SMG_ION_BIG 0x8u         /* scored by the big-ion LDS pass (1024-thread workgroup, whole LDS) */
+#define SMG_ION_TWO_LEVEL 0x10u  /* LDS pass with the two-level pixel set (images > 2^18 pixels) */
 
 /* hit formats accepted by smg_ion_metrics */
 #define SMG_HITS_PACKED_F32 0    /* uint64: low 32 bits pixel index, high 32 bits float32 intensity */
@@ -139,6 +140,9 @@ int smg_isotope_centroids_batch(const char* formulas, const int64_t* offsets, in
  * the ion kernel's access width (one coalesced 8-byte load per lane) and XOR-folds them into out[n_blocks]
  * (device), so that FETCH_SIZE can be converted to bytes for this access pattern (bench.py `traffic`). */
 int smg_debug_stream_read(const uint64_t* data, int64_t n_words, uint64_t* out, int32_t n_blocks, void* stream);
+/* Test switch: on != 0 makes smg_ion_metrics score every image size with the two-level LDS passes (normally only
+ * images above 2^18 pixels), so that the parity suite covers them on small images.  Process-wide; returns 0. */
+int smg_debug_force_two_level(int32_t on);
 
 #ifdef __cplusplus
 }

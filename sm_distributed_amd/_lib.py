@@ -16,6 +16,7 @@ SMG_ION_HAS_HITS = 0x1
 SMG_ION_DENSE = 0x2
 SMG_ION_CHAOS_NAN = 0x4
 SMG_ION_BIG = 0x8
+SMG_ION_TWO_LEVEL = 0x10
 SMG_HITS_PACKED_F32 = 0
 PIXEL_MASK = 0x7FFFFFFF   # bit 31 of the pixel field = duplicate-candidate flag
 SMG_HITS_SPLIT_F64 = 1
@@ -41,6 +42,7 @@ PROTOTYPES = {
                                        _I32, _I32, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "smg_sample_spectra": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _I64, _P, _P, _P, _I64, _P, _P]),
     "smg_debug_stream_read": (ctypes.c_int, [_P, _I64, _P, _I32, _P]),
+    "smg_debug_force_two_level": (ctypes.c_int, [_I32]),
     "smg_isotope_centroids": (ctypes.c_int, [ctypes.c_char_p, _I32, _D, _I32, _I32, _I32, _P, _P,
                                              ctypes.POINTER(_I32)]),
     "smg_isotope_centroids_batch": (ctypes.c_int, [_P, _P, _I64, _I32, _D, _I32, _I32, _I32, _P, _P, _P, _I32]),

@@ -254,21 +254,19 @@ __device__ __forceinline__ int bm_rank(const uint32_t* bm, const uint16_t* pf, i
   return (int)pf[p >> 6] + __popcll(m);
 }
 
-// exclusive popcount prefix over the first n64 <= NPX_LDS_MAX/64 64-bit words: thread t scans WPT consecutive
-// words serially, thread totals are scanned across the wave (DPP) and the waves.  Returns the total.
-template <int NW_>
-__device__ int bm_build_prefix(const uint32_t* bm, uint16_t* pf, int n64, int* wscratch) {
+// exclusive popcount prefix over the first n <= CAP 64-bit words w: thread t scans WPT consecutive words
+// serially, thread totals are scanned across the wave (DPP) and the waves.  Returns the total.
+template <int NW_, int CAP>
+__device__ int prefix_words(const uint64_t* w, uint16_t* pf, int n, int* wscratch) {
   constexpr int NW = NW_;
-  constexpr int WPT = (NPX_LDS_MAX / 64) / (NW * WAVE);
-  static_assert(WPT >= 1 && WPT * NW * WAVE * 64 == NPX_LDS_MAX, "prefix geometry");
+  constexpr int WPT = (CAP + NW * WAVE - 1) / (NW * WAVE);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(bm);
   const int a = tid * WPT;
   int c[WPT];
   int tot = 0;
 #pragma unroll
   for (int i = 0; i < WPT; ++i) {
-    c[i] = (a + i < n64) ? __popcll(bm64[a + i]) : 0;
+    c[i] = (a + i < n) ? __popcll(w[a + i]) : 0;
     tot += c[i];
   }
   const int inc = wave_incl_scan_dpp(tot);
@@ -276,18 +274,25 @@ __device__ int bm_build_prefix(const uint32_t* bm, uint16_t* pf, int n64, int* w
   __syncthreads();
   int off = inc - tot, all = 0;
 #pragma unroll
-  for (int w = 0; w < NW; ++w) {
-    const int x = wscratch[w];
-    off += (w < wid) ? x : 0;
+  for (int v = 0; v < NW; ++v) {
+    const int x = wscratch[v];
+    off += (v < wid) ? x : 0;
     all += x;
   }
 #pragma unroll
   for (int i = 0; i < WPT; ++i) {
-    if (a + i < n64) pf[a + i] = (uint16_t)off;
+    if (a + i < n) pf[a + i] = (uint16_t)off;
     off += c[i];
   }
   __syncthreads();
   return all;
+}
+
+// the same over the pixel bitmap (n64 <= NPX_LDS_MAX/64 words)
+template <int NW_>
+__device__ int bm_build_prefix(const uint32_t* bm, uint16_t* pf, int n64, int* wscratch) {
+  static_assert((NPX_LDS_MAX / 64) % (NW_ * WAVE) == 0, "prefix geometry");
+  return prefix_words<NW_, NPX_LDS_MAX / 64>(reinterpret_cast<const uint64_t*>(bm), pf, n64, wscratch);
 }
 
 // bits of image row `row`, columns c0..c0+6 (bit j <-> column c0+j), masked by the valid-column mask cv;
@@ -360,6 +365,28 @@ struct Lay {
   static uint32_t o_pf(int npx) { return cal16(o_bm + (uint32_t)w32(npx) * 4); }
   static size_t bytes(int npx) { return cal16(o_pf(npx) + (uint32_t)(w32(npx) / 2) * 2); }
 };
+
+// Two-level carve for images above NPX_LDS_MAX pixels (ion_pipe_kernel<..., TWO = true>): the principal
+// pixel set is kept as its non-empty 64-pixel words only, compacted in word order (W[r] at o_bm, their rank
+// prefix B[r] at o_B), behind a top-level bitmap of words (T at o_T, one bit per 64-pixel word, two zero guard
+// words at the end) with its own rank prefix (TP at Params::o_pf).  W holds up to CAPC words (a word per
+// principal point at worst), so LDS no longer scales with the image: 1000x1000 px needs 2 KB of T.
+template <int NW, int CAPC>
+struct Lay2 : Lay<NW, CAPC> {
+  using Base = Lay<NW, CAPC>;
+  static constexpr uint32_t o_B = cal16(Base::o_desc + 2 * 384);
+  static constexpr uint32_t o_guard = cal16(o_B + (uint32_t)CAPC * 2);
+  static constexpr uint32_t o_bm = o_guard + 16;
+  static constexpr uint32_t o_T = o_bm + (uint32_t)CAPC * 8;
+  __host__ __device__ static int nT(int npx) { return ((((npx + 63) / 64) / 64 + 2) + 1) & ~1; }  // even: uint4 zeroing
+  // u32 words of W and T together (zeroed as one range, like the direct bitmap)
+  static int w32(int npx) { return (int)((CAPC * 8 + nT(npx) * 8) / 4); }
+  static uint32_t o_pf(int npx) { return o_T + (uint32_t)nT(npx) * 8; }
+  static size_t bytes(int npx) { return cal16(o_pf(npx) + (uint32_t)nT(npx) * 2); }
+  static_assert(CAPC % 2 == 0, "W zeroed in uint4s");
+};
+constexpr int NPX_TWO_MAX = 1 << 23;  // two-level pass: top-level prefix over <= 2^23/4096 + 2 words
+constexpr int TOPCAP = NPX_TWO_MAX / 4096 + 2;
 
 // open-addressing f64 accumulators keyed by u32 (EMPTY = 0xFFFFFFFF); returns false when full
 template <int NSLOT>
@@ -562,7 +589,7 @@ __device__ __forceinline__ bool desc_lds_ok(const IonDesc* D, int capc) {
 // Ions that do not fit (K > MAXK, principal window > CAPC, list/table overflows) go to `rej_list`: positions
 // (SRC_RANGES pass, read by the big-ion pass) or ion indices (SRC_LIST pass, read by the dense kernel).
 // ---------------------------------------------------------------------------------------------
-template <int FMT, int LB, int LRMAX, int LRC, int WPE, int SRC>
+template <int FMT, int LB, int LRMAX, int LRC, int WPE, int SRC, bool TWO>
 __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     Hits<FMT> hits, const IonDesc* __restrict__ desc, Sched S, Params P, double* __restrict__ oc,
     double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags,
@@ -574,10 +601,10 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   constexpr int GPC = BLOCK * RC / 64;  // 64-point groups per chunk
   constexpr int CAPC = BLOCK * RMAX;
   using Reg = typename Hits<FMT>::Reg;
-  using LY = Lay<NW, CAPC>;
+  using LY = std::conditional_t<TWO, Lay2<NW, CAPC>, Lay<NW, CAPC>>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t* Hbm = reinterpret_cast<uint32_t*>(smem + LY::o_bm);  // a zero guard word in front, for bits7
-  uint16_t* pf = reinterpret_cast<uint16_t*>(smem + P.o_pf);
+  uint16_t* pf = reinterpret_cast<uint16_t*>(smem + P.o_pf);      // two-level: TP (top-level rank prefix)
   double* vals = reinterpret_cast<double*>(smem + LY::o_vals);
   uint8_t* Lv = reinterpret_cast<uint8_t*>(smem + LY::o_L);
   uint32_t* filtA = reinterpret_cast<uint32_t*>(smem + LY::o_filt);
@@ -600,6 +627,53 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   uint32_t* epix_r = reinterpret_cast<uint32_t*>(vals);                 // E pixels, rank order
   uint8_t* eLr = Lv;                                                    // rank order
   uint32_t* par = reinterpret_cast<uint32_t*>(vals) + CAPC;             // rank order
+
+  // two-level pixel set (TWO): compact words W = Hbm as u64, their rank prefix B, top-level bitmap T
+  const uint64_t* W64 = reinterpret_cast<const uint64_t*>(Hbm);
+  uint16_t* Bpf = reinterpret_cast<uint16_t*>(smem + (TWO ? Lay2<NW, CAPC>::o_B : 0));
+  uint32_t* T32 = reinterpret_cast<uint32_t*>(smem + (TWO ? Lay2<NW, CAPC>::o_T : 0));
+  const uint64_t* T64 = reinterpret_cast<const uint64_t*>(T32);
+  const int nT = TWO ? Lay2<NW, CAPC>::nT(P.npx) : 0;
+  // two-level lookups: index r of word q among the non-empty words (-1: empty or outside the image)
+  auto top_rank = [&](int q) -> int {
+    if (q < 0) return -1;
+    const uint64_t t = T64[q >> 6], b = 1ull << (q & 63);
+    return (t & b) ? (int)pf[q >> 6] + __popcll(t & (b - 1ull)) : -1;
+  };
+  // word q (0 when empty) and the rank of its first pixel
+  auto word2 = [&](int q, int& base) -> uint64_t {
+    const int r = top_rank(q);
+    base = r >= 0 ? (int)Bpf[r] : 0;
+    return r >= 0 ? W64[r] : 0ull;
+  };
+  // rank of pixel p in the set (-1: not in it)
+  auto rank2 = [&](int p) -> int {
+    const int r = top_rank(p >> 6);
+    if (r < 0) return -1;
+    const uint64_t w = W64[r], b = 1ull << (p & 63);
+    return (w & b) ? (int)Bpf[r] + __popcll(w & (b - 1ull)) : -1;
+  };
+  // builds the set from up to CAPC pixels (two passes: top-level bits, then the compact words); each(f) calls
+  // f(j, p) for every pixel p (slot j) of this thread and records the slots for which f returns true (the
+  // atomicOr of the second pass set the pixel's bit: its owner).  W and T are zero on entry.  Returns the
+  // number of distinct pixels.
+  auto build2 = [&](auto&& each) -> int {
+    each([&](int, uint32_t p) {
+      const uint32_t q = p >> 6;
+      atomicOr(&T32[q >> 5], 1u << (q & 31));
+      return false;
+    });
+    __syncthreads();
+    const int nwords = prefix_words<NW, TOPCAP>(T64, pf, nT, wsc);
+    (void)nwords;
+    each([&](int, uint32_t p) {
+      const int r = top_rank((int)(p >> 6));
+      const uint32_t bit = 1u << (p & 31);
+      return !(atomicOr(&Hbm[2 * r + ((p >> 5) & 1)], bit) & bit);
+    });
+    __syncthreads();
+    return prefix_words<NW, CAPC>(W64, Bpf, nwords, wsc);
+  };
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -734,17 +808,27 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       vm_wait<2 * RC>(pd);
       vm_wait<2 * RC>(pe);
       uint32_t own = 0;     // slots whose atomicOr set the pixel's bit (one owner per distinct pixel)
+      if constexpr (TWO) {
+        nnz = build2([&](auto&& f) {
 #pragma unroll
-      for (int j = 0; j < RMAX; ++j) {
-        const int i = tid + j * BLOCK;
-        if (i < n0) {
-          const uint32_t p = Hits<FMT>::pix(hs(j));
-          const uint32_t bit = 1u << (p & 31);
-          if (!(atomicOr(&Hbm[p >> 5], bit) & bit)) own |= 1u << j;
+          for (int j = 0; j < RMAX; ++j) {
+            const int i = tid + j * BLOCK;
+            if (i < n0 && f(j, Hits<FMT>::pix(hs(j)))) own |= 1u << j;
+          }
+        });
+      } else {
+#pragma unroll
+        for (int j = 0; j < RMAX; ++j) {
+          const int i = tid + j * BLOCK;
+          if (i < n0) {
+            const uint32_t p = Hits<FMT>::pix(hs(j));
+            const uint32_t bit = 1u << (p & 31);
+            if (!(atomicOr(&Hbm[p >> 5], bit) & bit)) own |= 1u << j;
+          }
         }
+        __syncthreads();
+        nnz = bm_build_prefix<NW>(Hbm, pf, n64, wsc);
       }
-      __syncthreads();
-      nnz = bm_build_prefix<NW>(Hbm, pf, n64, wsc);
       olist = reinterpret_cast<uint32_t*>(vals) + (nnz <= OL_MAX ? ((2 * nnz + 3) & ~3) : 0);
       // A point without the duplicate-candidate flag is the only point of its pixel in this window
       // (smg_flag_duplicates), so it stores its value; flagged points (true duplicates and a few false
@@ -754,7 +838,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       for (int j = 0; j < RMAX; ++j) {
         const int i = tid + j * BLOCK;
         if (i < n0) {
-          const int r = bm_rank(Hbm, pf, (int)Hits<FMT>::pix(hs(j)));
+          const int r = TWO ? rank2((int)Hits<FMT>::pix(hs(j))) : bm_rank(Hbm, pf, (int)Hits<FMT>::pix(hs(j)));
           const bool d = Hits<FMT>::dup(hs(j));
           vals[r] = d ? 0.0 : Hits<FMT>::val(hs(j));
           any_dup |= d;
@@ -768,7 +852,8 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         for (int j = 0; j < RMAX; ++j) {
           const int i = tid + j * BLOCK;
           if (i < n0 && Hits<FMT>::dup(hs(j)))
-            atomicAdd(&vals[bm_rank(Hbm, pf, (int)Hits<FMT>::pix(hs(j)))], Hits<FMT>::val(hs(j)));
+            atomicAdd(&vals[TWO ? rank2((int)Hits<FMT>::pix(hs(j))) : bm_rank(Hbm, pf, (int)Hits<FMT>::pix(hs(j)))],
+                      Hits<FMT>::val(hs(j)));
         }
       }
     }
@@ -866,8 +951,27 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       // candidates.
       auto process = [&](int c, Reg (&buf)[RC]) {
         uint64_t bw[RC];
+        int br[RC];  // two-level: index of the slot's word among the non-empty words
+        if constexpr (TWO) {
+          uint64_t tw[RC];
+          int tp[RC];
 #pragma unroll
-        for (int j = 0; j < RC; ++j) bw[j] = reinterpret_cast<const uint64_t*>(Hbm)[Hits<FMT>::pix(buf[j]) >> 6];
+          for (int j = 0; j < RC; ++j) {
+            const uint32_t q = Hits<FMT>::pix(buf[j]) >> 6;
+            tw[j] = T64[q >> 6];
+            tp[j] = pf[q >> 6];
+          }
+#pragma unroll
+          for (int j = 0; j < RC; ++j) {
+            const uint32_t q = Hits<FMT>::pix(buf[j]) >> 6;
+            const uint64_t b = 1ull << (q & 63);
+            br[j] = (tw[j] & b) ? tp[j] + __popcll(tw[j] & (b - 1ull)) : -1;
+            bw[j] = br[j] >= 0 ? W64[br[j]] : 0ull;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < RC; ++j) bw[j] = reinterpret_cast<const uint64_t*>(Hbm)[Hits<FMT>::pix(buf[j]) >> 6];
+        }
 #pragma unroll
         for (int j = 0; j < RC; ++j) {
           const int G = c * GPC + j * NW + wid;
@@ -883,7 +987,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
             const uint64_t bit = 1ull << (p & 63);
             const bool in = valid && (bw[j] & bit) != 0ull && !(SMG_ABL & 16);
             if (__ballot(in)) {
-              const double x = in ? vals[(int)pf[p >> 6] + __popcll(bw[j] & (bit - 1ull))] : 0.0;
+              double x;
+              if constexpr (TWO) x = in ? vals[(int)Bpf[br[j]] + __popcll(bw[j] & (bit - 1ull))] : 0.0;
+              else x = in ? vals[(int)pf[p >> 6] + __popcll(bw[j] & (bit - 1ull))] : 0.0;
               const double v = Hits<FMT>::val(buf[j]);
               psxy += x * v;
               if (x > 0.0) psk += v;
@@ -987,20 +1093,39 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       if (nnz > OL_MAX) {
         // olist did not fit behind the values: the distinct principal pixels from the bitmap, rank order
         // (olist[pf[w] + i] = i-th set bit of word w); the values are dead
-        const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(Hbm);
-        constexpr int WPT = (NPX_LDS_MAX / 64) / BLOCK;
-        uint64_t wb[WPT];
+        if constexpr (TWO) {
+          // top-level words strided over the threads; word q's pixels start at rank B[r]
+          for (int tw = tid; tw < nT; tw += BLOCK) {
+            uint64_t t = T64[tw];
+            int r = pf[tw];
+            while (t) {
+              const int q = tw * 64 + __builtin_ctzll(t);
+              uint64_t bits = W64[r];
+              int o = Bpf[r];
+              while (bits) {
+                olist[o++] = (uint32_t)(q * 64 + __builtin_ctzll(bits));
+                bits &= bits - 1;
+              }
+              ++r;
+              t &= t - 1;
+            }
+          }
+        } else {
+          const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(Hbm);
+          constexpr int WPT = (NPX_LDS_MAX / 64) / BLOCK;
+          uint64_t wb[WPT];
 #pragma unroll
-        for (int i = 0; i < WPT; ++i) wb[i] = (tid * WPT + i < n64) ? bm64[tid * WPT + i] : 0ull;
+          for (int i = 0; i < WPT; ++i) wb[i] = (tid * WPT + i < n64) ? bm64[tid * WPT + i] : 0ull;
 #pragma unroll
-        for (int i = 0; i < WPT; ++i) {
-          uint64_t bits = wb[i];
-          if (!bits) continue;
-          const int w = tid * WPT + i;
-          int r = pf[w];
-          while (bits) {
-            olist[r++] = (uint32_t)(w * 64 + __builtin_ctzll(bits));
-            bits &= bits - 1;
+          for (int i = 0; i < WPT; ++i) {
+            uint64_t bits = wb[i];
+            if (!bits) continue;
+            const int w = tid * WPT + i;
+            int r = pf[w];
+            while (bits) {
+              olist[r++] = (uint32_t)(w * 64 + __builtin_ctzll(bits));
+              bits &= bits - 1;
+            }
           }
         }
         __syncthreads();
@@ -1015,7 +1140,21 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         const uint32_t cv = ((1u << chi) - 1u) & ~((1u << clo) - 1u);
         uint32_t H[7];
 #pragma unroll
-        for (int d = 0; d < 7; ++d) H[d] = bits7(Hbm, rs - 3 + d, cs - 3, cv, P);
+        for (int d = 0; d < 7; ++d) {
+          if constexpr (TWO) {
+            // columns cs-3..cs+3 of row rs-3+d from words q and q+1 of the two-level set
+            const int row = rs - 3 + d;
+            const bool rv = (unsigned)row < (unsigned)P.nrows;
+            const int st = (rv ? row : 0) * P.ncols + cs - 3;
+            const int q = st >> 6, b = st & 63;  // st >= -3: q >= -1 (empty)
+            int dummy;
+            const uint64_t w0 = word2(q, dummy), w1 = b > 57 ? word2(q + 1, dummy) : 0ull;
+            const uint32_t v = (uint32_t)((b ? ((w0 >> b) | (w1 << (64 - b))) : w0) & 0x7Full) & cv;
+            H[d] = rv ? v : 0u;
+          } else {
+            H[d] = bits7(Hbm, rs - 3 + d, cs - 3, cv, P);
+          }
+        }
         // isolation pre-filter (erosion border = background only): an eL>0 pixel in the cross of s needs
         // another principal pixel in s's 7x7, since the 4-cross of s alone cannot cover a 3x3 box
         const bool isolated = !P.erosion_border && (H[0] | H[1] | H[2] | (H[3] & ~8u) | H[4] | H[5] | H[6]) == 0u;
@@ -1096,8 +1235,17 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
             const bool rv = (unsigned)row < (unsigned)P.nrows;
             const int st = (rv ? row : 0) * P.ncols + cp - 2;  // >= -2: the guard word in front reads as zero
             const int w = st >> 6, b = st & 63;
-            const uint64_t w0 = bm64[w], w1 = bm64[w + 1];
-            const int r0 = pf[w], r1 = pf[w + 1];
+            uint64_t w0, w1;
+            int r0, r1;
+            if constexpr (TWO) {
+              w0 = word2(w, r0);
+              w1 = word2(w + 1, r1);
+            } else {
+              w0 = bm64[w];
+              w1 = bm64[w + 1];
+              r0 = pf[w];
+              r1 = pf[w + 1];
+            }
             const uint32_t bits = rv ? (uint32_t)((b ? ((w0 >> b) | (w1 << (64 - b))) : w0) & 31u) & cv5 : 0u;
             uint32_t packed = 0;
             for (uint32_t rest = bits; rest; rest &= rest - 1u) {
@@ -1183,17 +1331,25 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
             sum_c = wave_sum_dpp(e >= 1 ? (double)e : 0.0) - wave_sum_dpp(wsum);
           }
         } else if (emax_all > 0) {
-          uint4* z = reinterpret_cast<uint4*>(Hbm);
+          uint4* z = reinterpret_cast<uint4*>(Hbm);  // two-level: W and T
           for (int i = tid; i < P.w32 / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);  // guard stays zero
           __syncthreads();
-          for (int i = tid; i < ncand; i += BLOCK)
-            if (eL8[i]) atomicOr(&Hbm[epix[i] >> 5], 1u << (epix[i] & 31));
-          __syncthreads();
-          const int m = bm_build_prefix<NW>(Hbm, pf, n64, wsc);
+          int m;
+          if constexpr (TWO) {
+            m = build2([&](auto&& f) {
+              for (int i = tid; i < ncand; i += BLOCK)
+                if (eL8[i]) f(0, epix[i]);
+            });
+          } else {
+            for (int i = tid; i < ncand; i += BLOCK)
+              if (eL8[i]) atomicOr(&Hbm[epix[i] >> 5], 1u << (epix[i] & 31));
+            __syncthreads();
+            m = bm_build_prefix<NW>(Hbm, pf, n64, wsc);
+          }
           for (int i = tid; i < ncand; i += BLOCK) {
             if (!eL8[i]) continue;
             const uint32_t p = epix[i];
-            const int r = bm_rank(Hbm, pf, (int)p);
+            const int r = TWO ? rank2((int)p) : bm_rank(Hbm, pf, (int)p);
             epix_r[r] = p;
             eLr[r] = eL8[i];
           }
@@ -1211,8 +1367,14 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
               int rp, cp;
               rowcol(p, P, rp, cp);
               auto edge = [&](int q) {
-                if (!bm_test(Hbm, q)) return;
-                const int rq = bm_rank(Hbm, pf, q);
+                int rq;
+                if constexpr (TWO) {
+                  rq = rank2(q);
+                  if (rq < 0) return;
+                } else {
+                  if (!bm_test(Hbm, q)) return;
+                  rq = bm_rank(Hbm, pf, q);
+                }
                 const int eq = eLr[rq];
                 if ((e < eq ? e : eq) == t) {
                   if (uf_unite(par, (uint32_t)r, (uint32_t)rq)) wsum += (double)t;
@@ -1292,7 +1454,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         osp[ion] = spatial;
         osc[ion] = spectral;
         omsm[ion] = chaos * spatial * spectral;
-        oflags[ion] = flags | big_flag | (uint32_t)D->hits;
+        oflags[ion] = flags | big_flag | (TWO ? SMG_ION_TWO_LEVEL : 0u) | (uint32_t)D->hits;
       }
     }
     if (npos < 0) break;
@@ -1621,6 +1783,11 @@ static size_t ws_bytes_for(int64_t n_ions, int npx) {
 
 using MainLay = Lay<MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX>;
 using BigLay = Lay<BIG_BLOCK / WAVE, BIG_BLOCK * BIG_RMAX>;
+// two-level passes: the big-ion pass takes principal windows of up to 4096 points (W needs 8 B per point)
+static constexpr int BIG2_RMAX = 4;
+using Main2Lay = Lay2<MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX>;
+using Big2Lay = Lay2<BIG_BLOCK / WAVE, BIG_BLOCK * BIG2_RMAX>;
+static int g_force_two_level = 0;  // smg_debug_force_two_level: two-level passes for every image size
 
 static int device_cus() {
   int dev = 0, cus = 0;
@@ -1644,14 +1811,17 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   unsigned char* slots = reinterpret_cast<unsigned char*>(desc) + (size_t)n_ions * sizeof(IonDesc);
   const size_t slot_bytes = dense_slot_bytes(P.npx);
   SMG_HIP(hipMemsetAsync(ws, 0, WS_HEADER, st));
+  // images above NPX_LDS_MAX pixels (or forced, smg_debug_force_two_level) take the two-level LDS passes
+  const bool two = (P.npx > NPX_LDS_MAX || g_force_two_level) && P.npx <= NPX_TWO_MAX;
   Params PM = P, PB = P;
-  PM.w32 = MainLay::w32(P.npx);
-  PM.o_pf = MainLay::o_pf(P.npx);
-  PB.w32 = BigLay::w32(P.npx);
-  PB.o_pf = BigLay::o_pf(P.npx);
-  const size_t lds_main = MainLay::bytes(P.npx), lds_big = BigLay::bytes(P.npx);
-  const bool main_ok = P.npx <= NPX_LDS_MAX && lds_main <= MAIN_LDS;
-  const bool big_ok = P.npx <= NPX_LDS_MAX && lds_big <= BIG_LDS;
+  PM.w32 = two ? Main2Lay::w32(P.npx) : MainLay::w32(P.npx);
+  PM.o_pf = two ? Main2Lay::o_pf(P.npx) : MainLay::o_pf(P.npx);
+  PB.w32 = two ? Big2Lay::w32(P.npx) : BigLay::w32(P.npx);
+  PB.o_pf = two ? Big2Lay::o_pf(P.npx) : BigLay::o_pf(P.npx);
+  const size_t lds_main = two ? Main2Lay::bytes(P.npx) : MainLay::bytes(P.npx);
+  const size_t lds_big = two ? Big2Lay::bytes(P.npx) : BigLay::bytes(P.npx);
+  const bool main_ok = (two || P.npx <= NPX_LDS_MAX) && lds_main <= MAIN_LDS;
+  const bool big_ok = (two || P.npx <= NPX_LDS_MAX) && lds_big <= BIG_LDS;
   const int cus = device_cus();
   if (main_ok || big_ok) {
     hipLaunchKernelGGL(ion_desc_kernel<FMT>, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, hits, lo, hi,
@@ -1660,7 +1830,8 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   }
   if (main_ok) {
     Sched SA{n_ions, hdr + HDR_XCD, nullptr, nullptr};
-    auto k1 = &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES>;
+    auto k1 = two ? &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, true>
+                  : &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, false>;
     SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k1), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_main));
     // two resident workgroups per CU, a multiple of the XCD count
@@ -1676,7 +1847,8 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   }
   if (big_ok) {
     Sched SB{0, hdr + 1, list_a, hdr + 0};
-    auto k2 = &ion_pipe_kernel<FMT, BIG_BLOCK, BIG_RMAX, BIG_RC, 1, SRC_LIST>;
+    auto k2 = two ? &ion_pipe_kernel<FMT, BIG_BLOCK, BIG2_RMAX, BIG_RC, 1, SRC_LIST, true>
+                  : &ion_pipe_kernel<FMT, BIG_BLOCK, BIG_RMAX, BIG_RC, 1, SRC_LIST, false>;
     SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k2), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_big));
     const int nwg2 = (int)(n_ions < cus ? n_ions : cus);
@@ -1717,6 +1889,11 @@ int smg_debug_stamps(unsigned long long* host_out, int n) {
   set_error("library built without -DSMG_STAMPS");
   return SMG_ERR_UNSUPPORTED;
 #endif
+}
+
+int smg_debug_force_two_level(int32_t on) {
+  g_force_two_level = on ? 1 : 0;
+  return SMG_OK;
 }
 
 int smg_ion_metrics_workspace_size(int64_t n_ions, int32_t nrows, int32_t ncols, size_t* bytes) {

@@ -130,6 +130,14 @@ def make_case(name: str):
         ds = syn.make_dataset_np(520, 520, 3, seed=63, ions=ions, plant_fraction=1.0, plant_seed=64,
                                  blob_sigma=(3.0, 8.0))
         return ds, ions, 50.0, {}
+    if name == "large_blobs":  # > 2^18 pixels with big blobs: two-level main / big-ion passes, chaos with many
+        full = syn.make_ion_table(4, seed=111, decoy_seed=112)  # candidates, olist from the set (nnz > OL_MAX)
+        tgt = np.nonzero(np.isin(full.adducts, list(full.target_adducts)))[0][:8]
+        dec = np.nonzero(~np.isin(full.adducts, list(full.target_adducts)))[0][:4]
+        ions = subset_ions(full, np.concatenate([tgt, dec]))
+        ds = syn.make_dataset_np(600, 600, 10, seed=113, ions=ions, plant_fraction=1.0, plant_seed=114,
+                                 blob_sigma=(14.0, 30.0))
+        return add_duplicates(ds, 0.01, 115), ions, 20.0, {}
     if name == "long_tail":    # tails of several register chunks (chunk refills, window changes inside chunks)
         full = syn.make_ion_table(12, seed=91, decoy_seed=92)
         ions = subset_ions(full, np.arange(0, full.n_ions, 6))
@@ -149,7 +157,7 @@ def make_case(name: str):
 
 
 CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels", "nlevels1", "big_window", "huge_window",
-         "large_image", "boundary", "long_tail", "dups_heavy", "kmix"]
+         "large_image", "large_blobs", "boundary", "long_tail", "dups_heavy", "kmix"]
 
 
 def oracle_run(ds, ions, ppm, nlevels=30, connectivity=4, erosion_border=0):

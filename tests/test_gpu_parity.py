@@ -97,9 +97,43 @@ def test_dense_path_used_when_needed():
     assert ((m["flags"] & 8) != 0).any()      # big-ion LDS pass
     _, _, _, _, _, _, _, m, _, _ = _run_case("huge_window")
     assert ((m["flags"] & 2) != 0).any()      # dense global-scratch pass
+    # images above 2^18 pixels: two-level LDS passes (main, big-ion) instead of the dense path
     _, _, _, _, _, _, _, m, _, _ = _run_case("large_image")
     has = (m["flags"] & 1) != 0
-    assert ((m["flags"][has] & 2) != 0).all()
+    assert ((m["flags"][has] & (0x10 | 2)) == 0x10).all()
+    ds, ions, ppm, kw, imgs, df, peaks, m, lo, hi = _run_case("large_blobs")
+    has = (m["flags"] & 1) != 0
+    assert ((m["flags"][has] & 0x10) != 0).sum() >= 8
+    assert ((m["flags"][has] & (0x10 | 8)) == (0x10 | 8)).any()   # two-level big-ion pass
+    n0 = hi[ions.win_off[:-1]] - lo[ions.win_off[:-1]]
+    assert (has & (n0 > 1706) & (n0 <= 2560)).any()              # olist rebuilt from the two-level set
+
+
+# every LDS-path case again with the two-level pixel set forced (smg_debug_force_two_level)
+TWO_LEVEL_CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels",
+                   "big_window", "boundary", "long_tail", "dups_heavy", "kmix"]
+
+
+@pytest.mark.parametrize("name", TWO_LEVEL_CASES)
+def test_forced_two_level_matches_oracle(name):
+    from sm_distributed_amd import _lib
+    ds, ions, ppm, kw, imgs, df, _, _, _, _ = _run_case(name)
+    L = _lib.lib()
+    L.smg_debug_force_two_level(1)
+    try:
+        _, m, _, _ = _device_run(ds, ions, ppm, **kw)
+    finally:
+        L.smg_debug_force_two_level(0)
+    has = (m["flags"] & 1) != 0
+    lds = has & ((m["flags"] & 2) == 0)
+    assert ((m["flags"][lds] & 0x10) != 0).all()
+    assert lds.any() or name == "dups_heavy"  # its duplicate lists overflow every LDS pass
+    idx = {k: i for i, k in enumerate(zip(ions.sf_ids.tolist(), ions.adducts.tolist()))}
+    assert set(zip(ions.sf_ids[has].tolist(), ions.adducts[has].tolist())) == set(df.index.tolist())
+    rows = np.array([idx[k] for k in df.index.tolist()], dtype=np.int64)
+    for col in ("chaos", "spatial", "spectral", "msm"):
+        err = np.abs(df[col].to_numpy() - m[col][rows])
+        assert err.max(initial=0.0) <= METRIC_ATOL, (col, float(err.max()), int(np.argmax(err)))
 
 
 def test_sort_is_a_permutation():
