@@ -74,6 +74,8 @@ struct Params {
   float inv_ncols;  // 1/ncols for the LDS path's row/column split (npx < 2^24)
   int32_t w32;      // LDS path: bitmap words (Lay::w32)
   uint32_t o_pf;    // LDS path: byte offset of the rank prefix (Lay::o_pf)
+  double q;         // hot-spot clip percentile (dense path, when clip != 0)
+  int32_t clip;     // image_generation.do_preprocessing
 };
 
 // row and column of pixel p < 2^24 from a float reciprocal: the estimate is off by at most one row
@@ -1569,6 +1571,80 @@ __device__ void scatter_window(const Hits<FMT>& hits, int64_t a, int64_t b, doub
   }
 }
 
+// k-th smallest (0-based) of n positive doubles (list, written by this block): MSB-first radix select over
+// the IEEE bits (monotonic for positive values), 8 passes of an 8-bit LDS histogram.
+__device__ double block_select_pos(const double* list, int n, int k, uint32_t* hist, int* sh) {
+  const int tid = threadIdx.x;
+  uint64_t prefix = 0ull, mask = 0ull;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int i = tid; i < 256; i += BLOCK) hist[i] = 0u;
+    __syncthreads();
+    for (int i = tid; i < n; i += BLOCK) {
+      const uint64_t b = (uint64_t)__double_as_longlong(ld_agent(&list[i]));
+      if ((b & mask) == prefix) atomicAdd(&hist[(b >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int c = 0, d = 0;
+      for (; d < 255; ++d) {
+        if (c + (int)hist[d] > k) break;
+        c += (int)hist[d];
+      }
+      sh[0] = d;
+      sh[1] = k - c;
+    }
+    __syncthreads();
+    prefix |= (uint64_t)sh[0] << shift;
+    mask |= 255ull << shift;
+    k = sh[1];
+    __syncthreads();
+  }
+  return __longlong_as_double((long long)prefix);
+}
+
+// Gated hot-spot clip (image_generation.do_preprocessing / q; the oracle's quantile_clip): every pixel above
+// np.percentile(positive pixels, q) ('linear' method) is set to that value.  `list` is npx doubles of scratch.
+__device__ void clip_image(double* img, double* list, int npx, double q, uint32_t* hist, int* sh) {
+  const int tid = threadIdx.x;
+  if (tid == 0) sh[2] = 0;
+  __syncthreads();
+  for (int p = tid; p < npx; p += BLOCK) {
+    const double v = ld_agent(&img[p]);
+    if (v > 0.0) list[atomicAdd(&sh[2], 1)] = v;
+  }
+  __threadfence();
+  __syncthreads();
+  const int n = sh[2];
+  __syncthreads();
+  if (n == 0) return;
+  // numpy _compute_virtual_index (alpha = beta = 1), _get_indexes, _get_gamma, _lerp
+  const double qq = q / 100.0;
+  const double vi = (double)n * qq + (1.0 + qq * (1.0 - 1.0 - 1.0)) - 1.0;
+  int i0, i1;
+  double gamma;
+  if (vi >= (double)(n - 1)) {
+    i0 = i1 = n - 1;
+    gamma = 0.0;
+  } else if (vi < 0.0) {
+    i0 = i1 = 0;
+    gamma = 0.0;
+  } else {
+    i0 = (int)floor(vi);
+    i1 = i0 + 1;
+    gamma = vi - floor(vi);
+  }
+  const double a = block_select_pos(list, n, i0, hist, sh);
+  const double b = (i1 == i0) ? a : block_select_pos(list, n, i1, hist, sh);
+  const double d = b - a;
+  const double thr = gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
+  for (int p = tid; p < npx; p += BLOCK) {
+    const double v = ld_agent(&img[p]);
+    if (v > thr) img[p] = thr;
+  }
+  __threadfence();
+  __syncthreads();
+}
+
 template <int FMT>
 __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
     Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
@@ -1580,6 +1656,8 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
   __shared__ double kst[4 * MAXK_DENSE];
   __shared__ int sh_ion;
   __shared__ int sh_ctr[4];
+  __shared__ uint32_t sh_hist[256];
+  __shared__ int sh_sel[4];
   const int tid = threadIdx.x;
   DenseSlot S = dense_slot(scratch + (size_t)blockIdx.x * slot_bytes, P.npx);
   const int npx = P.npx;
@@ -1617,6 +1695,7 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
     scatter_window<FMT>(hits, lo[w0], hi[w0], S.x);
     __threadfence();
     __syncthreads();
+    if (P.clip) clip_image(S.x, S.y, npx, P.q, sh_hist, sh_sel);  // y is free until the other windows
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     double mx = -INFINITY;
     for (int p = tid; p < npx; p += BLOCK) {
@@ -1642,6 +1721,8 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
       scatter_window<FMT>(hits, lo[w0 + k], hi[w0 + k], S.y);
       __threadfence();
       __syncthreads();
+      // par and elist (contiguous, 8*npx bytes) are free until chaos
+      if (P.clip) clip_image(S.y, reinterpret_cast<double*>(S.par), npx, P.q, sh_hist, sh_sel);
       double a2[4] = {0.0, 0.0, 0.0, 0.0};
       for (int p = tid; p < npx; p += BLOCK) {
         const double y = ld_agent(&S.y[p]);
@@ -1820,8 +1901,9 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   PB.o_pf = two ? Big2Lay::o_pf(P.npx) : BigLay::o_pf(P.npx);
   const size_t lds_main = two ? Main2Lay::bytes(P.npx) : MainLay::bytes(P.npx);
   const size_t lds_big = two ? Big2Lay::bytes(P.npx) : BigLay::bytes(P.npx);
-  const bool main_ok = (two || P.npx <= NPX_LDS_MAX) && lds_main <= MAIN_LDS;
-  const bool big_ok = (two || P.npx <= NPX_LDS_MAX) && lds_big <= BIG_LDS;
+  // the hot-spot clip needs whole images: every ion takes the dense path
+  const bool main_ok = !P.clip && (two || P.npx <= NPX_LDS_MAX) && lds_main <= MAIN_LDS;
+  const bool big_ok = !P.clip && (two || P.npx <= NPX_LDS_MAX) && lds_big <= BIG_LDS;
   const int cus = device_cus();
   if (main_ok || big_ok) {
     hipLaunchKernelGGL(ion_desc_kernel<FMT>, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, hits, lo, hi,
@@ -1910,7 +1992,6 @@ int smg_ion_metrics(int32_t hit_format, const void* hits, const double* hit_vals
                     double q, int32_t do_preprocessing, int32_t connectivity, int32_t erosion_border,
                     double* out_chaos, double* out_spatial, double* out_spectral, double* out_msm,
                     uint32_t* out_flags, void* workspace, size_t workspace_bytes, void* stream) {
-  (void)q;
   SMG_CHECK_ARG(n_ions >= 0 && n_ions < (1ll << 31), "n_ions out of range");
   if (n_ions == 0) return SMG_OK;
   SMG_CHECK_ARG(nrows > 0 && ncols > 0 && (int64_t)nrows * ncols < (1ll << 31), "bad image shape");
@@ -1921,10 +2002,7 @@ int smg_ion_metrics(int32_t hit_format, const void* hits, const double* hit_vals
   SMG_CHECK_ARG(hit_cum && lo && hi && ion_win_off && theor_int && out_chaos && out_spatial && out_spectral &&
                     out_msm && out_flags && workspace,
                 "null pointer");
-  if (do_preprocessing) {
-    set_error("do_preprocessing (q-percentile hot-spot clip) is not implemented on the device path yet");
-    return SMG_ERR_UNSUPPORTED;
-  }
+  SMG_CHECK_ARG(!do_preprocessing || (q >= 0.0 && q <= 100.0), "q must be in [0, 100]");
   const size_t need = ws_bytes_for(n_ions, nrows * ncols);
   if (workspace_bytes < need) {
     set_error("ion_metrics workspace too small: %zu < %zu", workspace_bytes, need);
@@ -1941,6 +2019,8 @@ int smg_ion_metrics(int32_t hit_format, const void* hits, const double* hit_vals
   P.inv_ncols = 1.0f / (float)ncols;
   P.w32 = 0;
   P.o_pf = 0;
+  P.q = q;
+  P.clip = do_preprocessing ? 1 : 0;
   unsigned char* ws = reinterpret_cast<unsigned char*>(workspace);
   hipStream_t st = as_stream(stream);
   if (hit_format == SMG_HITS_PACKED_F32) {

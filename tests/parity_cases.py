@@ -150,6 +150,12 @@ def make_case(name: str):
         ions = syn.make_ion_table(25, seed=101, decoy_seed=102, k_range=(1, 10))
         ds = syn.make_dataset_np(40, 40, 500, seed=103, ions=ions, plant_fraction=0.4, plant_seed=104)
         return ds, ions, 30.0, {}
+    if name == "clip99":       # gated q-percentile hot-spot clip (do_preprocessing): dense path, radix select
+        ds, ions, ppm, _ = make_case("dups")
+        return ds, ions, ppm, {"do_preprocessing": True, "q": 99.0}
+    if name == "clip_q50_conn8":
+        ds, ions, ppm, _ = make_case("zeros_rect")
+        return ds, ions, ppm, {"do_preprocessing": True, "q": 50.0, "connectivity": 8}
     if name == "boundary":
         ds = syn.make_dataset_np(16, 16, 300, seed=71)
         return ds, boundary_ions(ds, 5.0, 40, 72), 5.0, {}
@@ -157,13 +163,13 @@ def make_case(name: str):
 
 
 CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels", "nlevels1", "big_window", "huge_window",
-         "large_image", "large_blobs", "boundary", "long_tail", "dups_heavy", "kmix"]
+         "large_image", "large_blobs", "boundary", "long_tail", "dups_heavy", "kmix", "clip99", "clip_q50_conn8"]
 
 
-def oracle_run(ds, ions, ppm, nlevels=30, connectivity=4, erosion_border=0):
+def oracle_run(ds, ions, ppm, nlevels=30, connectivity=4, erosion_border=0, q=99.0, do_preprocessing=False):
     from oracle import msm_oracle as O
     pm, dims = ds.pixel_map_dims()
     imgs = O.compute_sf_images(ds.spectra(), pm, dims, sf_peak_df(ions), ppm)
     df = O.sf_image_metrics(imgs, sf_peak_ints(ions), dims[0], dims[1], nlevels, connectivity=connectivity,
-                            erosion_border=erosion_border)
+                            erosion_border=erosion_border, q=q, do_preprocessing=do_preprocessing)
     return imgs, df
