@@ -143,6 +143,9 @@ int smg_debug_stream_read(const uint64_t* data, int64_t n_words, uint64_t* out, 
 /* Test switch: on != 0 makes smg_ion_metrics score every image size with the two-level LDS passes (normally only
  * images above 2^18 pixels), so that the parity suite covers them on small images.  Process-wide; returns 0. */
 int smg_debug_force_two_level(int32_t on);
+/* Test switch: on != 0 makes smg_ion_metrics score every ion with the dense (global-scratch) path, so that the
+ * parity suite covers it on every case.  Process-wide; returns 0. */
+int smg_debug_force_dense(int32_t on);
 
 #ifdef __cplusplus
 }

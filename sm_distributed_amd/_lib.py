@@ -43,6 +43,7 @@ PROTOTYPES = {
     "smg_sample_spectra": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _I64, _P, _P, _P, _I64, _P, _P]),
     "smg_debug_stream_read": (ctypes.c_int, [_P, _I64, _P, _I32, _P]),
     "smg_debug_force_two_level": (ctypes.c_int, [_I32]),
+    "smg_debug_force_dense": (ctypes.c_int, [_I32]),
     "smg_isotope_centroids": (ctypes.c_int, [ctypes.c_char_p, _I32, _D, _I32, _I32, _I32, _P, _P,
                                              ctypes.POINTER(_I32)]),
     "smg_isotope_centroids_batch": (ctypes.c_int, [_P, _P, _I64, _I32, _D, _I32, _I32, _I32, _P, _P, _P, _I32]),

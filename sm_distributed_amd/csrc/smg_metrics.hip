@@ -1497,18 +1497,28 @@ __global__ void list_positions_kernel(uint32_t* list, uint32_t* count, int64_t n
 // ---------------------------------------------------------------------------------------------
 // dense path: persistent workgroups, one global scratch slot each
 // ---------------------------------------------------------------------------------------------
+// Sparse over the slot's pixel-sized arrays: x / y (f64 images), L8 (level index) and E8 (eL) are zero
+// between ions and only the pixels a window touches are written and cleared again, so an ion costs
+// O(window points + chaos candidates), not O(K * N_px).  mark holds generation tags (one fresh tag per window
+// and per candidate pass): the first lane to tag a pixel owns it and lists it (plist: principal owners,
+// ylist: current tail window's owners).  par and elist are free until chaos and double as the clip's value
+// list (vals, 8 B per pixel).
 struct DenseSlot {
   double* x;
   double* y;
   uint32_t* par;
   uint32_t* elist;
+  uint32_t* mark;
+  uint32_t* plist;
+  uint32_t* ylist;
   uint8_t* L8;
-  uint8_t* T8;
   uint8_t* E8;
+  double* vals;  // aliases par + elist
 };
 
 static inline size_t dense_slot_bytes(int npx) {
-  return al16((size_t)npx * 8) * 2 + al16((size_t)npx * 4) * 2 + al16((size_t)npx) * 3 + 256;
+  return al16((size_t)npx * 8) * 2 + al16((size_t)npx * 8) + al16((size_t)npx * 4) * 3 + al16((size_t)npx) * 2 +
+         256;
 }
 
 __device__ __forceinline__ DenseSlot dense_slot(unsigned char* base, int npx) {
@@ -1519,13 +1529,17 @@ __device__ __forceinline__ DenseSlot dense_slot(unsigned char* base, int npx) {
   o += a16((size_t)npx * 8);
   S.y = reinterpret_cast<double*>(base + o);
   o += a16((size_t)npx * 8);
-  S.par = reinterpret_cast<uint32_t*>(base + o);
+  S.par = reinterpret_cast<uint32_t*>(base + o);  // par (npx u32) then elist (npx u32): 8*npx bytes
+  S.elist = S.par + npx;
+  S.vals = reinterpret_cast<double*>(base + o);
+  o += a16((size_t)npx * 8);
+  S.mark = reinterpret_cast<uint32_t*>(base + o);
   o += a16((size_t)npx * 4);
-  S.elist = reinterpret_cast<uint32_t*>(base + o);
+  S.plist = reinterpret_cast<uint32_t*>(base + o);
+  o += a16((size_t)npx * 4);
+  S.ylist = reinterpret_cast<uint32_t*>(base + o);
   o += a16((size_t)npx * 4);
   S.L8 = base + o;
-  o += a16((size_t)npx);
-  S.T8 = base + o;
   o += a16((size_t)npx);
   S.E8 = base + o;
   return S;
@@ -1561,14 +1575,43 @@ __device__ __forceinline__ bool guf_unite(uint32_t* par, uint32_t a, uint32_t b)
   }
 }
 
+// index of this lane's item in a block-wide list when pred holds (wave-aggregated LDS counter)
+__device__ __forceinline__ int wave_append(bool pred, int* cnt) {
+  const uint64_t m = __ballot(pred);
+  if (m == 0ull) return -1;
+  const int lane = threadIdx.x & 63;
+  const int first = __ffsll((unsigned long long)m) - 1;
+  int base = 0;
+  if (lane == first) base = atomicAdd(cnt, __popcll(m));
+  base = __shfl(base, first);
+  return pred ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+
+// img[p] += v over the window's points; the first lane to tag a pixel with `gen` lists it.  Returns the number
+// of listed pixels (caller: __threadfence + __syncthreads before reading img).
 template <int FMT>
-__device__ void scatter_window(const Hits<FMT>& hits, int64_t a, int64_t b, double* img) {
-  for (int64_t i = a + threadIdx.x; i < b; i += BLOCK) {
-    uint32_t p;
-    double v;
-    hits.get(i, p, v);
-    atomicAdd(&img[p], v);
+__device__ int scatter_window(const Hits<FMT>& hits, int64_t a, int64_t b, double* img, uint32_t* mark,
+                              uint32_t gen, uint32_t* list, int* cnt) {
+  if (threadIdx.x == 0) *cnt = 0;
+  __syncthreads();
+  for (int64_t i0 = a; i0 < b; i0 += BLOCK) {
+    const int64_t i = i0 + threadIdx.x;
+    bool own = false;
+    uint32_t p = 0;
+    if (i < b) {
+      double v;
+      hits.get(i, p, v);
+      atomicAdd(&img[p], v);
+      own = atomicExch(&mark[p], gen) != gen;
+    }
+    const int idx = wave_append(own, cnt);
+    if (own) list[idx] = p;
   }
+  __threadfence();
+  __syncthreads();
+  const int n = *cnt;
+  __syncthreads();
+  return n;
 }
 
 // k-th smallest (0-based) of n positive doubles (list, written by this block): MSB-first radix select over
@@ -1603,14 +1646,19 @@ __device__ double block_select_pos(const double* list, int n, int k, uint32_t* h
 }
 
 // Gated hot-spot clip (image_generation.do_preprocessing / q; the oracle's quantile_clip): every pixel above
-// np.percentile(positive pixels, q) ('linear' method) is set to that value.  `list` is npx doubles of scratch.
-__device__ void clip_image(double* img, double* list, int npx, double q, uint32_t* hist, int* sh) {
+// np.percentile(positive pixels, q) ('linear' method) is set to that value.  The image is zero outside its n
+// listed pixels; vals is scratch for their values.
+__device__ void clip_image(double* img, const uint32_t* list, int n_list, double* vals, double q, uint32_t* hist,
+                           int* sh) {
   const int tid = threadIdx.x;
   if (tid == 0) sh[2] = 0;
   __syncthreads();
-  for (int p = tid; p < npx; p += BLOCK) {
-    const double v = ld_agent(&img[p]);
-    if (v > 0.0) list[atomicAdd(&sh[2], 1)] = v;
+  for (int i0 = 0; i0 < n_list; i0 += BLOCK) {
+    const int i = i0 + tid;
+    double v = 0.0;
+    if (i < n_list) v = ld_agent(&img[list[i]]);
+    const int idx = wave_append(v > 0.0, &sh[2]);
+    if (v > 0.0) vals[idx] = v;
   }
   __threadfence();
   __syncthreads();
@@ -1633,16 +1681,28 @@ __device__ void clip_image(double* img, double* list, int npx, double q, uint32_
     i1 = i0 + 1;
     gamma = vi - floor(vi);
   }
-  const double a = block_select_pos(list, n, i0, hist, sh);
-  const double b = (i1 == i0) ? a : block_select_pos(list, n, i1, hist, sh);
+  const double a = block_select_pos(vals, n, i0, hist, sh);
+  const double b = (i1 == i0) ? a : block_select_pos(vals, n, i1, hist, sh);
   const double d = b - a;
   const double thr = gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
-  for (int p = tid; p < npx; p += BLOCK) {
+  for (int i = tid; i < n_list; i += BLOCK) {
+    const uint32_t p = list[i];
     const double v = ld_agent(&img[p]);
     if (v > thr) img[p] = thr;
   }
   __threadfence();
   __syncthreads();
+}
+
+// dilation of the level image with the 4-cross at (r, c) (outside = 0)
+__device__ __forceinline__ int dilate_at(const uint8_t* L8, int r, int c, int nr, int nc) {
+  const int p = r * nc + c;
+  int d = L8[p];
+  if (r > 0) d = max(d, (int)L8[p - nc]);
+  if (r + 1 < nr) d = max(d, (int)L8[p + nc]);
+  if (c > 0) d = max(d, (int)L8[p - 1]);
+  if (c + 1 < nc) d = max(d, (int)L8[p + 1]);
+  return d;
 }
 
 template <int FMT>
@@ -1662,6 +1722,8 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
   DenseSlot S = dense_slot(scratch + (size_t)blockIdx.x * slot_bytes, P.npx);
   const int npx = P.npx;
   const uint32_t total = *dense_count;
+  bool fresh = true;
+  uint32_t gen = 0;
 
   while (true) {
     if (tid == 0) {
@@ -1686,20 +1748,26 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
       __syncthreads();
       continue;
     }
+    if (fresh) {  // the slot's first ion: clean images, levels, tags (plain stores land in L2 before atomics)
+      for (int p = tid; p < npx; p += BLOCK) {
+        S.x[p] = 0.0;
+        S.y[p] = 0.0;
+        S.mark[p] = 0u;
+        S.L8[p] = 0;
+        S.E8[p] = 0;
+      }
+      __threadfence();
+      __syncthreads();
+      fresh = false;
+    }
 
-    // principal image (agent fences: plain zero stores must land in L2 before the L2 atomics,
-    // and the atomics before the loads that follow)
-    for (int p = tid; p < npx; p += BLOCK) S.x[p] = 0.0;
-    __threadfence();
-    __syncthreads();
-    scatter_window<FMT>(hits, lo[w0], hi[w0], S.x);
-    __threadfence();
-    __syncthreads();
-    if (P.clip) clip_image(S.x, S.y, npx, P.q, sh_hist, sh_sel);  // y is free until the other windows
+    // principal image
+    const int np = scatter_window<FMT>(hits, lo[w0], hi[w0], S.x, S.mark, ++gen, S.plist, &sh_ctr[2]);
+    if (P.clip) clip_image(S.x, S.plist, np, S.vals, P.q, sh_hist, sh_sel);
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     double mx = -INFINITY;
-    for (int p = tid; p < npx; p += BLOCK) {
-      const double v = ld_agent(&S.x[p]);
+    for (int i = tid; i < np; i += BLOCK) {
+      const double v = ld_agent(&S.x[S.plist[i]]);
       acc[0] += v;
       acc[1] += v * v;
       if (v > 0.0) {
@@ -1708,23 +1776,19 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
       }
       mx = v > mx ? v : mx;
     }
+    if (np < npx) mx = mx > 0.0 ? mx : 0.0;  // unlisted pixels are zero
     block_sum<BLOCK, 4>(acc, red);
     const double sx = acc[0], sxx = acc[1], s0 = acc[2], npos = acc[3];
     const double vmax = block_max(mx, red);
     const bool chaos_ok = (sx > 0.0) && (npos >= 4.0);
 
-    // other windows
+    // other windows, joined against x through the dense principal image
     for (int k = 1; k < K; ++k) {
-      for (int p = tid; p < npx; p += BLOCK) S.y[p] = 0.0;
-      __threadfence();
-      __syncthreads();
-      scatter_window<FMT>(hits, lo[w0 + k], hi[w0 + k], S.y);
-      __threadfence();
-      __syncthreads();
-      // par and elist (contiguous, 8*npx bytes) are free until chaos
-      if (P.clip) clip_image(S.y, reinterpret_cast<double*>(S.par), npx, P.q, sh_hist, sh_sel);
+      const int ny = scatter_window<FMT>(hits, lo[w0 + k], hi[w0 + k], S.y, S.mark, ++gen, S.ylist, &sh_ctr[2]);
+      if (P.clip) clip_image(S.y, S.ylist, ny, S.vals, P.q, sh_hist, sh_sel);
       double a2[4] = {0.0, 0.0, 0.0, 0.0};
-      for (int p = tid; p < npx; p += BLOCK) {
+      for (int i = tid; i < ny; i += BLOCK) {
+        const uint32_t p = S.ylist[i];
         const double y = ld_agent(&S.y[p]);
         const double x = ld_agent(&S.x[p]);
         a2[0] += y;
@@ -1739,48 +1803,62 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
         kst[2 * MAXK_DENSE + k] = a2[1];
         kst[3 * MAXK_DENSE + k] = a2[2];
       }
+      for (int i = tid; i < ny; i += BLOCK) S.y[S.ylist[i]] = 0.0;
+      __threadfence();
+      __syncthreads();
     }
     __syncthreads();
 
     double chaos_raw = NAN;
+    int m = 0;
     if (chaos_ok) {
       const int nr = P.nrows, nc = P.ncols;
-      for (int p = tid; p < npx; p += BLOCK) S.L8[p] = (uint8_t)level_of(ld_agent(&S.x[p]), vmax, P);
-      __syncthreads();
-      for (int p = tid; p < npx; p += BLOCK) {  // dilation with the 4-cross (outside = 0)
-        const int r = p / nc, c = p - r * nc;
-        int d = S.L8[p];
-        if (r > 0) d = max(d, (int)S.L8[p - nc]);
-        if (r + 1 < nr) d = max(d, (int)S.L8[p + nc]);
-        if (c > 0) d = max(d, (int)S.L8[p - 1]);
-        if (c + 1 < nc) d = max(d, (int)S.L8[p + 1]);
-        S.T8[p] = (uint8_t)d;
+      for (int i = tid; i < np; i += BLOCK) {
+        const uint32_t p = S.plist[i];
+        S.L8[p] = (uint8_t)level_of(ld_agent(&S.x[p]), vmax, P);
       }
       __syncthreads();
-      for (int p = tid; p < npx; p += BLOCK) {  // erosion with the 3x3 box
-        const int r = p / nc, c = p - r * nc;
-        int e = 1 << 20;
-        for (int a = -1; a <= 1; ++a)
-          for (int b = -1; b <= 1; ++b) {
-            const int rr = r + a, cc = c + b;
-            if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) {
-              if (!P.erosion_border) e = 0;
-              continue;
-            }
-            e = min(e, (int)S.T8[rr * nc + cc]);
+      // eL = erode_box(dilate_cross(L)) > 0 only on the 4-cross around a pixel with L > 0: those are the candidates
+      const uint32_t gc = ++gen;
+      for (int i0 = 0; i0 < np; i0 += BLOCK) {
+        const int i = i0 + tid;
+        int p = -1;
+        if (i < np && S.L8[S.plist[i]] > 0) p = (int)S.plist[i];
+        const int r0 = p >= 0 ? p / nc : 0, c0 = p >= 0 ? p - r0 * nc : 0;
+        for (int j = 0; j < 5; ++j) {
+          int q = -1, r = r0, c = c0;
+          if (p >= 0) {
+            r += (j == 1) ? -1 : (j == 2) ? 1 : 0;
+            c += (j == 3) ? -1 : (j == 4) ? 1 : 0;
+            if (r >= 0 && r < nr && c >= 0 && c < nc) q = r * nc + c;
           }
-        if (e >= (1 << 20)) e = 0;
-        S.E8[p] = (uint8_t)e;
-        if (e >= 1) {
-          const int idx = atomicAdd(&sh_ctr[0], 1);
-          S.elist[idx] = (uint32_t)p;
-          S.par[p] = (uint32_t)p;
-          atomicMax(&sh_ctr[1], e);
+          int e = 0;
+          if (q >= 0 && atomicExch(&S.mark[q], gc) != gc) {
+            e = 1 << 20;
+            for (int a = -1; a <= 1; ++a)
+              for (int b = -1; b <= 1; ++b) {
+                const int rr = r + a, cc = c + b;
+                if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) {
+                  if (!P.erosion_border) e = 0;
+                  continue;
+                }
+                e = min(e, dilate_at(S.L8, rr, cc, nr, nc));
+              }
+            if (e >= (1 << 20)) e = 0;
+          }
+          const int idx = wave_append(e >= 1, &sh_ctr[0]);
+          if (e >= 1) {
+            S.E8[q] = (uint8_t)e;
+            S.elist[idx] = (uint32_t)q;
+            S.par[q] = (uint32_t)q;
+            atomicMax(&sh_ctr[1], e);
+          }
         }
       }
       __threadfence();
       __syncthreads();
-      const int m = sh_ctr[0], emax = sh_ctr[1];
+      m = sh_ctr[0];
+      const int emax = sh_ctr[1];
       double esum = 0.0, wsum = 0.0;
       for (int i = tid; i < m; i += BLOCK) esum += (double)S.E8[S.elist[i]];
       for (int t = emax; t >= 1; --t) {
@@ -1830,6 +1908,14 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
       finalize_ion(K, t, s, sx, sxx, sy, syy, sxy, (double)npx, chaos_raw, ion, flags, oc, osp, osc, omsm,
                    oflags);
     }
+    // clean what this ion wrote
+    for (int i = tid; i < m; i += BLOCK) S.E8[S.elist[i]] = 0;
+    for (int i = tid; i < np; i += BLOCK) {
+      const uint32_t p = S.plist[i];
+      S.x[p] = 0.0;
+      S.L8[p] = 0;
+    }
+    __threadfence();
     __syncthreads();
   }
 }
@@ -1869,6 +1955,7 @@ static constexpr int BIG2_RMAX = 4;
 using Main2Lay = Lay2<MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX>;
 using Big2Lay = Lay2<BIG_BLOCK / WAVE, BIG_BLOCK * BIG2_RMAX>;
 static int g_force_two_level = 0;  // smg_debug_force_two_level: two-level passes for every image size
+static int g_force_dense = 0;      // smg_debug_force_dense: every ion on the dense path
 
 static int device_cus() {
   int dev = 0, cus = 0;
@@ -1902,8 +1989,8 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   const size_t lds_main = two ? Main2Lay::bytes(P.npx) : MainLay::bytes(P.npx);
   const size_t lds_big = two ? Big2Lay::bytes(P.npx) : BigLay::bytes(P.npx);
   // the hot-spot clip needs whole images: every ion takes the dense path
-  const bool main_ok = !P.clip && (two || P.npx <= NPX_LDS_MAX) && lds_main <= MAIN_LDS;
-  const bool big_ok = !P.clip && (two || P.npx <= NPX_LDS_MAX) && lds_big <= BIG_LDS;
+  const bool main_ok = !P.clip && !g_force_dense && (two || P.npx <= NPX_LDS_MAX) && lds_main <= MAIN_LDS;
+  const bool big_ok = !P.clip && !g_force_dense && (two || P.npx <= NPX_LDS_MAX) && lds_big <= BIG_LDS;
   const int cus = device_cus();
   if (main_ok || big_ok) {
     hipLaunchKernelGGL(ion_desc_kernel<FMT>, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, hits, lo, hi,
@@ -1975,6 +2062,11 @@ int smg_debug_stamps(unsigned long long* host_out, int n) {
 
 int smg_debug_force_two_level(int32_t on) {
   g_force_two_level = on ? 1 : 0;
+  return SMG_OK;
+}
+
+int smg_debug_force_dense(int32_t on) {
+  g_force_dense = on ? 1 : 0;
   return SMG_OK;
 }
 

@@ -136,6 +136,30 @@ def test_forced_two_level_matches_oracle(name):
         assert err.max(initial=0.0) <= METRIC_ATOL, (col, float(err.max()), int(np.argmax(err)))
 
 
+@pytest.mark.parametrize("name", CASES)
+def test_forced_dense_matches_oracle(name):
+    """Every case again with every ion on the dense path (smg_debug_force_dense): sparse scatter into the slot's
+    pixel-sized images, owner lists, candidate-only chaos."""
+    from sm_distributed_amd import _lib
+    ds, ions, ppm, kw, imgs, df, _, _, _, _ = _run_case(name)
+    L = _lib.lib()
+    L.smg_debug_force_dense(1)
+    try:
+        _, m, _, _ = _device_run(ds, ions, ppm, **kw)
+        _, m2, _, _ = _device_run(ds, ions, ppm, **kw)  # a second launch: slots start clean every launch
+    finally:
+        L.smg_debug_force_dense(0)
+    has = (m["flags"] & 1) != 0
+    assert ((m["flags"][has] & 2) != 0).all()
+    idx = {k: i for i, k in enumerate(zip(ions.sf_ids.tolist(), ions.adducts.tolist()))}
+    assert set(zip(ions.sf_ids[has].tolist(), ions.adducts[has].tolist())) == set(df.index.tolist())
+    rows = np.array([idx[k] for k in df.index.tolist()], dtype=np.int64)
+    for col in ("chaos", "spatial", "spectral", "msm"):
+        err = np.abs(df[col].to_numpy() - m[col][rows])
+        assert err.max(initial=0.0) <= METRIC_ATOL, (col, float(err.max()), int(np.argmax(err)))
+        assert np.abs(m2[col][rows] - m[col][rows]).max(initial=0.0) <= 1e-9
+
+
 def test_sort_is_a_permutation():
     ds, ions, ppm, kw, imgs, df, peaks, m, lo, hi = _run_case("basic")
     a = np.sort(peaks.hits.cpu().numpy())  # flags are set before the sort, so both sides carry them
