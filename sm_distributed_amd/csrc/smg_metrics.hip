@@ -1497,11 +1497,16 @@ __global__ void list_positions_kernel(uint32_t* list, uint32_t* count, int64_t n
 // ---------------------------------------------------------------------------------------------
 // dense path: persistent workgroups, one global scratch slot each
 // ---------------------------------------------------------------------------------------------
+#ifndef SMG_DBLOCK
+#define SMG_DBLOCK 1024
+#endif
+constexpr int DBLOCK = SMG_DBLOCK;  // dense kernel workgroup size
+constexpr int DNW = DBLOCK / WAVE;
 // Sparse over the slot's pixel-sized arrays: x / y (f64 images), L8 (level index) and E8 (eL) are zero
 // between ions and only the pixels a window touches are written and cleared again, so an ion costs
-// O(window points + chaos candidates), not O(K * N_px).  mark holds generation tags (one fresh tag per window
-// and per candidate pass): the first lane to tag a pixel owns it and lists it (plist: principal owners,
-// ylist: current tail window's owners).  par and elist are free until chaos and double as the clip's value
+// O(window points + chaos candidates), not O(K * N_px).  Each window lists its distinct pixels (plist: principal,
+// ylist: current tail window); mark holds generation tags (one fresh tag per window) through which
+// duplicate-flagged points claim their pixel.  par and elist are free until chaos and double as the clip's value
 // list (vals, 8 B per pixel).
 struct DenseSlot {
   double* x;
@@ -1545,6 +1550,14 @@ __device__ __forceinline__ DenseSlot dense_slot(unsigned char* base, int npx) {
   return S;
 }
 
+// A slot is private to one workgroup (one CU, one XCD's L2): its global atomics complete in that L2 and its
+// readers load past L1 (ld_agent), so phases only need every lane's memory operations acknowledged and a
+// barrier -- no agent-scope fence (on gfx950 that writes back and invalidates the XCD's L2).
+__device__ __forceinline__ void slot_sync() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 template <typename T>
 __device__ __forceinline__ T ld_agent(const T* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1575,6 +1588,23 @@ __device__ __forceinline__ bool guf_unite(uint32_t* par, uint32_t a, uint32_t b)
   }
 }
 
+// block-wide sum of NV doubles for the 16-wave dense workgroup: wave partials in LDS, then every wave reduces
+// the 16 partials with one lane each (same order everywhere; keeps the reduction out of the register budget)
+template <int NV>
+__device__ __forceinline__ void dblock_sum(double (&v)[NV], double* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = wave_sum(v[j]);
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) scratch[j * DNW + wid] = v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = wave_sum(lane < DNW ? scratch[j * DNW + lane] : 0.0);
+  __syncthreads();
+}
+
 // index of this lane's item in a block-wide list when pred holds (wave-aggregated LDS counter)
 __device__ __forceinline__ int wave_append(bool pred, int* cnt) {
   const uint64_t m = __ballot(pred);
@@ -1587,28 +1617,36 @@ __device__ __forceinline__ int wave_append(bool pred, int* cnt) {
   return pred ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
 }
 
-// img[p] += v over the window's points; the first lane to tag a pixel with `gen` lists it.  Returns the number
-// of listed pixels (caller: __threadfence + __syncthreads before reading img).
+// The window's image into img (zero outside its listed pixels).  A point without the duplicate-candidate flag is
+// alone on its pixel in the window: it stores its value and lists the pixel.  Flagged points add atomically and
+// the first lane to tag the pixel with `gen` lists it.  Returns the number of listed pixels (ends with slot_sync:
+// the image is complete in L2 for ld_agent readers).
 template <int FMT>
 __device__ int scatter_window(const Hits<FMT>& hits, int64_t a, int64_t b, double* img, uint32_t* mark,
                               uint32_t gen, uint32_t* list, int* cnt) {
+  using H = Hits<FMT>;
   if (threadIdx.x == 0) *cnt = 0;
   __syncthreads();
-  for (int64_t i0 = a; i0 < b; i0 += BLOCK) {
+  for (int64_t i0 = a; i0 < b; i0 += DBLOCK) {
     const int64_t i = i0 + threadIdx.x;
     bool own = false;
     uint32_t p = 0;
     if (i < b) {
-      double v;
-      hits.get(i, p, v);
-      atomicAdd(&img[p], v);
-      own = atomicExch(&mark[p], gen) != gen;
+      const typename H::Reg r = hits.load(i);
+      p = H::pix(r);
+      const double v = H::val(r);
+      if (H::dup(r)) {
+        atomicAdd(&img[p], v);
+        own = atomicExch(&mark[p], gen) != gen;
+      } else {
+        img[p] = v;
+        own = true;
+      }
     }
     const int idx = wave_append(own, cnt);
     if (own) list[idx] = p;
   }
-  __threadfence();
-  __syncthreads();
+  slot_sync();
   const int n = *cnt;
   __syncthreads();
   return n;
@@ -1620,9 +1658,9 @@ __device__ double block_select_pos(const double* list, int n, int k, uint32_t* h
   const int tid = threadIdx.x;
   uint64_t prefix = 0ull, mask = 0ull;
   for (int shift = 56; shift >= 0; shift -= 8) {
-    for (int i = tid; i < 256; i += BLOCK) hist[i] = 0u;
+    for (int i = tid; i < 256; i += DBLOCK) hist[i] = 0u;
     __syncthreads();
-    for (int i = tid; i < n; i += BLOCK) {
+    for (int i = tid; i < n; i += DBLOCK) {
       const uint64_t b = (uint64_t)__double_as_longlong(ld_agent(&list[i]));
       if ((b & mask) == prefix) atomicAdd(&hist[(b >> shift) & 255u], 1u);
     }
@@ -1653,15 +1691,14 @@ __device__ void clip_image(double* img, const uint32_t* list, int n_list, double
   const int tid = threadIdx.x;
   if (tid == 0) sh[2] = 0;
   __syncthreads();
-  for (int i0 = 0; i0 < n_list; i0 += BLOCK) {
+  for (int i0 = 0; i0 < n_list; i0 += DBLOCK) {
     const int i = i0 + tid;
     double v = 0.0;
     if (i < n_list) v = ld_agent(&img[list[i]]);
     const int idx = wave_append(v > 0.0, &sh[2]);
     if (v > 0.0) vals[idx] = v;
   }
-  __threadfence();
-  __syncthreads();
+  slot_sync();
   const int n = sh[2];
   __syncthreads();
   if (n == 0) return;
@@ -1685,34 +1722,22 @@ __device__ void clip_image(double* img, const uint32_t* list, int n_list, double
   const double b = (i1 == i0) ? a : block_select_pos(vals, n, i1, hist, sh);
   const double d = b - a;
   const double thr = gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
-  for (int i = tid; i < n_list; i += BLOCK) {
+  for (int i = tid; i < n_list; i += DBLOCK) {
     const uint32_t p = list[i];
     const double v = ld_agent(&img[p]);
     if (v > thr) img[p] = thr;
   }
-  __threadfence();
-  __syncthreads();
-}
-
-// dilation of the level image with the 4-cross at (r, c) (outside = 0)
-__device__ __forceinline__ int dilate_at(const uint8_t* L8, int r, int c, int nr, int nc) {
-  const int p = r * nc + c;
-  int d = L8[p];
-  if (r > 0) d = max(d, (int)L8[p - nc]);
-  if (r + 1 < nr) d = max(d, (int)L8[p + nc]);
-  if (c > 0) d = max(d, (int)L8[p - 1]);
-  if (c + 1 < nc) d = max(d, (int)L8[p + 1]);
-  return d;
+  slot_sync();
 }
 
 template <int FMT>
-__global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
+__global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
     Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
     const int64_t* __restrict__ ion_off, const double* __restrict__ theor, int64_t n_ions, Params P,
     const uint32_t* __restrict__ dense_list, const uint32_t* __restrict__ dense_count, uint32_t* next,
     unsigned char* scratch, size_t slot_bytes, double* __restrict__ oc, double* __restrict__ osp,
     double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags) {
-  __shared__ double red[8 * NW];
+  __shared__ double red[8 * DNW];
   __shared__ double kst[4 * MAXK_DENSE];
   __shared__ int sh_ion;
   __shared__ int sh_ctr[4];
@@ -1724,6 +1749,7 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
   const uint32_t total = *dense_count;
   bool fresh = true;
   uint32_t gen = 0;
+  STAMP_DECL();
 
   while (true) {
     if (tid == 0) {
@@ -1735,6 +1761,7 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
     __syncthreads();
     const int64_t ion = sh_ion;
     if (ion < 0) break;
+    STAMP(15);
     const int64_t w0 = ion_off[ion];
     const int K = (int)(ion_off[ion + 1] - w0);
     uint32_t flags = SMG_ION_DENSE;
@@ -1749,24 +1776,24 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
       continue;
     }
     if (fresh) {  // the slot's first ion: clean images, levels, tags (plain stores land in L2 before atomics)
-      for (int p = tid; p < npx; p += BLOCK) {
+      for (int p = tid; p < npx; p += DBLOCK) {
         S.x[p] = 0.0;
         S.y[p] = 0.0;
         S.mark[p] = 0u;
         S.L8[p] = 0;
         S.E8[p] = 0;
       }
-      __threadfence();
-      __syncthreads();
+      slot_sync();
       fresh = false;
     }
 
+    STAMP(10);
     // principal image
     const int np = scatter_window<FMT>(hits, lo[w0], hi[w0], S.x, S.mark, ++gen, S.plist, &sh_ctr[2]);
     if (P.clip) clip_image(S.x, S.plist, np, S.vals, P.q, sh_hist, sh_sel);
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     double mx = -INFINITY;
-    for (int i = tid; i < np; i += BLOCK) {
+    for (int i = tid; i < np; i += DBLOCK) {
       const double v = ld_agent(&S.x[S.plist[i]]);
       acc[0] += v;
       acc[1] += v * v;
@@ -1777,17 +1804,18 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
       mx = v > mx ? v : mx;
     }
     if (np < npx) mx = mx > 0.0 ? mx : 0.0;  // unlisted pixels are zero
-    block_sum<BLOCK, 4>(acc, red);
+    dblock_sum<4>(acc, red);
     const double sx = acc[0], sxx = acc[1], s0 = acc[2], npos = acc[3];
-    const double vmax = block_max(mx, red);
+    const double vmax = block_max<DNW>(mx, red);
     const bool chaos_ok = (sx > 0.0) && (npos >= 4.0);
 
+    STAMP(11);
     // other windows, joined against x through the dense principal image
     for (int k = 1; k < K; ++k) {
       const int ny = scatter_window<FMT>(hits, lo[w0 + k], hi[w0 + k], S.y, S.mark, ++gen, S.ylist, &sh_ctr[2]);
       if (P.clip) clip_image(S.y, S.ylist, ny, S.vals, P.q, sh_hist, sh_sel);
       double a2[4] = {0.0, 0.0, 0.0, 0.0};
-      for (int i = tid; i < ny; i += BLOCK) {
+      for (int i = tid; i < ny; i += DBLOCK) {
         const uint32_t p = S.ylist[i];
         const double y = ld_agent(&S.y[p]);
         const double x = ld_agent(&S.x[p]);
@@ -1796,53 +1824,78 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
         a2[2] += x * y;
         if (x > 0.0) a2[3] += y;
       }
-      block_sum<BLOCK, 4>(a2, red);
+      dblock_sum<4>(a2, red);
       if (tid == 0) {
         kst[0 * MAXK_DENSE + k] = a2[3];
         kst[1 * MAXK_DENSE + k] = a2[0];
         kst[2 * MAXK_DENSE + k] = a2[1];
         kst[3 * MAXK_DENSE + k] = a2[2];
       }
-      for (int i = tid; i < ny; i += BLOCK) S.y[S.ylist[i]] = 0.0;
-      __threadfence();
-      __syncthreads();
+      for (int i = tid; i < ny; i += DBLOCK) S.y[S.ylist[i]] = 0.0;
+      slot_sync();
     }
     __syncthreads();
 
+    STAMP(12);
     double chaos_raw = NAN;
     int m = 0;
     if (chaos_ok) {
       const int nr = P.nrows, nc = P.ncols;
-      for (int i = tid; i < np; i += BLOCK) {
+      for (int i = tid; i < np; i += DBLOCK) {
         const uint32_t p = S.plist[i];
         S.L8[p] = (uint8_t)level_of(ld_agent(&S.x[p]), vmax, P);
       }
       __syncthreads();
-      // eL = erode_box(dilate_cross(L)) > 0 only on the 4-cross around a pixel with L > 0: those are the candidates
-      const uint32_t gc = ++gen;
-      for (int i0 = 0; i0 < np; i0 += BLOCK) {
+      // eL = erode_box(dilate_cross(L)) > 0 only on the 4-cross around a pixel with L > 0: those are the
+      // candidates.  Candidate q is evaluated once, by the smallest-index pixel with L > 0 on its 4-cross.  Each
+      // such pixel s loads the 7x7 level window around it in one batch (clamped addresses, 0 outside the image),
+      // then decides ownership and eL for its five candidates in registers.
+      for (int i0 = 0; i0 < np; i0 += DBLOCK) {
         const int i = i0 + tid;
         int p = -1;
         if (i < np && S.L8[S.plist[i]] > 0) p = (int)S.plist[i];
         const int r0 = p >= 0 ? p / nc : 0, c0 = p >= 0 ? p - r0 * nc : 0;
+        int W[7][7];
+#pragma unroll
+        for (int dr = -3; dr <= 3; ++dr)
+#pragma unroll
+          for (int dc = -3; dc <= 3; ++dc) {
+            const int rr = r0 + dr, cc = c0 + dc;
+            const int rc = min(max(rr, 0), nr - 1), ccl = min(max(cc, 0), nc - 1);
+            const int v = (p >= 0) ? (int)S.L8[rc * nc + ccl] : 0;
+            W[dr + 3][dc + 3] = (rr == rc && cc == ccl) ? v : 0;
+          }
+#pragma unroll
         for (int j = 0; j < 5; ++j) {
-          int q = -1, r = r0, c = c0;
-          if (p >= 0) {
-            r += (j == 1) ? -1 : (j == 2) ? 1 : 0;
-            c += (j == 3) ? -1 : (j == 4) ? 1 : 0;
-            if (r >= 0 && r < nr && c >= 0 && c < nc) q = r * nc + c;
+          const int qr = (j == 1) ? -1 : (j == 2) ? 1 : 0, qc = (j == 3) ? -1 : (j == 4) ? 1 : 0;
+          const int r = r0 + qr, c = c0 + qc;
+          int q = -1;
+          if (p >= 0 && r >= 0 && r < nr && c >= 0 && c < nc) {
+            // the first pixel with L > 0 among q-nc, q-1, q, q+1, q+nc (ascending index) must be p
+            const int wr = qr + 3, wc = qc + 3;
+            int orr = 9, occ = 9;
+            if (W[wr + 1][wc] > 0) orr = 1, occ = 0;
+            if (W[wr][wc + 1] > 0) orr = 0, occ = 1;
+            if (W[wr][wc] > 0) orr = 0, occ = 0;
+            if (W[wr][wc - 1] > 0) orr = 0, occ = -1;
+            if (W[wr - 1][wc] > 0) orr = -1, occ = 0;
+            if (qr + orr == 0 && qc + occ == 0) q = r * nc + c;
           }
           int e = 0;
-          if (q >= 0 && atomicExch(&S.mark[q], gc) != gc) {
+          if (q >= 0) {
             e = 1 << 20;
+#pragma unroll
             for (int a = -1; a <= 1; ++a)
+#pragma unroll
               for (int b = -1; b <= 1; ++b) {
                 const int rr = r + a, cc = c + b;
                 if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) {
                   if (!P.erosion_border) e = 0;
                   continue;
                 }
-                e = min(e, dilate_at(S.L8, rr, cc, nr, nc));
+                const int wr = qr + a + 3, wc = qc + b + 3;
+                const int t = max(max(W[wr][wc], W[wr - 1][wc]), max(max(W[wr + 1][wc], W[wr][wc - 1]), W[wr][wc + 1]));
+                e = min(e, t);
               }
             if (e >= (1 << 20)) e = 0;
           }
@@ -1855,14 +1908,14 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
           }
         }
       }
-      __threadfence();
-      __syncthreads();
+      slot_sync();
       m = sh_ctr[0];
       const int emax = sh_ctr[1];
+      STAMP(13);
       double esum = 0.0, wsum = 0.0;
-      for (int i = tid; i < m; i += BLOCK) esum += (double)S.E8[S.elist[i]];
+      for (int i = tid; i < m; i += DBLOCK) esum += (double)S.E8[S.elist[i]];
       for (int t = emax; t >= 1; --t) {
-        for (int i = tid; i < m; i += BLOCK) {
+        for (int i = tid; i < m; i += DBLOCK) {
           const int p = (int)S.elist[i];
           const int e = S.E8[p];
           if (e < t) continue;
@@ -1885,39 +1938,29 @@ __global__ void __launch_bounds__(BLOCK) ion_dense_kernel(
         __syncthreads();
       }
       double a3[2] = {esum, wsum};
-      block_sum<BLOCK, 2>(a3, red);
+      dblock_sum<2>(a3, red);
       chaos_raw = 1.0 - (a3[0] - a3[1]) / (double)P.nlevels / npos;
     } else {
       flags |= SMG_ION_CHAOS_NAN;
     }
 
-    if (tid == 0) {
-      double t[MAXK_DENSE], s[MAXK_DENSE], sy[MAXK_DENSE], syy[MAXK_DENSE], sxy[MAXK_DENSE];
-      for (int k = 0; k < K; ++k) {
-        t[k] = theor[w0 + k];
-        if (k == 0) {
-          s[k] = s0;
-          sy[k] = syy[k] = sxy[k] = 0.0;
-        } else {
-          s[k] = kst[0 * MAXK_DENSE + k];
-          sy[k] = kst[1 * MAXK_DENSE + k];
-          syy[k] = kst[2 * MAXK_DENSE + k];
-          sxy[k] = kst[3 * MAXK_DENSE + k];
-        }
-      }
-      finalize_ion(K, t, s, sx, sxx, sy, syy, sxy, (double)npx, chaos_raw, ion, flags, oc, osp, osc, omsm,
-                   oflags);
+    STAMP(14);
+    if (tid == 0) {  // per-window sums straight from LDS (kst rows: s, sy, syy, sxy; window 0 = principal)
+      kst[0] = s0;
+      kst[1 * MAXK_DENSE] = kst[2 * MAXK_DENSE] = kst[3 * MAXK_DENSE] = 0.0;
+      finalize_ion(K, theor + w0, kst, sx, sxx, kst + MAXK_DENSE, kst + 2 * MAXK_DENSE, kst + 3 * MAXK_DENSE,
+                   (double)npx, chaos_raw, ion, flags, oc, osp, osc, omsm, oflags);
     }
     // clean what this ion wrote
-    for (int i = tid; i < m; i += BLOCK) S.E8[S.elist[i]] = 0;
-    for (int i = tid; i < np; i += BLOCK) {
+    for (int i = tid; i < m; i += DBLOCK) S.E8[S.elist[i]] = 0;
+    for (int i = tid; i < np; i += DBLOCK) {
       const uint32_t p = S.plist[i];
       S.x[p] = 0.0;
       S.L8[p] = 0;
     }
-    __threadfence();
-    __syncthreads();
+    slot_sync();
   }
+  STAMP_FLUSH();
 }
 
 __global__ void list_all_kernel(uint32_t* list, uint32_t* count, const int64_t* ion_order, int64_t n) {
@@ -2033,7 +2076,7 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
     SMG_LAUNCH_CHECK();
   }
   const int nslots = (int)(n_ions < DENSE_SLOTS ? n_ions : DENSE_SLOTS);
-  hipLaunchKernelGGL(ion_dense_kernel<FMT>, dim3((unsigned)nslots), dim3(BLOCK), 0, st, hits, lo, hi, ion_off,
+  hipLaunchKernelGGL(ion_dense_kernel<FMT>, dim3((unsigned)nslots), dim3(DBLOCK), 0, st, hits, lo, hi, ion_off,
                      theor, n_ions, P, list_b, hdr + 2, hdr + 3, slots, slot_bytes, oc, osp, osc, omsm, oflags);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
