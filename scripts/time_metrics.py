@@ -9,8 +9,10 @@ import numpy as np
 import torch
 from sm_distributed_amd import engine as E, synthetic as syn, _lib
 
-ions = syn.make_ion_table(20000, seed=43, decoy_seed=44)
-mz, hits, dims, info = syn.make_dataset_torch(500, 500, 2000, seed=42, device="cuda", ions=ions)
+a = sys.argv[1:]  # optional workload: nrows ncols peaks n_sf (default config 3)
+nrows, ncols, pk, n_sf = (int(a[0]), int(a[1]), float(a[2]), int(a[3])) if len(a) >= 4 else (500, 500, 2000.0, 20000)
+ions = syn.make_ion_table(n_sf, seed=43, decoy_seed=44)
+mz, hits, dims, info = syn.make_dataset_torch(nrows, ncols, pk, seed=42, device="cuda", ions=ions)
 peaks = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
 dions = E.DeviceIons.from_arrays(ions.win_off, ions.peak_mz, ions.peak_int)
 m, lo, hi = E.run_hot_path(peaks, dions, 2.0, 30)

@@ -1518,12 +1518,13 @@ struct DenseSlot {
   uint32_t* ylist;
   uint8_t* L8;
   uint8_t* E8;
-  double* vals;  // aliases par + elist
+  uint32_t* gbm;  // presence bitmap when it does not fit the LDS (npx bits)
+  double* vals;   // aliases par + elist
 };
 
 static inline size_t dense_slot_bytes(int npx) {
   return al16((size_t)npx * 8) * 2 + al16((size_t)npx * 8) + al16((size_t)npx * 4) * 3 + al16((size_t)npx) * 2 +
-         256;
+         al16(((size_t)npx + 31) / 32 * 4) + 256;
 }
 
 __device__ __forceinline__ DenseSlot dense_slot(unsigned char* base, int npx) {
@@ -1547,6 +1548,8 @@ __device__ __forceinline__ DenseSlot dense_slot(unsigned char* base, int npx) {
   S.L8 = base + o;
   o += a16((size_t)npx);
   S.E8 = base + o;
+  o += a16((size_t)npx);
+  S.gbm = reinterpret_cast<uint32_t*>(base + o);
   return S;
 }
 
@@ -1623,7 +1626,7 @@ __device__ __forceinline__ int wave_append(bool pred, int* cnt) {
 // the image is complete in L2 for ld_agent readers).
 template <int FMT>
 __device__ int scatter_window(const Hits<FMT>& hits, int64_t a, int64_t b, double* img, uint32_t* mark,
-                              uint32_t gen, uint32_t* list, int* cnt) {
+                              uint32_t gen, uint32_t* list, int* cnt, uint32_t* bm = nullptr) {
   using H = Hits<FMT>;
   if (threadIdx.x == 0) *cnt = 0;
   __syncthreads();
@@ -1641,6 +1644,45 @@ __device__ int scatter_window(const Hits<FMT>& hits, int64_t a, int64_t b, doubl
       } else {
         img[p] = v;
         own = true;
+      }
+      if (bm && own) atomicOr(&bm[p >> 5], 1u << (p & 31));
+    }
+    const int idx = wave_append(own, cnt);
+    if (own) list[idx] = p;
+  }
+  slot_sync();
+  const int n = *cnt;
+  __syncthreads();
+  return n;
+}
+
+// A tail window joined against the principal image x (presence bitmap bm) without materialising it: a point
+// without the duplicate-candidate flag is alone on its pixel, so it adds (y, y^2, x*y, y[x>0]) to acc directly
+// (x loaded only when the pixel is in the principal image).  Flagged points are summed per pixel into y and
+// listed as with scatter_window; the caller adds their pixels.  Returns the number of listed pixels.
+template <int FMT>
+__device__ int tail_window(const Hits<FMT>& hits, int64_t a, int64_t b, const double* x, const uint32_t* bm,
+                           double* y, uint32_t* mark, uint32_t gen, uint32_t* list, int* cnt, double (&acc)[4]) {
+  using H = Hits<FMT>;
+  if (threadIdx.x == 0) *cnt = 0;
+  __syncthreads();
+  for (int64_t i0 = a; i0 < b; i0 += DBLOCK) {
+    const int64_t i = i0 + threadIdx.x;
+    bool own = false;
+    uint32_t p = 0;
+    if (i < b) {
+      const typename H::Reg r = hits.load(i);
+      p = H::pix(r);
+      const double v = H::val(r);
+      if (H::dup(r)) {
+        atomicAdd(&y[p], v);
+        own = atomicExch(&mark[p], gen) != gen;
+      } else {
+        const double xv = ((bm[p >> 5] >> (p & 31)) & 1u) ? ld_agent(&x[p]) : 0.0;
+        acc[0] += v;
+        acc[1] += v * v;
+        acc[2] += xv * v;
+        if (xv > 0.0) acc[3] += v;
       }
     }
     const int idx = wave_append(own, cnt);
@@ -1736,7 +1778,8 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
     const int64_t* __restrict__ ion_off, const double* __restrict__ theor, int64_t n_ions, Params P,
     const uint32_t* __restrict__ dense_list, const uint32_t* __restrict__ dense_count, uint32_t* next,
     unsigned char* scratch, size_t slot_bytes, double* __restrict__ oc, double* __restrict__ osp,
-    double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags) {
+    double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags, int bm_in_lds) {
+  extern __shared__ uint32_t dyn_bm[];  // presence bitmap of the principal image (when it fits)
   __shared__ double red[8 * DNW];
   __shared__ double kst[4 * MAXK_DENSE];
   __shared__ int sh_ion;
@@ -1749,6 +1792,10 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
   const uint32_t total = *dense_count;
   bool fresh = true;
   uint32_t gen = 0;
+  uint32_t* bm = bm_in_lds ? dyn_bm : S.gbm;
+  const int nbw = (npx + 31) / 32;
+  if (bm_in_lds)
+    for (int w = tid; w < nbw; w += DBLOCK) dyn_bm[w] = 0u;
   STAMP_DECL();
 
   while (true) {
@@ -1783,13 +1830,15 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
         S.L8[p] = 0;
         S.E8[p] = 0;
       }
+      if (!bm_in_lds)
+        for (int w = tid; w < nbw; w += DBLOCK) S.gbm[w] = 0u;
       slot_sync();
       fresh = false;
     }
 
     STAMP(10);
     // principal image
-    const int np = scatter_window<FMT>(hits, lo[w0], hi[w0], S.x, S.mark, ++gen, S.plist, &sh_ctr[2]);
+    const int np = scatter_window<FMT>(hits, lo[w0], hi[w0], S.x, S.mark, ++gen, S.plist, &sh_ctr[2], bm);
     if (P.clip) clip_image(S.x, S.plist, np, S.vals, P.q, sh_hist, sh_sel);
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     double mx = -INFINITY;
@@ -1812,13 +1861,18 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
     STAMP(11);
     // other windows, joined against x through the dense principal image
     for (int k = 1; k < K; ++k) {
-      const int ny = scatter_window<FMT>(hits, lo[w0 + k], hi[w0 + k], S.y, S.mark, ++gen, S.ylist, &sh_ctr[2]);
-      if (P.clip) clip_image(S.y, S.ylist, ny, S.vals, P.q, sh_hist, sh_sel);
-      double a2[4] = {0.0, 0.0, 0.0, 0.0};
+      double a2[4] = {0.0, 0.0, 0.0, 0.0};  // sy, syy, sxy, s (y[x > 0])
+      int ny;
+      if (P.clip) {  // the clip needs the whole tail image first
+        ny = scatter_window<FMT>(hits, lo[w0 + k], hi[w0 + k], S.y, S.mark, ++gen, S.ylist, &sh_ctr[2]);
+        clip_image(S.y, S.ylist, ny, S.vals, P.q, sh_hist, sh_sel);
+      } else {
+        ny = tail_window<FMT>(hits, lo[w0 + k], hi[w0 + k], S.x, bm, S.y, S.mark, ++gen, S.ylist, &sh_ctr[2], a2);
+      }
       for (int i = tid; i < ny; i += DBLOCK) {
         const uint32_t p = S.ylist[i];
         const double y = ld_agent(&S.y[p]);
-        const double x = ld_agent(&S.x[p]);
+        const double x = ((bm[p >> 5] >> (p & 31)) & 1u) ? ld_agent(&S.x[p]) : 0.0;
         a2[0] += y;
         a2[1] += y * y;
         a2[2] += x * y;
@@ -1846,41 +1900,85 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
         S.L8[p] = (uint8_t)level_of(ld_agent(&S.x[p]), vmax, P);
       }
       __syncthreads();
-      // eL = erode_box(dilate_cross(L)) > 0 only on the 4-cross around a pixel with L > 0: those are the
-      // candidates.  Candidate q is evaluated once, by the smallest-index pixel with L > 0 on its 4-cross.  Each
-      // such pixel s loads the 7x7 level window around it in one batch (clamped addresses, 0 outside the image),
-      // then decides ownership and eL for its five candidates in registers.
+      // eL = erode_box(dilate_cross(L)) > 0 only on the 4-cross around a pixel with L > 0, i.e. around a
+      // principal pixel: those are the candidates.  Candidate q is evaluated once, by the smallest-index
+      // principal pixel on its 4-cross.  Each principal pixel s reads the 7x7 presence window around it from the
+      // bitmap; a candidate survives only if every in-image pixel of its 3x3 box has a principal pixel on its
+      // cross (presence is a superset of L > 0), and only survivors load the 7x7 level window for the exact eL.
       for (int i0 = 0; i0 < np; i0 += DBLOCK) {
         const int i = i0 + tid;
-        int p = -1;
-        if (i < np && S.L8[S.plist[i]] > 0) p = (int)S.plist[i];
+        const int p = (i < np) ? (int)S.plist[i] : -1;
         const int r0 = p >= 0 ? p / nc : 0, c0 = p >= 0 ? p - r0 * nc : 0;
-        int W[7][7];
+        uint32_t B[7];  // bit (dc + 3) of B[dr + 3]: pixel (r0 + dr, c0 + dc) is in the image and principal
 #pragma unroll
-        for (int dr = -3; dr <= 3; ++dr)
+        for (int dr = -3; dr <= 3; ++dr) {
+          uint32_t row = 0u;
 #pragma unroll
           for (int dc = -3; dc <= 3; ++dc) {
             const int rr = r0 + dr, cc = c0 + dc;
-            const int rc = min(max(rr, 0), nr - 1), ccl = min(max(cc, 0), nc - 1);
-            const int v = (p >= 0) ? (int)S.L8[rc * nc + ccl] : 0;
-            W[dr + 3][dc + 3] = (rr == rc && cc == ccl) ? v : 0;
+            if (p >= 0 && rr >= 0 && rr < nr && cc >= 0 && cc < nc) {
+              const int qq = rr * nc + cc;
+              row |= ((bm[qq >> 5] >> (qq & 31)) & 1u) << (dc + 3);
+            }
           }
+          B[dr + 3] = row;
+        }
+        auto pres = [&](int wr, int wc) -> uint32_t { return (B[wr] >> wc) & 1u; };
+        bool cand[5];
+        bool any = false;
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
           const int qr = (j == 1) ? -1 : (j == 2) ? 1 : 0, qc = (j == 3) ? -1 : (j == 4) ? 1 : 0;
           const int r = r0 + qr, c = c0 + qc;
-          int q = -1;
-          if (p >= 0 && r >= 0 && r < nr && c >= 0 && c < nc) {
-            // the first pixel with L > 0 among q-nc, q-1, q, q+1, q+nc (ascending index) must be p
-            const int wr = qr + 3, wc = qc + 3;
+          bool ok = p >= 0 && r >= 0 && r < nr && c >= 0 && c < nc;
+          const int wr = qr + 3, wc = qc + 3;
+          if (ok) {  // owner: the first principal pixel among q-nc, q-1, q, q+1, q+nc must be s
             int orr = 9, occ = 9;
-            if (W[wr + 1][wc] > 0) orr = 1, occ = 0;
-            if (W[wr][wc + 1] > 0) orr = 0, occ = 1;
-            if (W[wr][wc] > 0) orr = 0, occ = 0;
-            if (W[wr][wc - 1] > 0) orr = 0, occ = -1;
-            if (W[wr - 1][wc] > 0) orr = -1, occ = 0;
-            if (qr + orr == 0 && qc + occ == 0) q = r * nc + c;
+            if (pres(wr + 1, wc)) orr = 1, occ = 0;
+            if (pres(wr, wc + 1)) orr = 0, occ = 1;
+            if (pres(wr, wc)) orr = 0, occ = 0;
+            if (pres(wr, wc - 1)) orr = 0, occ = -1;
+            if (pres(wr - 1, wc)) orr = -1, occ = 0;
+            ok = (qr + orr == 0 && qc + occ == 0);
           }
+          if (ok) {  // presence screen over the 3x3 box
+#pragma unroll
+            for (int a = -1; a <= 1; ++a)
+#pragma unroll
+              for (int b = -1; b <= 1; ++b) {
+                const int rr = r + a, cc = c + b;
+                if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) {
+                  if (!P.erosion_border) ok = false;
+                  continue;
+                }
+                const int ur = wr + a, uc = wc + b;
+                if (!(pres(ur, uc) | pres(ur - 1, uc) | pres(ur + 1, uc) | pres(ur, uc - 1) | pres(ur, uc + 1)))
+                  ok = false;
+              }
+          }
+          cand[j] = ok;
+          any |= ok;
+        }
+        uint64_t WL[7];  // byte (dc + 3) of WL[dr + 3]: level of pixel (r0 + dr, c0 + dc), 0 outside the image
+#pragma unroll
+        for (int dr = 0; dr < 7; ++dr) WL[dr] = 0ull;
+        if (any) {
+#pragma unroll
+          for (int dr = -3; dr <= 3; ++dr)
+#pragma unroll
+            for (int dc = -3; dc <= 3; ++dc) {
+              const int rr = r0 + dr, cc = c0 + dc;
+              const int rc = min(max(rr, 0), nr - 1), ccl = min(max(cc, 0), nc - 1);
+              const uint64_t v = (rr == rc && cc == ccl) ? (uint64_t)S.L8[rc * nc + ccl] : 0ull;
+              WL[dr + 3] |= v << (8 * (dc + 3));
+            }
+        }
+        auto W = [&](int wr, int wc) -> int { return (int)((WL[wr] >> (8 * wc)) & 0xFFull); };
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          const int qr = (j == 1) ? -1 : (j == 2) ? 1 : 0, qc = (j == 3) ? -1 : (j == 4) ? 1 : 0;
+          const int r = r0 + qr, c = c0 + qc;
+          const int q = cand[j] ? r * nc + c : -1;
           int e = 0;
           if (q >= 0) {
             e = 1 << 20;
@@ -1894,7 +1992,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
                   continue;
                 }
                 const int wr = qr + a + 3, wc = qc + b + 3;
-                const int t = max(max(W[wr][wc], W[wr - 1][wc]), max(max(W[wr + 1][wc], W[wr][wc - 1]), W[wr][wc + 1]));
+                const int t = max(max(W(wr, wc), W(wr - 1, wc)), max(max(W(wr + 1, wc), W(wr, wc - 1)), W(wr, wc + 1)));
                 e = min(e, t);
               }
             if (e >= (1 << 20)) e = 0;
@@ -1957,6 +2055,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
       const uint32_t p = S.plist[i];
       S.x[p] = 0.0;
       S.L8[p] = 0;
+      bm[p >> 5] = 0u;  // every bit of the word belongs to this ion
     }
     slot_sync();
   }
@@ -1969,7 +2068,11 @@ __global__ void list_all_kernel(uint32_t* list, uint32_t* count, const int64_t* 
   if (i == 0) *count = (uint32_t)n;
 }
 
-static constexpr int DENSE_SLOTS = 256;
+#ifndef SMG_DENSE_SLOTS
+#define SMG_DENSE_SLOTS 256
+#endif
+static constexpr int DENSE_SLOTS = SMG_DENSE_SLOTS;  // dense-path workgroups (one scratch slot each)
+static constexpr size_t DENSE_BM_LDS_MAX = 152 * 1024;  // dense kernel: LDS presence bitmap up to this size
 // workspace: header (pass counters at word 0.., per-XCD range counters at word 64..), two ion lists,
 // the ion descriptors, dense scratch slots
 static constexpr size_t WS_HEADER = 2048;
@@ -2076,8 +2179,15 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
     SMG_LAUNCH_CHECK();
   }
   const int nslots = (int)(n_ions < DENSE_SLOTS ? n_ions : DENSE_SLOTS);
-  hipLaunchKernelGGL(ion_dense_kernel<FMT>, dim3((unsigned)nslots), dim3(DBLOCK), 0, st, hits, lo, hi, ion_off,
-                     theor, n_ions, P, list_b, hdr + 2, hdr + 3, slots, slot_bytes, oc, osp, osc, omsm, oflags);
+  // the principal presence bitmap lives in the LDS when it fits (images up to ~1.2M pixels)
+  const size_t bm_bytes = ((size_t)P.npx + 31) / 32 * 4;
+  const int bm_in_lds = bm_bytes <= DENSE_BM_LDS_MAX ? 1 : 0;
+  if (bm_in_lds)
+    SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ion_dense_kernel<FMT>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)bm_bytes));
+  hipLaunchKernelGGL(ion_dense_kernel<FMT>, dim3((unsigned)nslots), dim3(DBLOCK), bm_in_lds ? bm_bytes : 0, st, hits,
+                     lo, hi, ion_off, theor, n_ions, P, list_b, hdr + 2, hdr + 3, slots, slot_bytes, oc, osp, osc,
+                     omsm, oflags, bm_in_lds);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }
