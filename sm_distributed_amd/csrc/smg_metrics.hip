@@ -1656,13 +1656,20 @@ __device__ int scatter_window(const Hits<FMT>& hits, int64_t a, int64_t b, doubl
   return n;
 }
 
+// word w of the presence bitmap: the LDS copy, or the slot's global copy, whose bits are set by atomics in L2
+// (read past L1)
+__device__ __forceinline__ uint32_t bm_word(const uint32_t* bm, int w, bool in_lds) {
+  return in_lds ? bm[w] : ld_agent(&bm[w]);
+}
+
 // A tail window joined against the principal image x (presence bitmap bm) without materialising it: a point
 // without the duplicate-candidate flag is alone on its pixel, so it adds (y, y^2, x*y, y[x>0]) to acc directly
 // (x loaded only when the pixel is in the principal image).  Flagged points are summed per pixel into y and
 // listed as with scatter_window; the caller adds their pixels.  Returns the number of listed pixels.
 template <int FMT>
 __device__ int tail_window(const Hits<FMT>& hits, int64_t a, int64_t b, const double* x, const uint32_t* bm,
-                           double* y, uint32_t* mark, uint32_t gen, uint32_t* list, int* cnt, double (&acc)[4]) {
+                           bool bm_lds, double* y, uint32_t* mark, uint32_t gen, uint32_t* list, int* cnt,
+                           double (&acc)[4]) {
   using H = Hits<FMT>;
   if (threadIdx.x == 0) *cnt = 0;
   __syncthreads();
@@ -1678,7 +1685,7 @@ __device__ int tail_window(const Hits<FMT>& hits, int64_t a, int64_t b, const do
         atomicAdd(&y[p], v);
         own = atomicExch(&mark[p], gen) != gen;
       } else {
-        const double xv = ((bm[p >> 5] >> (p & 31)) & 1u) ? ld_agent(&x[p]) : 0.0;
+        const double xv = ((bm_word(bm, p >> 5, bm_lds) >> (p & 31)) & 1u) ? ld_agent(&x[p]) : 0.0;
         acc[0] += v;
         acc[1] += v * v;
         acc[2] += xv * v;
@@ -1867,12 +1874,13 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
         ny = scatter_window<FMT>(hits, lo[w0 + k], hi[w0 + k], S.y, S.mark, ++gen, S.ylist, &sh_ctr[2]);
         clip_image(S.y, S.ylist, ny, S.vals, P.q, sh_hist, sh_sel);
       } else {
-        ny = tail_window<FMT>(hits, lo[w0 + k], hi[w0 + k], S.x, bm, S.y, S.mark, ++gen, S.ylist, &sh_ctr[2], a2);
+        ny = tail_window<FMT>(hits, lo[w0 + k], hi[w0 + k], S.x, bm, bm_in_lds != 0, S.y, S.mark, ++gen, S.ylist,
+                                &sh_ctr[2], a2);
       }
       for (int i = tid; i < ny; i += DBLOCK) {
         const uint32_t p = S.ylist[i];
         const double y = ld_agent(&S.y[p]);
-        const double x = ((bm[p >> 5] >> (p & 31)) & 1u) ? ld_agent(&S.x[p]) : 0.0;
+        const double x = ((bm_word(bm, p >> 5, bm_in_lds != 0) >> (p & 31)) & 1u) ? ld_agent(&S.x[p]) : 0.0;
         a2[0] += y;
         a2[1] += y * y;
         a2[2] += x * y;
@@ -1918,7 +1926,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
             const int rr = r0 + dr, cc = c0 + dc;
             if (p >= 0 && rr >= 0 && rr < nr && cc >= 0 && cc < nc) {
               const int qq = rr * nc + cc;
-              row |= ((bm[qq >> 5] >> (qq & 31)) & 1u) << (dc + 3);
+              row |= ((bm_word(bm, qq >> 5, bm_in_lds != 0) >> (qq & 31)) & 1u) << (dc + 3);
             }
           }
           B[dr + 3] = row;

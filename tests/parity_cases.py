@@ -130,6 +130,13 @@ def make_case(name: str):
         ds = syn.make_dataset_np(520, 520, 3, seed=63, ions=ions, plant_fraction=1.0, plant_seed=64,
                                  blob_sigma=(3.0, 8.0))
         return ds, ions, 50.0, {}
+    if name == "xl_image":     # 1.32M pixels: the dense path's presence bitmap no longer fits the LDS (global)
+        full = syn.make_ion_table(2, seed=121, decoy_seed=122)
+        tgt = np.nonzero(np.isin(full.adducts, list(full.target_adducts)))[0][:3]
+        ions = subset_ions(full, np.concatenate([tgt, [0]]))
+        ds = syn.make_dataset_np(1200, 1100, 1, seed=123, ions=ions, plant_fraction=1.0, plant_seed=124,
+                                 blob_sigma=(4.0, 9.0))
+        return ds, ions, 50.0, {}
     if name == "large_blobs":  # > 2^18 pixels with big blobs: two-level main / big-ion passes, chaos with many
         full = syn.make_ion_table(4, seed=111, decoy_seed=112)  # candidates, olist from the set (nnz > OL_MAX)
         tgt = np.nonzero(np.isin(full.adducts, list(full.target_adducts)))[0][:8]
@@ -163,7 +170,7 @@ def make_case(name: str):
 
 
 CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels", "nlevels1", "big_window", "huge_window",
-         "large_image", "large_blobs", "boundary", "long_tail", "dups_heavy", "kmix", "clip99", "clip_q50_conn8"]
+         "large_image", "xl_image", "large_blobs", "boundary", "long_tail", "dups_heavy", "kmix", "clip99", "clip_q50_conn8"]
 
 
 def oracle_run(ds, ions, ppm, nlevels=30, connectivity=4, erosion_border=0, q=99.0, do_preprocessing=False):
