@@ -231,29 +231,40 @@ struct VVAdd {
   __host__ __device__ VV operator()(const VV& x, const VV& y) const { return VV{x.a + y.a, x.b + y.b}; }
 };
 
+// Each wave takes BS_PER_WAVE consecutive 64-point blocks and has all their loads in flight at once.
+constexpr int BS_PER_WAVE = 8;
+
 template <int FMT>
 __global__ void __launch_bounds__(256) block_sums64_kernel(const void* __restrict__ hits,
                                                            const double* __restrict__ hit_vals, int64_t n,
                                                            VV* __restrict__ out) {
-  const int64_t blk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t blk0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * BS_PER_WAVE;
   const int lane = threadIdx.x & 63;
   const int64_t nblk = (n + 63) >> 6;
-  if (blk >= nblk) return;  // whole waves exit together
-  const int64_t i = blk * 64 + lane;
-  double v = 0.0;
-  bool dup = false;
-  if (i < n) {
-    if constexpr (FMT == SMG_HITS_PACKED_F32) {
-      const uint64_t h = reinterpret_cast<const uint64_t*>(hits)[i];
-      v = (double)__uint_as_float((uint32_t)(h >> 32));
-      dup = ((uint32_t)h >> 31) != 0u;
-    } else {
-      v = hit_vals[i];
-      dup = (reinterpret_cast<const uint32_t*>(hits)[i] >> 31) != 0u;
+  if (blk0 >= nblk) return;  // whole waves exit together
+  double v[BS_PER_WAVE];
+  bool dup[BS_PER_WAVE];
+#pragma unroll
+  for (int j = 0; j < BS_PER_WAVE; ++j) {
+    const int64_t i = (blk0 + j) * 64 + lane;
+    v[j] = 0.0;
+    dup[j] = false;
+    if (i < n) {
+      if constexpr (FMT == SMG_HITS_PACKED_F32) {
+        const uint64_t h = reinterpret_cast<const uint64_t*>(hits)[i];
+        v[j] = (double)__uint_as_float((uint32_t)(h >> 32));
+        dup[j] = ((uint32_t)h >> 31) != 0u;
+      } else {
+        v[j] = hit_vals[i];
+        dup[j] = (reinterpret_cast<const uint32_t*>(hits)[i] >> 31) != 0u;
+      }
     }
   }
-  const double a = wave_sum_dpp(v), b = wave_sum_dpp(dup ? 0.0 : v * v);
-  if (lane == 0) out[blk] = VV{a, b};
+#pragma unroll
+  for (int j = 0; j < BS_PER_WAVE; ++j) {
+    const double a = wave_sum_dpp(v[j]), b = wave_sum_dpp(dup[j] ? 0.0 : v[j] * v[j]);
+    if (lane == 0 && blk0 + j < nblk) out[blk0 + j] = VV{a, b};
+  }
 }
 
 }  // namespace smg
@@ -428,7 +439,8 @@ int smg_hit_prefix_sums(int32_t hit_format, const void* hits, const double* hit_
   VV* bs = reinterpret_cast<VV*>(reinterpret_cast<unsigned char*>(workspace) + 256);
   unsigned char* tmp = reinterpret_cast<unsigned char*>(bs) + ((size_t)nblk * sizeof(VV) + 255) / 256 * 256;
   size_t tb = need - (size_t)(tmp - reinterpret_cast<unsigned char*>(workspace));
-  const int64_t grid = (nblk * 64 + 255) / 256;
+  const int64_t nwaves = (nblk + BS_PER_WAVE - 1) / BS_PER_WAVE;
+  const int64_t grid = (nwaves * 64 + 255) / 256;
   if (hit_format == SMG_HITS_PACKED_F32)
     hipLaunchKernelGGL(block_sums64_kernel<SMG_HITS_PACKED_F32>, dim3((unsigned)grid), dim3(256), 0, st, hits,
                        hit_vals, n_points, bs);
