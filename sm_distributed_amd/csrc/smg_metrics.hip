@@ -443,6 +443,26 @@ template <int FMT>
 __device__ __forceinline__ double2 cum_at(const Hits<FMT>& hits, const double2* __restrict__ cum64, int64_t i) {
   double2 c = cum64[i >> 6];
   const int64_t a = i & ~(int64_t)63;
+  if constexpr (FMT == SMG_HITS_PACKED_F32) {  // 16-byte loads: two hits per load (a is even)
+    const ulonglong2* h2 = reinterpret_cast<const ulonglong2*>(hits.h + a);
+    const int m = (int)(i - a);
+#pragma unroll 8
+    for (int q = 0; q < (m >> 1); ++q) {
+      const ulonglong2 hh = h2[q];
+      const double v0 = Hits<FMT>::val(hh.x), v1 = Hits<FMT>::val(hh.y);
+      c.x += v0;
+      if (!Hits<FMT>::dup(hh.x)) c.y += v0 * v0;
+      c.x += v1;
+      if (!Hits<FMT>::dup(hh.y)) c.y += v1 * v1;
+    }
+    if (m & 1) {  // never reads past hit i - 1
+      const uint64_t h = hits.h[i - 1];
+      const double v = Hits<FMT>::val(h);
+      c.x += v;
+      if (!Hits<FMT>::dup(h)) c.y += v * v;
+    }
+    return c;
+  }
 #pragma unroll 4
   for (int64_t j = a; j < i; ++j) {
     const auto h = hits.load(j);
