@@ -169,14 +169,21 @@ struct Hits<SMG_HITS_SPLIT_F64> {
 };
 
 // level index L = #{i : linspace(0,1,n)[i] < v/vmax}  (measure_of_chaos: bw = im_clean > level)
+// The levels are nondecreasing in i, so L is the lower bound of norm among them (binary search).
 __device__ __forceinline__ int level_of(double v, double vmax, const Params& P) {
   const double norm = v / vmax;
-  int L = 0;
-  for (int i = 0; i < P.nlevels; ++i) {
-    const double lev = (P.nlevels > 1 && i == P.nlevels - 1) ? 1.0 : (double)i * P.step;
-    L += (lev < norm) ? 1 : 0;
+  int lo = 0, len = P.nlevels;
+  while (len > 0) {
+    const int half = len >> 1, mid = lo + half;
+    const double lev = (P.nlevels > 1 && mid == P.nlevels - 1) ? 1.0 : (double)mid * P.step;
+    if (lev < norm) {
+      lo = mid + 1;
+      len -= half + 1;
+    } else {
+      len = half;
+    }
   }
-  return L;
+  return lo;
 }
 
 __device__ __forceinline__ double clean(double v) {  // ImgMeasures._replace_nan
@@ -1544,7 +1551,7 @@ struct DenseSlot {
 
 static inline size_t dense_slot_bytes(int npx) {
   return al16((size_t)npx * 8) * 2 + al16((size_t)npx * 8) + al16((size_t)npx * 4) * 3 + al16((size_t)npx) * 2 +
-         al16(((size_t)npx + 31) / 32 * 4) + 256;
+         al16(((size_t)npx + 31) / 32 * 4 + 4) + 256;
 }
 
 __device__ __forceinline__ DenseSlot dense_slot(unsigned char* base, int npx) {
@@ -1640,35 +1647,76 @@ __device__ __forceinline__ int wave_append(bool pred, int* cnt) {
   return pred ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
 }
 
+// Presence bitmap of the principal image: in the LDS (ds ops; LDS = true) or, for images too large for it, in
+// the slot's global memory, whose bits are set by atomics in L2 and read past L1.
+template <bool LDS>
+struct PresenceBits {
+  uint32_t* w;
+  __device__ __forceinline__ uint32_t word(int i) const {
+    if constexpr (LDS) return w[i];
+    else return ld_agent(&w[i]);
+  }
+  __device__ __forceinline__ bool test(uint32_t p) const { return (word((int)(p >> 5)) >> (p & 31)) & 1u; }
+  __device__ __forceinline__ void set(uint32_t p) const { atomicOr(&w[p >> 5], 1u << (p & 31)); }
+  __device__ __forceinline__ void clear_word_of(uint32_t p) const { w[p >> 5] = 0u; }
+  // bits of columns c0-3 .. c0+3 of row r (bit j = column c0-3+j; 0 outside the image); one extra zero word
+  // follows the bitmap
+  __device__ __forceinline__ uint32_t row7(int r, int c0, int nr, int nc) const {
+    if (r < 0 || r >= nr) return 0u;
+    const int lc = c0 - 3;
+    const int64_t g = (int64_t)r * nc + lc;
+    uint32_t v;
+    if (g >= 0) {
+      const int wi = (int)(g >> 5);
+      v = __builtin_amdgcn_alignbit(word(wi + 1), word(wi), (uint32_t)(g & 31));
+    } else {
+      v = word(0) << (uint32_t)(-g);
+    }
+    uint32_t cm = 0x7Fu;
+    if (lc < 0) cm &= 0x7Fu << (uint32_t)(-lc);
+    if (c0 + 3 >= nc) cm &= 0x7Fu >> (uint32_t)(c0 + 3 - (nc - 1));
+    return v & cm;
+  }
+};
+
+constexpr int DU = 4;  // dense kernel: points per thread with loads in flight together
+
 // The window's image into img (zero outside its listed pixels).  A point without the duplicate-candidate flag is
 // alone on its pixel in the window: it stores its value and lists the pixel.  Flagged points add atomically and
-// the first lane to tag the pixel with `gen` lists it.  Returns the number of listed pixels (ends with slot_sync:
-// the image is complete in L2 for ld_agent readers).
-template <int FMT>
+// the first lane to tag the pixel with `gen` lists it; listed pixels go into the presence bitmap when one is given.
+// Returns the number of listed pixels (ends with slot_sync: the image is complete in L2 for ld_agent readers).
+template <int FMT, bool SET, bool LDS>
 __device__ int scatter_window(const Hits<FMT>& hits, int64_t a, int64_t b, double* img, uint32_t* mark,
-                              uint32_t gen, uint32_t* list, int* cnt, uint32_t* bm = nullptr) {
+                              uint32_t gen, uint32_t* list, int* cnt, PresenceBits<LDS> bm) {
   using H = Hits<FMT>;
   if (threadIdx.x == 0) *cnt = 0;
   __syncthreads();
-  for (int64_t i0 = a; i0 < b; i0 += DBLOCK) {
-    const int64_t i = i0 + threadIdx.x;
-    bool own = false;
-    uint32_t p = 0;
-    if (i < b) {
-      const typename H::Reg r = hits.load(i);
-      p = H::pix(r);
-      const double v = H::val(r);
-      if (H::dup(r)) {
-        atomicAdd(&img[p], v);
-        own = atomicExch(&mark[p], gen) != gen;
-      } else {
-        img[p] = v;
-        own = true;
-      }
-      if (bm && own) atomicOr(&bm[p >> 5], 1u << (p & 31));
+  for (int64_t i0 = a; i0 < b; i0 += (int64_t)DBLOCK * DU) {
+    typename H::Reg r[DU];
+#pragma unroll
+    for (int u = 0; u < DU; ++u) {
+      const int64_t i = i0 + (int64_t)u * DBLOCK + threadIdx.x;
+      r[u] = i < b ? hits.load(i) : H::zero();
     }
-    const int idx = wave_append(own, cnt);
-    if (own) list[idx] = p;
+#pragma unroll
+    for (int u = 0; u < DU; ++u) {
+      const int64_t i = i0 + (int64_t)u * DBLOCK + threadIdx.x;
+      bool own = false;
+      const uint32_t p = H::pix(r[u]);
+      if (i < b) {
+        const double v = H::val(r[u]);
+        if (H::dup(r[u])) {
+          atomicAdd(&img[p], v);
+          own = atomicExch(&mark[p], gen) != gen;
+        } else {
+          img[p] = v;
+          own = true;
+        }
+        if (SET && own) bm.set(p);
+      }
+      const int idx = wave_append(own, cnt);
+      if (own) list[idx] = p;
+    }
   }
   slot_sync();
   const int n = *cnt;
@@ -1676,44 +1724,44 @@ __device__ int scatter_window(const Hits<FMT>& hits, int64_t a, int64_t b, doubl
   return n;
 }
 
-// word w of the presence bitmap: the LDS copy, or the slot's global copy, whose bits are set by atomics in L2
-// (read past L1)
-__device__ __forceinline__ uint32_t bm_word(const uint32_t* bm, int w, bool in_lds) {
-  return in_lds ? bm[w] : ld_agent(&bm[w]);
-}
-
 // A tail window joined against the principal image x (presence bitmap bm) without materialising it: a point
 // without the duplicate-candidate flag is alone on its pixel, so it adds (y, y^2, x*y, y[x>0]) to acc directly
 // (x loaded only when the pixel is in the principal image).  Flagged points are summed per pixel into y and
 // listed as with scatter_window; the caller adds their pixels.  Returns the number of listed pixels.
-template <int FMT>
-__device__ int tail_window(const Hits<FMT>& hits, int64_t a, int64_t b, const double* x, const uint32_t* bm,
-                           bool bm_lds, double* y, uint32_t* mark, uint32_t gen, uint32_t* list, int* cnt,
-                           double (&acc)[4]) {
+template <int FMT, bool LDS>
+__device__ int tail_window(const Hits<FMT>& hits, int64_t a, int64_t b, const double* x, PresenceBits<LDS> bm,
+                           double* y, uint32_t* mark, uint32_t gen, uint32_t* list, int* cnt, double (&acc)[4]) {
   using H = Hits<FMT>;
   if (threadIdx.x == 0) *cnt = 0;
   __syncthreads();
-  for (int64_t i0 = a; i0 < b; i0 += DBLOCK) {
-    const int64_t i = i0 + threadIdx.x;
-    bool own = false;
-    uint32_t p = 0;
-    if (i < b) {
-      const typename H::Reg r = hits.load(i);
-      p = H::pix(r);
-      const double v = H::val(r);
-      if (H::dup(r)) {
-        atomicAdd(&y[p], v);
-        own = atomicExch(&mark[p], gen) != gen;
-      } else {
-        const double xv = ((bm_word(bm, p >> 5, bm_lds) >> (p & 31)) & 1u) ? ld_agent(&x[p]) : 0.0;
-        acc[0] += v;
-        acc[1] += v * v;
-        acc[2] += xv * v;
-        if (xv > 0.0) acc[3] += v;
-      }
+  for (int64_t i0 = a; i0 < b; i0 += (int64_t)DBLOCK * DU) {
+    typename H::Reg r[DU];
+#pragma unroll
+    for (int u = 0; u < DU; ++u) {
+      const int64_t i = i0 + (int64_t)u * DBLOCK + threadIdx.x;
+      r[u] = i < b ? hits.load(i) : H::zero();
     }
-    const int idx = wave_append(own, cnt);
-    if (own) list[idx] = p;
+#pragma unroll
+    for (int u = 0; u < DU; ++u) {
+      const int64_t i = i0 + (int64_t)u * DBLOCK + threadIdx.x;
+      bool own = false;
+      const uint32_t p = H::pix(r[u]);
+      if (i < b) {
+        const double v = H::val(r[u]);
+        if (H::dup(r[u])) {
+          atomicAdd(&y[p], v);
+          own = atomicExch(&mark[p], gen) != gen;
+        } else {
+          const double xv = bm.test(p) ? ld_agent(&x[p]) : 0.0;
+          acc[0] += v;
+          acc[1] += v * v;
+          acc[2] += xv * v;
+          if (xv > 0.0) acc[3] += v;
+        }
+      }
+      const int idx = wave_append(own, cnt);
+      if (own) list[idx] = p;
+    }
   }
   slot_sync();
   const int n = *cnt;
@@ -1799,13 +1847,13 @@ __device__ void clip_image(double* img, const uint32_t* list, int n_list, double
   slot_sync();
 }
 
-template <int FMT>
+template <int FMT, bool BML>
 __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
     Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
     const int64_t* __restrict__ ion_off, const double* __restrict__ theor, int64_t n_ions, Params P,
     const uint32_t* __restrict__ dense_list, const uint32_t* __restrict__ dense_count, uint32_t* next,
     unsigned char* scratch, size_t slot_bytes, double* __restrict__ oc, double* __restrict__ osp,
-    double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags, int bm_in_lds) {
+    double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags) {
   extern __shared__ uint32_t dyn_bm[];  // presence bitmap of the principal image (when it fits)
   __shared__ double red[8 * DNW];
   __shared__ double kst[4 * MAXK_DENSE];
@@ -1819,9 +1867,9 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
   const uint32_t total = *dense_count;
   bool fresh = true;
   uint32_t gen = 0;
-  uint32_t* bm = bm_in_lds ? dyn_bm : S.gbm;
-  const int nbw = (npx + 31) / 32;
-  if (bm_in_lds)
+  const PresenceBits<BML> bm{BML ? dyn_bm : S.gbm};
+  const int nbw = (npx + 31) / 32 + 1;  // + one zero word for row7
+  if (BML)
     for (int w = tid; w < nbw; w += DBLOCK) dyn_bm[w] = 0u;
   STAMP_DECL();
 
@@ -1857,7 +1905,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
         S.L8[p] = 0;
         S.E8[p] = 0;
       }
-      if (!bm_in_lds)
+      if (!BML)
         for (int w = tid; w < nbw; w += DBLOCK) S.gbm[w] = 0u;
       slot_sync();
       fresh = false;
@@ -1865,7 +1913,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
 
     STAMP(10);
     // principal image
-    const int np = scatter_window<FMT>(hits, lo[w0], hi[w0], S.x, S.mark, ++gen, S.plist, &sh_ctr[2], bm);
+    const int np = scatter_window<FMT, true>(hits, lo[w0], hi[w0], S.x, S.mark, ++gen, S.plist, &sh_ctr[2], bm);
     if (P.clip) clip_image(S.x, S.plist, np, S.vals, P.q, sh_hist, sh_sel);
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     double mx = -INFINITY;
@@ -1891,16 +1939,15 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
       double a2[4] = {0.0, 0.0, 0.0, 0.0};  // sy, syy, sxy, s (y[x > 0])
       int ny;
       if (P.clip) {  // the clip needs the whole tail image first
-        ny = scatter_window<FMT>(hits, lo[w0 + k], hi[w0 + k], S.y, S.mark, ++gen, S.ylist, &sh_ctr[2]);
+        ny = scatter_window<FMT, false>(hits, lo[w0 + k], hi[w0 + k], S.y, S.mark, ++gen, S.ylist, &sh_ctr[2], bm);
         clip_image(S.y, S.ylist, ny, S.vals, P.q, sh_hist, sh_sel);
       } else {
-        ny = tail_window<FMT>(hits, lo[w0 + k], hi[w0 + k], S.x, bm, bm_in_lds != 0, S.y, S.mark, ++gen, S.ylist,
-                                &sh_ctr[2], a2);
+        ny = tail_window<FMT>(hits, lo[w0 + k], hi[w0 + k], S.x, bm, S.y, S.mark, ++gen, S.ylist, &sh_ctr[2], a2);
       }
       for (int i = tid; i < ny; i += DBLOCK) {
         const uint32_t p = S.ylist[i];
         const double y = ld_agent(&S.y[p]);
-        const double x = ((bm_word(bm, p >> 5, bm_in_lds != 0) >> (p & 31)) & 1u) ? ld_agent(&S.x[p]) : 0.0;
+        const double x = bm.test(p) ? ld_agent(&S.x[p]) : 0.0;
         a2[0] += y;
         a2[1] += y * y;
         a2[2] += x * y;
@@ -1939,18 +1986,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
         const int r0 = p >= 0 ? p / nc : 0, c0 = p >= 0 ? p - r0 * nc : 0;
         uint32_t B[7];  // bit (dc + 3) of B[dr + 3]: pixel (r0 + dr, c0 + dc) is in the image and principal
 #pragma unroll
-        for (int dr = -3; dr <= 3; ++dr) {
-          uint32_t row = 0u;
-#pragma unroll
-          for (int dc = -3; dc <= 3; ++dc) {
-            const int rr = r0 + dr, cc = c0 + dc;
-            if (p >= 0 && rr >= 0 && rr < nr && cc >= 0 && cc < nc) {
-              const int qq = rr * nc + cc;
-              row |= ((bm_word(bm, qq >> 5, bm_in_lds != 0) >> (qq & 31)) & 1u) << (dc + 3);
-            }
-          }
-          B[dr + 3] = row;
-        }
+        for (int dr = -3; dr <= 3; ++dr) B[dr + 3] = p >= 0 ? bm.row7(r0 + dr, c0, nr, nc) : 0u;
         auto pres = [&](int wr, int wc) -> uint32_t { return (B[wr] >> wc) & 1u; };
         bool cand[5];
         bool any = false;
@@ -2083,7 +2119,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
       const uint32_t p = S.plist[i];
       S.x[p] = 0.0;
       S.L8[p] = 0;
-      bm[p >> 5] = 0u;  // every bit of the word belongs to this ion
+      bm.clear_word_of(p);  // every bit of the word belongs to this ion
     }
     slot_sync();
   }
@@ -2208,14 +2244,18 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   }
   const int nslots = (int)(n_ions < DENSE_SLOTS ? n_ions : DENSE_SLOTS);
   // the principal presence bitmap lives in the LDS when it fits (images up to ~1.2M pixels)
-  const size_t bm_bytes = ((size_t)P.npx + 31) / 32 * 4;
-  const int bm_in_lds = bm_bytes <= DENSE_BM_LDS_MAX ? 1 : 0;
-  if (bm_in_lds)
-    SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ion_dense_kernel<FMT>),
+  const size_t bm_bytes = (((size_t)P.npx + 31) / 32 + 1) * 4;
+  if (bm_bytes <= DENSE_BM_LDS_MAX) {
+    SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ion_dense_kernel<FMT, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)bm_bytes));
-  hipLaunchKernelGGL(ion_dense_kernel<FMT>, dim3((unsigned)nslots), dim3(DBLOCK), bm_in_lds ? bm_bytes : 0, st, hits,
-                     lo, hi, ion_off, theor, n_ions, P, list_b, hdr + 2, hdr + 3, slots, slot_bytes, oc, osp, osc,
-                     omsm, oflags, bm_in_lds);
+    hipLaunchKernelGGL((ion_dense_kernel<FMT, true>), dim3((unsigned)nslots), dim3(DBLOCK), bm_bytes, st, hits, lo,
+                       hi, ion_off, theor, n_ions, P, list_b, hdr + 2, hdr + 3, slots, slot_bytes, oc, osp, osc, omsm,
+                       oflags);
+  } else {
+    hipLaunchKernelGGL((ion_dense_kernel<FMT, false>), dim3((unsigned)nslots), dim3(DBLOCK), 0, st, hits, lo, hi,
+                       ion_off, theor, n_ions, P, list_b, hdr + 2, hdr + 3, slots, slot_bytes, oc, osp, osc, omsm,
+                       oflags);
+  }
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }
