@@ -28,6 +28,7 @@ def _stream(stream=None):
 def require_gpu():
     if not torch.cuda.is_available():
         raise RuntimeError("sm_distributed_amd device path needs a ROCm GPU (no CPU fallback)")
+    torch.cuda.init()  # the HIP runtime is torch's: initialise it before the library's first call
     lib()  # fail loudly if libsmg.so is missing
 
 
@@ -229,6 +230,10 @@ def ion_metrics_raw(hit_format: int, hits: torch.Tensor, hit_vals, hit_cum, lo, 
         f64 = lambda: torch.empty(n_ions, dtype=torch.float64, device=device)
         out = IonMetrics(f64(), f64(), f64(), f64(), torch.empty(n_ions, dtype=torch.int32, device=device))
     if n_ions == 0:
+        return out
+    if hits.numel() == 0:  # no data points: every window is empty, no ion is scored (formula_img_validator.py:115-118)
+        for t in (out.chaos, out.spatial, out.spectral, out.msm, out.flags):
+            t.zero_()
         return out
     sz = ctypes.c_size_t(0)
     check(lib().smg_ion_metrics_workspace_size(n_ions, nrows, ncols, ctypes.byref(sz)),

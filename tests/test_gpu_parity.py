@@ -204,3 +204,51 @@ def test_lds_pipeline_paths_exercised():
     has = (m["flags"] & 1) != 0
     assert (has & (K == 1)).any() and (has & (K > 8)).any()
     assert ((m["flags"][has & (K > 8)] & 2) != 0).all()
+
+
+# ---- edge inputs: empty dataset, empty ion list, a 1x1 image, every point of a window on one pixel ----------
+def _edge_case(name):
+    from sm_distributed_amd import synthetic as syn
+    from tests.parity_cases import subset_ions
+    ions = syn.make_ion_table(6, seed=141, decoy_seed=142)
+    if name == "no_points":
+        ds = syn.make_dataset_np(4, 5, 0.0, seed=143)
+        return ds, ions, 20.0
+    if name == "no_ions":
+        return syn.make_dataset_np(8, 8, 50, seed=144), subset_ions(ions, np.zeros(0, np.int64)), 20.0
+    if name == "one_pixel":
+        return syn.make_dataset_np(1, 1, 4000, seed=145, ions=ions, plant_fraction=1.0, plant_seed=146), ions, 30.0
+    if name == "one_hot_pixel":  # a 6x6 image whose points all sit in spectrum 7 (heavy same-pixel duplicates)
+        ds = syn.make_dataset_np(6, 6, 0.0, seed=147)
+        rng = np.random.default_rng(148)
+        mz = np.sort(np.concatenate([ions.peak_mz * (1 + rng.normal(0, 2e-6, ions.peak_mz.size)) for _ in range(8)])
+                     ).astype(np.float32)
+        off = np.zeros(37, np.int64)
+        off[8:] = mz.size
+        ints = rng.lognormal(6.0, 1.0, mz.size).astype(np.float32)
+        return syn.SpectraSet(sp_off=off, mz=mz, ints=ints, coords=ds.coords), ions, 20.0
+    raise KeyError(name)
+
+
+@pytest.mark.parametrize("name", ["no_points", "no_ions", "one_pixel", "one_hot_pixel"])
+@pytest.mark.parametrize("dense", [False, True])
+def test_edge_inputs_match_oracle(name, dense):
+    from sm_distributed_amd import _lib
+    ds, ions, ppm = _edge_case(name)
+    _, df = oracle_run(ds, ions, ppm)
+    L = _lib.lib()
+    L.smg_debug_force_dense(1 if dense else 0)
+    try:
+        _, m, lo, hi = _device_run(ds, ions, ppm)
+    finally:
+        L.smg_debug_force_dense(0)
+    has = (m["flags"] & 1) != 0 if ions.n_ions else np.zeros(0, bool)
+    assert set(zip(ions.sf_ids[has].tolist(), ions.adducts[has].tolist())) == set(df.index.tolist())
+    if len(df):
+        idx = {k: i for i, k in enumerate(zip(ions.sf_ids.tolist(), ions.adducts.tolist()))}
+        rows = np.array([idx[k] for k in df.index.tolist()], dtype=np.int64)
+        for col in ("chaos", "spatial", "spectral", "msm"):
+            err = np.abs(df[col].to_numpy() - m[col][rows])
+            assert err.max(initial=0.0) <= METRIC_ATOL, (col, float(err.max()))
+    if name == "one_hot_pixel":
+        assert len(df) > 0
