@@ -1724,6 +1724,62 @@ __device__ int scatter_window(const Hits<FMT>& hits, int64_t a, int64_t b, doubl
   return n;
 }
 
+// The principal window without the clip: scatter_window plus the principal statistics.  An unflagged point's
+// value is final (it is alone on its pixel): it goes to pvals[list index] and into acc / mx at once.  Flagged
+// owners are listed by list index in fidx (their sums are complete only after the scatter): the caller reads
+// them back from img.  Returns the number of listed pixels; *fcnt holds the number of flagged owners.
+template <int FMT, bool LDS>
+__device__ int scatter_principal(const Hits<FMT>& hits, int64_t a, int64_t b, double* img, uint32_t* mark,
+                                 uint32_t gen, uint32_t* list, double* pvals, uint32_t* fidx, int* cnt, int* fcnt,
+                                 PresenceBits<LDS> bm, double (&acc)[4], double& mx) {
+  using H = Hits<FMT>;
+  if (threadIdx.x == 0) *cnt = *fcnt = 0;
+  __syncthreads();
+  for (int64_t i0 = a; i0 < b; i0 += (int64_t)DBLOCK * DU) {
+    typename H::Reg r[DU];
+#pragma unroll
+    for (int u = 0; u < DU; ++u) {
+      const int64_t i = i0 + (int64_t)u * DBLOCK + threadIdx.x;
+      r[u] = i < b ? hits.load(i) : H::zero();
+    }
+#pragma unroll
+    for (int u = 0; u < DU; ++u) {
+      const int64_t i = i0 + (int64_t)u * DBLOCK + threadIdx.x;
+      bool own = false, fl = false;
+      const uint32_t p = H::pix(r[u]);
+      const double v = H::val(r[u]);
+      if (i < b) {
+        if (H::dup(r[u])) {
+          atomicAdd(&img[p], v);
+          own = fl = atomicExch(&mark[p], gen) != gen;
+        } else {
+          img[p] = v;
+          own = true;
+          acc[0] += v;
+          acc[1] += v * v;
+          if (v > 0.0) {
+            acc[2] += v;
+            acc[3] += 1.0;
+          }
+          mx = v > mx ? v : mx;
+        }
+        if (own) bm.set(p);
+      }
+      const int idx = wave_append(own, cnt);
+      if (own) {
+        list[idx] = p;
+        if (!fl) pvals[idx] = v;
+      }
+      const int fi = wave_append(fl, fcnt);
+      if (fl) fidx[fi] = (uint32_t)idx;
+    }
+  }
+  slot_sync();
+  const int n = *cnt;
+  __syncthreads();
+  return n;
+}
+
 // A tail window joined against the principal image x (presence bitmap bm) without materialising it: a point
 // without the duplicate-candidate flag is alone on its pixel, so it adds (y, y^2, x*y, y[x>0]) to acc directly
 // (x loaded only when the pixel is in the principal image).  Flagged points are summed per pixel into y and
@@ -1913,19 +1969,39 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
 
     STAMP(10);
     // principal image
-    const int np = scatter_window<FMT, true>(hits, lo[w0], hi[w0], S.x, S.mark, ++gen, S.plist, &sh_ctr[2], bm);
-    if (P.clip) clip_image(S.x, S.plist, np, S.vals, P.q, sh_hist, sh_sel);
+    // pvals (values in list order, for the levels) alias par + elist, which are free until the candidates
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     double mx = -INFINITY;
-    for (int i = tid; i < np; i += DBLOCK) {
-      const double v = ld_agent(&S.x[S.plist[i]]);
-      acc[0] += v;
-      acc[1] += v * v;
-      if (v > 0.0) {
-        acc[2] += v;
-        acc[3] += 1.0;
+    int np;
+    if (P.clip) {  // the clip needs the whole image first; statistics and levels then read x
+      np = scatter_window<FMT, true>(hits, lo[w0], hi[w0], S.x, S.mark, ++gen, S.plist, &sh_ctr[2], bm);
+      clip_image(S.x, S.plist, np, S.vals, P.q, sh_hist, sh_sel);
+      for (int i = tid; i < np; i += DBLOCK) {
+        const double v = ld_agent(&S.x[S.plist[i]]);
+        acc[0] += v;
+        acc[1] += v * v;
+        if (v > 0.0) {
+          acc[2] += v;
+          acc[3] += 1.0;
+        }
+        mx = v > mx ? v : mx;
       }
-      mx = v > mx ? v : mx;
+    } else {
+      np = scatter_principal<FMT>(hits, lo[w0], hi[w0], S.x, S.mark, ++gen, S.plist, S.vals, S.ylist, &sh_ctr[2],
+                                  &sh_ctr[3], bm, acc, mx);
+      const int nfl = sh_ctr[3];
+      for (int j = tid; j < nfl; j += DBLOCK) {  // flagged owners: their per-pixel sums are complete now
+        const uint32_t i = S.ylist[j];
+        const double v = ld_agent(&S.x[S.plist[i]]);
+        S.vals[i] = v;
+        acc[0] += v;
+        acc[1] += v * v;
+        if (v > 0.0) {
+          acc[2] += v;
+          acc[3] += 1.0;
+        }
+        mx = v > mx ? v : mx;
+      }
     }
     if (np < npx) mx = mx > 0.0 ? mx : 0.0;  // unlisted pixels are zero
     dblock_sum<4>(acc, red);
@@ -1970,9 +2046,9 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
     int m = 0;
     if (chaos_ok) {
       const int nr = P.nrows, nc = P.ncols;
-      for (int i = tid; i < np; i += DBLOCK) {
+      for (int i = tid; i < np; i += DBLOCK) {  // with the clip, vals served the tail clips: read x
         const uint32_t p = S.plist[i];
-        S.L8[p] = (uint8_t)level_of(ld_agent(&S.x[p]), vmax, P);
+        S.L8[p] = (uint8_t)level_of(P.clip ? ld_agent(&S.x[p]) : S.vals[i], vmax, P);
       }
       __syncthreads();
       // eL = erode_box(dilate_cross(L)) > 0 only on the 4-cross around a pixel with L > 0, i.e. around a
