@@ -247,6 +247,63 @@ def _plant_np(ions: IonTable, nrows, ncols, fraction, seed, blob_sigma, mz_range
     return np.concatenate(sp_l), np.concatenate(mz_l), np.concatenate(in_l)
 
 
+# At or above this many background points (config 5: 1000x1000 px x Poisson(5000) = 5e9) the dataset is
+# generated block by block of spectra, straight into the resident arrays: the one-shot recipe below needs a
+# global 64-bit key sort whose temporaries alone would exceed HBM.  Smaller datasets (config 3) keep the
+# one-shot recipe and its RNG stream, so their contents do not change.
+CHUNKED_GEN_POINTS = 1 << 31
+CHUNK_POINTS = 1 << 28
+
+
+def _assemble_chunked(g, counts, n_sp, mz_range, extra_pix, extra_mz, extra_int, device):
+    """Spectrum-major (mz f32[N], hits i64[N], sp_off i64[n_sp+1]) built one block of spectra at a time."""
+    import torch
+    if extra_pix:
+        e_pix = torch.cat(extra_pix)
+        e_mz = torch.cat(extra_mz)
+        e_int = torch.cat(extra_int)
+        o = torch.argsort(e_pix, stable=True)
+        e_pix, e_mz, e_int = e_pix[o], e_mz[o], e_int[o]
+        tot = counts + torch.bincount(e_pix, minlength=n_sp)
+    else:
+        e_pix = torch.zeros(0, dtype=torch.int64, device=device)
+        e_mz = torch.zeros(0, dtype=torch.float32, device=device)
+        e_int = torch.zeros(0, dtype=torch.float32, device=device)
+        tot = counts
+    sp_off = torch.zeros(n_sp + 1, dtype=torch.int64, device=device)
+    sp_off[1:] = torch.cumsum(tot, 0)
+    n_all = int(sp_off[-1].item())
+    mz_out = torch.empty(n_all, dtype=torch.float32, device=device)
+    hits_out = torch.empty(n_all, dtype=torch.int64, device=device)
+    off_h = sp_off.cpu().numpy()
+    bg_h = np.concatenate([[0], np.cumsum(counts.cpu().numpy())])
+    s0 = 0
+    while s0 < n_sp:
+        s1 = int(np.searchsorted(off_h, off_h[s0] + CHUNK_POINTS, side="right")) - 1
+        s1 = min(max(s1, s0 + 1), n_sp)
+        nb = int(bg_h[s1] - bg_h[s0])
+        mz = (torch.rand(nb, generator=g, dtype=torch.float64, device=device) * (mz_range[1] - mz_range[0])
+              + mz_range[0]).to(torch.float32)
+        ints = torch.exp(torch.randn(nb, generator=g, dtype=torch.float32, device=device) * 1.5 + 6.0)
+        pix = torch.repeat_interleave(torch.arange(s0, s1, device=device, dtype=torch.int64), counts[s0:s1])
+        if e_pix.numel():
+            a, b = torch.searchsorted(e_pix, torch.tensor([s0, s1], device=device, dtype=torch.int64)).tolist()
+            if b > a:
+                pix = torch.cat([pix, e_pix[a:b]])
+                mz = torch.cat([mz, e_mz[a:b]])
+                ints = torch.cat([ints, e_int[a:b]])
+        key = (pix << 32) | mz.view(torch.int32).to(torch.int64)
+        order = torch.sort(key).indices
+        del key
+        lo, hi = int(off_h[s0]), int(off_h[s1])
+        assert hi - lo == order.numel()
+        mz_out[lo:hi] = mz[order]
+        hits_out[lo:hi] = (pix[order] & 0xFFFFFFFF) | (ints[order].view(torch.int32).to(torch.int64) << 32)
+        del mz, ints, pix, order
+        s0 = s1
+    return mz_out, hits_out, sp_off
+
+
 def make_dataset_torch(nrows: int, ncols: int, peaks_per_spectrum: float, seed: int = 42, device="cuda",
                        mz_range=(100.0, 1000.0), ions: IonTable | None = None, plant_fraction: float = 0.02,
                        plant_seed: int = 45, blob_sigma=(3.0, 12.0)):
@@ -262,10 +319,12 @@ def make_dataset_torch(nrows: int, ncols: int, peaks_per_spectrum: float, seed: 
     counts = torch.poisson(torch.full((n_sp,), float(peaks_per_spectrum), device=device, dtype=torch.float32),
                            generator=g).to(torch.int64)
     n = int(counts.sum().item())
-    mz = (torch.rand(n, generator=g, dtype=torch.float64, device=device) * (mz_range[1] - mz_range[0])
-          + mz_range[0]).to(torch.float32)
-    ints = torch.exp(torch.randn(n, generator=g, dtype=torch.float32, device=device) * 1.5 + 6.0)
-    pix = torch.repeat_interleave(torch.arange(n_sp, device=device, dtype=torch.int64), counts)
+    chunked = n >= CHUNKED_GEN_POINTS
+    if not chunked:
+        mz = (torch.rand(n, generator=g, dtype=torch.float64, device=device) * (mz_range[1] - mz_range[0])
+              + mz_range[0]).to(torch.float32)
+        ints = torch.exp(torch.randn(n, generator=g, dtype=torch.float32, device=device) * 1.5 + 6.0)
+        pix = torch.repeat_interleave(torch.arange(n_sp, device=device, dtype=torch.int64), counts)
     extra_pix, extra_mz, extra_int = [], [], []
     n_planted = 0
     if ions is not None and plant_fraction > 0:
@@ -300,6 +359,11 @@ def make_dataset_torch(nrows: int, ncols: int, peaks_per_spectrum: float, seed: 
                 extra_mz.append(jit.to(torch.float32))
                 extra_int.append((amp * gv * float(ions.peak_int[k]) / 100.0).to(torch.float32))
             n_planted += 1
+    if chunked:
+        mz, hits, sp_off = _assemble_chunked(g, counts, n_sp, mz_range, extra_pix, extra_mz, extra_int, device)
+        info = {"n_points": int(mz.numel()), "n_spectra": n_sp, "n_planted_ions": n_planted,
+                "n_planted_points": int(sum(t.numel() for t in extra_mz)), "sp_off": sp_off}
+        return mz, hits, (nrows, ncols), info
     if extra_pix:
         pix = torch.cat([pix] + extra_pix)
         mz = torch.cat([mz] + extra_mz)
