@@ -244,9 +244,16 @@ def cpu_baseline(args, ions, mz, hits, dims, out):
     pick = np.sort(rng.choice(cand, size=min(args.cpu_ions, len(cand)), replace=False))
     lo_b = min(ions.peak_mz[ions.win_off[i]] for i in pick) * (1 - 2 * args.ppm * 1e-6) - 1e-3
     hi_b = max(ions.peak_mz[ions.win_off[i + 1] - 1] for i in pick) * (1 + 2 * args.ppm * 1e-6) + 1e-3
-    sel = (mz >= lo_b) & (mz <= hi_b)
-    b_mz = mz[sel].cpu().numpy()
-    b_hits = hits[sel].cpu().numpy().view(np.uint64)
+    # masked selection block by block: torch's boolean indexing fails on tensors of >= 2^32 elements (config 5)
+    parts_mz, parts_hits = [], []
+    blk = 1 << 30
+    for a in range(0, mz.numel(), blk):
+        m, h = mz[a:a + blk], hits[a:a + blk]
+        sel = (m >= lo_b) & (m <= hi_b)
+        parts_mz.append(m[sel].cpu().numpy())
+        parts_hits.append(h[sel].cpu().numpy())
+    b_mz = np.concatenate(parts_mz)
+    b_hits = np.concatenate(parts_hits).view(np.uint64)
     b_pix = (b_hits & np.uint64(0x7FFFFFFF)).astype(np.int64)
     b_int = (b_hits >> np.uint64(32)).astype(np.uint32).view(np.float32)
     tasks = [(int(i), ions.peak_mz[ions.win_off[i]:ions.win_off[i + 1]].copy(),
