@@ -1679,7 +1679,10 @@ struct PresenceBits {
   }
 };
 
-constexpr int DU = 4;  // dense kernel: points per thread with loads in flight together
+#ifndef SMG_DU
+#define SMG_DU 4
+#endif
+constexpr int DU = SMG_DU;  // dense kernel: points per thread with loads in flight together
 
 // The window's image into img (zero outside its listed pixels).  A point without the duplicate-candidate flag is
 // alone on its pixel in the window: it stores its value and lists the pixel.  Flagged points add atomically and
