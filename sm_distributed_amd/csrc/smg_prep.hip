@@ -49,36 +49,10 @@ __global__ void __launch_bounds__(256) pack_hits_kernel(const int64_t* __restric
 // (`mz - mz*ppm*1e-6`: ((mz*ppm)*1e-6) then subtract; the library is built with
 // -ffp-contract=off so no FMA changes the rounding), compared in f64 against the f32 keys.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ int64_t lower_bound_f64(const float* __restrict__ a, int64_t n, double x) {
-  int64_t lo = 0, len = n;
-  while (len > 0) {
-    const int64_t half = len >> 1;
-    const int64_t mid = lo + half;
-    if ((double)a[mid] < x) {
-      lo = mid + 1;
-      len -= half + 1;
-    } else {
-      len = half;
-    }
-  }
-  return lo;
-}
-
-__device__ __forceinline__ int64_t upper_bound_f64(const float* __restrict__ a, int64_t n, double x) {
-  int64_t lo = 0, len = n;
-  while (len > 0) {
-    const int64_t half = len >> 1;
-    const int64_t mid = lo + half;
-    if ((double)a[mid] <= x) {
-      lo = mid + 1;
-      len -= half + 1;
-    } else {
-      len = half;
-    }
-  }
-  return lo;
-}
-
+// Both bounds of a window in one branch-free loop: the trip count (ceil(log2 n)) does not depend on the data, so
+// the two searches advance together with their loads in flight side by side (half the dependent-load chain of
+// two binary searches run one after the other).  Invariant: the answer lies in [b, b + len]; at len == 1 it is
+// b + (a[b] < x) (lower) / b + (a[b] <= x) (upper).  Same results as searchsorted 'left' / 'right'.
 __global__ void __launch_bounds__(256) window_bounds_kernel(const double* __restrict__ peak_mz,
                                                             const int64_t* __restrict__ order,
                                                             int64_t n_windows, double ppm,
@@ -92,8 +66,21 @@ __global__ void __launch_bounds__(256) window_bounds_kernel(const double* __rest
   const double d = mz * ppm * 1e-6;
   const double lower = mz - d;
   const double upper = mz + d;
-  lo[w] = lower_bound_f64(mz_sorted, n_points, lower);
-  hi[w] = upper_bound_f64(mz_sorted, n_points, upper);
+  if (n_points <= 0) {
+    lo[w] = hi[w] = 0;
+    return;
+  }
+  int64_t bl = 0, bu = 0, len = n_points;
+  while (len > 1) {
+    const int64_t half = len >> 1;
+    const double vl = (double)mz_sorted[bl + half - 1];
+    const double vu = (double)mz_sorted[bu + half - 1];
+    bl += (vl < lower) ? half : 0;
+    bu += (vu <= upper) ? half : 0;
+    len -= half;
+  }
+  lo[w] = bl + (((double)mz_sorted[bl] < lower) ? 1 : 0);
+  hi[w] = bu + (((double)mz_sorted[bu] <= upper) ? 1 : 0);
 }
 
 // ---------------------------------------------------------------------------------------------
