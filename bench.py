@@ -162,11 +162,13 @@ def main():
             stages[n] += ev[j].elapsed_time(ev[j + 1])
     stages = {n: v / max(len(events), 1) for n, v in stages.items()}
 
+    sort_passes = -(-peaks.key_bits() // 9)  # smg_sort_points: 9-bit onesweep passes
     # algorithmic bytes per launch
     alg = {
         "ion_metrics": 8.0 * sum_hits,                   # one 8-B (pixel, f32) hit read per window point
-        # flags: read m/z + hits; sort: 4 passes of read + write (f32 key, 8-B hit); scan: read hits, write 16 B
-        "flag+sort+scan": (12.0 + 4 * 24.0 + 24.0) * info["n_points"],
+        # flags: read m/z + hits; sort: ceil(key bits / 9) passes of read + write (f32 key, 8-B hit);
+        # scan: read hits, write 16 B per 64 points
+        "flag+sort+scan": (12.0 + sort_passes * 24.0 + 8.25) * info["n_points"],
         "window_search": 24.0 * dions.n_windows,         # peak m/z in, (lo, hi) out
     }
     dominant = max(("flag+sort+scan", "window_search", "ion_metrics"), key=lambda n: stages[n])
