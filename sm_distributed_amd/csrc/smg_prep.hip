@@ -130,67 +130,109 @@ __global__ void __launch_bounds__(256) sample_spectra_kernel(
 // (one byte per point: the flag the hit currently carries), a hit is read and written only when its flag
 // changes, so a repeated pass reads 5 B per point instead of 12; without it every hit is read.
 constexpr int FLAG_TILE = 4096;
-__device__ __forceinline__ void flag_store(uint64_t* __restrict__ hits, uint8_t* __restrict__ state, int64_t i,
-                                           bool f) {
-  if (state) {
-    if (state[i] != (uint8_t)f) {
-      state[i] = (uint8_t)f;
-      const uint64_t h = hits[i];
-      hits[i] = f ? (h | 0x80000000ull) : (h & ~0x80000000ull);
-    }
-  } else {
-    const uint64_t h = hits[i];
-    const uint64_t nh = f ? (h | 0x80000000ull) : (h & ~0x80000000ull);
-    if (nh != h) hits[i] = nh;
+constexpr int FLAG_THREADS = 256;
+constexpr int FLAG_U = FLAG_TILE / FLAG_THREADS;  // points per thread of a tile, loads in flight together
+
+// m/z of spectrum positions [l0, l0 + n) into smz[0, n), n <= FLAG_TILE: all of a thread's loads issued at once
+__device__ __forceinline__ void flag_load_tile(const float* __restrict__ mz, int64_t l0, int n, float* smz) {
+  float r[FLAG_U];
+#pragma unroll
+  for (int u = 0; u < FLAG_U; ++u) {
+    const int i = threadIdx.x + u * FLAG_THREADS;
+    r[u] = i < n ? mz[l0 + i] : 0.0f;
+  }
+#pragma unroll
+  for (int u = 0; u < FLAG_U; ++u) {
+    const int i = threadIdx.x + u * FLAG_THREADS;
+    if (i < n) smz[i] = r[u];
   }
 }
 
-__global__ void __launch_bounds__(256) flag_duplicates_kernel(const int64_t* __restrict__ sp_off, int64_t n_spectra,
-                                                              const float* __restrict__ mz,
-                                                              uint64_t* __restrict__ hits, double ppm,
-                                                              const uint8_t* __restrict__ force,
-                                                              uint8_t* __restrict__ state) {
+__device__ __forceinline__ int flag_tile_unsorted(const float* smz, int n) {
+  int un = 0;
+  for (int i = threadIdx.x + 1; i < n; i += FLAG_THREADS) un |= (smz[i] < smz[i - 1]);
+  return un;
+}
+
+// Flags of tile entries [j0, j1) (spectrum position l0 + j).  The tile holds a point's spectrum neighbours
+// whenever they exist (one halo point each side), so "has a previous / next point" is j > 0 / j + 1 < n.
+// The state bytes are loaded together up front; a hit is read and written only when its flag changes.
+__device__ __forceinline__ void flag_tile_store(const float* smz, int n, int j0, int j1, int64_t l0, bool all,
+                                                double slack, uint64_t* __restrict__ hits,
+                                                uint8_t* __restrict__ state) {
+  uint8_t st[FLAG_U];
+#pragma unroll
+  for (int u = 0; u < FLAG_U; ++u) {
+    const int j = j0 + threadIdx.x + u * FLAG_THREADS;
+    st[u] = (state && j < j1) ? state[l0 + j] : (uint8_t)0;
+  }
+#pragma unroll
+  for (int u = 0; u < FLAG_U; ++u) {
+    const int j = j0 + threadIdx.x + u * FLAG_THREADS;
+    if (j >= j1) continue;
+    bool f = all;
+    if (!f) {
+      const double m = (double)smz[j];
+      if (j > 0) f = f || (m - (double)smz[j - 1] <= slack * m);
+      if (j + 1 < n) {
+        const double m2 = (double)smz[j + 1];
+        f = f || (m2 - m <= slack * m2);
+      }
+    }
+    const int64_t i = l0 + j;
+    if (state) {
+      if (st[u] != (uint8_t)f) {
+        state[i] = (uint8_t)f;
+        const uint64_t h = hits[i];
+        hits[i] = f ? (h | 0x80000000ull) : (h & ~0x80000000ull);
+      }
+    } else {
+      const uint64_t h = hits[i];
+      const uint64_t nh = f ? (h | 0x80000000ull) : (h & ~0x80000000ull);
+      if (nh != h) hits[i] = nh;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(FLAG_THREADS) flag_duplicates_kernel(const int64_t* __restrict__ sp_off,
+                                                                       int64_t n_spectra,
+                                                                       const float* __restrict__ mz,
+                                                                       uint64_t* __restrict__ hits, double ppm,
+                                                                       const uint8_t* __restrict__ force,
+                                                                       uint8_t* __restrict__ state) {
   __shared__ float smz[FLAG_TILE];
   const double slack = 2.0 * ppm * 1e-6 / (1.0 - ppm * 1e-6) * (1.0 + 1e-9);
+  constexpr int CORE = FLAG_TILE - 2;  // points flagged per tile of a long spectrum (plus one halo point a side)
   for (int64_t s = blockIdx.x; s < n_spectra; s += gridDim.x) {
     const int64_t a = sp_off[s], b = sp_off[s + 1];
     if (b - a <= FLAG_TILE) {
       const int n = (int)(b - a);
-      for (int i = threadIdx.x; i < n; i += blockDim.x) smz[i] = mz[a + i];
+      flag_load_tile(mz, a, n, smz);
       __syncthreads();
-      int unsorted = 0;
-      for (int i = threadIdx.x + 1; i < n; i += blockDim.x) unsorted |= (smz[i] < smz[i - 1]);
-      const bool all = __syncthreads_or(unsorted) || (force && force[s]);
-      for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        bool f = all;
-        if (!f) {
-          const double m = (double)smz[i];
-          if (i > 0) f = f || (m - (double)smz[i - 1] <= slack * m);
-          if (i + 1 < n) {
-            const double m2 = (double)smz[i + 1];
-            f = f || (m2 - m <= slack * m2);
-          }
-        }
-        flag_store(hits, state, a + i, f);
-      }
+      const bool all = __syncthreads_or(flag_tile_unsorted(smz, n)) || (force && force[s]);
+      flag_tile_store(smz, n, 0, n, a, all, slack, hits, state);
       __syncthreads();  // smz is reused by the next spectrum
     } else {
-      int unsorted = 0;
-      for (int64_t i = a + 1 + threadIdx.x; i < b; i += blockDim.x) unsorted |= (mz[i] < mz[i - 1]);
-      const bool all = __syncthreads_or(unsorted) || (force && force[s]);
-      for (int64_t i = a + threadIdx.x; i < b; i += blockDim.x) {
-        bool f = all;
-        if (!f) {
-          const double m = (double)mz[i];
-          if (i > a) f = f || (m - (double)mz[i - 1] <= slack * m);
-          if (i + 1 < b) {
-            const double m2 = (double)mz[i + 1];
-            f = f || (m2 - m <= slack * m2);
-          }
-        }
-        flag_store(hits, state, i, f);
+      // longer spectra (config 5: Poisson(5000)): tiles of CORE points with their halo; a sortedness pass over
+      // every tile first (an unsorted spectrum flags all of its points), then the flags tile by tile
+      int un = 0;
+      for (int64_t c0 = a; c0 < b; c0 += CORE) {
+        const int64_t c1 = c0 + CORE < b ? c0 + CORE : b;
+        const int64_t l0 = c0 > a ? c0 - 1 : a, l1 = c1 < b ? c1 + 1 : b;
+        flag_load_tile(mz, l0, (int)(l1 - l0), smz);
+        __syncthreads();
+        un |= flag_tile_unsorted(smz, (int)(l1 - l0));
+        __syncthreads();
       }
-      __syncthreads();
+      const bool all = __syncthreads_or(un) || (force && force[s]);
+      for (int64_t c0 = a; c0 < b; c0 += CORE) {
+        const int64_t c1 = c0 + CORE < b ? c0 + CORE : b;
+        const int64_t l0 = c0 > a ? c0 - 1 : a, l1 = c1 < b ? c1 + 1 : b;
+        flag_load_tile(mz, l0, (int)(l1 - l0), smz);
+        __syncthreads();
+        flag_tile_store(smz, (int)(l1 - l0), (int)(c0 - l0), (int)(c1 - l0), l0, all, slack, hits, state);
+        __syncthreads();
+      }
     }
   }
 }
@@ -282,7 +324,7 @@ int smg_flag_duplicates(const int64_t* sp_off, int64_t n_spectra, const float* m
   if (n_spectra == 0 || n_points == 0) return SMG_OK;
   SMG_CHECK_ARG(sp_off && mz && hits, "null pointer");
   const int64_t grid = n_spectra < (1 << 20) ? n_spectra : (1 << 20);
-  hipLaunchKernelGGL(flag_duplicates_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream), sp_off,
+  hipLaunchKernelGGL(flag_duplicates_kernel, dim3((unsigned)grid), dim3(FLAG_THREADS), 0, as_stream(stream), sp_off,
                      n_spectra, mz, hits, ppm, force, flag_state);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
