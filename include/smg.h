@@ -10,8 +10,10 @@
  *    tensor.data_ptr()), sizes are int64_t, `stream` is a hipStream_t passed as void* (NULL = the
  *    null stream).  Hot entry points never allocate: size the workspace with the matching
  *    *_workspace_size() call first;
- *  - all calls are asynchronous on `stream` and re-entrant (no global mutable state except the
- *    thread-local error string).
+ *  - all calls are asynchronous on `stream` and re-entrant.  The only global mutable state is the
+ *    thread-local error string and the two process-wide TEST switches smg_debug_force_two_level /
+ *    smg_debug_force_dense (off by default; a test that sets one must not run concurrently with other
+ *    callers of smg_ion_metrics in the same process).
  *
  * Each entry point cites the reference interface it replaces (paths under frulo/SM_distributed).
  */
@@ -42,6 +44,7 @@ extern "C" {
 #define SMG_HITS_PACKED_F32 0    /* uint64: low 32 bits pixel index, high 32 bits float32 intensity */
 #define SMG_HITS_SPLIT_F64 1     /* uint32 pixel[] + double intensity[] */
 
+/* "smg <version> (gfx950) git <source revision>[-dirty]": the tree the library was built from */
 const char* smg_version(void);
 const char* smg_last_error(void);
 

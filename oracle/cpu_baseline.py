@@ -52,6 +52,35 @@ def _work(task):
     return rows, time.perf_counter() - t0
 
 
+def available_cpus():
+    """Cores this process may use: the affinity mask, capped by a cgroup-v2 CPU quota when one is set (on a
+    shared GPU box nproc / os.cpu_count() report the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(float(quota) / float(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def default_workers(cap=None):
+    n = available_cpus()
+    return min(n, cap) if cap else n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def run_pool(pix, mz, ints, dims, ppm, nlevels, ions, workers):
     """ions: list of (ion_id, peak_mz, theor).  Returns (rows, wall_seconds, per_worker_seconds)."""
     import multiprocessing as mp

@@ -302,7 +302,10 @@ using namespace smg;
 
 extern "C" {
 
-const char* smg_version(void) { return "smg 0.1.0 (gfx950)"; }
+#ifndef SMG_GIT_REV
+#define SMG_GIT_REV "unknown"
+#endif
+const char* smg_version(void) { return "smg 0.2.0 (gfx950) git " SMG_GIT_REV; }
 
 const char* smg_last_error(void) { return g_last_error.c_str(); }
 

@@ -27,8 +27,6 @@ def ion_costs(win_off, peak_mz, mz_hist=None, mz_edges=None):
     else:
         w = peak_mz
     w = np.where(np.isfinite(w), w, 0.0)
-    c = np.zeros(len(win_off), dtype=np.float64)
-    np.cumsum(w, out=c[1:]) if len(w) == len(win_off) - 1 else None
     cs = np.concatenate([[0.0], np.cumsum(w)])
     return cs[win_off[1:]] - cs[win_off[:-1]] + 1.0  # +1: per-ion fixed cost
 

@@ -65,6 +65,7 @@ class DevicePeaks:
     sort_key_bits: int | None = None
     cum: torch.Tensor | None = None  # 64-point block prefix sums of the sorted hits (smg_hit_prefix_sums)
     cum_valid: bool = False          # cum describes the current hits_sorted
+    version: int = 0                 # bumped by every flag pass / sort: an IonImageSet records the one it used
 
     @property
     def n_points(self) -> int:
@@ -108,6 +109,7 @@ class DevicePeaks:
                                         float(ppm), _p(self.force), _p(self.flag_state), _stream(stream)),
               "smg_flag_duplicates")
         self.flag_ppm = float(ppm)
+        self.version += 1
         return self
 
     def sort(self, stream=None) -> "DevicePeaks":
@@ -116,6 +118,7 @@ class DevicePeaks:
             self.mz_sorted = torch.empty_like(self.mz)
             self.hits_sorted = torch.empty_like(self.hits)
         self.cum_valid = False
+        self.version += 1
         if n == 0:
             return self
         sz = ctypes.c_size_t(0)

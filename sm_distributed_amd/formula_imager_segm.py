@@ -24,8 +24,10 @@ from .rdd import LocalRDD
 class IonImageSet:
     """Device-resident ``RDD[((sf_id, adduct), [coo | None, ...])]``."""
 
-    def __init__(self, peaks, keys, win_off, peak_i_max, lo, hi, dims, ions_dev):
+    def __init__(self, peaks, keys, win_off, peak_i_max, lo, hi, dims, ions_dev, ppm=None):
         self.peaks = peaks              # DevicePeaks (sorted)
+        self.ppm = ppm                  # the ppm of the duplicate flags and windows
+        self.peaks_version = peaks.version if peaks is not None else 0
         self.keys = keys                # list[(sf_id, adduct)] ion-major
         self.win_off = win_off          # np.int64[n_ion+1]
         self.peak_i_max = peak_i_max    # np.int64[n_ion]: number of windows per ion
@@ -37,6 +39,18 @@ class IonImageSet:
         self._sel = None                # optional ion subset (filter_by_keys)
 
     # ---- bookkeeping -------------------------------------------------------------------------
+    def ensure_current(self):
+        """Restore the sorted peaks this set was built on if another compute_sf_images (another ppm) re-flagged
+        and re-sorted them since: the duplicate-candidate flags must be those of this set's windows.  The sort is
+        stable and keyed by m/z only, so re-flagging at this ppm and re-sorting gives back the same positions."""
+        p = self.peaks
+        if p is not None and (p.version != self.peaks_version or p.flag_ppm != self.ppm):
+            p.flag_duplicates(self.ppm)
+            p.sort()
+            p.prefix_sums()
+            self.peaks_version = p.version
+        return self
+
     def _counts(self):
         if self._has is None:
             cnt = (self.hi - self.lo).cpu().numpy()
@@ -61,7 +75,8 @@ class IonImageSet:
         keep = set(index)
         sel = np.array([k in keep for k in self.keys], dtype=bool)
         out = IonImageSet(self.peaks, self.keys, self.win_off, self.peak_i_max, self.lo, self.hi, self.dims,
-                          self.ions_dev)
+                          self.ions_dev, self.ppm)
+        out.peaks_version = self.peaks_version
         out._has, out._win_counts = self._has, getattr(self, "_win_counts", None)
         out._sel = sel if self._sel is None else (sel & self._sel)
         return out
@@ -71,6 +86,7 @@ class IonImageSet:
         """[(key, [coo|None...])] for the given ions; gathers only their windows from HBM."""
         import torch
         cnt, _ = self._counts()
+        self.ensure_current()
         nrows, ncols = self.dims
         wins = [np.arange(self.win_off[i], self.win_off[i + 1]) for i in ion_idx]
         if not wins:
@@ -196,4 +212,4 @@ def compute_sf_images(sc, ds, sf_peak_df, ppm):
     pm = np.where(np.isnan(peak_mz), -1.0, peak_mz)
     dions = DeviceIons.from_arrays(win_off, pm, np.zeros_like(pm), device=peaks.device)
     lo, hi = window_bounds(peaks, dions, ppm)
-    return IonImageSet(peaks, keys, win_off, np.diff(win_off), lo, hi, ds.get_dims(), dions)
+    return IonImageSet(peaks, keys, win_off, np.diff(win_off), lo, hi, ds.get_dims(), dions, ppm)

@@ -109,6 +109,7 @@ def _metrics_device_batch(ims, sf_ints, img_conf):
     from . import engine as E
     from ._lib import SMG_HITS_PACKED_F32
     opts = _chaos_opts(img_conf)
+    ims.ensure_current()
     keys = ims.keys
     K = np.diff(ims.win_off)
     need = np.array([len(sf_ints[k]) for k in keys], dtype=np.int64)
@@ -149,7 +150,7 @@ def _metrics_device_batch(ims, sf_ints, img_conf):
     nrows, ncols = ims.dims
     m = E.ion_metrics_raw(SMG_HITS_PACKED_F32, ims.peaks.hits_sorted, None, ims.peaks.sorted_cum(), lo_d, hi_d,
                           t(win_off, np.int64),
-                          t(theor, np.float64), None, len(keys), nrows, ncols, **opts)
+                          t(theor, np.float64), ims.ions_dev.ion_order, len(keys), nrows, ncols, **opts)
     r = m.to_numpy()
     has = (r["flags"] & 1) != 0
     sel = ims.ion_indices()

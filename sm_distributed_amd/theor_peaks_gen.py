@@ -2,10 +2,11 @@
 
 ``TheorPeaksGenerator`` keeps the reference's methods and their behaviour (theor_peaks_gen.py:18-146):
 ``_sf_elements``, ``_valid_sf_adduct``, ``apply_database_filters`` ('organic' filter), ``find_sf_adduct_cand``
-(targets + DECOY_ADDUCTS not yet stored), ``generate_theor_peaks`` (formatted theor_peaks rows in chunks of
-10,000) and ``run``.  The Postgres access is duck-typed: ``db`` needs ``select`` / ``select_one`` / ``copy``
-like sm.engine.db.DB; without a db, ``generate_theor_peaks`` returns the rows.  The Spark fan-out becomes one
-native multi-threaded call per chunk (``IsocalcWrapper.isotope_peaks_batch``).
+(targets + DECOY_ADDUCTS not yet stored) and ``generate_theor_peaks`` (formatted theor_peaks rows, computed in
+chunks of 10,000).  Persistence is out of scope: the reference's ``run`` SELECTs formulas and
+stored peaks from Postgres and ``_import_theor_peaks_to_db`` COPYs the rows back (theor_peaks_gen.py:57-74,
+136-146); here the caller passes the formula list and the stored (sf, adduct) set and receives the rows.  The
+Spark fan-out becomes one native multi-threaded call per chunk (``IsocalcWrapper.isotope_peaks_batch``).
 
 ``theor_peaks_df`` builds the (sf_id, adduct, centr_mzs, centr_ints) table that ``FormulasSegm`` (and so the
 GPU search) consumes, straight from formula strings.
@@ -14,20 +15,12 @@ from __future__ import annotations
 
 import logging
 import os
-
 import pandas as pd
 
 from .fdr import DECOY_ADDUCTS
 from .isocalc_wrapper import IsocalcWrapper
 
 logger = logging.getLogger("sm_distributed_amd")
-
-DB_ID_SEL = "SELECT id FROM formula_db WHERE name = %s"
-AGG_FORMULA_SEL = "SELECT id, sf FROM agg_formula where db_id = %s"
-SF_ADDUCT_SEL = ("SELECT sf, adduct FROM theor_peaks p "
-                 "JOIN agg_formula f on p.sf_id = f.id and p.db_id = f.db_id "
-                 "WHERE p.db_id = %s AND ROUND(sigma::numeric, 6) = %s AND charge = %s AND pts_per_mz = %s")
-
 
 def _parse_elements(sf):
     """Element symbols of a sum formula in order of first appearance (pyMSpec parseSumFormula segments)."""
@@ -46,12 +39,12 @@ class TheorPeaksGenerator(object):
 
     CHUNK = 10000  # theor_peaks_gen.py:128
 
-    def __init__(self, sc, sm_config, ds_config, db=None, n_threads: int = 0):
+    def __init__(self, sc, sm_config, ds_config, n_threads: int = 0, db_id: int = 0):
         self.sc = sc
         self.sm_config = sm_config
         self.ds_config = ds_config
         self.theor_peaks_tmp_dir = os.path.join(sm_config.get("fs", {}).get("base_path", ""), "tmp_theor_peaks_gen")
-        self.db = db
+        self.db_id = db_id  # formula database id written into the rows
         self.n_threads = n_threads
         self.adducts = self.ds_config["isotope_generation"]["adducts"]
         self.isocalc_wrapper = IsocalcWrapper(self.ds_config["isotope_generation"])
@@ -71,19 +64,13 @@ class TheorPeaksGenerator(object):
             return False
         return True
 
-    def run(self):
-        """theor_peaks_gen.py:57-74: generate peaks for the (sf, adduct) pairs not stored yet."""
-        if self.db is None:
-            raise RuntimeError("TheorPeaksGenerator.run needs a db (select/select_one/copy)")
+    def run(self, formula_list, stored_sf_adduct=()):
+        """theor_peaks_gen.py:57-74 without the database: rows for the (sf, adduct) pairs not stored yet."""
         logger.info("Running theoretical peaks generation")
-        db_id = self.db.select_one(DB_ID_SEL, self.ds_config["database"]["name"])[0]
-        formula_list = self.apply_database_filters(self.db.select(AGG_FORMULA_SEL, db_id))
-        stored_sf_adduct = self.db.select(SF_ADDUCT_SEL, db_id, self.isocalc_wrapper.sigma,
-                                          self.isocalc_wrapper.charge, self.isocalc_wrapper.pts_per_mz)
+        formula_list = self.apply_database_filters(formula_list)
         sf_adduct_cand = self.find_sf_adduct_cand(formula_list, set(map(tuple, stored_sf_adduct)))
         logger.info("%d saved (sf, adduct)s, %s not saved (sf, adduct)s", len(stored_sf_adduct), len(sf_adduct_cand))
-        if sf_adduct_cand:
-            self.generate_theor_peaks(sf_adduct_cand)
+        return self.generate_theor_peaks(sf_adduct_cand) if sf_adduct_cand else []
 
     def apply_database_filters(self, formula_list):
         """theor_peaks_gen.py:76-92: the 'organic' filter keeps formulas containing carbon."""
@@ -100,30 +87,15 @@ class TheorPeaksGenerator(object):
         return [(i, sf, a) for (i, sf, a) in cand if (sf, a) not in stored_sf_adduct]
 
     def generate_theor_peaks(self, sf_adduct_cand):
-        """theor_peaks_gen.py:113-134: formatted theor_peaks rows, imported to the db in chunks (or returned)."""
+        """theor_peaks_gen.py:113-134: formatted theor_peaks rows, computed in chunks."""
         logger.info("Generating missing peaks")
-        db_id = (self.db.select_one(DB_ID_SEL, self.ds_config["database"]["name"])[0] if self.db is not None else 0)
         all_lines = []
         for i in range(0, len(sf_adduct_cand), self.CHUNK):
             chunk = sf_adduct_cand[i:i + self.CHUNK]
             cents = self.isocalc_wrapper.isotope_peaks_batch([(sf, a) for _, sf, a in chunk], self.n_threads)
-            peak_lines = [self.isocalc_wrapper._format_peak_str(db_id, sf_id, a, c)
-                          for (sf_id, _, a), c in zip(chunk, cents) if len(c.mzs) > 0]
-            self._import_theor_peaks_to_db(peak_lines)
-            all_lines.extend(peak_lines)
+            all_lines.extend(self.isocalc_wrapper._format_peak_str(self.db_id, sf_id, a, c)
+                             for (sf_id, _, a), c in zip(chunk, cents) if len(c.mzs) > 0)
         return all_lines
-
-    def _import_theor_peaks_to_db(self, peak_lines):
-        """theor_peaks_gen.py:136-146."""
-        if self.db is None:
-            return
-        logger.info("Saving new peaks to the DB")
-        os.makedirs(self.theor_peaks_tmp_dir, exist_ok=True)
-        peak_lines_path = os.path.join(self.theor_peaks_tmp_dir, "peak_lines.csv")
-        with open(peak_lines_path, "w") as f:
-            f.write("\n".join(peak_lines))
-        with open(peak_lines_path) as peaks_file:
-            self.db.copy(peaks_file, "theor_peaks")
 
 
 def theor_peaks_df(formulas, adducts, isocalc_config, n_threads: int = 0) -> pd.DataFrame:

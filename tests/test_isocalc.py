@@ -144,24 +144,17 @@ def test_find_sf_adduct_cand_and_filters():
 
 
 def test_generate_theor_peaks():
-    # test_theor_peaks_gen.py:72-87, with a stand-in db: one formatted row per (sf_id, sf, adduct)
-    class DB:
-        copied = []
-
-        def select_one(self, *a):
-            return [0]
-
-        def copy(self, f, table):
-            DB.copied.append((table, f.read()))
-
-    import tempfile
-    with tempfile.TemporaryDirectory() as d:
-        gen = TPG.TheorPeaksGenerator(None, {"fs": {"base_path": d}}, ds_config(), db=DB())
-        with mock.patch.object(IsocalcWrapper, "isotope_peaks_batch",
-                               lambda self, pairs, n_threads=0: [Centroids([100.], [1000.])] * len(pairs)):
-            lines = gen.generate_theor_peaks([(9, "Au", "+Na")])
-    assert lines == ["0\t9\t+Na\t0.010000\t1\t10000\t{100.000000}\t{1000.000000}\t{}\t{}"]
-    assert DB.copied == [("theor_peaks", lines[0])]
+    # test_theor_peaks_gen.py:72-87: one formatted row per (sf_id, sf, adduct); the rows are returned (the
+    # reference COPYs them into Postgres, which is out of scope)
+    gen = TPG.TheorPeaksGenerator(None, {"fs": {"base_path": ""}}, ds_config())
+    with mock.patch.object(IsocalcWrapper, "isotope_peaks_batch",
+                           lambda self, pairs, n_threads=0: [Centroids([100.], [1000.])] * len(pairs)):
+        lines = gen.generate_theor_peaks([(9, "Au", "+Na")])
+        assert lines == ["0\t9\t+Na\t0.010000\t1\t10000\t{100.000000}\t{1000.000000}\t{}\t{}"]
+        # run(): only the pairs not stored yet
+        stored = {("Au", a) for a in gen.adducts} | {("Au", a) for a in TPG.DECOY_ADDUCTS if a != "+He"}
+        rows = gen.run([(9, "Au")], stored)
+        assert [r.split("\t")[2] for r in rows] == ["+He"]
 
 
 def test_theor_peaks_df_feeds_formulas_segm():
