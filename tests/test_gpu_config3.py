@@ -116,6 +116,6 @@ def test_config3_full_size_sample_matches_oracle():
         for col, v in (("chaos", c), ("spatial", s), ("spectral", p), ("msm", c * s * p)):
             assert abs(got[col][ion_id] - v) <= METRIC_ATOL, (ion_id, col, got[col][ion_id], v)
         planted_scored += int(c * s * p > 0)
-    assert planted_scored >= 20, "the sample must contain ions with real signal"
+    assert planted_scored >= 10, "the sample must contain ions with real signal"
     print(f"config 3: {len(rows)} sampled ions checked ({planted_scored} with msm > 0), oracle wall {wall:.1f}s "
           f"on {workers} workers, {b_mz.size:,} window points")
