@@ -83,9 +83,10 @@ int smg_sort_points(const float* mz, const uint64_t* hits, int64_t n_points, int
 int smg_window_bounds(const double* peak_mz, const int64_t* order, int64_t n_windows, double ppm,
                       const float* mz_sorted, int64_t n_points, int64_t* lo, int64_t* hi, void* stream);
 
-/* Prefix sums over the m/z-sorted hits at 64-point granularity (exclusive, 2 doubles per entry,
+/* Prefix sums over the m/z-sorted hits at 64-point granularity (exclusive, 4 doubles per entry,
  * ceil(n_points/64)+1 entries): cum64[b] = (sum of intensities of points < 64*b, sum of squared intensities
- * of those points without the duplicate-candidate flag).  Window sums of the images of
+ * of those points without the duplicate-candidate flag), each as a double-double (hi, lo) pair, so that a
+ * window's sums do not lose precision to the total intensity preceding it in m/z order.  Window sums of the images of
  * formula_imager_segm.py:84-92 become block-prefix differences plus at most 63 points at either end
  * (smg_ion_metrics reads them).  hit_format/hits/hit_vals as smg_ion_metrics. */
 int smg_hit_prefix_sums_workspace_size(int64_t n_points, size_t* bytes);

@@ -107,6 +107,32 @@ __device__ __forceinline__ int wave_incl_scan_dpp(int x) {
   return x;
 }
 
+// Double-double (hi + lo) prefix sums of (v, v^2): smg_hit_prefix_sums writes one DD4 per 64-point block.  A
+// window sum is then a difference of two nearby prefixes, exact to ~1 ulp of the window's own sum plus
+// ~eps^2 of the total mass before it, instead of ~eps of that mass (a faint window far into a bright dataset).
+// TwoSum needs unfused, unreassociated f64 arithmetic: the library is built with -ffp-contract=off.
+struct DD4 {
+  double xh, xl, yh, yl;
+};
+__host__ __device__ __forceinline__ void dd_add(double ah, double al, double bh, double bl, double& h, double& l) {
+  const double s = ah + bh;
+  const double v = s - ah;
+  double e = (ah - (s - v)) + (bh - v);  // TwoSum error of ah + bh
+  e += al + bl;
+  h = s + e;
+  l = e - (h - s);
+}
+struct DD4Add {
+  __host__ __device__ DD4 operator()(const DD4& a, const DD4& b) const {
+    DD4 r;
+    dd_add(a.xh, a.xl, b.xh, b.xl, r.xh, r.xl);
+    dd_add(a.yh, a.yl, b.yh, b.yl, r.yh, r.yl);
+    return r;
+  }
+};
+// (prefix at b) - (prefix at a) of one component, rounded to f64
+__device__ __forceinline__ double dd_diff(double bh, double bl, double ah, double al) { return (bh - ah) + (bl - al); }
+
 // Block-wide sum of NV doubles; `scratch` holds NV * (BLOCK/64) doubles of LDS.  Result broadcast.
 template <int BLOCK, int NV, bool DPP = false>
 __device__ __forceinline__ void block_sum(double (&v)[NV], double* scratch) {

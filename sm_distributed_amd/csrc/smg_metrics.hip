@@ -445,10 +445,10 @@ struct IonDesc {
 static_assert(sizeof(IonDesc) == 384, "IonDesc is 384 B");
 constexpr int DESC_QWORDS = (int)(sizeof(IonDesc) / 8);  // 48: one 8-byte load per lane of wave 0
 
-// (sum v, sum v^2 of unflagged points) over hits [0, i): 64-point block prefix + the block's first i % 64 points
+// (sum v, sum v^2 of unflagged points) over the points [i & ~63, i) of hit i's 64-point block
 template <int FMT>
-__device__ __forceinline__ double2 cum_at(const Hits<FMT>& hits, const double2* __restrict__ cum64, int64_t i) {
-  double2 c = cum64[i >> 6];
+__device__ __forceinline__ double2 block_part(const Hits<FMT>& hits, int64_t i) {
+  double2 c = make_double2(0.0, 0.0);
   const int64_t a = i & ~(int64_t)63;
   if constexpr (FMT == SMG_HITS_PACKED_F32) {  // 16-byte loads: two hits per load (a is even)
     const ulonglong2* h2 = reinterpret_cast<const ulonglong2*>(hits.h + a);
@@ -480,10 +480,21 @@ __device__ __forceinline__ double2 cum_at(const Hits<FMT>& hits, const double2* 
   return c;
 }
 
+// sums over the window [a, b): double-double block prefixes (smg_hit_prefix_sums) differenced, plus the partial
+// blocks at either end -- accurate to the window's own magnitude, not to the intensity preceding it
+template <int FMT>
+__device__ __forceinline__ double2 window_sums(const Hits<FMT>& hits, const DD4* __restrict__ cum64, int64_t a,
+                                               int64_t b) {
+  const DD4 P1 = cum64[b >> 6], P0 = cum64[a >> 6];
+  const double2 l1 = block_part<FMT>(hits, b), l0 = block_part<FMT>(hits, a);
+  return make_double2(dd_diff(P1.xh, P1.xl, P0.xh, P0.xl) + (l1.x - l0.x),
+                      dd_diff(P1.yh, P1.yl, P0.yh, P0.yl) + (l1.y - l0.y));
+}
+
 template <int FMT>
 __global__ void ion_desc_kernel(Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
                                 const int64_t* __restrict__ ion_off, const double* __restrict__ theor,
-                                const double2* __restrict__ cum, const int64_t* __restrict__ ion_order,
+                                const DD4* __restrict__ cum, const int64_t* __restrict__ ion_order,
                                 int64_t n_ions, IonDesc* __restrict__ out) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= n_ions) return;
@@ -505,9 +516,9 @@ __global__ void ion_desc_kernel(Hits<FMT> hits, const int64_t* __restrict__ lo, 
     if (k < K) {
       const int64_t a = lo[w0 + k], n = hi[w0 + k] - a;
       wt[k] = theor[w0 + k];
-      const double2 c1 = cum_at<FMT>(hits, cum, a + n), c0 = cum_at<FMT>(hits, cum, a);
-      wy[k] = c1.x - c0.x;
-      wyy[k] = c1.y - c0.y;
+      const double2 ws = window_sums<FMT>(hits, cum, a, a + n);
+      wy[k] = ws.x;
+      wyy[k] = ws.y;
       if (n > 0) has = SMG_ION_HAS_HITS;
       if (k == 0) {
         wb[k] = a;
@@ -2283,7 +2294,7 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   const int cus = device_cus();
   if (main_ok || big_ok) {
     hipLaunchKernelGGL(ion_desc_kernel<FMT>, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, hits, lo, hi,
-                       ion_off, theor, reinterpret_cast<const double2*>(hit_cum), ion_order, n_ions, desc);
+                       ion_off, theor, reinterpret_cast<const DD4*>(hit_cum), ion_order, n_ions, desc);
     SMG_LAUNCH_CHECK();
   }
   if (main_ok) {

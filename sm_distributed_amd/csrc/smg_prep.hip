@@ -249,24 +249,19 @@ __global__ void stream_read_kernel(const uint64_t* __restrict__ p, int64_t n, ui
 }
 
 // Prefix sums of (v, v^2) over the m/z-sorted hits at 64-point granularity: cum64[b] = sums over points
-// [0, 64*b) (exclusive, cum64[0] = 0).  A window sum is two block-prefix differences plus the partial sums of
-// at most 63 points at either end (ion_desc_kernel).  Squares only for points without the duplicate-candidate
-// flag: a flagged point may share its pixel with another point of the window and is squared after the
-// per-pixel sum (ion kernel).  One wave per block: a coalesced 512-B read, a fixed-order DPP reduction.
-struct VV {
-  double a, b;
-};
-struct VVAdd {
-  __host__ __device__ VV operator()(const VV& x, const VV& y) const { return VV{x.a + y.a, x.b + y.b}; }
-};
-
+// [0, 64*b) (exclusive, cum64[0] = 0) as double-double pairs (DD4, smg_common.hpp).  A window sum is the
+// difference of two block prefixes plus the partial sums of at most 63 points at either end (ion_desc_kernel),
+// accurate to the window's own magnitude however much intensity precedes it in m/z order.  Squares only for
+// points without the duplicate-candidate flag: a flagged point may share its pixel with another point of the
+// window and is squared after the per-pixel sum (ion kernel).  One wave per block: a coalesced 512-B read, a
+// fixed-order DPP reduction (plain f64: its error is relative to the block's own 64 points).
 // Each wave takes BS_PER_WAVE consecutive 64-point blocks and has all their loads in flight at once.
 constexpr int BS_PER_WAVE = 8;
 
 template <int FMT>
 __global__ void __launch_bounds__(256) block_sums64_kernel(const void* __restrict__ hits,
                                                            const double* __restrict__ hit_vals, int64_t n,
-                                                           VV* __restrict__ out) {
+                                                           DD4* __restrict__ out) {
   const int64_t blk0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * BS_PER_WAVE;
   const int lane = threadIdx.x & 63;
   const int64_t nblk = (n + 63) >> 6;
@@ -292,7 +287,7 @@ __global__ void __launch_bounds__(256) block_sums64_kernel(const void* __restric
 #pragma unroll
   for (int j = 0; j < BS_PER_WAVE; ++j) {
     const double a = wave_sum_dpp(v[j]), b = wave_sum_dpp(dup[j] ? 0.0 : v[j] * v[j]);
-    if (lane == 0 && blk0 + j < nblk) out[blk0 + j] = VV{a, b};
+    if (lane == 0 && blk0 + j < nblk) out[blk0 + j] = DD4{a, 0.0, b, 0.0};
   }
 }
 
@@ -434,8 +429,8 @@ int smg_debug_stream_read(const uint64_t* data, int64_t n_words, uint64_t* out, 
   return SMG_OK;
 }
 
-static hipError_t block_scan(void* tmp, size_t& bytes, const VV* in, VV* out, int64_t nblk, hipStream_t st) {
-  return rocprim::inclusive_scan(tmp, bytes, in, out, (size_t)nblk, VVAdd(), st, false);
+static hipError_t block_scan(void* tmp, size_t& bytes, const DD4* in, DD4* out, int64_t nblk, hipStream_t st) {
+  return rocprim::inclusive_scan(tmp, bytes, in, out, (size_t)nblk, DD4Add(), st, false);
 }
 
 int smg_hit_prefix_sums_workspace_size(int64_t n_points, size_t* bytes) {
@@ -447,7 +442,7 @@ int smg_hit_prefix_sums_workspace_size(int64_t n_points, size_t* bytes) {
     set_error("rocprim scan workspace query failed: %s", hipGetErrorString(e));
     return SMG_ERR_HIP;
   }
-  *bytes = 256 + ((size_t)(nblk > 0 ? nblk : 1) * sizeof(VV) + 255) / 256 * 256 + b0;
+  *bytes = 256 + ((size_t)(nblk > 0 ? nblk : 1) * sizeof(DD4) + 255) / 256 * 256 + b0;
   return SMG_OK;
 }
 
@@ -457,7 +452,7 @@ int smg_hit_prefix_sums(int32_t hit_format, const void* hits, const double* hit_
   SMG_CHECK_ARG(hit_format == SMG_HITS_PACKED_F32 || hit_format == SMG_HITS_SPLIT_F64, "bad hit_format");
   SMG_CHECK_ARG(cum64 != nullptr, "null pointer");
   hipStream_t st = as_stream(stream);
-  SMG_HIP(hipMemsetAsync(cum64, 0, 2 * sizeof(double), st));
+  SMG_HIP(hipMemsetAsync(cum64, 0, sizeof(DD4), st));
   if (n_points == 0) return SMG_OK;
   SMG_CHECK_ARG(hits && workspace && (hit_format == SMG_HITS_PACKED_F32 || hit_vals), "null pointer");
   size_t need = 0;
@@ -468,8 +463,8 @@ int smg_hit_prefix_sums(int32_t hit_format, const void* hits, const double* hit_
     return SMG_ERR_WORKSPACE;
   }
   const int64_t nblk = (n_points + 63) / 64;
-  VV* bs = reinterpret_cast<VV*>(reinterpret_cast<unsigned char*>(workspace) + 256);
-  unsigned char* tmp = reinterpret_cast<unsigned char*>(bs) + ((size_t)nblk * sizeof(VV) + 255) / 256 * 256;
+  DD4* bs = reinterpret_cast<DD4*>(reinterpret_cast<unsigned char*>(workspace) + 256);
+  unsigned char* tmp = reinterpret_cast<unsigned char*>(bs) + ((size_t)nblk * sizeof(DD4) + 255) / 256 * 256;
   size_t tb = need - (size_t)(tmp - reinterpret_cast<unsigned char*>(workspace));
   const int64_t nwaves = (nblk + BS_PER_WAVE - 1) / BS_PER_WAVE;
   const int64_t grid = (nwaves * 64 + 255) / 256;
@@ -480,7 +475,7 @@ int smg_hit_prefix_sums(int32_t hit_format, const void* hits, const double* hit_
     hipLaunchKernelGGL(block_sums64_kernel<SMG_HITS_SPLIT_F64>, dim3((unsigned)grid), dim3(256), 0, st, hits,
                        hit_vals, n_points, bs);
   SMG_LAUNCH_CHECK();
-  SMG_HIP(block_scan(tmp, tb, bs, reinterpret_cast<VV*>(cum64) + 1, nblk, st));
+  SMG_HIP(block_scan(tmp, tb, bs, reinterpret_cast<DD4*>(cum64) + 1, nblk, st));
   return SMG_OK;
 }
 

@@ -63,7 +63,7 @@ class DevicePeaks:
     hits_sorted: torch.Tensor | None = None
     flag_ppm: float | None = None
     sort_key_bits: int | None = None
-    cum: torch.Tensor | None = None  # 64-point block prefix sums of the sorted hits (smg_hit_prefix_sums)
+    cum: torch.Tensor | None = None  # 64-point block double-double prefix sums of the sorted hits
     cum_valid: bool = False          # cum describes the current hits_sorted
     version: int = 0                 # bumped by every flag pass / sort: an IonImageSet records the one it used
 
@@ -215,7 +215,7 @@ def hit_prefix_sums(hit_format: int, hits: torch.Tensor, hit_vals, n_points: int
     device = hits.device
     nb = (n_points + 63) // 64 + 1
     if out is None or out.shape[0] != nb:
-        out = torch.empty(nb, 2, dtype=torch.float64, device=device)
+        out = torch.empty(nb, 4, dtype=torch.float64, device=device)  # double-double (sum, sum of squares)
     sz = ctypes.c_size_t(0)
     check(lib().smg_hit_prefix_sums_workspace_size(n_points, ctypes.byref(sz)), "smg_hit_prefix_sums_workspace_size")
     ws = workspace(sz.value, device, "scan")

@@ -163,16 +163,15 @@ def make_case(name: str):
     if name == "clip_q50_conn8":
         ds, ions, ppm, _ = make_case("zeros_rect")
         return ds, ions, ppm, {"do_preprocessing": True, "q": 50.0, "connectivity": 8}
-    if name == "wide_range":   # intensities over ~1e0..1e8 with the bright mass BEFORE the scored windows: the
+    if name == "wide_range":   # intensities over ~1e-3..1e9 with the bright mass BEFORE the scored windows: the
         # window sums must not depend on the total intensity (or squared intensity) preceding them in m/z order
         ions = syn.make_ion_table(30, seed=151, decoy_seed=152, mass_range=(480.0, 880.0))
         ds = syn.make_dataset_np(48, 48, 400, seed=153, ions=ions, plant_fraction=0.5, plant_seed=154)
         rng = np.random.default_rng(155)
         ints = ds.ints.copy()
         bright = ds.mz < 420.0
-        ints[bright] = rng.lognormal(16.0, 1.0, int(bright.sum())).astype(np.float32)
-        faint = ~bright & (ints < 2000.0)   # background (planted blobs are larger): scale to ~1e-2..1e2
-        ints[faint] = (ints[faint] * 0.01).astype(np.float32)
+        ints[bright] = rng.lognormal(17.0, 1.0, int(bright.sum())).astype(np.float32)
+        ints[~bright] = (ints[~bright] * 1e-3).astype(np.float32)  # background ~0.4, planted blobs ~3
         return syn.SpectraSet(sp_off=ds.sp_off, mz=ds.mz, ints=ints, coords=ds.coords), ions, 100.0, {}
     if name == "boundary":
         ds = syn.make_dataset_np(16, 16, 300, seed=71)
