@@ -11,9 +11,9 @@
  *    null stream).  Hot entry points never allocate: size the workspace with the matching
  *    *_workspace_size() call first;
  *  - all calls are asynchronous on `stream` and re-entrant.  The only global mutable state is the
- *    thread-local error string and the two process-wide TEST switches smg_debug_force_two_level /
- *    smg_debug_force_dense (off by default; a test that sets one must not run concurrently with other
- *    callers of smg_ion_metrics in the same process).
+ *    thread-local error string and the process-wide diagnostic switches smg_debug_force_two_level /
+ *    smg_debug_force_dense / smg_debug_time_main_pass (off by default; a test or benchmark that sets one must
+ *    not run concurrently with other callers of smg_ion_metrics in the same process).
  *
  * Each entry point cites the reference interface it replaces (paths under frulo/SM_distributed).
  */
@@ -75,6 +75,21 @@ int smg_sort_points_workspace_size(int64_t n_points, size_t* bytes);
 int smg_sort_points(const float* mz, const uint64_t* hits, int64_t n_points, int32_t key_bits,
                     float* mz_sorted, uint64_t* hits_sorted, void* workspace, size_t workspace_bytes,
                     void* stream);
+
+/* m/z slice of the resident dataset for one rank of a multi-GPU search (the formula list is sharded by m/z,
+ * SURVEY.md §8e; the reference instead shuffles every point into m/z segments, formula_imager_segm.py:45-49,
+ * 112-121, 152-155): the points with lo <= mz <= hi (compared in float64, as smg_window_bounds compares), in
+ * dataset order.  Spectra must be m/z-sorted.  Two calls: smg_slice_mz_count writes the slice's spectrum
+ * offsets out_sp_off (device int64[n_spectra+1]; out_sp_off[n_spectra] = slice size) and keeps each spectrum's
+ * first selected point in the workspace; smg_slice_mz_copy (same workspace, unchanged) copies the points and
+ * sets bit 31 of each copied hit to its duplicate-candidate flag for `ppm` (smg_flag_duplicates semantics;
+ * force: optional uint8[n_spectra]), so the slice needs no separate flag pass. */
+int smg_slice_mz_workspace_size(int64_t n_spectra, size_t* bytes);
+int smg_slice_mz_count(const int64_t* sp_off, int64_t n_spectra, const float* mz, double lo, double hi,
+                       int64_t* out_sp_off, void* workspace, size_t workspace_bytes, void* stream);
+int smg_slice_mz_copy(const int64_t* sp_off, int64_t n_spectra, const float* mz, const uint64_t* hits,
+                      const int64_t* out_sp_off, double ppm, const uint8_t* force, float* out_mz,
+                      uint64_t* out_hits, const void* workspace, void* stream);
 
 /* Window search (formula_imager_segm.py:79-82): lower = mz - mz*ppm*1e-6, upper = mz + mz*ppm*1e-6
  * in float64, lo = searchsorted(mz_sorted, lower, 'left'), hi = searchsorted(mz_sorted, upper, 'right'),
@@ -150,6 +165,12 @@ int smg_debug_force_two_level(int32_t on);
 /* Test switch: on != 0 makes smg_ion_metrics score every ion with the dense (global-scratch) path, so that the
  * parity suite covers it on every case.  Process-wide; returns 0. */
 int smg_debug_force_dense(int32_t on);
+
+/* Diagnostics: on != 0 records HIP events on the launch stream around every main-pass (ion_pipe_kernel<512>)
+ * launch of smg_ion_metrics; smg_debug_main_pass_times waits for the recorded launches, writes up to `cap`
+ * elapsed times in ms (launch order), the number recorded to *n, and forgets them.  Process-wide. */
+int smg_debug_time_main_pass(int32_t on);
+int smg_debug_main_pass_times(double* ms, int32_t cap, int32_t* n);
 
 #ifdef __cplusplus
 }

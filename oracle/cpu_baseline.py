@@ -97,3 +97,79 @@ def run_pool(pix, mz, ints, dims, ppm, nlevels, ions, workers):
 
 def _noop(_):
     return 0
+
+
+def _work_segment(task):
+    """One worker's share: (pix, mz, ints, dims, ppm, nlevels, ions); returns (rows, seconds)."""
+    pix, mz, ints, dims, ppm, nlevels, ions = task
+    _init(pix, mz, ints, dims, ppm, nlevels)
+    return _work(ions)
+
+
+def _merge_intervals(lower, upper, rel=1e-6):
+    lo = np.asarray(lower, np.float64) * (1 - rel)
+    hi = np.asarray(upper, np.float64) * (1 + rel)
+    order = np.argsort(lo)
+    lo, hi = lo[order], hi[order]
+    ms, me = [lo[0]], [hi[0]]
+    for a, b in zip(lo[1:], hi[1:]):
+        if a <= me[-1]:
+            me[-1] = max(me[-1], b)
+        else:
+            ms.append(a)
+            me.append(b)
+    return np.array(ms), np.array(me)
+
+
+def select_window_points(mz, hits, lower, upper, block=1 << 27):
+    """Points of a resident dataset (torch device tensors: mz f32, packed hits) whose m/z lies in the union of
+    the windows [lower, upper] (f64, widened by 1e-6 relative so f32 rounding cannot drop a point); returns
+    host (pix, mz, int).  Every point of every window is included, so searchsorted over the selection gives the
+    windows of the whole dataset."""
+    import torch
+    ms, me = _merge_intervals(lower, upper)
+    A = torch.tensor(ms, dtype=torch.float64, device=mz.device)
+    B = torch.tensor(me, dtype=torch.float64, device=mz.device)
+    pm, ph = [], []
+    for a in range(0, mz.numel(), block):
+        x = mz[a:a + block].to(torch.float64)
+        j = torch.searchsorted(A, x, right=True) - 1
+        inside = (j >= 0) & (x <= B[j.clamp(min=0)])
+        pm.append(mz[a:a + block][inside].cpu().numpy())
+        ph.append(hits[a:a + block][inside].cpu().numpy())
+    b_mz = np.concatenate(pm)
+    b_hits = np.concatenate(ph).view(np.uint64)
+    b_pix = (b_hits & np.uint64(0x7FFFFFFF)).astype(np.int64)
+    b_int = (b_hits >> np.uint64(32)).astype(np.uint32).view(np.float32)
+    return b_pix, b_mz, b_int
+
+
+def run_pool_split(pix, mz, ints, dims, ppm, nlevels, ions, workers):
+    """Like run_pool, but each worker receives only the points of its own ions' windows (its m/z segments, the
+    way a Spark executor holds only its partition): ions are split into ``workers`` contiguous groups by
+    principal m/z.  Returns (rows, wall_seconds, per_worker_seconds)."""
+    import multiprocessing as mp
+
+    from oracle import msm_oracle as O
+    ions = sorted(ions, key=lambda t: float(t[1][0]))
+    chunks = [ions[len(ions) * w // workers: len(ions) * (w + 1) // workers] for w in range(workers)]
+    order = np.argsort(mz, kind="stable")
+    mz_s = mz[order].astype(np.float64)
+    tasks = []
+    for ch in chunks:
+        if not ch:
+            continue
+        lower, upper = O.window_bounds(np.concatenate([t[1] for t in ch]), ppm)
+        ms, me = _merge_intervals(lower, upper)
+        a = np.searchsorted(mz_s, ms, "left")
+        b = np.searchsorted(mz_s, me, "right")
+        sel = order[np.concatenate([np.arange(x, y) for x, y in zip(a, b)])] if len(a) else np.zeros(0, np.int64)
+        tasks.append((pix[sel], mz[sel], ints[sel], dims, ppm, nlevels, ch))
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(len(tasks)) as pool:
+        pool.map(_noop, range(len(tasks)))  # every worker up before timing
+        t0 = time.perf_counter()
+        res = pool.map(_work_segment, tasks, chunksize=1)
+        wall = time.perf_counter() - t0
+    rows = [r for rr, _ in res for r in rr]
+    return rows, wall, [t for _, t in res]

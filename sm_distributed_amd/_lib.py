@@ -35,6 +35,9 @@ PROTOTYPES = {
     "smg_sort_points_workspace_size": (ctypes.c_int, [_I64, ctypes.POINTER(_SZ)]),
     "smg_sort_points": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _SZ, _P]),
     "smg_window_bounds": (ctypes.c_int, [_P, _P, _I64, _D, _P, _I64, _P, _P, _P]),
+    "smg_slice_mz_workspace_size": (ctypes.c_int, [_I64, ctypes.POINTER(_SZ)]),
+    "smg_slice_mz_count": (ctypes.c_int, [_P, _I64, _P, _D, _D, _P, _P, _SZ, _P]),
+    "smg_slice_mz_copy": (ctypes.c_int, [_P, _I64, _P, _P, _P, _D, _P, _P, _P, _P, _P]),
     "smg_ion_metrics_workspace_size": (ctypes.c_int, [_I64, _I32, _I32, ctypes.POINTER(_SZ)]),
     "smg_hit_prefix_sums_workspace_size": (ctypes.c_int, [_I64, ctypes.POINTER(_SZ)]),
     "smg_hit_prefix_sums": (ctypes.c_int, [_I32, _P, _P, _I64, _P, _P, _SZ, _P]),
@@ -44,6 +47,8 @@ PROTOTYPES = {
     "smg_debug_stream_read": (ctypes.c_int, [_P, _I64, _P, _I32, _P]),
     "smg_debug_force_two_level": (ctypes.c_int, [_I32]),
     "smg_debug_force_dense": (ctypes.c_int, [_I32]),
+    "smg_debug_time_main_pass": (ctypes.c_int, [_I32]),
+    "smg_debug_main_pass_times": (ctypes.c_int, [_P, _I32, ctypes.POINTER(_I32)]),
     "smg_isotope_centroids": (ctypes.c_int, [ctypes.c_char_p, _I32, _D, _I32, _I32, _I32, _P, _P,
                                              ctypes.POINTER(_I32)]),
     "smg_isotope_centroids_batch": (ctypes.c_int, [_P, _P, _I64, _I32, _D, _I32, _I32, _I32, _P, _P, _P, _I32]),

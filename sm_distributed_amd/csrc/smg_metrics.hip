@@ -20,6 +20,10 @@
 //    images, for what the LDS passes cannot take (K > 8, principal window > 8192 points, images > 2^18 px).
 #include <stdarg.h>
 
+#include <mutex>
+#include <utility>
+#include <vector>
+
 #include "smg_common.hpp"
 
 namespace smg {
@@ -2256,6 +2260,11 @@ using Main2Lay = Lay2<MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX>;
 using Big2Lay = Lay2<BIG_BLOCK / WAVE, BIG_BLOCK * BIG2_RMAX>;
 static int g_force_two_level = 0;  // smg_debug_force_two_level: two-level passes for every image size
 static int g_force_dense = 0;      // smg_debug_force_dense: every ion on the dense path
+// smg_debug_time_main_pass: HIP events recorded on the launch stream around every main-pass launch, so a
+// benchmark measures the dominant kernel itself (not the descriptor kernel and the later passes around it)
+static int g_time_main = 0;
+static std::mutex g_ev_mu;
+static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_main_events;
 
 static int device_cus() {
   int dev = 0, cus = 0;
@@ -2306,9 +2315,20 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
     // two resident workgroups per CU, a multiple of the XCD count
     int64_t nwg = (int64_t)cus * 2;
     if (nwg > n_ions) nwg = ((n_ions + XCDS - 1) / XCDS) * XCDS;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    if (g_time_main) {
+      SMG_HIP(hipEventCreate(&ev0));
+      SMG_HIP(hipEventCreate(&ev1));
+      SMG_HIP(hipEventRecord(ev0, st));
+    }
     hipLaunchKernelGGL(k1, dim3((unsigned)nwg), dim3(MAIN_BLOCK), lds_main, st, hits, desc, SA, PM, oc, osp, osc,
                        omsm, oflags, list_a, hdr + 0);
     SMG_LAUNCH_CHECK();
+    if (g_time_main) {
+      SMG_HIP(hipEventRecord(ev1, st));
+      std::lock_guard<std::mutex> g(g_ev_mu);
+      g_main_events.emplace_back(ev0, ev1);
+    }
   } else if (big_ok) {
     hipLaunchKernelGGL(list_positions_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, list_a,
                        hdr + 0, n_ions);
@@ -2373,6 +2393,29 @@ int smg_debug_stamps(unsigned long long* host_out, int n) {
 
 int smg_debug_force_two_level(int32_t on) {
   g_force_two_level = on ? 1 : 0;
+  return SMG_OK;
+}
+
+int smg_debug_time_main_pass(int32_t on) {
+  g_time_main = on ? 1 : 0;
+  return SMG_OK;
+}
+
+int smg_debug_main_pass_times(double* ms, int32_t cap, int32_t* n) {
+  SMG_CHECK_ARG(n != nullptr && (ms != nullptr || cap == 0), "bad arguments");
+  std::lock_guard<std::mutex> g(g_ev_mu);
+  int32_t k = 0;
+  for (auto& e : g_main_events) {
+    SMG_HIP(hipEventSynchronize(e.second));
+    float t = 0.0f;
+    SMG_HIP(hipEventElapsedTime(&t, e.first, e.second));
+    if (k < cap) ms[k] = (double)t;
+    ++k;
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  g_main_events.clear();
+  *n = k;
   return SMG_OK;
 }
 

@@ -237,6 +237,74 @@ __global__ void __launch_bounds__(FLAG_THREADS) flag_duplicates_kernel(const int
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// m/z slice of the resident dataset (the points one rank's windows can touch, multi-GPU strong scaling):
+// every point with lo <= mz <= hi (compared in f64, as the window search compares), in dataset order, with
+// the duplicate-candidate flag of smg_flag_duplicates computed on the way.  Spectra must be m/z-sorted (a
+// centroided imzML spectrum is), so each spectrum's slice is one contiguous run found by two binary searches.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) slice_count_kernel(const int64_t* __restrict__ sp_off, int64_t n_spectra,
+                                                          const float* __restrict__ mz, double lo, double hi,
+                                                          int64_t* __restrict__ first, int64_t* __restrict__ count) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_spectra) return;
+  const int64_t a = sp_off[s], b = sp_off[s + 1];
+  int64_t l = a, len = b - a;  // first point with mz >= lo
+  while (len > 0) {
+    const int64_t h = len >> 1;
+    if ((double)mz[l + h] < lo) {
+      l += h + 1;
+      len -= h + 1;
+    } else {
+      len = h;
+    }
+  }
+  int64_t u = l;  // first point with mz > hi
+  len = b - l;
+  while (len > 0) {
+    const int64_t h = len >> 1;
+    if ((double)mz[u + h] <= hi) {
+      u += h + 1;
+      len -= h + 1;
+    } else {
+      len = h;
+    }
+  }
+  first[s] = l;
+  count[s] = u - l;
+}
+
+// one workgroup per spectrum (grid-stride): copies its run [first, first + n) to out at out_off[s], flagging a
+// point when its spectrum neighbour (inside or outside the slice) lies within one window width, or when the
+// spectrum's pixel is shared (force)
+__global__ void __launch_bounds__(256) slice_copy_kernel(const int64_t* __restrict__ sp_off, int64_t n_spectra,
+                                                         const float* __restrict__ mz,
+                                                         const uint64_t* __restrict__ hits,
+                                                         const int64_t* __restrict__ first,
+                                                         const int64_t* __restrict__ out_off, double ppm,
+                                                         const uint8_t* __restrict__ force,
+                                                         float* __restrict__ out_mz, uint64_t* __restrict__ out_hits) {
+  const double slack = 2.0 * ppm * 1e-6 / (1.0 - ppm * 1e-6) * (1.0 + 1e-9);
+  for (int64_t s = blockIdx.x; s < n_spectra; s += gridDim.x) {
+    const int64_t a = sp_off[s], b = sp_off[s + 1];
+    const int64_t f = first[s], o = out_off[s], n = out_off[s + 1] - o;
+    const bool all = force && force[s];
+    for (int64_t j = threadIdx.x; j < n; j += blockDim.x) {
+      const int64_t i = f + j;
+      const double m = (double)mz[i];
+      bool fl = all;
+      if (i > a) fl = fl || (m - (double)mz[i - 1] <= slack * m);
+      if (i + 1 < b) {
+        const double m2 = (double)mz[i + 1];
+        fl = fl || (m2 - m <= slack * m2);
+      }
+      const uint64_t h = hits[i];
+      out_mz[o + j] = mz[i];
+      out_hits[o + j] = fl ? (h | 0x80000000ull) : (h & ~0x80000000ull);
+    }
+  }
+}
+
 // calibration stream: every lane reads 8-byte words, grid-stride, coalesced (the access width of the ion
 // kernel's hit loads); XOR-folded per block so nothing is elided
 __global__ void stream_read_kernel(const uint64_t* __restrict__ p, int64_t n, uint64_t* __restrict__ out) {
@@ -416,6 +484,66 @@ int smg_sample_spectra(const int64_t* sp_off, const double* mzs, const double* c
   hipLaunchKernelGGL(sample_spectra_kernel, grid, dim3(256), 0, as_stream(stream), sp_off, mzs, cum_ints,
                      n_spectra, lower, upper, n_windows, out_window, out_spectrum, out_value, capacity,
                      reinterpret_cast<unsigned long long*>(count));
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+static hipError_t slice_scan(void* tmp, size_t& bytes, const int64_t* in, int64_t* out, int64_t n, hipStream_t st) {
+  return rocprim::exclusive_scan(tmp, bytes, in, out, (int64_t)0, (size_t)n, rocprim::plus<int64_t>(), st, false);
+}
+
+int smg_slice_mz_workspace_size(int64_t n_spectra, size_t* bytes) {
+  SMG_CHECK_ARG(bytes != nullptr && n_spectra >= 0, "bad arguments");
+  size_t b0 = 0;
+  hipError_t e = slice_scan(nullptr, b0, nullptr, nullptr, n_spectra + 1, 0);
+  if (e != hipSuccess) {
+    set_error("rocprim scan workspace query failed: %s", hipGetErrorString(e));
+    return SMG_ERR_HIP;
+  }
+  *bytes = 256 + 2 * (((size_t)(n_spectra + 1) * 8 + 255) / 256 * 256) + b0;
+  return SMG_OK;
+}
+
+int smg_slice_mz_count(const int64_t* sp_off, int64_t n_spectra, const float* mz, double lo, double hi,
+                       int64_t* out_sp_off, void* workspace, size_t workspace_bytes, void* stream) {
+  SMG_CHECK_ARG(n_spectra >= 0 && sp_off && out_sp_off, "bad arguments");
+  hipStream_t st = as_stream(stream);
+  if (n_spectra == 0) {
+    SMG_HIP(hipMemsetAsync(out_sp_off, 0, sizeof(int64_t), st));
+    return SMG_OK;
+  }
+  SMG_CHECK_ARG(mz && workspace, "null pointer");
+  size_t need = 0;
+  int rc = smg_slice_mz_workspace_size(n_spectra, &need);
+  if (rc) return rc;
+  if (workspace_bytes < need) {
+    set_error("slice workspace too small: %zu < %zu", workspace_bytes, need);
+    return SMG_ERR_WORKSPACE;
+  }
+  unsigned char* w = reinterpret_cast<unsigned char*>(workspace) + 256;
+  const size_t arr = ((size_t)(n_spectra + 1) * 8 + 255) / 256 * 256;
+  int64_t* first = reinterpret_cast<int64_t*>(w);
+  int64_t* count = reinterpret_cast<int64_t*>(w + arr);
+  unsigned char* tmp = w + 2 * arr;
+  size_t tb = need - 256 - 2 * arr;
+  SMG_HIP(hipMemsetAsync(count + n_spectra, 0, sizeof(int64_t), st));
+  hipLaunchKernelGGL(slice_count_kernel, dim3((unsigned)((n_spectra + 255) / 256)), dim3(256), 0, st, sp_off,
+                     n_spectra, mz, lo, hi, first, count);
+  SMG_LAUNCH_CHECK();
+  SMG_HIP(slice_scan(tmp, tb, count, out_sp_off, n_spectra + 1, st));
+  return SMG_OK;
+}
+
+int smg_slice_mz_copy(const int64_t* sp_off, int64_t n_spectra, const float* mz, const uint64_t* hits,
+                      const int64_t* out_sp_off, double ppm, const uint8_t* force, float* out_mz,
+                      uint64_t* out_hits, const void* workspace, void* stream) {
+  SMG_CHECK_ARG(n_spectra >= 0 && ppm >= 0 && ppm < 1e6, "bad arguments");
+  if (n_spectra == 0) return SMG_OK;
+  SMG_CHECK_ARG(sp_off && mz && hits && out_sp_off && out_mz && out_hits && workspace, "null pointer");
+  const int64_t* first = reinterpret_cast<const int64_t*>(reinterpret_cast<const unsigned char*>(workspace) + 256);
+  const int64_t grid = n_spectra < (1 << 20) ? n_spectra : (1 << 20);
+  hipLaunchKernelGGL(slice_copy_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream), sp_off, n_spectra,
+                     mz, hits, first, out_sp_off, ppm, force, out_mz, out_hits);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

@@ -82,3 +82,28 @@ def spectra_from_duck(ds):
     mz = np.concatenate(mzs) if n else np.zeros(0, np.float32)
     it = np.concatenate(its) if n else np.zeros(0, np.float32)
     return off, mz, it
+
+
+class ResidentDataset:
+    """A dataset already resident in HBM (e.g. generated there, or loaded by another rank's reader): the same
+    accessors as DeviceDataset over a DevicePeaks.  ``pixel_map`` defaults to the identity (spectrum i is
+    pixel i, the row-major grid of dataset.py:52-66)."""
+
+    def __init__(self, peaks, pixel_map=None):
+        self._peaks = peaks
+        self._dims = (peaks.nrows, peaks.ncols)
+        n_sp = int(peaks.sp_off.numel()) - 1 if peaks.sp_off is not None else peaks.nrows * peaks.ncols
+        self.norm_img_pixel_inds = (np.arange(n_sp, dtype=np.int32) if pixel_map is None
+                                    else np.asarray(pixel_map, dtype=np.int32))
+
+    def device_peaks(self):
+        return self._peaks
+
+    def get_norm_img_pixel_inds(self):
+        return self.norm_img_pixel_inds
+
+    def get_dims(self):
+        return self._dims
+
+    def get_spectra(self):
+        raise NotImplementedError("ResidentDataset holds device arrays only")

@@ -1,96 +1,221 @@
-"""Multi-GPU layer: ion sharding + one collective for the per-ion metric rows.
+"""Multi-GPU hot path: the formula list sharded over ranks by m/z, one collective for the metric rows
+(BASELINE.json config 4: strong scaling of config 3 over 2/4/8 GPUs).
 
-One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  Ions are independent, so the
-formula list is sharded with the peak list replicated on every rank; the only exchange is a single
-all-gather of fixed-size metric rows (chaos, spatial, spectral, msm, flags as f64 = 40 B/row), after
-which rank 0 builds the reference DataFrame and runs FDR.  Images stay on the rank that scored them.
+One process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI).  Every rank holds the resident
+dataset (replicated: each rank loads it, as each Spark executor reads ds.txt).  The reference partitions the
+*data* by m/z segment and shuffles every point to its segment (formula_imager_segm.py:45-49, 112-121, 152-155),
+then groups images per ion (:134-138) and collects metric tuples to the driver (formula_img_validator.py:
+115-118).  Here the *formulas* are partitioned by m/z instead, so no point ever moves between GPUs:
 
-Sharding balances an estimated per-ion cost: the number of window points grows linearly with m/z for a
-uniform-density dataset, and the reference's own workload model is exactly a product of histograms
-(formula_imager_segm.py:9-14 _estimate_mz_workload); ``ion_costs`` uses the dataset's m/z histogram when
-given, else sum of window m/z.  Contiguous shards in ion-table order keep each rank's windows spread over
-the whole m/z range (ions are ordered by formula, not by mass).
+* ``plan_shards`` (once per dataset / formula table / ppm): ions ordered by principal m/z are cut into
+  ``world`` contiguous ranges of equal estimated cost.  The cost model is the analogue of
+  ``_estimate_mz_workload`` (formula_imager_segm.py:9-14, a product of the data and theoretical-peak m/z
+  histograms): per ion, the expected window points from the dataset's m/z histogram (ion kernel, ~6.5 ps per
+  window point on MI355X), a fixed per-ion cost, and the data points its m/z range adds to the rank's slice
+  (slice copy + sort, ~33 ps per point).  A rank's slice is [min lower bound, max upper bound] of its windows;
+* ``score_sharded`` (per search): each rank copies its m/z slice of the resident peaks (smg_slice_mz_*, with the
+  duplicate flags fused into the copy), so its sort covers ~1/world of the points; runs compute_sf_images +
+  sf_image_metrics' device batch on its shard; packs fixed-size rows (global ion index, chaos, spatial,
+  spectral, msm; 40 B) and all-gathers them (one RCCL all_gather_into_tensor over xGMI, ~40 MB at config 3);
+  rank 0 builds the reference DataFrame from codes;
+* ``search``: MSMBasicSearch.search (msm_basic_search.py:13-20) over the ranks: the table of ``score_sharded``,
+  then FDR and the filter on rank 0, the images staying on the rank that made them.
 """
 from __future__ import annotations
 
+from dataclasses import dataclass, field
+
 import numpy as np
+import pandas as pd
+
+# cost model constants (MI355X, config 3, round-1/2 measurements: 42 ms for 6.45e9 window points and 0.98M
+# ions in the ion kernel; 16.4 ms for flag + sort + scan of 5.0e8 points)
+C_WINDOW_POINT = 6.5e-12
+C_ION = 2.0e-9
+C_SLICE_POINT = 33e-12
+
+ROW_FIELDS = ("ion", "chaos", "spatial", "spectral", "msm")
 
 
-def ion_costs(win_off, peak_mz, mz_hist=None, mz_edges=None):
-    """Estimated points read per ion: sum over its windows of (histogram density at m/z) * window width."""
+@dataclass
+class ShardPlan:
+    rank: int
+    world: int
+    ion_idx: np.ndarray            # this rank's ions (positions in the formula table's (sf_id, adduct) order)
+    formulas: object               # FormulasSegm of this rank's ions
+    mz_lo: float                   # the m/z slice this rank's windows touch (f64, inclusive)
+    mz_hi: float
+    ppm: float
+    counts: list                   # ions per rank
+    bounds: list                   # [(first, last) principal-order positions] per rank
+    global_keys: object            # IonKeys of the whole table (rank 0 builds the DataFrame from codes)
+    est_cost: list = field(default_factory=list)  # estimated seconds per rank
+    _sf_peak_df: object = None
+
+    @property
+    def sf_peak_df(self):
+        if self._sf_peak_df is None:
+            self._sf_peak_df = self.formulas.get_sf_peak_df()
+        return self._sf_peak_df
+
+
+def ion_costs(win_off, peak_mz, ppm, mz_hist=None, mz_edges=None):
+    """Estimated seconds per ion: expected window points (dataset m/z density x window width) x C_WINDOW_POINT +
+    C_ION.  Without a histogram the density is taken as uniform (window points ~ window width ~ m/z)."""
     win_off = np.asarray(win_off)
     peak_mz = np.asarray(peak_mz, dtype=np.float64)
+    width = 2.0 * ppm * 1e-6 * peak_mz
     if mz_hist is not None:
-        idx = np.clip(np.searchsorted(mz_edges, peak_mz) - 1, 0, len(mz_hist) - 1)
+        idx = np.clip(np.searchsorted(mz_edges, peak_mz, side="right") - 1, 0, len(mz_hist) - 1)
         dens = np.asarray(mz_hist, dtype=np.float64)[idx] / np.diff(mz_edges)[idx]
-        w = dens * peak_mz
+        inside = (peak_mz >= mz_edges[0]) & (peak_mz <= mz_edges[-1])
+        pts = np.where(inside, dens * width, 0.0)
     else:
-        w = peak_mz
-    w = np.where(np.isfinite(w), w, 0.0)
-    cs = np.concatenate([[0.0], np.cumsum(w)])
-    return cs[win_off[1:]] - cs[win_off[:-1]] + 1.0  # +1: per-ion fixed cost
+        pts = width
+    pts = np.where(np.isfinite(pts), pts, 0.0)
+    cs = np.concatenate([[0.0], np.cumsum(pts)])
+    return (cs[win_off[1:]] - cs[win_off[:-1]]) * C_WINDOW_POINT + C_ION
 
 
 def shard_bounds(costs, world):
-    """Contiguous [a, b) ion ranges with ~equal summed cost (greedy cut on the cost prefix sum)."""
+    """Contiguous [a, b) ranges with ~equal summed cost (greedy cut on the cost prefix sum)."""
     costs = np.asarray(costs, dtype=np.float64)
     n = len(costs)
     if world <= 1 or n == 0:
         return [(0, n)] + [(n, n)] * max(0, world - 1)
     pref = np.concatenate([[0.0], np.cumsum(costs)])
     total = pref[-1]
-    cuts = [0]
-    for r in range(1, world):
-        cuts.append(int(np.searchsorted(pref, total * r / world)))
-    cuts.append(n)
+    cuts = [0] + [int(np.searchsorted(pref, total * r / world)) for r in range(1, world)] + [n]
     cuts = np.maximum.accumulate(np.array(cuts))
     return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
 
 
-ROW_FIELDS = ("chaos", "spatial", "spectral", "msm", "flags")
-
-
-def pack_rows(metrics, n_max, device=None):
-    """[n_max, 5] f64 row block of one rank (zero padded)."""
+def mz_histogram(mz, bins=8192):
+    """(counts, edges) of the resident m/z values (a torch tensor, device or host): one pass over the data."""
     import torch
-    n = metrics.chaos.numel()
-    dev = device if device is not None else metrics.chaos.device
-    out = torch.zeros(n_max, len(ROW_FIELDS), dtype=torch.float64, device=dev)
-    for j, f in enumerate(ROW_FIELDS):
-        out[:n, j] = getattr(metrics, f).to(dev, dtype=torch.float64)
-    return out
+    lo, hi = (float(v) for v in torch.aminmax(mz))
+    hi = hi if hi > lo else lo + 1.0
+    h = torch.histc(mz.to(torch.float32), bins=bins, min=lo, max=hi).double().cpu().numpy()
+    return h, np.linspace(lo, hi, bins + 1)
 
 
-def gather_rows(rows, counts, group=None):
-    """All-gather every rank's [n_max, 5] block; returns the concatenated [sum(counts), 5] table (every rank)."""
+def plan_shards(formulas, peaks_or_mz, ppm, world, rank, bins=8192):
+    """Shard ``formulas`` (FormulasSegm) over ``world`` ranks by principal m/z; returns this rank's ShardPlan.
+    ``peaks_or_mz``: the resident DevicePeaks (or an m/z tensor) whose histogram drives the cost model."""
+    from .formula_imager_segm import IonKeys
+    mz = getattr(peaks_or_mz, "mz", peaks_or_mz)
+    hist, edges = mz_histogram(mz, bins)
+    off, pmz = formulas.ion_off, formulas.peak_mz
+    first = pmz[off[:-1]]
+    order = np.argsort(first, kind="stable")           # principal m/z order
+    cost = ion_costs(off, pmz, ppm, hist, edges)[order]
+    # slice growth: the data points between consecutive principal m/z values enter the slice of whichever rank
+    # holds the ion before them
+    cum_pts = np.concatenate([[0.0], np.cumsum(hist)])
+    pos = np.interp(first[order], edges, cum_pts)
+    grow = np.diff(np.concatenate([pos, [cum_pts[-1]]]))
+    cost = cost + np.maximum(grow, 0.0) * C_SLICE_POINT
+    bounds = shard_bounds(cost, world)
+    a, b = bounds[rank]
+    mine = np.sort(order[a:b])                        # back to (sf_id, adduct) order
+    shard = formulas.subset(mine)
+    if len(mine) and len(shard.peak_mz):
+        lower = shard.peak_mz - shard.peak_mz * ppm * 1e-6   # formula_imager_segm.py:79-80, left to right
+        upper = shard.peak_mz + shard.peak_mz * ppm * 1e-6
+        mz_lo, mz_hi = float(lower.min()), float(upper.max())
+    else:
+        mz_lo, mz_hi = 1.0, 0.0  # empty slice
+    keys = formulas.ion_sf.astype(np.int64) * max(len(formulas.adducts), 1) + formulas.ion_adduct_code
+    return ShardPlan(rank=rank, world=world, ion_idx=mine, formulas=shard, mz_lo=mz_lo, mz_hi=mz_hi, ppm=ppm,
+                     counts=[int(y - x) for x, y in bounds], bounds=bounds,
+                     global_keys=IonKeys(keys, formulas.adducts), est_cost=[float(cost[x:y].sum()) for x, y in bounds])
+
+
+def slice_peaks(peaks, plan):
+    """This rank's m/z slice of the resident dataset, duplicate flags set for plan.ppm."""
+    return peaks.slice_mz(plan.mz_lo, plan.mz_hi, plan.ppm)
+
+
+def _device_rows(plan, peaks, ds_config):
+    """Score this rank's shard on its GPU: [n_shard, 5] float64 rows (global ion index or -1, chaos, spatial,
+    spectral, msm) and this rank's IonImageSet."""
+    import torch
+
+    from .dataset import ResidentDataset
+    from .formula_imager_segm import compute_sf_images
+    from .formula_img_validator import _metrics_device_rows
+    dev = peaks.device
+    n = len(plan.ion_idx)
+    rows = torch.full((n, len(ROW_FIELDS)), -1.0, dtype=torch.float64, device=dev)
+    if n == 0:
+        return rows, None
+    sl = slice_peaks(peaks, plan)
+    dds = ResidentDataset(sl)
+    ims = compute_sf_images(None, dds, plan.sf_peak_df, plan.ppm)
+    keep, m = _metrics_device_rows(ims, plan.formulas.get_sf_peak_ints(), ds_config["image_generation"])
+    # the image set's ions are the shard's ions in the same (sf_id, adduct) order; map by key to be exact
+    skeys = plan.global_keys.keys[plan.ion_idx]
+    pos = np.searchsorted(skeys, ims.ion_keys.keys)
+    glob = torch.from_numpy(plan.ion_idx[pos].astype(np.float64)).to(dev)
+    k = len(pos)
+    rows[:k, 0] = torch.where(keep, glob, torch.full_like(glob, -1.0))
+    rows[:k, 1] = m.chaos
+    rows[:k, 2] = m.spatial
+    rows[:k, 3] = m.spectral
+    rows[:k, 4] = m.msm
+    return rows, ims
+
+
+def gather_rows(rows, plan, group=None):
+    """All-gather every rank's row block, padded to the largest shard (one RCCL all_gather_into_tensor);
+    returns the [world * n_max, 5] table on every rank."""
     import torch
     import torch.distributed as dist
-    world = dist.get_world_size(group)
-    n_max = rows.shape[0]
-    recv = torch.empty(world * n_max, rows.shape[1], dtype=rows.dtype, device=rows.device)
-    dist.all_gather_into_tensor(recv, rows, group=group)
-    parts = [recv[r * n_max: r * n_max + counts[r]] for r in range(world)]
-    return torch.cat(parts, 0)
+    n_max = max(plan.counts) if plan.counts else 0
+    send = torch.full((n_max, rows.shape[1]), -1.0, dtype=rows.dtype, device=rows.device)
+    send[:rows.shape[0]] = rows
+    recv = torch.empty(plan.world * n_max, rows.shape[1], dtype=rows.dtype, device=rows.device)
+    dist.all_gather_into_tensor(recv, send, group=group)
+    return recv
 
 
-def exchange_counts(n_local, device, group=None):
-    import torch
-    import torch.distributed as dist
-    world = dist.get_world_size(group)
-    t = torch.tensor([n_local], dtype=torch.int64, device=device)
-    out = [torch.zeros_like(t) for _ in range(world)]
-    dist.all_gather(out, t, group=group)
-    return [int(x.item()) for x in out]
-
-
-def rows_to_frame(table, keys):
-    """Rank-0 assembly: rows (global ion order) -> reference DataFrame for ions with images."""
-    import pandas as pd
+def rows_to_frame(table, global_keys):
+    """Rank-0 assembly: gathered rows -> the reference DataFrame (index [sf_id, adduct] in table order,
+    columns chaos, spatial, spectral, msm), one row per ion with images."""
     t = table.cpu().numpy() if hasattr(table, "cpu") else np.asarray(table)
-    has = (t[:, 4].astype(np.int64) & 1) != 0
-    idx = np.nonzero(has)[0]
-    df = pd.DataFrame({"sf_id": [keys[i][0] for i in idx], "adduct": [keys[i][1] for i in idx],
-                       "chaos": t[idx, 0], "spatial": t[idx, 1], "spectral": t[idx, 2]},
-                      columns=["sf_id", "adduct", "chaos", "spatial", "spectral"]).set_index(["sf_id", "adduct"])
-    df["msm"] = df.chaos * df.spatial * df.spectral
-    return df
+    t = t[t[:, 0] >= 0]
+    idx = t[:, 0].astype(np.int64)
+    o = np.argsort(idx, kind="stable")
+    idx, t = idx[o], t[o]
+    return pd.DataFrame(t[:, 1:5], index=global_keys.multi_index(idx), columns=["chaos", "spatial", "spectral", "msm"])
+
+
+def score_sharded(plan, peaks, ds_config, group=None, score_local=None):
+    """compute_sf_images + sf_image_metrics over all ranks: returns (the reference metrics table on rank 0,
+    None elsewhere; this rank's IonImageSet).  ``score_local(plan, peaks, ds_config) -> (rows, images)``
+    replaces the device scorer (tests on CPU ranks)."""
+    import torch.distributed as dist
+    rows, ims = (score_local or _device_rows)(plan, peaks, ds_config)
+    table = gather_rows(rows, plan, group)
+    df = rows_to_frame(table, plan.global_keys) if dist.get_rank(group) == 0 else None
+    return df, ims
+
+
+def search(plan, peaks, formulas, fdr, ds_config, group=None, score_local=None):
+    """MSMBasicSearch.search (msm_basic_search.py:13-31) over the ranks: on rank 0 the FDR-annotated, filtered
+    metrics table (sf_image_metrics_est_fdr + filter_sf_metrics); on every rank the images of its reported
+    ions (filter_sf_images)."""
+    import torch.distributed as dist
+
+    from .formula_img_validator import sf_image_metrics_est_fdr
+    from .search_algorithm import MSMBasicSearch
+    df, ims = score_sharded(plan, peaks, ds_config, group, score_local)
+    msm = MSMBasicSearch(None, None, formulas, fdr, ds_config)
+    out = None
+    if dist.get_rank(group) == 0:
+        out = msm.filter_sf_metrics(sf_image_metrics_est_fdr(df, formulas, fdr))
+    # every rank filters its own images by the reported keys (broadcast of the reported index)
+    obj = [None if out is None else out.index]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    images = msm.filter_sf_images(ims, obj[0]) if ims is not None else None
+    return out, images

@@ -58,7 +58,6 @@ class DevicePeaks:
     ncols: int
     sp_off: torch.Tensor | None = None     # int64[n_spectra+1] (dataset order), for duplicate flags
     force: torch.Tensor | None = None      # uint8[n_spectra]: spectra whose pixel is shared (non-injective map)
-    flag_state: torch.Tensor | None = None  # uint8[n_points]: duplicate flag each hit carries (smg_flag_duplicates)
     mz_sorted: torch.Tensor | None = None
     hits_sorted: torch.Tensor | None = None
     flag_ppm: float | None = None
@@ -66,6 +65,8 @@ class DevicePeaks:
     cum: torch.Tensor | None = None  # 64-point block double-double prefix sums of the sorted hits
     cum_valid: bool = False          # cum describes the current hits_sorted
     version: int = 0                 # bumped by every flag pass / sort: an IonImageSet records the one it used
+    flags_preset_ppm: float | None = None  # a slice's copy set the flags for this ppm (no flag pass needed)
+    _sorted: bool | None = None      # spectra_sorted() result
 
     @property
     def n_points(self) -> int:
@@ -98,19 +99,57 @@ class DevicePeaks:
         return cls(mz=mz, hits=hits, nrows=int(dims[0]), ncols=int(dims[1]), sp_off=sp_off, force=force)
 
     def flag_duplicates(self, ppm: float, stream=None) -> "DevicePeaks":
-        """Duplicate-candidate flags for this ppm (smg_flag_duplicates); idempotent, writes only changes."""
+        """Duplicate-candidate flags for this ppm (smg_flag_duplicates).  Every call recomputes them from the
+        m/z values (12 B read per point), except on a slice whose copy already set them for this ppm."""
         if self.sp_off is None:
             raise ValueError("DevicePeaks needs sp_off (spectrum offsets) for duplicate flags")
+        if self.flags_preset_ppm is not None and float(ppm) == self.flags_preset_ppm:
+            self.flag_ppm = float(ppm)
+            return self
+        self.flags_preset_ppm = None
         n_sp = int(self.sp_off.numel()) - 1
-        if self.flag_state is None or self.flag_state.numel() != self.n_points:
-            # the flag each hit carries now (one byte per point): later passes touch only hits that change
-            self.flag_state = ((self.hits >> 31) & 1).to(torch.uint8)
         check(lib().smg_flag_duplicates(_p(self.sp_off), n_sp, _p(self.mz), _p(self.hits), self.n_points,
-                                        float(ppm), _p(self.force), _p(self.flag_state), _stream(stream)),
+                                        float(ppm), _p(self.force), None, _stream(stream)),
               "smg_flag_duplicates")
         self.flag_ppm = float(ppm)
         self.version += 1
         return self
+
+    def spectra_sorted(self) -> bool:
+        """Every spectrum's m/z values are nondecreasing (checked once; the m/z array does not change)."""
+        if self._sorted is None:
+            n = self.n_points
+            if n < 2:
+                self._sorted = True
+            else:
+                starts = torch.zeros(n, dtype=torch.bool, device=self.device)
+                so = self.sp_off[1:-1]
+                starts[so[so < n]] = True
+                bad = (self.mz[1:] < self.mz[:-1]) & ~starts[1:]
+                self._sorted = not bool(bad.any().item())
+        return self._sorted
+
+    def slice_mz(self, lo: float, hi: float, ppm: float, stream=None) -> "DevicePeaks":
+        """The points with lo <= mz <= hi (f64 comparison), in dataset order, as a new DevicePeaks whose
+        duplicate-candidate flags for ``ppm`` are set by the copy (smg_slice_mz_count / _copy)."""
+        if not self.spectra_sorted():
+            raise ValueError("slice_mz needs m/z-sorted spectra")
+        n_sp = int(self.sp_off.numel()) - 1
+        sz = ctypes.c_size_t(0)
+        check(lib().smg_slice_mz_workspace_size(n_sp, ctypes.byref(sz)), "smg_slice_mz_workspace_size")
+        ws = workspace(sz.value, self.device, "slice")
+        off = torch.empty(n_sp + 1, dtype=torch.int64, device=self.device)
+        check(lib().smg_slice_mz_count(_p(self.sp_off), n_sp, _p(self.mz), float(lo), float(hi), _p(off), _p(ws),
+                                       ws.numel(), _stream(stream)), "smg_slice_mz_count")
+        n = int(off[-1].item())
+        mz = torch.empty(n, dtype=torch.float32, device=self.device)
+        hits = torch.empty(n, dtype=torch.int64, device=self.device)
+        check(lib().smg_slice_mz_copy(_p(self.sp_off), n_sp, _p(self.mz), _p(self.hits), _p(off), float(ppm),
+                                      _p(self.force), _p(mz), _p(hits), _p(ws), _stream(stream)), "smg_slice_mz_copy")
+        out = DevicePeaks(mz=mz, hits=hits, nrows=self.nrows, ncols=self.ncols, sp_off=off, force=self.force)
+        out.flags_preset_ppm = float(ppm)
+        out._sorted = True
+        return out
 
     def sort(self, stream=None) -> "DevicePeaks":
         n = self.n_points

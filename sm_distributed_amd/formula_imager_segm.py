@@ -11,6 +11,10 @@ matrices only when a caller iterates them.  Semantics (complete-window, SURVEY.m
 
 The reference's m/z segmentation and chunking (:9-49, :68-69) only partition this same computation
 over Spark workers; on one GPU the whole sorted peak list is resident, so neither exists here.
+
+Host work is O(columns), never O(ions) in Python: the ion layout of ``sf_peak_df`` (ion identity, windows per
+ion, window m/z in ion-major order, processing orders) is built on the device from three uploaded columns
+(``device_layout``), on a side stream while the resident peaks are flagged and sorted on the main stream.
 """
 from __future__ import annotations
 
@@ -21,24 +25,205 @@ from scipy.sparse import coo_matrix
 from .rdd import LocalRDD
 
 
+class IonKeys:
+    """(sf_id, adduct) of every ion of a layout, encoded ``key = sf_code * n_adducts + adduct_code`` and
+    sorted, so ion order = (sf_id, adduct) order, the order of the reference's sf_df (formulas_segm.py:43-44).
+
+    ``sf_code`` is the sf_id itself for integer ids (``sf_levels`` None), else its position in the sorted
+    ``sf_levels``; ``adducts`` are the sorted adduct strings."""
+
+    def __init__(self, keys: np.ndarray, adducts, sf_levels=None, keys_dev=None):
+        self.keys = keys
+        self.keys_dev = keys_dev  # the same keys in HBM (device_layout keeps them)
+        self.adducts = list(adducts)
+        self.sf_levels = sf_levels
+        self.n_cat = max(len(self.adducts), 1)
+        self._tuples = None
+
+    def __len__(self):
+        return len(self.keys)
+
+    @property
+    def sf_code(self):
+        return self.keys // self.n_cat
+
+    @property
+    def adduct_code(self):
+        return (self.keys % self.n_cat).astype(np.int64)
+
+    def sf_values(self, idx=None):
+        c = self.sf_code if idx is None else self.keys[idx] // self.n_cat
+        return c if self.sf_levels is None else np.asarray(self.sf_levels)[c]
+
+    def tuples(self):
+        if self._tuples is None:
+            ad = np.asarray(self.adducts, dtype=object)[self.adduct_code]
+            self._tuples = list(zip(self.sf_values().tolist(), ad.tolist()))
+        return self._tuples
+
+    def encode_codes(self, sf, adduct_codes, adducts):
+        """encode() for adducts given as codes into the string list ``adducts`` (no per-row string hashing)."""
+        cmap = pd.Index(self.adducts, dtype=object).get_indexer(pd.Index(list(adducts), dtype=object))
+        code = cmap[np.asarray(adduct_codes, dtype=np.int64)] if len(cmap) else np.zeros(len(sf), np.int64)
+        sf = np.asarray(sf)
+        if self.sf_levels is None:
+            sfc = sf.astype(np.int64) if sf.dtype.kind in "iu" else np.full(len(sf), -1, np.int64)
+            ok = code >= 0
+        else:
+            sfc = pd.Index(self.sf_levels).get_indexer(pd.Index(sf)).astype(np.int64)
+            ok = (code >= 0) & (sfc >= 0)
+        return np.where(ok, sfc * self.n_cat + code, -1), ok
+
+    def encode(self, sf, adducts):
+        """Keys of (sf_id, adduct) pairs in this encoding; -1 for pairs that cannot be in it."""
+        code = pd.Index(self.adducts, dtype=object).get_indexer(pd.Index(np.asarray(adducts, dtype=object)))
+        sf = np.asarray(sf)
+        if self.sf_levels is None:
+            sfc = sf.astype(np.int64) if sf.dtype.kind in "iu" else np.full(len(sf), -1, np.int64)
+            ok = code >= 0
+        else:
+            sfc = pd.Index(self.sf_levels).get_indexer(pd.Index(sf)).astype(np.int64)
+            ok = (code >= 0) & (sfc >= 0)
+        return np.where(ok, sfc * self.n_cat + code, -1), ok
+
+    def multi_index(self, idx):
+        """pd.MultiIndex [sf_id, adduct] of the ions ``idx`` (ascending positions), built from codes."""
+        k = self.keys[idx]
+        sfc = k // self.n_cat
+        adc = (k % self.n_cat).astype(np.int64)
+        if self.sf_levels is None:
+            new = np.ones(len(sfc), bool)
+            new[1:] = sfc[1:] != sfc[:-1]  # idx ascending -> sf codes nondecreasing
+            sf_lv = sfc[new]
+            sf_codes = np.cumsum(new) - 1
+        else:
+            sf_lv, sf_codes = np.asarray(self.sf_levels), sfc
+        return pd.MultiIndex(levels=[pd.Index(sf_lv), pd.Index(self.adducts, dtype=object)],
+                             codes=[sf_codes, adc], names=["sf_id", "adduct"], verify_integrity=False)
+
+
+def _adduct_codes(col):
+    """(int64 codes, sorted category strings) of an adduct column, Categorical or not."""
+    if isinstance(col.dtype, pd.CategoricalDtype):
+        cats = [str(c) for c in col.cat.categories]
+        codes = col.cat.codes.to_numpy().astype(np.int64)
+        order = np.argsort(np.array(cats, dtype=object), kind="stable")
+        if not (order == np.arange(len(cats))).all():
+            rank = np.empty(len(cats), np.int64)
+            rank[order] = np.arange(len(cats))
+            codes = np.where(codes >= 0, rank[np.maximum(codes, 0)], -1)
+            cats = [cats[i] for i in order]
+    else:
+        codes, uniq = pd.factorize(col.to_numpy(dtype=object), sort=True)
+        cats = [str(u) for u in uniq]
+    if len(codes) and codes.min() < 0:
+        raise ValueError("sf_peak_df has missing adducts")
+    return codes, cats
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
+    """Ion-major window table of FormulasSegm.get_sf_peak_df rows (sf_id, adduct, peak_i, mz), on the device.
+
+    An ion gets max(peak_i)+1 windows (formula_imager_segm.py:95-109: list length max(peak_i)+1); windows
+    without a row are padding (m/z -1: no point can match).  Returns (IonKeys, DeviceIons, K per ion)."""
+    import torch
+
+    from .engine import DeviceIons
+    sf = sf_peak_df["sf_id"].to_numpy()
+    codes, cats = _adduct_codes(sf_peak_df["adduct"])
+    n_cat = max(len(cats), 1)
+    sf_levels = None
+    if sf.dtype.kind in "iu":
+        sf_code = sf.astype(np.int64)
+        if len(sf_code) and (np.abs(sf_code).max() >= (1 << 62) // n_cat):
+            raise ValueError("sf_id out of range")
+    else:
+        sf_code, sf_levels = pd.factorize(sf, sort=True)
+        sf_code = sf_code.astype(np.int64)
+    key = sf_code * n_cat + codes
+    peak_i = sf_peak_df["peak_i"].to_numpy().astype(np.int64)
+    mz = sf_peak_df["mz"].to_numpy().astype(np.float64)
+    n_rows = len(key)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+    with torch.cuda.stream(stream) if stream is not None else _nullctx():
+        if n_rows == 0:
+            z = torch.zeros(1, dtype=torch.int64, device=device)
+            e = torch.zeros(0, dtype=torch.int64, device=device)
+            ions = DeviceIons(win_off=z, peak_mz=torch.zeros(0, dtype=torch.float64, device=device), theor=None,
+                              win_order=e, ion_order=e, n_ions=0, n_windows=0, max_k=0)
+            return IonKeys(np.zeros(0, np.int64), cats, sf_levels), ions, e
+        key_d, pk_d, mz_d = t(key), t(peak_i), t(mz)
+        uniq, inv = torch.unique(key_d, sorted=True, return_inverse=True)
+        n_ions = uniq.numel()
+        K = torch.zeros(n_ions, dtype=torch.int64, device=device)
+        K.scatter_reduce_(0, inv, pk_d + 1, reduce="amax", include_self=True)
+        win_off = torch.zeros(n_ions + 1, dtype=torch.int64, device=device)
+        torch.cumsum(K, 0, out=win_off[1:])
+        slot = win_off[inv] + pk_d
+        # one synchronisation for the sizes and the first check: windows, smallest peak_i, largest K
+        n_win, pk_min, kmax = (int(v) for v in torch.stack([win_off[-1], pk_d.min(), K.max()]).cpu().tolist())
+        if pk_min < 0:
+            raise ValueError("negative peak_i in sf_peak_df")
+        per_slot = torch.bincount(slot, minlength=n_win)
+        peak_mz = torch.full((n_win,), -1.0, dtype=torch.float64, device=device)
+        peak_mz.scatter_(0, slot, mz_d)
+        if n_win == n_rows:
+            win_order = slot  # rows come in m/z order (get_sf_peak_df sorts by mz): the search's locality order
+        else:
+            win_order = torch.cat([slot, torch.nonzero(per_slot == 0).flatten()])
+        first = peak_mz[win_off[:-1]]
+        first = torch.where(first < 0, torch.full_like(first, float("inf")), first)
+        ion_order = torch.sort(first, stable=True).indices
+        keys = uniq.cpu().numpy()
+        if int(per_slot.max().item()) > 1:
+            raise AssertionError("duplicate (sf_id, adduct, peak_i) rows in sf_peak_df")
+    ions = DeviceIons(win_off=win_off, peak_mz=peak_mz, theor=None, win_order=win_order, ion_order=ion_order,
+                      n_ions=n_ions, n_windows=n_win, max_k=kmax)
+    return IonKeys(keys, cats, sf_levels, keys_dev=uniq), ions, K
+
+
 class IonImageSet:
     """Device-resident ``RDD[((sf_id, adduct), [coo | None, ...])]``."""
 
-    def __init__(self, peaks, keys, win_off, peak_i_max, lo, hi, dims, ions_dev, ppm=None):
+    def __init__(self, peaks, ion_keys: IonKeys, ions_dev, K, lo, hi, dims, ppm=None):
         self.peaks = peaks              # DevicePeaks (sorted)
-        self.ppm = ppm                  # the ppm of the duplicate flags and windows
-        self.peaks_version = peaks.version if peaks is not None else 0
-        self.keys = keys                # list[(sf_id, adduct)] ion-major
-        self.win_off = win_off          # np.int64[n_ion+1]
-        self.peak_i_max = peak_i_max    # np.int64[n_ion]: number of windows per ion
+        self.ion_keys = ion_keys        # IonKeys: ion i = (sf_id, adduct), (sf_id, adduct) order
+        self.ions_dev = ions_dev        # engine.DeviceIons: win_off, window m/z, ion_order (principal m/z)
+        self.K = K                      # device int64[n_ion]: windows per ion (max(peak_i) + 1)
         self.lo = lo                    # device int64[n_win]
         self.hi = hi
         self.dims = dims
-        self.ions_dev = ions_dev        # engine.DeviceIons (theor filled later)
+        self.ppm = ppm                  # the ppm of the duplicate flags and windows
+        self.peaks_version = peaks.version if peaks is not None else 0
+        self._has_dev = None
         self._has = None
+        self._win_counts = None
+        self._win_off = None
         self._sel = None                # optional ion subset (filter_by_keys)
 
-    # ---- bookkeeping -------------------------------------------------------------------------
+    @property
+    def n_ions(self):
+        return len(self.ion_keys)
+
+    @property
+    def keys(self):
+        """list[(sf_id, adduct)] in ion order (built on first use)."""
+        return self.ion_keys.tuples()
+
+    @property
+    def win_off(self):
+        if self._win_off is None:
+            self._win_off = self.ions_dev.win_off.cpu().numpy()
+        return self._win_off
+
     def ensure_current(self):
         """Restore the sorted peaks this set was built on if another compute_sf_images (another ppm) re-flagged
         and re-sorted them since: the duplicate-candidate flags must be those of this set's windows.  The sort is
@@ -51,16 +236,22 @@ class IonImageSet:
             self.peaks_version = p.version
         return self
 
+    # ---- bookkeeping -------------------------------------------------------------------------
+    def has_images_device(self):
+        """device bool[n_ion]: the ion has >= 1 window with >= 1 point (it appears in the RDD)."""
+        import torch
+        if self._has_dev is None:
+            n = self.n_ions
+            owner = torch.repeat_interleave(torch.arange(n, device=self.lo.device), self.K)
+            cnt = torch.zeros(n, dtype=torch.int64, device=self.lo.device)
+            cnt.index_add_(0, owner, ((self.hi - self.lo) > 0).to(torch.int64))
+            self._has_dev = cnt > 0
+        return self._has_dev
+
     def _counts(self):
         if self._has is None:
-            cnt = (self.hi - self.lo).cpu().numpy()
-            self._win_counts = cnt
-            has = np.zeros(len(self.keys), dtype=bool)
-            nz = np.nonzero(cnt)[0]
-            if nz.size:
-                owner = np.searchsorted(self.win_off, nz, side="right") - 1
-                has[owner] = True
-            self._has = has
+            self._win_counts = (self.hi - self.lo).cpu().numpy()
+            self._has = self.has_images_device().cpu().numpy()
         return self._win_counts, self._has
 
     def ion_indices(self):
@@ -72,12 +263,16 @@ class IonImageSet:
 
     def filter_by_keys(self, index) -> "IonImageSet":
         """Keep ions whose key is in ``index`` without materialising anything (filter_sf_images)."""
-        keep = set(index)
-        sel = np.array([k in keep for k in self.keys], dtype=bool)
-        out = IonImageSet(self.peaks, self.keys, self.win_off, self.peak_i_max, self.lo, self.hi, self.dims,
-                          self.ions_dev, self.ppm)
+        if isinstance(index, pd.MultiIndex) and index.nlevels == 2:
+            k, ok = self.ion_keys.encode(index.get_level_values(0).to_numpy(), index.get_level_values(1))
+            sel = np.isin(self.ion_keys.keys, k[ok])
+        else:
+            keep = set(index)
+            sel = np.array([t in keep for t in self.keys], dtype=bool)
+        out = IonImageSet(self.peaks, self.ion_keys, self.ions_dev, self.K, self.lo, self.hi, self.dims, self.ppm)
         out.peaks_version = self.peaks_version
-        out._has, out._win_counts = self._has, getattr(self, "_win_counts", None)
+        out._has_dev, out._has, out._win_counts, out._win_off = self._has_dev, self._has, self._win_counts, \
+            self._win_off
         out._sel = sel if self._sel is None else (sel & self._sel)
         return out
 
@@ -88,10 +283,12 @@ class IonImageSet:
         cnt, _ = self._counts()
         self.ensure_current()
         nrows, ncols = self.dims
-        wins = [np.arange(self.win_off[i], self.win_off[i + 1]) for i in ion_idx]
-        if not wins:
+        win_off = self.win_off
+        ion_idx = np.asarray(ion_idx, dtype=np.int64)
+        if ion_idx.size == 0:
             return []
-        w = np.concatenate(wins)
+        Kp = win_off[ion_idx + 1] - win_off[ion_idx]
+        w = np.repeat(win_off[ion_idx], Kp) + np.arange(Kp.sum()) - np.repeat(np.cumsum(Kp) - Kp, Kp)
         c = cnt[w]
         total = int(c.sum())
         out_hits = np.zeros(0, np.uint64)
@@ -106,12 +303,13 @@ class IonImageSet:
             out_hits = self.peaks.hits_sorted[idx].cpu().numpy().view(np.uint64)
         pix = (out_hits & np.uint64(0x7FFFFFFF)).astype(np.int64)
         val = (out_hits >> np.uint64(32)).astype(np.uint32).view(np.float32).astype(np.float64)
+        keys = self.keys
         res = []
         pos = 0
         wpos = 0
-        for i, ws in zip(ion_idx, wins):
+        for i, k in zip(ion_idx.tolist(), Kp.tolist()):
             imgs = []
-            for _ in ws:
+            for _ in range(k):
                 n = int(c[wpos])
                 if n:
                     p = pix[pos:pos + n]
@@ -121,7 +319,7 @@ class IonImageSet:
                 pos += n
                 wpos += 1
             last = max((j for j, m in enumerate(imgs) if m is not None), default=-1)
-            res.append((self.keys[i], imgs[:last + 1]))
+            res.append((keys[i], imgs[:last + 1]))
         return res
 
     def _items(self):
@@ -153,7 +351,8 @@ class IonImageSet:
         f(iter(self._items()))
 
     def keys_with_images(self):
-        return [self.keys[i] for i in self.ion_indices()]
+        keys = self.keys
+        return [keys[i] for i in self.ion_indices()]
 
     def cache(self):
         return self
@@ -162,54 +361,41 @@ class IonImageSet:
         return iter(self._items())
 
 
-def ion_layout(sf_peak_df: pd.DataFrame, sf_peak_ints: dict | None = None):
-    """Ion-major window table from FormulasSegm.get_sf_peak_df rows (sf_id, adduct, peak_i, mz).
+_SIDE = {}
 
-    Returns keys, win_off, peak_mz (window m/z, NaN for padding windows), theor ints (or NaN).
-    An ion gets max(peak_i)+1 windows, or len(sf_ints) if larger (formula_img_validator.py:73-75 padding).
-    """
-    df = sf_peak_df[["sf_id", "adduct", "peak_i", "mz"]]
-    keys_arr = list(zip(df.sf_id.tolist(), df.adduct.tolist()))
-    codes, uniq = pd.factorize(pd.Series(keys_arr, dtype=object), sort=False)
-    order = sorted(range(len(uniq)), key=lambda j: (uniq[j][0], str(uniq[j][1])))
-    remap = np.empty(len(uniq), np.int64)
-    remap[order] = np.arange(len(uniq))
-    ion = remap[codes]
-    keys = [tuple(uniq[j]) for j in order]
-    pk = df.peak_i.to_numpy().astype(np.int64)
-    K = np.zeros(len(keys), np.int64)
-    np.maximum.at(K, ion, pk + 1)
-    if sf_peak_ints is not None:
-        K = np.maximum(K, np.array([len(sf_peak_ints[k]) for k in keys], dtype=np.int64))
-    win_off = np.zeros(len(keys) + 1, np.int64)
-    np.cumsum(K, out=win_off[1:])
-    peak_mz = np.full(int(win_off[-1]), np.nan)
-    slot = win_off[ion] + pk
-    if len(np.unique(slot)) != len(slot):
-        raise AssertionError("duplicate (sf_id, adduct, peak_i) rows in sf_peak_df")
-    peak_mz[slot] = df.mz.to_numpy(np.float64)
-    theor = np.full(int(win_off[-1]), np.nan)
-    if sf_peak_ints is not None:
-        for i, k in enumerate(keys):
-            v = sf_peak_ints[k]
-            theor[win_off[i]:win_off[i] + len(v)] = v
-    return keys, win_off, peak_mz, theor
+
+def _side_stream(device):
+    import torch
+    key = str(device)
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=device)
+    return _SIDE[key]
 
 
 def compute_sf_images(sc, ds, sf_peak_df, ppm):
-    """formula_imager_segm.py:142-161.  ``sc`` is accepted for signature compatibility and ignored."""
-    from .engine import DeviceIons, DevicePeaks, window_bounds
+    """formula_imager_segm.py:142-161.  ``sc`` is accepted for signature compatibility and ignored.
+
+    Device order: the resident peaks are flagged, sorted and prefix-summed on the current stream while the
+    ion layout is uploaded and built on a side stream; the window search joins both."""
+    import torch
+
     from .dataset import spectra_from_duck
+    from .engine import DevicePeaks, window_bounds
     if hasattr(ds, "device_peaks"):
         peaks = ds.device_peaks()
     else:
         off, mz, it = spectra_from_duck(ds)
         peaks = DevicePeaks.from_arrays(off, mz, it, np.asarray(ds.norm_img_pixel_inds), ds.get_dims())
+    main = torch.cuda.current_stream(peaks.device)
+    side = _side_stream(peaks.device)
+    side.wait_stream(main)  # the side stream may reuse memory the main stream released
     peaks.flag_duplicates(ppm)
     peaks.sort()
-    keys, win_off, peak_mz, _ = ion_layout(sf_peak_df)
-    # padding windows (NaN m/z) must stay empty: give them an m/z no point can match
-    pm = np.where(np.isnan(peak_mz), -1.0, peak_mz)
-    dions = DeviceIons.from_arrays(win_off, pm, np.zeros_like(pm), device=peaks.device)
+    peaks.prefix_sums()
+    keys, dions, K = device_layout(sf_peak_df, peaks.device, side)
+    main.wait_stream(side)
+    for t in (dions.win_off, dions.peak_mz, dions.win_order, dions.ion_order, K, keys.keys_dev):
+        if t is not None:
+            t.record_stream(main)
     lo, hi = window_bounds(peaks, dions, ppm)
-    return IonImageSet(peaks, keys, win_off, np.diff(win_off), lo, hi, ds.get_dims(), dions, ppm)
+    return IonImageSet(peaks, keys, dions, K, lo, hi, ds.get_dims(), ppm)

@@ -102,60 +102,107 @@ def sf_image_metrics(sf_images, sc, formulas, ds, ds_config):
     return _frame([r[0] for r in rows], [r[1] for r in rows], [r[2] for r in rows], [r[3] for r in rows])
 
 
-def _metrics_device_batch(ims, sf_ints, img_conf):
-    """Score every ion of an IonImageSet with one fused launch (rows only for ions with images)."""
+def _theor_arrays(ims, sf_ints, device):
+    """Theoretical intensities aligned with the ions of ``ims``: device (Kt int64[n_ion], values f64[sum Kt])
+    with Kt = len(sf_ints[key]).  A PeakInts mapping (FormulasSegm) is aligned on the device by key search; any
+    other mapping is read key by key."""
+    import torch
+
+    from .formulas import PeakInts
+    ik = ims.ion_keys
+    n = len(ik)
+    if isinstance(sf_ints, PeakInts):
+        cache = sf_ints.__dict__.setdefault("_dev_cache", {})
+        sig = (str(device), tuple(ik.adducts), None if ik.sf_levels is None else id(ik.sf_levels))
+        if sig not in cache:
+            k, ok = ik.encode_codes(sf_ints.sf_ids, sf_ints.adduct_codes, sf_ints.adducts)
+            rows = np.nonzero(ok)[0]
+            k = k[rows]
+            if len(k) > 1 and not (k[1:] > k[:-1]).all():
+                o = np.argsort(k, kind="stable")
+                k, rows = k[o], rows[o]
+            t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+            cache.clear()
+            cache[sig] = (t(k), t(rows), t(np.asarray(sf_ints.off, np.int64)), t(np.asarray(sf_ints.values, np.float64)))
+        pk_key, pk_row, pk_off, pk_val = cache[sig]
+        ion_key = ik.keys_dev if ik.keys_dev is not None else torch.from_numpy(ik.keys).to(device)
+        if n == 0:
+            return torch.zeros(0, dtype=torch.int64, device=device), torch.zeros(0, dtype=torch.float64, device=device)
+        if pk_key.numel() == 0:
+            raise KeyError(ims.keys[0])
+        j = torch.searchsorted(pk_key, ion_key).clamp_(max=pk_key.numel() - 1)
+        miss = pk_key[j] != ion_key
+        if bool(miss.any().item()):  # formula_img_validator.py:117: sf_peak_ints[(sf_id, adduct)] raises
+            raise KeyError(ims.keys[int(torch.nonzero(miss)[0].item())])
+        row = pk_row[j]
+        Kt = pk_off[row + 1] - pk_off[row]
+        off_t = torch.zeros(n + 1, dtype=torch.int64, device=device)
+        torch.cumsum(Kt, 0, out=off_t[1:])
+        n_t = int(off_t[-1].item())
+        owner = torch.repeat_interleave(torch.arange(n, device=device), Kt, output_size=n_t)
+        k_in = torch.arange(n_t, device=device) - off_t[owner]
+        return Kt, pk_val[pk_off[row][owner] + k_in]
+    vals = [sf_ints[k] for k in ims.keys]
+    Kt = np.array([len(v) for v in vals], dtype=np.int64)
+    flat = np.concatenate([np.asarray(v, np.float64) for v in vals]) if n else np.zeros(0)
+    return torch.from_numpy(Kt).to(device), torch.from_numpy(flat).to(device)
+
+
+def _metrics_device_rows(ims, sf_ints, img_conf):
+    """Score every ion of an IonImageSet with one fused launch; returns (device bool[n_ion]: the ion gets a row,
+    engine.IonMetrics).
+
+    The kernel sees exactly len(sf_ints[key]) windows per ion: compute() pads the image list with empty images
+    up to that length (formula_img_validator.py:73-75), and windows of sf_peak_df beyond it do not enter the
+    metrics.  The alignment runs on the side stream (it needs only the layout, not the sorted peaks)."""
     import torch
 
     from . import engine as E
     from ._lib import SMG_HITS_PACKED_F32
+    from .formula_imager_segm import _side_stream
     opts = _chaos_opts(img_conf)
     ims.ensure_current()
-    keys = ims.keys
-    K = np.diff(ims.win_off)
-    need = np.array([len(sf_ints[k]) for k in keys], dtype=np.int64)
-    if np.any(need > K):
-        # theoretical patterns longer than the windows of sf_peak_df: re-layout with empty padding windows
-        lo = ims.lo.cpu().numpy()
-        hi = ims.hi.cpu().numpy()
-        Kn = np.maximum(K, need)
-        off = np.zeros(len(keys) + 1, np.int64)
-        np.cumsum(Kn, out=off[1:])
-        nlo = np.zeros(off[-1], np.int64)
-        nhi = np.zeros(off[-1], np.int64)
-        for i in range(len(keys)):
-            a, b = ims.win_off[i], ims.win_off[i + 1]
-            nlo[off[i]:off[i] + (b - a)] = lo[a:b]
-            nhi[off[i]:off[i] + (b - a)] = hi[a:b]
-        win_off = off
-        dev = ims.lo.device
-        lo_d, hi_d = torch.from_numpy(nlo).to(dev), torch.from_numpy(nhi).to(dev)
-    else:
-        win_off, lo_d, hi_d = ims.win_off, ims.lo, ims.hi
-        Kn = K
-    theor = np.zeros(int(win_off[-1]))
-    for i, k in enumerate(keys):
-        v = sf_ints[k]
-        theor[win_off[i]:win_off[i] + len(v)] = v
-    # windows beyond len(sf_ints) (sf_peak_df longer than the pattern) keep theor 0 -- the reference would
-    # use len(sf_ints) images only; trim them by giving the kernel exactly len(sf_ints) windows
-    if np.any(need < Kn):
-        sel = np.concatenate([np.arange(win_off[i], win_off[i] + need[i]) for i in range(len(keys))])
-        off2 = np.zeros(len(keys) + 1, np.int64)
-        np.cumsum(need, out=off2[1:])
-        dev = ims.lo.device
-        st = torch.from_numpy(sel).to(dev)
-        lo_d, hi_d, theor, win_off = lo_d[st], hi_d[st], theor[sel], off2
     dev = ims.lo.device
-    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)
+    n = ims.n_ions
+    main = torch.cuda.current_stream(dev)
+    side = _side_stream(dev)
+    with torch.cuda.stream(side):
+        Kt, theor = _theor_arrays(ims, sf_ints, dev)
+        K_img = ims.K
+        win_off_img = ims.ions_dev.win_off
+        n_t = theor.numel()
+        off_t = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(Kt, 0, out=off_t[1:])
+        owner = torch.repeat_interleave(torch.arange(n, device=dev), Kt, output_size=n_t)
+        k_in = torch.arange(n_t, device=dev) - off_t[owner]
+        valid = k_in < K_img[owner]
+        src = win_off_img[owner] + torch.minimum(k_in, (K_img[owner] - 1).clamp_(min=0))
+        sel_dev = None if ims._sel is None else torch.from_numpy(ims._sel).to(dev)
+    main.wait_stream(side)
+    for t in (Kt, theor, off_t, valid, src) + ((sel_dev,) if sel_dev is not None else ()):
+        t.record_stream(main)
+    has = ims.has_images_device()  # reads lo / hi: on the main stream, after the window search
+    zero = torch.zeros((), dtype=torch.int64, device=dev)
+    lo2 = torch.where(valid, ims.lo[src], zero)
+    hi2 = torch.where(valid, ims.hi[src], zero)
     nrows, ncols = ims.dims
-    m = E.ion_metrics_raw(SMG_HITS_PACKED_F32, ims.peaks.hits_sorted, None, ims.peaks.sorted_cum(), lo_d, hi_d,
-                          t(win_off, np.int64),
-                          t(theor, np.float64), ims.ions_dev.ion_order, len(keys), nrows, ncols, **opts)
-    r = m.to_numpy()
-    has = (r["flags"] & 1) != 0
-    sel = ims.ion_indices()
-    sel = sel[has[sel]]
-    return _frame([keys[i] for i in sel], r["chaos"][sel], r["spatial"][sel], r["spectral"][sel])
+    m = E.ion_metrics_raw(SMG_HITS_PACKED_F32, ims.peaks.hits_sorted, None, ims.peaks.sorted_cum(), lo2, hi2,
+                          off_t, theor, ims.ions_dev.ion_order, n, nrows, ncols, **opts)
+    keep = has & ((m.flags & 1) != 0)
+    if sel_dev is not None:
+        keep &= sel_dev
+    return keep, m
+
+
+def _metrics_device_batch(ims, sf_ints, img_conf):
+    """The reference table (index [sf_id, adduct], columns chaos, spatial, spectral, msm) of an IonImageSet:
+    one row per ion with images (formula_img_validator.py:115-121), built from codes, not tuples."""
+    import torch
+    keep, m = _metrics_device_rows(ims, sf_ints, img_conf)
+    idx = torch.nonzero(keep).flatten()
+    vals = torch.stack([m.chaos[idx], m.spatial[idx], m.spectral[idx], m.msm[idx]], 1).cpu().numpy()
+    idx = idx.cpu().numpy()
+    return pd.DataFrame(vals, index=ims.ion_keys.multi_index(idx), columns=["chaos", "spatial", "spectral", "msm"])
 
 
 def sf_image_metrics_est_fdr(sf_metrics_df, formulas, fdr):

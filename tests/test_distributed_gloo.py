@@ -1,6 +1,9 @@
-"""N>1 path on CPU: world_size-2 gloo ranks shard the ions, score their shard, all-gather the fixed-size
-metric rows; rank 0 must rebuild exactly the single-process table.  (On the GPU the same code runs over
-RCCL with the device scorer; here the oracle stands in for the scorer.)"""
+"""The multi-GPU product path on CPU ranks: world_size-2 (and 3) gloo process groups run
+``distributed.plan_shards`` / ``score_sharded`` / ``search`` -- the same code the GPU ranks run over RCCL --
+with the per-rank scorer replaced by the oracle (there is no device path on CPU).  The oracle scorer images
+each rank's ions from the points of the rank's m/z slice only, so the test also proves the slice bounds hold
+every window.  Rank 0 must rebuild exactly the single-process table, and ``search`` must give the
+single-process annotations (msm_basic_search.py:13-31)."""
 import os
 import socket
 
@@ -20,36 +23,59 @@ def _free_port():
     return p
 
 
+def _case():
+    from sm_distributed_amd.formulas import FormulasSegm
+    from tests.parity_cases import make_case
+    ds, ions, ppm, kw = make_case("basic")
+    return ds, ions, ppm, FormulasSegm.from_ion_table(ions, ppm)
+
+
+def _oracle_scorer(ds):
+    """score_local for CPU ranks: the oracle on the rank's m/z slice, rows in the device scorer's format."""
+    from oracle import msm_oracle as O
+    from tests.parity_cases import sf_peak_ints
+
+    def score(plan, peaks, ds_config):
+        pm, dims = ds.pixel_map_dims()
+        sp = np.repeat(np.arange(ds.n_spectra), np.diff(ds.sp_off))
+        m64 = ds.mz.astype(np.float64)
+        sel = (m64 >= plan.mz_lo) & (m64 <= plan.mz_hi)  # the rank's slice (smg_slice_mz semantics)
+        spectra = [(int(s), ds.mz[sel & (sp == s)], ds.ints[sel & (sp == s)].astype(np.float64))
+                   for s in range(ds.n_spectra)]
+        shard = plan.formulas
+        imgs = O.compute_sf_images(spectra, pm, dims, shard.get_sf_peak_df(), plan.ppm)
+        ints = shard.get_sf_peak_ints()
+        rows = np.full((len(plan.ion_idx), 5), -1.0)
+        keys = list(zip(shard.ion_sf.tolist(), np.asarray(shard.adducts, dtype=object)[shard.ion_adduct_code].tolist()))
+        for i, key in enumerate(keys):
+            if key in imgs:
+                c, s, p = O.compute_img_metrics(imgs[key], ints[key], dims[0], dims[1],
+                                                ds_config["image_generation"]["nlevels"])
+                rows[i] = (plan.ion_idx[i], c, s, p, c * s * p)
+        return torch.from_numpy(rows), None
+    return score
+
+
 def _worker(rank, world, port, out_path):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from oracle import msm_oracle as O
         from sm_distributed_amd import distributed as D
-        from sm_distributed_amd.engine import IonMetrics
-        from tests.parity_cases import make_case, sf_peak_df, sf_peak_ints, subset_ions
-        ds, ions, ppm, kw = make_case("basic")
-        costs = D.ion_costs(ions.win_off, ions.peak_mz)
-        a, b = D.shard_bounds(costs, world)[rank]
-        shard = subset_ions(ions, np.arange(a, b))
-        pm, dims = ds.pixel_map_dims()
-        imgs = O.compute_sf_images(ds.spectra(), pm, dims, sf_peak_df(shard), ppm)
-        ints = sf_peak_ints(shard)
-        n = shard.n_ions
-        vals = np.zeros((n, 5))
-        for i, key in enumerate(zip(shard.sf_ids.tolist(), shard.adducts.tolist())):
-            if key in imgs:
-                c, s, p = O.compute_img_metrics(imgs[key], ints[key], dims[0], dims[1], 30)
-                vals[i] = (c, s, p, c * s * p, 1)
-        t = lambda j: torch.tensor(vals[:, j])
-        m = IonMetrics(t(0), t(1), t(2), t(3), torch.tensor(vals[:, 4].astype(np.int32)))
-        counts = D.exchange_counts(n, "cpu")
-        rows = D.pack_rows(m, max(counts), device="cpu")
-        table = D.gather_rows(rows, counts)
+        from sm_distributed_amd.fdr import FDR
+        ds, ions, ppm, formulas = _case()
+        conf = {"image_generation": {"ppm": ppm, "nlevels": 30, "q": 99, "do_preprocessing": False}}
+        plan = D.plan_shards(formulas, torch.from_numpy(ds.mz), ppm, world, rank)
+        scorer = _oracle_scorer(ds)
+        df, _ = D.score_sharded(plan, None, conf, score_local=scorer)
+        fdr = FDR(0, 0, ions.decoy_sample_size, list(ions.target_adducts))
+        sf, ta, da = ions.td
+        fdr.td_df = pd.DataFrame({"sf_id": sf, "ta": ta, "da": da})
+        res, _ = D.search(plan, None, formulas, fdr, conf, score_local=scorer)
         if rank == 0:
-            keys = list(zip(ions.sf_ids.tolist(), ions.adducts.tolist()))
-            D.rows_to_frame(table, keys).to_pickle(out_path)
+            pd.to_pickle({"table": df, "search": res, "counts": plan.counts}, out_path)
+        else:
+            assert df is None and res is None
     finally:
         dist.destroy_process_group()
 
@@ -64,16 +90,49 @@ def test_shard_bounds_balanced():
     assert max(sums) / min(sums) < 1.1
 
 
-def test_two_rank_gather_matches_single_process(tmp_path):
+def test_plan_shards_partitions_ions_and_slices_cover_windows():
+    from sm_distributed_amd import distributed as D
+    from sm_distributed_amd import synthetic as syn
+    from sm_distributed_amd.formulas import FormulasSegm
+    ions = syn.make_ion_table(2000, seed=5, decoy_seed=6)
+    formulas = FormulasSegm.from_ion_table(ions)
+    mz = torch.from_numpy(np.random.default_rng(1).uniform(100, 1000, 200000).astype(np.float32))
+    for world in (2, 4, 8):
+        plans = [D.plan_shards(formulas, mz, 2.0, world, r) for r in range(world)]
+        allidx = np.concatenate([p.ion_idx for p in plans])
+        assert np.array_equal(np.sort(allidx), np.arange(formulas.n_ions))
+        for p in plans:
+            pm = p.formulas.peak_mz
+            assert (pm - pm * 2e-6 >= p.mz_lo).all() and (pm + pm * 2e-6 <= p.mz_hi).all()
+        cost = plans[0].est_cost
+        assert max(cost) / min(cost) < 1.05, cost
+        # contiguous in principal m/z: slices overlap only by the isotope tails (< 6 Da)
+        lo = sorted((p.mz_lo, p.mz_hi) for p in plans)
+        assert all(lo[i + 1][0] > lo[i][0] for i in range(world - 1))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_search_matches_single_process(tmp_path, world):
     from oracle import msm_oracle as O
-    from tests.parity_cases import make_case, oracle_run
+    from tests.parity_cases import oracle_run
     out = str(tmp_path / "rank0.pkl")
-    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     got = pd.read_pickle(out)
-    ds, ions, ppm, kw = make_case("basic")
+    ds, ions, ppm, formulas = _case()
     _, exp = oracle_run(ds, ions, ppm)
-    got = got.sort_index()
+    table = got["table"]
+    assert list(table.index) == sorted(exp.index.tolist())  # (sf_id, adduct) order, as the single-GPU table
     exp = exp.sort_index()
-    assert got.index.equals(exp.index)
     for c in ("chaos", "spatial", "spectral", "msm"):
-        np.testing.assert_allclose(got[c].values, exp[c].values, atol=1e-12)
+        np.testing.assert_array_equal(table[c].values, exp[c].values)
+    assert min(got["counts"]) > 0
+    # search: FDR + filter on rank 0 == the single-process pipeline
+    sf, ta, da = ions.td
+    td = pd.DataFrame({"sf_id": sf, "ta": ta, "da": da})
+    msm = formulas.get_sf_adduct_sorted_df().join(exp.msm).fillna(0)
+    ofdr = O.estimate_fdr(msm, td, list(ions.target_adducts), ions.decoy_sample_size)
+    e = exp.join(ofdr, how="inner")[["chaos", "spatial", "spectral", "msm", "fdr"]]
+    e = e[(e.chaos > 0) | (e.spatial > 0) | (e.spectral > 0)].sort_index()
+    r = got["search"].sort_index()
+    assert list(r.index) == list(e.index)
+    np.testing.assert_array_equal(r.fdr.values, e.fdr.values)

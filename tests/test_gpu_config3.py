@@ -11,46 +11,12 @@ scored / unscored status identical, chaos / spatial / spectral / msm within 1e-5
 properties cover the rest: the sort is a permutation of the resident points and every scored ion has a
 window with points.
 """
-import os
-
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 METRIC_ATOL = 1e-5
-
-
-def _select_windows(mz, hits, lower, upper, block=1 << 27):
-    """Points of the resident dataset whose m/z lies in the union of [lower, upper] (f64, widened by 1e-6
-    relative so f32 rounding cannot drop a point); returns host (pix, mz, int)."""
-    import torch
-    lo = np.asarray(lower) * (1 - 1e-6)
-    hi = np.asarray(upper) * (1 + 1e-6)
-    order = np.argsort(lo)
-    lo, hi = lo[order], hi[order]
-    ms, me = [lo[0]], [hi[0]]  # merge overlapping intervals
-    for a, b in zip(lo[1:], hi[1:]):
-        if a <= me[-1]:
-            me[-1] = max(me[-1], b)
-        else:
-            ms.append(a)
-            me.append(b)
-    dev = mz.device
-    A = torch.tensor(ms, dtype=torch.float64, device=dev)
-    B = torch.tensor(me, dtype=torch.float64, device=dev)
-    pm, ph = [], []
-    for a in range(0, mz.numel(), block):
-        x = mz[a:a + block].to(torch.float64)
-        j = torch.searchsorted(A, x, right=True) - 1
-        inside = (j >= 0) & (x <= B[j.clamp(min=0)])
-        pm.append(mz[a:a + block][inside].cpu().numpy())
-        ph.append(hits[a:a + block][inside].cpu().numpy())
-    b_mz = np.concatenate(pm)
-    b_hits = np.concatenate(ph).view(np.uint64)
-    b_pix = (b_hits & np.uint64(0x7FFFFFFF)).astype(np.int64)
-    b_int = (b_hits >> np.uint64(32)).astype(np.uint32).view(np.float32)
-    return b_pix, b_mz, b_int
 
 
 @pytest.mark.timeout(600)
@@ -93,7 +59,7 @@ def test_config3_full_size_sample_matches_oracle():
     assert first.min() < 250 and first.max() > 850, "sample must span the m/z range"
     wins = np.concatenate([np.arange(ions.win_off[i], ions.win_off[i + 1]) for i in pick])
     lower, upper = O.window_bounds(ions.peak_mz[wins], ppm)
-    b_pix, b_mz, b_int = _select_windows(peaks.mz, peaks.hits, lower, upper)
+    b_pix, b_mz, b_int = CB.select_window_points(peaks.mz, peaks.hits, lower, upper)
     del peaks, mz, hits, lo, hi, m
     for k in list(E._ws_cache):
         E._ws_cache.pop(k)

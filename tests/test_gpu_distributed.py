@@ -1,0 +1,101 @@
+"""The multi-GPU path's device pieces on one GPU (GPU only): the m/z slice of the resident peaks
+(smg_slice_mz_count / _copy, flags fused into the copy) and the per-rank scorer of distributed.score_sharded.
+The world-size > 1 collectives run in tests/test_distributed_gloo.py (CPU ranks); here every rank's shard is
+scored in turn on the one GPU and the union must equal the single-GPU table, and a world-size-1 RCCL group
+runs score_sharded end to end."""
+import socket
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from tests.parity_cases import make_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["dups", "basic", "zeros_rect"])
+def test_slice_equals_masked_flagged_points(name):
+    import torch
+    from sm_distributed_amd import engine as E
+    ds, ions, ppm, kw = make_case(name)
+    pm, dims = ds.pixel_map_dims()
+    full = E.DevicePeaks.from_arrays(ds.sp_off, ds.mz, ds.ints, pm, dims)
+    full.flag_duplicates(ppm)
+    mz = full.mz.cpu().numpy()
+    hits = full.hits.cpu().numpy()
+    sp = np.repeat(np.arange(ds.n_spectra), np.diff(ds.sp_off))
+    rng = np.random.default_rng(5)
+    for lo, hi in [(mz.min(), mz.max()), (300.0, 301.5), tuple(np.sort(rng.uniform(100, 1000, 2))), (2000.0, 3000.0)]:
+        sl = full.slice_mz(float(lo), float(hi), ppm)
+        sel = (mz.astype(np.float64) >= lo) & (mz.astype(np.float64) <= hi)
+        np.testing.assert_array_equal(sl.mz.cpu().numpy(), mz[sel])
+        np.testing.assert_array_equal(sl.hits.cpu().numpy(), hits[sel])  # same duplicate flags as the full pass
+        off = sl.sp_off.cpu().numpy()
+        np.testing.assert_array_equal(np.diff(off), np.bincount(sp[sel], minlength=ds.n_spectra))
+        assert sl.flag_duplicates(ppm).flags_preset_ppm == ppm  # no second flag pass
+    torch.cuda.synchronize()
+
+
+def _api_table(peaks, formulas, ppm):
+    from sm_distributed_amd.dataset import ResidentDataset
+    from sm_distributed_amd.formula_imager_segm import compute_sf_images
+    from sm_distributed_amd.formula_img_validator import sf_image_metrics
+    dds = ResidentDataset(peaks)
+    conf = {"image_generation": {"ppm": ppm, "nlevels": 30, "q": 99, "do_preprocessing": False}}
+    ims = compute_sf_images(None, dds, formulas.get_sf_peak_df(), ppm)
+    return sf_image_metrics(ims, None, formulas, dds, conf)
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_every_rank_shard_on_one_gpu_equals_single_gpu_table(world):
+    from sm_distributed_amd import distributed as D
+    from sm_distributed_amd import engine as E
+    from sm_distributed_amd.formulas import FormulasSegm
+    from tests.parity_cases import oracle_run
+    ds, ions, ppm, kw = make_case("dups")
+    pm, dims = ds.pixel_map_dims()
+    peaks = E.DevicePeaks.from_arrays(ds.sp_off, ds.mz, ds.ints, pm, dims)
+    formulas = FormulasSegm.from_ion_table(ions, ppm)
+    conf = {"image_generation": {"ppm": ppm, "nlevels": 30, "q": 99, "do_preprocessing": False}}
+    rows = []
+    for r in range(world):
+        plan = D.plan_shards(formulas, peaks, ppm, world, r)
+        rr, _ = D._device_rows(plan, peaks, conf)
+        rows.append(rr.cpu())
+    import torch
+    df = D.rows_to_frame(torch.cat(rows), D.plan_shards(formulas, peaks, ppm, world, 0).global_keys)
+    ref = _api_table(peaks, formulas, ppm)
+    assert list(df.index) == list(ref.index)
+    for c in ("chaos", "spatial", "spectral", "msm"):
+        np.testing.assert_allclose(df[c].values, ref[c].values, rtol=0, atol=1e-12)
+    _, exp = oracle_run(ds, ions, ppm)
+    exp = exp.sort_index()
+    assert list(df.index) == list(exp.index)
+    for c in ("chaos", "spatial", "spectral", "msm"):
+        assert np.abs(df[c].values - exp[c].values).max() <= 1e-5
+
+
+def test_score_sharded_world1_rccl():
+    import torch.distributed as dist
+    from sm_distributed_amd import distributed as D
+    from sm_distributed_amd import engine as E
+    from sm_distributed_amd.formulas import FormulasSegm
+    ds, ions, ppm, kw = make_case("basic")
+    pm, dims = ds.pixel_map_dims()
+    peaks = E.DevicePeaks.from_arrays(ds.sp_off, ds.mz, ds.ints, pm, dims)
+    formulas = FormulasSegm.from_ion_table(ions, ppm)
+    conf = {"image_generation": {"ppm": ppm, "nlevels": 30, "q": 99, "do_preprocessing": False}}
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        plan = D.plan_shards(formulas, peaks, ppm, 1, 0)
+        df, ims = D.score_sharded(plan, peaks, conf)
+        ref = _api_table(peaks, formulas, ppm)
+        pd.testing.assert_frame_equal(df, ref, check_exact=False, rtol=0, atol=1e-12)
+        assert sorted(k for k, _ in ims.collect()) == sorted(ref.index.tolist())
+    finally:
+        dist.destroy_process_group()
