@@ -144,8 +144,10 @@ class DevicePeaks:
         n = int(off[-1].item())
         mz = torch.empty(n, dtype=torch.float32, device=self.device)
         hits = torch.empty(n, dtype=torch.int64, device=self.device)
-        check(lib().smg_slice_mz_copy(_p(self.sp_off), n_sp, _p(self.mz), _p(self.hits), _p(off), float(ppm),
-                                      _p(self.force), _p(mz), _p(hits), _p(ws), _stream(stream)), "smg_slice_mz_copy")
+        if n:
+            check(lib().smg_slice_mz_copy(_p(self.sp_off), n_sp, _p(self.mz), _p(self.hits), _p(off), float(ppm),
+                                          _p(self.force), _p(mz), _p(hits), _p(ws), _stream(stream)),
+                  "smg_slice_mz_copy")
         out = DevicePeaks(mz=mz, hits=hits, nrows=self.nrows, ncols=self.ncols, sp_off=off, force=self.force)
         out.flags_preset_ppm = float(ppm)
         out._sorted = True
