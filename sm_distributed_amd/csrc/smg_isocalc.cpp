@@ -78,6 +78,62 @@ const std::vector<Element>& table() {
       {"Br", {{78.9183371, 0.5069}, {80.9162906, 0.4931}}},
       {"I", {{126.904473, 1.0}}},
       {"Au", {{196.9665687, 1.0}}},
+      // the remaining decoy-adduct elements of fdr.py:8 (NIST isotope masses, IUPAC representative abundances)
+      {"Be", {{9.0121822, 1.0}}},
+      {"Ne", {{19.9924401754, 0.9048}, {20.99384668, 0.0027}, {21.991385114, 0.0925}}},
+      {"Ar", {{35.967545106, 0.003365}, {37.9627324, 0.000632}, {39.9623831225, 0.996003}}},
+      {"Sc", {{44.9559119, 1.0}}},
+      {"Ti", {{45.9526316, 0.0825}, {46.9517631, 0.0744}, {47.9479463, 0.7372}, {48.94787, 0.0541}, {49.9447912, 0.0518}}},
+      {"V", {{49.9471585, 0.0025}, {50.9439595, 0.9975}}},
+      {"Cr", {{49.9460442, 0.04345}, {51.9405075, 0.83789}, {52.9406494, 0.09501}, {53.9388804, 0.02365}}},
+      {"Ga", {{68.9255736, 0.60108}, {70.9247013, 0.39892}}},
+      {"Ge", {{69.9242474, 0.2038}, {71.9220758, 0.2731}, {72.9234589, 0.0776}, {73.9211778, 0.3672}, {75.9214026, 0.0783}}},
+      {"Kr", {{77.9203648, 0.00355}, {79.916379, 0.02286}, {81.9134836, 0.11593}, {82.914136, 0.115}, {83.911507, 0.56987}, {85.91061073, 0.17279}}},
+      {"Rb", {{84.911789738, 0.7217}, {86.909180527, 0.2783}}},
+      {"Sr", {{83.913425, 0.0056}, {85.9092602, 0.0986}, {86.9088771, 0.07}, {87.9056121, 0.8258}}},
+      {"Y", {{88.9058483, 1.0}}},
+      {"Zr", {{89.9047044, 0.5145}, {90.9056458, 0.1122}, {91.9050408, 0.1715}, {93.9063152, 0.1738}, {95.9082734, 0.028}}},
+      {"Nb", {{92.9063781, 1.0}}},
+      {"Mo", {{91.906811, 0.1477}, {93.9050883, 0.0923}, {94.9058421, 0.159}, {95.9046795, 0.1668}, {96.9060215, 0.0956}, {97.9054082, 0.2419}, {99.907477, 0.0967}}},
+      {"Ru", {{95.907598, 0.0554}, {97.905287, 0.0187}, {98.9059393, 0.1276}, {99.9042195, 0.126}, {100.9055821, 0.1706}, {101.9043493, 0.3155}, {103.905433, 0.1862}}},
+      {"Rh", {{102.905504, 1.0}}},
+      {"Pd", {{101.905609, 0.0102}, {103.904036, 0.1114}, {104.905085, 0.2233}, {105.903486, 0.2733}, {107.903892, 0.2646}, {109.905153, 0.1172}}},
+      {"Ag", {{106.905097, 0.51839}, {108.904752, 0.48161}}},
+      {"Cd", {{105.906459, 0.0125}, {107.904184, 0.0089}, {109.9030021, 0.1249}, {110.9041781, 0.128}, {111.9027578, 0.2413}, {112.9044017, 0.1222}, {113.9033585, 0.2873}, {115.904756, 0.0749}}},
+      {"In", {{112.904058, 0.0429}, {114.903878, 0.9571}}},
+      {"Sn", {{111.904818, 0.0097}, {113.902779, 0.0066}, {114.903342, 0.0034}, {115.901741, 0.1454}, {116.902952, 0.0768}, {117.901603, 0.2422}, {118.903308, 0.0859}, {119.9021947, 0.3258}, {121.903439, 0.0463}, {123.9052739, 0.0579}}},
+      {"Sb", {{120.9038157, 0.5721}, {122.904214, 0.4279}}},
+      {"Te", {{119.90402, 0.0009}, {121.9030439, 0.0255}, {122.90427, 0.0089}, {123.9028179, 0.0474}, {124.9044307, 0.0707}, {125.9033117, 0.1884}, {127.9044631, 0.3174}, {129.9062244, 0.3408}}},
+      {"Xe", {{123.905893, 0.000952}, {125.904274, 0.00089}, {127.9035313, 0.019102}, {128.9047794, 0.264006}, {129.903508, 0.04071}, {130.9050824, 0.212324}, {131.9041535, 0.269086}, {133.9053945, 0.104357}, {135.907219, 0.088573}}},
+      {"Cs", {{132.905451933, 1.0}}},
+      {"Ba", {{129.9063208, 0.00106}, {131.9050613, 0.00101}, {133.9045084, 0.02417}, {134.9056886, 0.06592}, {135.9045759, 0.07854}, {136.9058274, 0.11232}, {137.9052472, 0.71698}}},
+      {"La", {{137.907112, 0.0009}, {138.9063533, 0.9991}}},
+      {"Ce", {{135.907172, 0.00185}, {137.905991, 0.00251}, {139.9054387, 0.8845}, {141.909244, 0.11114}}},
+      {"Pr", {{140.9076528, 1.0}}},
+      {"Nd", {{141.9077233, 0.272}, {142.9098143, 0.122}, {143.9100873, 0.238}, {144.9125736, 0.083}, {145.9131169, 0.172}, {147.916893, 0.057}, {149.920891, 0.056}}},
+      {"Sm", {{143.911999, 0.0307}, {146.9148979, 0.1499}, {147.9148227, 0.1124}, {148.9171847, 0.1382}, {149.9172755, 0.0738}, {151.9197324, 0.2675}, {153.9222093, 0.2275}}},
+      {"Eu", {{150.9198502, 0.4781}, {152.9212303, 0.5219}}},
+      {"Gd", {{151.919791, 0.002}, {153.9208656, 0.0218}, {154.922622, 0.148}, {155.9221227, 0.2047}, {156.9239601, 0.1565}, {157.9241039, 0.2484}, {159.9270541, 0.2186}}},
+      {"Tb", {{158.9253468, 1.0}}},
+      {"Dy", {{155.924283, 0.00056}, {157.924409, 0.00095}, {159.9251975, 0.02329}, {160.9269334, 0.18889}, {161.9267984, 0.25475}, {162.9287312, 0.24896}, {163.9291748, 0.2826}}},
+      {"Ho", {{164.9303221, 1.0}}},
+      {"Er", {{161.928778, 0.00139}, {163.9292, 0.01601}, {165.9302931, 0.33503}, {166.9320482, 0.22869}, {167.9323702, 0.26978}, {169.935464, 0.1491}}},
+      {"Tm", {{168.9342133, 1.0}}},
+      {"Yb", {{167.933897, 0.0013}, {169.9347618, 0.0304}, {170.9363258, 0.1428}, {171.9363815, 0.2183}, {172.9382108, 0.1613}, {173.9388621, 0.3183}, {175.9425717, 0.1276}}},
+      {"Lu", {{174.9407718, 0.9741}, {175.9426863, 0.0259}}},
+      {"Hf", {{173.940046, 0.0016}, {175.9414086, 0.0526}, {176.9432207, 0.186}, {177.9436988, 0.2728}, {178.9458161, 0.1362}, {179.94655, 0.3508}}},
+      {"Ta", {{179.9474648, 0.00012}, {180.9479958, 0.99988}}},
+      {"W", {{179.946704, 0.0012}, {181.9482042, 0.265}, {182.950223, 0.1431}, {183.9509312, 0.3064}, {185.9543641, 0.2843}}},
+      {"Re", {{184.952955, 0.374}, {186.9557531, 0.626}}},
+      {"Os", {{183.9524891, 0.0002}, {185.9538382, 0.0159}, {186.9557505, 0.0196}, {187.9558382, 0.1324}, {188.9581475, 0.1615}, {189.958447, 0.2626}, {191.9614807, 0.4078}}},
+      {"Ir", {{190.960594, 0.373}, {192.9629264, 0.627}}},
+      {"Pt", {{189.959932, 0.00014}, {191.961038, 0.00782}, {193.9626803, 0.32967}, {194.9647911, 0.33832}, {195.9649515, 0.25242}, {197.967893, 0.07163}}},
+      {"Hg", {{195.965833, 0.0015}, {197.966769, 0.0997}, {198.9682799, 0.1687}, {199.968326, 0.231}, {200.9703023, 0.1318}, {201.970643, 0.2986}, {203.9734939, 0.0687}}},
+      {"Tl", {{202.9723442, 0.2952}, {204.9744275, 0.7048}}},
+      {"Pb", {{203.9730436, 0.014}, {205.9744653, 0.241}, {206.9758969, 0.221}, {207.9766521, 0.524}}},
+      {"Bi", {{208.9803987, 1.0}}},
+      {"Th", {{232.0380553, 1.0}}},
+      {"U", {{234.0409521, 5.4e-05}, {235.0439299, 0.007204}, {238.0507882, 0.992742}}},
   };
   return t;
 }

@@ -153,10 +153,14 @@ def _device_rows(plan, peaks, ds_config):
     dds = ResidentDataset(sl)
     ims = compute_sf_images(None, dds, plan.sf_peak_df, plan.ppm)
     keep, m = _metrics_device_rows(ims, plan.formulas.get_sf_peak_ints(), ds_config["image_generation"])
-    # the image set's ions are the shard's ions in the same (sf_id, adduct) order; map by key to be exact
-    skeys = plan.global_keys.keys[plan.ion_idx]
-    pos = np.searchsorted(skeys, ims.ion_keys.keys)
-    glob = torch.from_numpy(plan.ion_idx[pos].astype(np.float64)).to(dev)
+    # global ion index of each image-set ion: re-encode its (sf_id, adduct) with the whole table's adduct codes
+    # (the shard's sf_peak_df may lack some adducts, so its own codes differ)
+    ik = ims.ion_keys
+    gk, ok = plan.global_keys.encode_codes(ik.sf_values(), ik.adduct_code, ik.adducts)
+    pos = np.searchsorted(plan.global_keys.keys, gk)
+    if not ok.all() or not (plan.global_keys.keys[np.minimum(pos, len(plan.global_keys.keys) - 1)] == gk).all():
+        raise AssertionError("shard ion missing from the formula table")
+    glob = torch.from_numpy(pos.astype(np.float64)).to(dev)
     k = len(pos)
     rows[:k, 0] = torch.where(keep, glob, torch.full_like(glob, -1.0))
     rows[:k, 1] = m.chaos

@@ -3,7 +3,8 @@
 The Postgres/Spark storage itself is out of scope; these generators produce the exact rows the reference
 inserts so a storage backend can consume them:
 
-* ``metrics_rows`` (:57-62): (job_id, db_id, sf_id, adduct, msm, fdr, json{chaos, spatial, spectral}, peaks_n)
+* ``metrics_rows`` (:57-62): (job_id, db_id, sf_id, adduct, msm, fdr, json{chaos, spatial, spectral}, peaks_n),
+  peaks_n positional as in the reference (or by key, a documented opt-in deviation)
 * ``iso_image_rows`` (:88-97): per (ion, peak) with any pixel > 0.001: (job_id, db_id, sf_id, adduct, peak,
   flattened pixel indices, intensities, min over the full image, max over the full image)
 """
@@ -15,11 +16,21 @@ from collections import OrderedDict
 import numpy as np
 
 
-def metrics_rows(job_id, db_id, sf_metrics_df, sf_adduct_peaksn, metrics=("chaos", "spatial", "spectral")):
-    peaksn = {(s, a): n for s, a, n in sf_adduct_peaksn}
-    for _, r in sf_metrics_df.reset_index().iterrows():
+def metrics_rows(job_id, db_id, sf_metrics_df, sf_adduct_peaksn, metrics=("chaos", "spatial", "spectral"),
+                 peaks_n="positional"):
+    """search_results.py:57-62.  ``peaks_n="positional"`` reproduces the reference exactly: row ``ind`` of the
+    metrics table takes ``sf_adduct_peaksn[ind][2]``, the peak count of the ``ind``-th (sf_id, adduct) of the
+    formula table -- which is the row's own count only when the two tables list the same ions in the same order
+    (the metrics table is filtered to reported targets, so in a real search it usually is not).
+    ``peaks_n="by_key"`` (documented deviation) looks the count up by the row's (sf_id, adduct) instead."""
+    if peaks_n not in ("positional", "by_key"):
+        raise ValueError("peaks_n must be 'positional' or 'by_key'")
+    peaksn = list(sf_adduct_peaksn)
+    by_key = {(s, a): n for s, a, n in peaksn} if peaks_n == "by_key" else None
+    for ind, r in sf_metrics_df.reset_index().iterrows():
         metr_json = json.dumps(OrderedDict([(m, float(r[m])) for m in metrics]))
-        yield (job_id, db_id, r.sf_id, r.adduct, float(r.msm), float(r.fdr), metr_json, peaksn[(r.sf_id, r.adduct)])
+        n = peaksn[ind][2] if by_key is None else by_key[(r.sf_id, r.adduct)]
+        yield (job_id, db_id, r.sf_id, r.adduct, float(r.msm), float(r.fdr), metr_json, n)
 
 
 def iso_image_rows(job_id, db_id, sf_iso_images, nrows, ncols):
