@@ -172,7 +172,9 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
         n_win, pk_min, kmax = (int(v) for v in torch.stack([win_off[-1], pk_d.min(), K.max()]).cpu().tolist())
         if pk_min < 0:
             raise ValueError("negative peak_i in sf_peak_df")
-        per_slot = torch.bincount(slot, minlength=n_win)
+        # rows per window (atomic adds; torch.bincount runs a slow histogram kernel on ROCm)
+        per_slot = torch.zeros(n_win, dtype=torch.int32, device=device)
+        per_slot.index_add_(0, slot, torch.ones(1, dtype=torch.int32, device=device).expand(n_rows))
         peak_mz = torch.full((n_win,), -1.0, dtype=torch.float64, device=device)
         peak_mz.scatter_(0, slot, mz_d)
         if n_win == n_rows:
