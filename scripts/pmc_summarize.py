@@ -10,7 +10,7 @@ for r in rows:
     m = re.search(r"ion_pipe_kernel<[^,]*, (\d+)", name)
     if m:
         short = "smg::ion_pipe_kernel[" + m.group(1) + "]"
-    if not any(k in name for k in ("smg::", "copy", "rocprim")):
+    if not any(k in name for k in ("smg::", "rocprim")):
         continue
     acc[(short[:60], r["Counter_Name"])].append(float(r["Counter_Value"]))
 for (k, c), v in sorted(acc.items()):

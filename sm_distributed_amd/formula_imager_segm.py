@@ -103,10 +103,11 @@ class IonKeys:
 
 
 def _adduct_codes(col):
-    """(int64 codes, sorted category strings) of an adduct column, Categorical or not."""
+    """(integer codes -- int8/16/32 straight from a Categorical, no copy --, sorted category strings) of an
+    adduct column; a non-Categorical column is factorized (slow path: hashes every string)."""
     if isinstance(col.dtype, pd.CategoricalDtype):
         cats = [str(c) for c in col.cat.categories]
-        codes = col.cat.codes.to_numpy().astype(np.int64)
+        codes = col.cat.codes.to_numpy()
         order = np.argsort(np.array(cats, dtype=object), kind="stable")
         if not (order == np.arange(len(cats))).all():
             rank = np.empty(len(cats), np.int64)
@@ -116,8 +117,6 @@ def _adduct_codes(col):
     else:
         codes, uniq = pd.factorize(col.to_numpy(dtype=object), sort=True)
         cats = [str(u) for u in uniq]
-    if len(codes) and codes.min() < 0:
-        raise ValueError("sf_peak_df has missing adducts")
     return codes, cats
 
 
@@ -137,21 +136,19 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
     import torch
 
     from .engine import DeviceIons
+    # the four columns go to the device as they are (no host-side arithmetic: zero-copy views of int64 / f64 /
+    # Categorical-code columns), and the ion key is formed there
     sf = sf_peak_df["sf_id"].to_numpy()
     codes, cats = _adduct_codes(sf_peak_df["adduct"])
     n_cat = max(len(cats), 1)
     sf_levels = None
-    if sf.dtype.kind in "iu":
-        sf_code = sf.astype(np.int64)
-        if len(sf_code) and (np.abs(sf_code).max() >= (1 << 62) // n_cat):
-            raise ValueError("sf_id out of range")
-    else:
-        sf_code, sf_levels = pd.factorize(sf, sort=True)
-        sf_code = sf_code.astype(np.int64)
-    key = sf_code * n_cat + codes
-    peak_i = sf_peak_df["peak_i"].to_numpy().astype(np.int64)
-    mz = sf_peak_df["mz"].to_numpy().astype(np.float64)
-    n_rows = len(key)
+    if sf.dtype.kind not in "iu":
+        sf, sf_levels = pd.factorize(sf, sort=True)
+    peak_i = sf_peak_df["peak_i"].to_numpy()
+    mz = sf_peak_df["mz"].to_numpy()
+    if peak_i.dtype.kind not in "iu" or mz.dtype != np.float64:
+        peak_i, mz = peak_i.astype(np.int64), mz.astype(np.float64)
+    n_rows = len(sf)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
     with torch.cuda.stream(stream) if stream is not None else _nullctx():
         if n_rows == 0:
@@ -160,7 +157,16 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
             ions = DeviceIons(win_off=z, peak_mz=torch.zeros(0, dtype=torch.float64, device=device), theor=None,
                               win_order=e, ion_order=e, n_ions=0, n_windows=0, max_k=0)
             return IonKeys(np.zeros(0, np.int64), cats, sf_levels), ions, e
-        key_d, pk_d, mz_d = t(key), t(peak_i), t(mz)
+        sf_d, code_d, pk_d, mz_d = t(sf).long(), t(codes).long(), t(peak_i).long(), t(mz)
+        key_d = sf_d * n_cat + code_d
+        # one synchronisation for the checks: sf range, missing adducts, negative peak_i
+        lims = torch.stack([sf_d.abs().max(), code_d.min(), pk_d.min()]).cpu().tolist()
+        if lims[0] >= (1 << 62) // n_cat:
+            raise ValueError("sf_id out of range")
+        if lims[1] < 0:
+            raise ValueError("sf_peak_df has missing adducts")
+        if lims[2] < 0:
+            raise ValueError("negative peak_i in sf_peak_df")
         uniq, inv = torch.unique(key_d, sorted=True, return_inverse=True)
         n_ions = uniq.numel()
         K = torch.zeros(n_ions, dtype=torch.int64, device=device)
@@ -168,10 +174,7 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
         win_off = torch.zeros(n_ions + 1, dtype=torch.int64, device=device)
         torch.cumsum(K, 0, out=win_off[1:])
         slot = win_off[inv] + pk_d
-        # one synchronisation for the sizes and the first check: windows, smallest peak_i, largest K
-        n_win, pk_min, kmax = (int(v) for v in torch.stack([win_off[-1], pk_d.min(), K.max()]).cpu().tolist())
-        if pk_min < 0:
-            raise ValueError("negative peak_i in sf_peak_df")
+        n_win, kmax = (int(v) for v in torch.stack([win_off[-1], K.max()]).cpu().tolist())
         # rows per window (atomic adds; torch.bincount runs a slow histogram kernel on ROCm)
         per_slot = torch.zeros(n_win, dtype=torch.int32, device=device)
         per_slot.index_add_(0, slot, torch.ones(1, dtype=torch.int32, device=device).expand(n_rows))
@@ -243,11 +246,11 @@ class IonImageSet:
         """device bool[n_ion]: the ion has >= 1 window with >= 1 point (it appears in the RDD)."""
         import torch
         if self._has_dev is None:
-            n = self.n_ions
-            owner = torch.repeat_interleave(torch.arange(n, device=self.lo.device), self.K)
-            cnt = torch.zeros(n, dtype=torch.int64, device=self.lo.device)
-            cnt.index_add_(0, owner, ((self.hi - self.lo) > 0).to(torch.int64))
-            self._has_dev = cnt > 0
+            # windows of an ion are contiguous: count non-empty windows per ion by prefix differences (no sync)
+            c = torch.zeros(self.lo.numel() + 1, dtype=torch.int64, device=self.lo.device)
+            torch.cumsum(((self.hi - self.lo) > 0).to(torch.int64), 0, out=c[1:])
+            off = self.ions_dev.win_off
+            self._has_dev = (c[off[1:]] - c[off[:-1]]) > 0
         return self._has_dev
 
     def _counts(self):
