@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--nlevels", type=int, default=30)
     ap.add_argument("--plant-fraction", type=float, default=0.02)
     ap.add_argument("--chain-steps", type=int, default=5, help="timed steps of the device-chain leg (0: skip)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="run the multi-GPU (sharded, RCCL) step even at N = 1 (a check of that path on one GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target wall of the CPU baseline sample")
     ap.add_argument("--cpu-workers", type=int, default=16,
@@ -84,8 +86,11 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+    sharded = world > 1 or args.sharded
+    if sharded:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("nccl", device_id=device, rank=rank, world_size=world)
 
     t_setup = time.perf_counter()
     ions = syn.make_ion_table(args.n_sf, seed=43, decoy_seed=44)
@@ -94,7 +99,7 @@ def main():
     peaks = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
     formulas = FormulasSegm.from_ion_table(ions, args.ppm)
     ds_config = {"image_generation": {"ppm": args.ppm, "nlevels": args.nlevels, "q": 99, "do_preprocessing": False}}
-    if world > 1:
+    if sharded:
         plan = D.plan_shards(formulas, peaks, args.ppm, world, rank)
         step_fn = lambda: D.score_sharded(plan, peaks, ds_config)[0]
         my_formulas = plan.formulas
@@ -118,20 +123,20 @@ def main():
     torch.cuda.synchronize()
     L.smg_debug_main_pass_times(None, 0, ctypes.byref(ctypes.c_int32(0)))  # discard
     L.smg_debug_time_main_pass(1)
-    if world > 1:
+    if sharded:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         df = step_fn()
     torch.cuda.synchronize()
-    if world > 1:
+    if sharded:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     L.smg_debug_time_main_pass(0)
     main_ms = _main_pass_times(L)
     n_rows = len(df) if df is not None else 0
-    if world > 1:
+    if sharded:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -180,7 +185,8 @@ def main():
                 "n_points": info["n_points"], "n_ions": formulas.n_ions, "n_rows_per_step": n_rows,
                 "n_windows": int(formulas.ion_off[-1]), "sum_window_points": sum_hits,
                 "parallelism": (f"formula shards by principal m/z x{world}, dataset replicated, per-rank m/z slice, "
-                                f"RCCL all-gather of metric rows" if world > 1 else "1 GPU"),
+                                f"RCCL all-gather of metric rows" if sharded else "1 GPU"),
+                "shard_est_cost_s": plan.est_cost if plan is not None else None,
             },
             "device_chain": chain,
             "roofline": roofline,
@@ -188,7 +194,7 @@ def main():
             "lib": _lib.version(),
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if sharded:
         dist.destroy_process_group()
 
 

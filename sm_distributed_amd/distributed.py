@@ -185,13 +185,22 @@ def gather_rows(rows, plan, group=None):
 
 def rows_to_frame(table, global_keys):
     """Rank-0 assembly: gathered rows -> the reference DataFrame (index [sf_id, adduct] in table order,
-    columns chaos, spatial, spectral, msm), one row per ion with images."""
-    t = table.cpu().numpy() if hasattr(table, "cpu") else np.asarray(table)
-    t = t[t[:, 0] >= 0]
-    idx = t[:, 0].astype(np.int64)
-    o = np.argsort(idx, kind="stable")
-    idx, t = idx[o], t[o]
-    return pd.DataFrame(t[:, 1:5], index=global_keys.multi_index(idx), columns=["chaos", "spatial", "spectral", "msm"])
+    columns chaos, spatial, spectral, msm), one row per ion with images.  The rows are put in table order by a
+    scatter on the device holding them (no sort), then copied to the host once, column-major."""
+    import torch
+    t = table if hasattr(table, "device") else torch.as_tensor(np.asarray(table))
+    n = len(global_keys)
+    valid = t[:, 0] >= 0
+    sel = t[valid]
+    gi = sel[:, 0].long()
+    full = torch.zeros(4, n, dtype=t.dtype, device=t.device)
+    full[:, gi] = sel[:, 1:5].T
+    has = torch.zeros(n, dtype=torch.bool, device=t.device)
+    has[gi] = True
+    idx = torch.nonzero(has).flatten()
+    cols = full[:, idx].cpu().numpy()
+    return pd.DataFrame(cols.T, index=global_keys.multi_index(idx.cpu().numpy()),
+                        columns=["chaos", "spatial", "spectral", "msm"], copy=False)
 
 
 def score_sharded(plan, peaks, ds_config, group=None, score_local=None):

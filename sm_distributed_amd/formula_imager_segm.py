@@ -32,13 +32,14 @@ class IonKeys:
     ``sf_code`` is the sf_id itself for integer ids (``sf_levels`` None), else its position in the sorted
     ``sf_levels``; ``adducts`` are the sorted adduct strings."""
 
-    def __init__(self, keys: np.ndarray, adducts, sf_levels=None, keys_dev=None):
+    def __init__(self, keys: np.ndarray, adducts, sf_levels=None, keys_dev=None, codes=None):
         self.keys = keys
         self.keys_dev = keys_dev  # the same keys in HBM (device_layout keeps them)
         self.adducts = list(adducts)
         self.sf_levels = sf_levels
         self.n_cat = max(len(self.adducts), 1)
         self._tuples = None
+        self._codes = codes       # (sf level values, sf code, adduct code) per ion, for multi_index
 
     def __len__(self):
         return len(self.keys)
@@ -86,20 +87,26 @@ class IonKeys:
             ok = (code >= 0) & (sfc >= 0)
         return np.where(ok, sfc * self.n_cat + code, -1), ok
 
+    def level_codes(self):
+        """(sf level values, int32 sf codes, int16 adduct codes) of every ion: the MultiIndex levels/codes."""
+        if self._codes is None:
+            sfc = self.keys // self.n_cat
+            adc = (self.keys - sfc * self.n_cat).astype(np.int16)
+            if self.sf_levels is None:
+                new = np.ones(len(sfc), bool)
+                new[1:] = sfc[1:] != sfc[:-1]  # keys sorted -> sf codes nondecreasing
+                self._codes = (sfc[new], (np.cumsum(new) - 1).astype(np.int32), adc)
+            else:
+                self._codes = (np.asarray(self.sf_levels), sfc.astype(np.int32), adc)
+        return self._codes
+
     def multi_index(self, idx):
-        """pd.MultiIndex [sf_id, adduct] of the ions ``idx`` (ascending positions), built from codes."""
-        k = self.keys[idx]
-        sfc = k // self.n_cat
-        adc = (k % self.n_cat).astype(np.int64)
-        if self.sf_levels is None:
-            new = np.ones(len(sfc), bool)
-            new[1:] = sfc[1:] != sfc[:-1]  # idx ascending -> sf codes nondecreasing
-            sf_lv = sfc[new]
-            sf_codes = np.cumsum(new) - 1
-        else:
-            sf_lv, sf_codes = np.asarray(self.sf_levels), sfc
+        """pd.MultiIndex [sf_id, adduct] of the ions ``idx`` (ascending positions), built from codes (two
+        gathers; the levels are those of the whole layout)."""
+        sf_lv, sf_codes, ad_codes = self.level_codes()
         return pd.MultiIndex(levels=[pd.Index(sf_lv), pd.Index(self.adducts, dtype=object)],
-                             codes=[sf_codes, adc], names=["sf_id", "adduct"], verify_integrity=False)
+                             codes=[sf_codes[idx], ad_codes[idx]], names=["sf_id", "adduct"],
+                             verify_integrity=False)
 
 
 def _adduct_codes(col):
@@ -187,12 +194,22 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
         first = peak_mz[win_off[:-1]]
         first = torch.where(first < 0, torch.full_like(first, float("inf")), first)
         ion_order = torch.sort(first, stable=True).indices
+        # MultiIndex codes of every ion, formed on the device (keys sorted: sf codes nondecreasing)
+        sfc = torch.div(uniq, n_cat, rounding_mode="floor")
+        adc = (uniq - sfc * n_cat).to(torch.int16)
+        new = torch.ones(n_ions, dtype=torch.bool, device=device)
+        new[1:] = sfc[1:] != sfc[:-1]
+        sf_code = (torch.cumsum(new.to(torch.int32), 0, dtype=torch.int32) - 1)
+        if sf_levels is None:
+            codes = (sfc[new].cpu().numpy(), sf_code.cpu().numpy(), adc.cpu().numpy())
+        else:
+            codes = (np.asarray(sf_levels), sfc.to(torch.int32).cpu().numpy(), adc.cpu().numpy())
         keys = uniq.cpu().numpy()
         if int(per_slot.max().item()) > 1:
             raise AssertionError("duplicate (sf_id, adduct, peak_i) rows in sf_peak_df")
     ions = DeviceIons(win_off=win_off, peak_mz=peak_mz, theor=None, win_order=win_order, ion_order=ion_order,
                       n_ions=n_ions, n_windows=n_win, max_k=kmax)
-    return IonKeys(keys, cats, sf_levels, keys_dev=uniq), ions, K
+    return IonKeys(keys, cats, sf_levels, keys_dev=uniq, codes=codes), ions, K
 
 
 class IonImageSet:

@@ -200,9 +200,11 @@ def _metrics_device_batch(ims, sf_ints, img_conf):
     import torch
     keep, m = _metrics_device_rows(ims, sf_ints, img_conf)
     idx = torch.nonzero(keep).flatten()
-    vals = torch.stack([m.chaos[idx], m.spatial[idx], m.spectral[idx], m.msm[idx]], 1).cpu().numpy()
+    # one device->host copy of the four columns, column-major: the DataFrame wraps it without a copy
+    cols = torch.stack([m.chaos[idx], m.spatial[idx], m.spectral[idx], m.msm[idx]], 0).cpu().numpy()
     idx = idx.cpu().numpy()
-    return pd.DataFrame(vals, index=ims.ion_keys.multi_index(idx), columns=["chaos", "spatial", "spectral", "msm"])
+    return pd.DataFrame(cols.T, index=ims.ion_keys.multi_index(idx), columns=["chaos", "spatial", "spectral", "msm"],
+                        copy=False)
 
 
 def sf_image_metrics_est_fdr(sf_metrics_df, formulas, fdr):
