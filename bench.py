@@ -69,6 +69,10 @@ def log(*a):
 
 def main():
     args = parse()
+    # the JSON line is the only thing on stdout: libraries that print at start-up (RCCL's version banner at
+    # communicator creation) write to fd 1 directly, so fd 1 points at stderr until the line is printed
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -193,7 +197,7 @@ def main():
             "cpu_baseline": cpu,
             "lib": _lib.version(),
         }
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     if sharded:
         dist.destroy_process_group()
 
