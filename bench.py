@@ -273,11 +273,13 @@ def measured_traffic():
     scripts/gpu_traffic.sh: FETCH_SIZE calibrated for the kernel's access width, + WRITE_SIZE).  The counters
     cannot be read from inside this process; None when no summary exists."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic_*.json")), key=os.path.getmtime)
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    return float(d["traffic_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic_*.json")))
+    best = None
+    for f in files:  # profiles/round<N>/..., newest round last; only summaries of the main ion kernel
+        d = json.load(open(f))
+        if d.get("kernel") == "ion_pipe_kernel[512]":
+            best = (float(d["traffic_bytes_per_launch"]), os.path.relpath(f, ROOT))
+    return best if best else (None, None)
 
 
 def cpu_baseline(args, ions, peaks, dims):
