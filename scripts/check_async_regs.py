@@ -1,6 +1,6 @@
 """Static check of the async-load discipline in the LDS kernel's ISA (hipcc -S output).
 
-For every inline-asm global_load into v[a:b], every control-flow path from the load (following s_branch /
+For every inline-asm global_load (or returning global_atomic) into v[a:b], every control-flow path from the load (following s_branch /
 s_cbranch_* targets and fall-through) must reach a counted wait (inline-asm s_waitcnt) or a full vmcnt(0)
 drain before any other instruction reads or writes v[a..b]; the only exception is another inline-asm load
 into the same registers (its "+v" operand keeps them allocated).  Spills are covered: a scratch_store of such
@@ -38,7 +38,8 @@ for st in [i for i, l in enumerate(src) if l.startswith(kern)]:
     labels = {l[:-1]: i for i, l in enumerate(body) if re.match(r"^\.LBB\w+:$", l)}
     dsts = set()
     for i, l in enumerate(body):
-        if not (in_asm[i] and l.startswith("global_load")):
+        # async loads and the async returning atomic (scheduling ticket): both write their first operand later
+        if not (in_asm[i] and (l.startswith("global_load") or (l.startswith("global_atomic") and " sc0" in l))):
             continue
         total += 1
         dst = regs(l.split()[1].rstrip(","))
@@ -58,7 +59,7 @@ for st in [i for i, l in enumerate(src) if l.startswith(kern)]:
                 touched = set()
                 for x in toks[1:]:
                     touched |= regs(x)
-                if touched & dst and not (in_asm[j] and t.startswith("global_load")):
+                if touched & dst and not (in_asm[j] and t.startswith(("global_load", "global_atomic"))):
                     hit = (j, t)
                     break
                 op = toks[0]

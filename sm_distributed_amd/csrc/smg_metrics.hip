@@ -146,6 +146,17 @@ __device__ __forceinline__ void vm_wait1(uint64_t& r) {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
   asm volatile("" : "+v"(r));
 }
+template <int N>
+__device__ __forceinline__ void vm_wait1(uint32_t& r) {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  asm volatile("" : "+v"(r));
+}
+// Returning atomic add issued like the async loads: the compiler would wait for its result with
+// s_waitcnt vmcnt(0) right away -- i.e. for every prefetch load of the wave in flight -- so it is waited
+// for with a counted vm_wait1 where the ticket is consumed.
+__device__ __forceinline__ void atomic_add_rtn_async(uint32_t& r, uint32_t* addr, uint32_t v) {
+  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "+v"(r) : "v"(addr), "v"(v) : "memory");
+}
 template <int N, int M>
 __device__ __forceinline__ void vm_wait(uint64_t (&r)[M]) {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -580,6 +591,12 @@ __device__ __forceinline__ uint32_t sched_issue(const Sched& S) {
   if constexpr (SRC == SRC_RANGES) return atomicAdd(&S.ctr[(blockIdx.x % XCDS) * CTR_STRIDE], 1u);
   else return atomicAdd(S.ctr, 1u);
 }
+// the same ticket, asynchronously (see atomic_add_rtn_async); valid after the counted wait
+template <int SRC>
+__device__ __forceinline__ void sched_issue_async(const Sched& S, uint32_t& t) {
+  if constexpr (SRC == SRC_RANGES) atomic_add_rtn_async(t, &S.ctr[(blockIdx.x % XCDS) * CTR_STRIDE], 1u);
+  else atomic_add_rtn_async(t, S.ctr, 1u);
+}
 
 // resolves a ticket of sched_issue into a position (-1: no work left)
 template <int SRC>
@@ -799,8 +816,14 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   while (true) {
     const IonDesc* D = &dsl[cur];
     IonDesc* DN = &dsl[cur ^ 1];
+    // the ticket of the ion after npos: issued now, consumed after phase 1 (wave 0 issues after it exactly one
+    // descriptor load, and the 2*RC loads of tail chunks 2 and 3 unless this iteration skips)
     uint32_t ticket = 0;
-    if (tid == 0) ticket = sched_issue<SRC>(S);
+    if constexpr (ASYNC) {
+      if (tid == 0) sched_issue_async<SRC>(S, ticket);
+    } else {
+      if (tid == 0) ticket = sched_issue<SRC>(S);
+    }
     // npos's descriptor: one async word per lane of wave 0 (exactly one load per lane, clamped), waited in
     // phase 2 behind the 2*RC loads of tail chunks 2 and 3
     uint64_t dword = 0;
@@ -904,6 +927,12 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     if (!skip) {  // the principal registers are consumed: tail chunks 2 and 3 go in flight
       issue_chunk(D, 2, pc);
       issue_chunk(D, 3, pd);
+    }
+    if constexpr (ASYNC) {
+      if (wid == 0) {  // counted waits are per wave: wave 0 waits, lane 0 uses the ticket
+        if (skip) vm_wait1<1>(ticket);
+        else vm_wait1<1 + 2 * RC>(ticket);
+      }
     }
     if (tid == 0) ctr[C_NEXT] = (int)sched_resolve<SRC>(S, ticket);
     __syncthreads();
