@@ -637,7 +637,7 @@ __device__ __forceinline__ bool desc_lds_ok(const IonDesc* D, int capc) {
 //      zero their slot, then add atomically); ion b+1 resolved and its descriptor fetched
 //   2  one fused reduction: sum x, sum x^2, sum x[x>0], #(x>0), max; level index per pixel
 //   5  tail windows as one stream of 64-point groups (each group in one window; a wave sees windows in
-//      increasing order, keeps running sums for its current window and flushes them when it moves on),
+//      increasing order; principal hits add into its LDS partials of the current window),
 //      chunks of BLOCK*RC points, two register buffers, next chunk in flight; duplicate-candidate points
 //      deferred to an LDS list.  Then the loads of ion b+1 are issued
 //   d  deferred duplicates summed per (pixel, window) in an LDS table, squared into the partials
@@ -1002,22 +1002,16 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       // Window sums of y and y^2 come from the prefix sums (descriptor); the stream only joins the tail against
       // the principal image (sum xy, sum y[x>0]: nonzero for the few points whose pixel is in the principal
       // image) and collects duplicate-candidate points.
-      double psk = 0.0, psxy = 0.0;
       int curk = 1;
       int nd = 0;  // this wave's deferred duplicate candidates (uniform)
       uint32_t* wdkey = dkey + wid * DSEG;
       double* wdval = dval + wid * DSEG;
       int gnext = uni(D->gs[2]);
       int wend = uni(D->end[1]);
-      auto flush = [&]() {
-        const double a0 = wave_sum_dpp(psk), a3 = wave_sum_dpp(psxy);
-        if (lane == 0) {
-          double* pk = part + ((size_t)curk * NW + wid) * 4;
-          pk[0] = a0;
-          pk[3] = a3;
-        }
-        psk = psxy = 0.0;
-      };
+      // A principal hit (a tail point on a principal pixel: ~0.5% of the points) adds x*y and y[x>0] straight
+      // into this wave's LDS partials of its current window (part[k][wid], zeroed in phase 0): only this wave
+      // writes that slot, in program order, lanes of one instruction in hardware order -- deterministic.  No
+      // per-window wave reduction (it cost two f64 DPP reductions per window change per wave).
       // Lanes past the end of their window hold a copy of its last point (masked by `valid`); groups past the
       // tail are skipped.  Stage 1 reads the bitmap words of every slot at once; stage 2 handles slot by slot:
       // window changes (flush), principal hits (rank + value lookups only in waves that have one), duplicate
@@ -1050,7 +1044,6 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
           const int G = c * GPC + j * NW + wid;
           if (G < ng) {
             while (G >= gnext) {  // this wave moves on to a later window (uniform)
-              flush();
               ++curk;
               gnext = curk + 1 < MAXK ? uni(D->gs[curk + 1]) : 0x7FFFFFFF;
               wend = uni(D->end[curk]);
@@ -1063,9 +1056,12 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
               double x;
               if constexpr (TWO) x = in ? vals[(int)Bpf[br[j]] + __popcll(bw[j] & (bit - 1ull))] : 0.0;
               else x = in ? vals[(int)pf[p >> 6] + __popcll(bw[j] & (bit - 1ull))] : 0.0;
-              const double v = Hits<FMT>::val(buf[j]);
-              psxy += x * v;
-              if (x > 0.0) psk += v;
+              if (in) {
+                const double v = Hits<FMT>::val(buf[j]);
+                double* pk = part + ((size_t)curk * NW + wid) * 4;
+                atomicAdd(&pk[3], x * v);
+                if (x > 0.0) atomicAdd(&pk[0], v);
+              }
             }
             // duplicate candidates are summed per (pixel, window) before squaring: appended to this wave's
             // list segment (ballot compaction, no atomics)
@@ -1101,7 +1097,6 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         process(c + 3, pd);
         issue_chunk(D, c + 7, pd);
       }
-      flush();
       if (lane == 0) dcnt[wid] = nd;
     } else if (!skip && tid < NW) {
       dcnt[tid] = 0;
