@@ -39,6 +39,7 @@ extern "C" {
 #define SMG_ION_CHAOS_NAN 0x4u   /* raw measure_of_chaos was NaN (empty / < 4 positive pixels) */
 #define SMG_ION_BIG 0x8u         /* scored by the big-ion LDS pass (1024-thread workgroup, whole LDS) */
 #define SMG_ION_TWO_LEVEL 0x10u  /* LDS pass with the two-level pixel set (images > 2^18 pixels) */
+#define SMG_ION_WIDE 0x20u       /* dense path, rank-indexed wide pass (LDS presence bitmap + rank prefix) */
 
 /* hit formats accepted by smg_ion_metrics */
 #define SMG_HITS_PACKED_F32 0    /* uint64: low 32 bits pixel index, high 32 bits float32 intensity */
@@ -162,8 +163,10 @@ int smg_debug_stream_read(const uint64_t* data, int64_t n_words, uint64_t* out, 
 /* Test switch: on != 0 makes smg_ion_metrics score every image size with the two-level LDS passes (normally only
  * images above 2^18 pixels), so that the parity suite covers them on small images.  Process-wide; returns 0. */
 int smg_debug_force_two_level(int32_t on);
-/* Test switch: on != 0 makes smg_ion_metrics score every ion with the dense (global-scratch) path, so that the
- * parity suite covers it on every case.  Process-wide; returns 0. */
+/* Test switch: on = 1 makes smg_ion_metrics score every ion with the dense (global-scratch) path -- the
+ * rank-indexed wide pass where the image fits it, the pixel-indexed slot kernel for the rest; on = 2 sends every
+ * ion to the pixel-indexed slot kernel; so that the parity suite covers both on every case.  Process-wide;
+ * returns 0. */
 int smg_debug_force_dense(int32_t on);
 
 /* Diagnostics: on != 0 records HIP events on the launch stream around every main-pass (ion_pipe_kernel<512>)

@@ -1,6 +1,7 @@
 """Workload for rocprofv3 --pmc passes (one counter set per run, scripts/gpu_pmc2.sh).
   c3    : config 3 (500x500, Poisson(2000), 20,000 formulas): the main LDS pass ion_pipe_kernel<512>
-  dense : 1000x1000, Poisson(2100), 1,000 formulas: most principal windows exceed the LDS passes -> ion_dense_kernel
+  dense : 1000x1000, Poisson(2100), 1,000 formulas: most principal windows exceed the LDS passes -> dense path
+  c5    : 1000x1000, Poisson(5000), 2,000 formulas (config-5-like windows): the wide dense pass ion_wide_kernel
 One warm hot-path pass, then two ion_metrics launches, then a calibration read of the sorted hits (known bytes,
 the kernels' 8-byte-per-lane access width) for FETCH_SIZE."""
 import ctypes, os, sys
@@ -12,6 +13,9 @@ which = sys.argv[1] if len(sys.argv) > 1 else "c3"
 if which == "c3":
     ions = syn.make_ion_table(20000, seed=43, decoy_seed=44)
     mz, hits, dims, info = syn.make_dataset_torch(500, 500, 2000, seed=42, device="cuda", ions=ions)
+elif which == "c5":
+    ions = syn.make_ion_table(2000, seed=43, decoy_seed=44)
+    mz, hits, dims, info = syn.make_dataset_torch(1000, 1000, 5000, seed=42, device="cuda", ions=ions)
 else:
     ions = syn.make_ion_table(1000, seed=43, decoy_seed=44)
     mz, hits, dims, info = syn.make_dataset_torch(1000, 1000, 2100, seed=42, device="cuda", ions=ions)

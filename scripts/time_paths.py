@@ -42,5 +42,13 @@ finally:
 err = max(float(np.abs(g_n[c] - g_d[c]).max()) for c in cols)
 print(f"forced dense {t_d:.2f} ms, max|d| vs normal {err:.1e}, scored set same "
       f"{bool(np.array_equal(g_n['flags'] & 1, g_d['flags'] & 1))}", flush=True)
+L.smg_debug_force_dense(2)
+try:
+    t_p, g_p = timed()
+finally:
+    L.smg_debug_force_dense(0)
+err = max(float(np.abs(g_n[c] - g_p[c]).max()) for c in cols)
+print(f"forced pixel-indexed dense {t_p:.2f} ms, max|d| vs normal {err:.1e}, wide ions normal "
+      f"{int(((g_n['flags'] & 0x20) != 0).sum())}", flush=True)
 t_c, g_c = timed(reps=2, do_preprocessing=True, q=99.0)
 print(f"do_preprocessing (q99 clip, dense path) {t_c:.2f} ms", flush=True)

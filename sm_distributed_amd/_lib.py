@@ -17,6 +17,7 @@ SMG_ION_DENSE = 0x2
 SMG_ION_CHAOS_NAN = 0x4
 SMG_ION_BIG = 0x8
 SMG_ION_TWO_LEVEL = 0x10
+SMG_ION_WIDE = 0x20
 SMG_HITS_PACKED_F32 = 0
 PIXEL_MASK = 0x7FFFFFFF   # bit 31 of the pixel field = duplicate-candidate flag
 SMG_HITS_SPLIT_F64 = 1

@@ -2244,6 +2244,640 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
   STAMP_FLUSH();
 }
 
+// ---------------------------------------------------------------------------------------------
+// wide pass: dense-path ions of images whose presence bitmap and rank prefix fit the LDS (no clip)
+// ---------------------------------------------------------------------------------------------
+// The pixel-indexed slot above turns every window point into a random read-modify-write of a 38-B-per-pixel
+// array far larger than the XCD's L2.  Here the principal image's presence bitmap lives in the LDS with a
+// two-level rank prefix (u32 per 65536 pixels, u16 per 64): a principal pixel's value, level and plist entry sit
+// at its dense rank in the slot's compact arrays (np entries, written in order of rank, L2-resident for ordinary
+// windows).  Tail points without the duplicate-candidate flag read x at the rank of their pixel; flagged tail
+// points are summed per pixel in a small open-addressing table that each window's owners clear again.  Chaos
+// candidates get their own bitmap + ranks for Kruskal (the principal bitmap is no longer needed by then).  Nothing
+// is pixel-indexed in global memory, so nothing has to be zeroed per slot; an ion whose flagged tail pixels
+// overflow the table is handed to the pixel-indexed kernel.
+constexpr int WIDE_HT_LOG2 = 14;
+constexpr int WIDE_HT = 1 << WIDE_HT_LOG2;  // tail duplicate table entries per slot
+constexpr int WIDE_PROBES = 64;
+#ifndef SMG_WIDE_EXP
+#define SMG_WIDE_EXP 0  // diagnostic builds only: 1 no x gathers, 2 no window-sum flushes, 4 no tail stream
+#endif
+constexpr int WIDE_DL = 2 * WIDE_HT;        // flagged tail points listed per ion
+constexpr uint32_t WIDE_EMPTY = 0xFFFFFFFFu;
+#ifndef SMG_WDU
+#define SMG_WDU 8
+#endif
+constexpr int WDU = SMG_WDU;  // wide pass: points per lane with loads in flight together
+#ifndef SMG_TDU
+#define SMG_TDU 4
+#endif
+constexpr int TDU = SMG_TDU;  // wide pass, pipelined tail stream: points per lane per batch (two batches live)
+
+struct WideSlot {
+  double* vals;     // principal values by rank
+  uint32_t* plist;  // principal pixels by rank
+  uint32_t* epix;   // chaos candidates in discovery order
+  uint32_t* epr;    // chaos candidates by rank
+  uint32_t* par;    // union-find over candidate ranks
+  uint8_t* L;       // levels by principal rank
+  uint8_t* eL;      // eL in discovery order
+  uint8_t* eLr;     // eL by candidate rank
+  uint32_t* hkey;   // tail duplicate table: pixel, summed value, entries claimed in the current window
+  double* hval;
+  uint32_t* hown;
+  uint32_t* dkey;   // flagged tail points of the ion: (window, pixel) key and value
+  double* dval;
+};
+
+static inline size_t wide_slot_bytes(int npx) {
+  return al16((size_t)npx * 8) + al16((size_t)npx * 4) * 4 + al16((size_t)npx) * 3 + al16((size_t)WIDE_HT * 4) * 2 +
+         al16((size_t)WIDE_HT * 8) + al16((size_t)WIDE_DL * 4) + al16((size_t)WIDE_DL * 8) + 256;
+}
+
+__device__ __forceinline__ WideSlot wide_slot(unsigned char* base, int npx) {
+  WideSlot S;
+  auto a16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  size_t o = 0;
+  S.vals = reinterpret_cast<double*>(base + o);
+  o += a16((size_t)npx * 8);
+  S.plist = reinterpret_cast<uint32_t*>(base + o);
+  o += a16((size_t)npx * 4);
+  S.epix = reinterpret_cast<uint32_t*>(base + o);
+  o += a16((size_t)npx * 4);
+  S.epr = reinterpret_cast<uint32_t*>(base + o);
+  o += a16((size_t)npx * 4);
+  S.par = reinterpret_cast<uint32_t*>(base + o);
+  o += a16((size_t)npx * 4);
+  S.L = base + o;
+  o += a16((size_t)npx);
+  S.eL = base + o;
+  o += a16((size_t)npx);
+  S.eLr = base + o;
+  o += a16((size_t)npx);
+  S.hval = reinterpret_cast<double*>(base + o);
+  o += a16((size_t)WIDE_HT * 8);
+  S.hkey = reinterpret_cast<uint32_t*>(base + o);
+  o += a16((size_t)WIDE_HT * 4);
+  S.hown = reinterpret_cast<uint32_t*>(base + o);
+  o += a16((size_t)WIDE_HT * 4);
+  S.dval = reinterpret_cast<double*>(base + o);
+  o += a16((size_t)WIDE_DL * 8);
+  S.dkey = reinterpret_cast<uint32_t*>(base + o);
+  return S;
+}
+
+// LDS bytes of the wide pass's bitmap (+ one zero word), superblock bases and word prefixes
+static inline size_t wide_lds_bytes(int npx) {
+  const size_t n64 = ((size_t)npx + 63) / 64;
+  return (n64 + 1) * 8 + ((n64 + 1023) / 1024) * 4 + ((n64 * 2 + 7) & ~(size_t)7);
+}
+
+// rank structure over the LDS bitmap: #set bits before word w = sb[w >> 10] + pf[w].  A superblock of 1024 words
+// (65536 bits, so pf fits 16 bits) is one wave's: its lanes read consecutive words (no bank conflicts) and scan them
+// 64 at a time with DPP.  Needs n64 <= DNW * 1024.  Returns the bit count.
+__device__ uint32_t build_rank(const uint64_t* bm, uint16_t* pf, uint32_t* sb, int n64, uint32_t* sc) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int w0 = wid * 1024, w1 = min(w0 + 1024, n64);
+  uint32_t run = 0;
+  for (int c = w0; c < w1; c += 64) {
+    const int w = c + lane;
+    const int x = w < w1 ? __popcll(bm[w]) : 0;
+    const int incl = wave_incl_scan_dpp(x);
+    if (w < w1) pf[w] = (uint16_t)(run + (uint32_t)(incl - x));
+    run += (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+  }
+  if (lane == 0) sc[wid] = run;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < DNW; ++w) {
+    const uint32_t t = sc[w];
+    base += (w < wid) ? t : 0u;
+    tot += t;
+  }
+  if (lane == 0 && w0 < n64) sb[wid] = base;
+  __syncthreads();
+  return tot;
+}
+
+// 8-byte load past L1 (agent scope, like ld_agent) issued asynchronously: waited for with vm_wait
+__device__ __forceinline__ void ld8_async_agent(uint64_t& r, const void* addr) {
+  asm volatile("global_load_dwordx2 %0, %1, off sc1" : "+v"(r) : "v"(addr) : "memory");
+}
+
+struct RankBits {
+  const uint64_t* bm;
+  const uint16_t* pf;
+  const uint32_t* sb;
+  __device__ __forceinline__ bool test(uint32_t p) const { return (bm[p >> 6] >> (p & 63)) & 1ull; }
+  __device__ __forceinline__ uint32_t rank(uint32_t p) const {  // number of set bits below pixel p
+    const uint32_t w = p >> 6;
+    return sb[w >> 10] + (uint32_t)pf[w] + (uint32_t)__popcll(bm[w] & ((1ull << (p & 63)) - 1ull));
+  }
+};
+
+template <int FMT>
+__global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
+    Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
+    const int64_t* __restrict__ ion_off, const double* __restrict__ theor, Params P,
+    const uint32_t* __restrict__ list, const uint32_t* __restrict__ count, uint32_t* next, uint32_t* rej_list,
+    uint32_t* rej_count, unsigned char* scratch, size_t slot_bytes, double* __restrict__ oc,
+    double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags) {
+  using H = Hits<FMT>;
+  extern __shared__ uint64_t wide_dyn[];
+  __shared__ double red[8 * DNW];
+  __shared__ double kst[4 * MAXK_DENSE];
+  __shared__ uint32_t sc[DNW];
+  __shared__ int sh_ion;
+  __shared__ int sh_ctr[4];  // candidates, max eL, listed flagged tail points, list / table overflow
+  __shared__ int sh_nown;    // claimed table entries
+  __shared__ int64_t sh_tb[MAXK_DENSE + 1];  // tail stream: offset of window k at k - 1 (+ the total)
+  __shared__ int64_t sh_tlo[MAXK_DENSE];     // first point of window k at k - 1
+  const int tid = threadIdx.x;
+  const int npx = P.npx, n64 = (npx + 63) / 64, nsb = (n64 + 1023) / 1024;
+  uint64_t* bm = wide_dyn;  // n64 words + one zero word (row7 reads one word past a row's start)
+  uint32_t* bm32 = reinterpret_cast<uint32_t*>(bm);
+  uint32_t* sb = reinterpret_cast<uint32_t*>(bm + n64 + 1);
+  uint16_t* pf = reinterpret_cast<uint16_t*>(sb + nsb);
+  const RankBits R{bm, pf, sb};
+  const PresenceBits<true> pres{bm32};
+  WideSlot S = wide_slot(scratch + (size_t)blockIdx.x * slot_bytes, npx);
+  const uint32_t total = *count;
+  for (int i = tid; i < WIDE_HT; i += DBLOCK) {
+    S.hkey[i] = WIDE_EMPTY;
+    S.hval[i] = 0.0;
+  }
+  slot_sync();
+  const int nr = P.nrows, nc = P.ncols;
+  STAMP_DECL();
+
+  while (true) {
+    if (tid == 0) {
+      const uint32_t k = atomicAdd(next, 1u);
+      sh_ion = (k < total) ? (int)list[k] : -1;
+      sh_ctr[0] = sh_ctr[1] = sh_ctr[2] = sh_ctr[3] = 0;
+      sh_nown = 0;
+    }
+    __syncthreads();
+    const int64_t ion = sh_ion;
+    if (ion < 0) break;
+    const int64_t w0 = ion_off[ion];
+    const int K = (int)(ion_off[ion + 1] - w0);
+    uint32_t flags = SMG_ION_DENSE | SMG_ION_WIDE;
+    for (int k = 0; k < K && k < MAXK_DENSE; ++k)
+      if (hi[w0 + k] > lo[w0 + k]) flags |= SMG_ION_HAS_HITS;
+    if (K > MAXK_DENSE || K == 0) {
+      if (tid == 0) {
+        oc[ion] = osp[ion] = osc[ion] = omsm[ion] = 0.0;
+        oflags[ion] = (K == 0) ? 0u : (flags | 0x80000000u);
+      }
+      __syncthreads();
+      continue;
+    }
+
+    STAMP(15);
+    // principal image: presence bits, ranks, then values and pixels at their ranks
+    for (int w = tid; w <= n64; w += DBLOCK) bm[w] = 0ull;
+    __syncthreads();
+    const int64_t a0 = lo[w0], b0 = hi[w0];
+    for (int64_t i0 = a0; i0 < b0; i0 += (int64_t)DBLOCK * WDU) {
+      typename H::Reg r[WDU];
+#pragma unroll
+      for (int u = 0; u < WDU; ++u) {
+        const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
+        r[u] = i < b0 ? hits.load(i) : H::zero();
+      }
+#pragma unroll
+      for (int u = 0; u < WDU; ++u) {
+        const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
+        if (i < b0) {
+          const uint32_t p = H::pix(r[u]);
+          atomicOr(&bm32[p >> 5], 1u << (p & 31));
+        }
+      }
+    }
+    __syncthreads();
+    const int np = (int)build_rank(bm, pf, sb, n64, sc);
+    STAMP(10);
+    for (int r = tid; r < np; r += DBLOCK) S.vals[r] = 0.0;  // flagged points add into their rank
+    slot_sync();
+    for (int64_t i0 = a0; i0 < b0; i0 += (int64_t)DBLOCK * WDU) {
+      typename H::Reg r[WDU];
+#pragma unroll
+      for (int u = 0; u < WDU; ++u) {
+        const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
+        r[u] = i < b0 ? hits.load(i) : H::zero();
+      }
+#pragma unroll
+      for (int u = 0; u < WDU; ++u) {
+        const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
+        if (i < b0) {
+          const uint32_t p = H::pix(r[u]);
+          const uint32_t k = R.rank(p);
+          S.plist[k] = p;
+          if (H::dup(r[u])) atomicAdd(&S.vals[k], H::val(r[u]));
+          else S.vals[k] = H::val(r[u]);
+        }
+      }
+    }
+    slot_sync();
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    double mx = -INFINITY;
+    for (int r0 = tid; r0 < np; r0 += DBLOCK * WDU) {  // WDU loads in flight per lane
+      uint64_t vb[WDU];
+#pragma unroll
+      for (int j = 0; j < WDU; ++j) {
+        vb[j] = 0ull;
+        ld8_async_agent(vb[j], &S.vals[(r0 + j * DBLOCK < np) ? r0 + j * DBLOCK : 0]);
+      }
+      vm_wait<0>(vb);
+#pragma unroll
+      for (int j = 0; j < WDU; ++j) {
+        if (r0 + j * DBLOCK >= np) continue;
+        const double v = __longlong_as_double((long long)vb[j]);
+        acc[0] += v;
+        acc[1] += v * v;
+        if (v > 0.0) {
+          acc[2] += v;
+          acc[3] += 1.0;
+        }
+        mx = v > mx ? v : mx;
+      }
+    }
+    if (np < npx) mx = mx > 0.0 ? mx : 0.0;  // unlisted pixels are zero
+    dblock_sum<4>(acc, red);
+    const double sx = acc[0], sxx = acc[1], s0 = acc[2], npos = acc[3];
+    const double vmax = block_max<DNW>(mx, red);
+    const bool chaos_ok = (sx > 0.0) && (npos >= 4.0);
+
+    STAMP(11);
+    // tail windows joined against x by rank, as one stream over their concatenated points (a lane's window index
+    // only grows along it): each lane sums into the window it is in and adds to the window's LDS row when it
+    // moves on.  Flagged points are summed per (window, pixel) in the duplicate table.
+    if (tid < 4 * MAXK_DENSE) kst[tid] = 0.0;
+    if (tid <= K - 1) {
+      int64_t n = 0;
+      for (int k = 1; k <= tid; ++k) n += hi[w0 + k] - lo[w0 + k];
+      sh_tb[tid] = n;  // sh_tb[k - 1]: stream offset of window k
+      if (tid < K - 1) sh_tlo[tid] = lo[w0 + 1 + tid];
+    }
+    __syncthreads();
+    {
+      const int64_t T = (SMG_WIDE_EXP & 4) ? 0 : sh_tb[K - 1];
+      double a2[4] = {0.0, 0.0, 0.0, 0.0};  // s (y[x > 0]), sy, syy, sxy of window kacc
+      int kacc = 0;
+      auto flush = [&]() {
+        if (!(SMG_WIDE_EXP & 2) && (a2[1] != 0.0 || a2[2] != 0.0 || a2[3] != 0.0 || a2[0] != 0.0)) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) atomicAdd(&kst[j * MAXK_DENSE + kacc + 1], a2[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a2[j] = 0.0;
+      };
+      // one tail point (stream window kk, hit r, x at its pixel xv when not flagged): into the window's sums, or
+      // (flagged) into the ion's list of flagged points, summed per (window, pixel) after the stream
+      auto point = [&](bool valid, int kk, typename H::Reg r, double xv) {
+        const bool fl = valid && H::dup(r);
+        if (valid) {
+          if (kk != kacc) {
+            flush();
+            kacc = kk;
+          }
+          if (!fl) {
+            const double y = H::val(r);
+            a2[1] += y;
+            a2[2] += y * y;
+            a2[3] += xv * y;
+            if (xv > 0.0) a2[0] += y;
+          }
+        }
+        const int idx = wave_append(fl, &sh_ctr[2]);
+        if (fl) {
+          if (idx < WIDE_DL) {
+            S.dkey[idx] = (uint32_t)kacc * (uint32_t)npx + H::pix(r);
+            S.dval[idx] = H::val(r);
+          } else {
+            sh_ctr[3] = 1;
+          }
+        }
+      };
+      if constexpr (FMT == SMG_HITS_PACKED_F32) {
+        // software pipeline over batches of TDU points per lane (two register sets): wait for a batch's hits,
+        // issue the x gathers of its principal pixels and then the next batch's hits, wait for the gathers only
+        // (all but the TDU youngest operations), accumulate.  Every lane issues every load (a safe address when
+        // it has none) so that the counted waits hold per wave.
+        constexpr int64_t STEP = (int64_t)DBLOCK * TDU;
+        const uint64_t* hb = hits.h;
+        uint64_t rA[TDU], rB[TDU], xb[TDU];
+        int kA[TDU], kB[TDU];
+#pragma unroll
+        for (int u = 0; u < TDU; ++u) {
+          rA[u] = rB[u] = xb[u] = 0ull;
+          kA[u] = kB[u] = 0;
+        }
+        auto issue = [&](int64_t v0, uint64_t (&r)[TDU], int (&kk)[TDU]) {
+#pragma unroll
+          for (int u = 0; u < TDU; ++u) {
+            const int64_t v = v0 + (int64_t)u * DBLOCK + tid;
+            int64_t i = 0;
+            if (v < T) {
+              while (v >= sh_tb[kk[u] + 1]) ++kk[u];
+              i = sh_tlo[kk[u]] + (v - sh_tb[kk[u]]);
+            }
+            ld8_async_v(r[u], hb + i);
+          }
+        };
+        auto batch = [&](int64_t v0, uint64_t (&r)[TDU], const int (&kk)[TDU], uint64_t (&rn)[TDU],
+                         int (&kn)[TDU]) {
+          vm_wait<0>(r);
+          uint32_t pm = 0u;
+#pragma unroll
+          for (int u = 0; u < TDU; ++u) {
+            const int64_t v = v0 + (int64_t)u * DBLOCK + tid;
+            const uint32_t p = H::pix(r[u]);
+            const bool pr = !(SMG_WIDE_EXP & 1) && v < T && !H::dup(r[u]) && R.test(p);
+            pm |= (uint32_t)pr << u;
+            ld8_async_agent(xb[u], pr ? (const void*)&S.vals[R.rank(p)] : (const void*)S.vals);
+          }
+          if (v0 + STEP < T) {
+            issue(v0 + STEP, rn, kn);
+            vm_wait<TDU>(xb);
+          } else {
+            vm_wait<0>(xb);
+          }
+#pragma unroll
+          for (int u = 0; u < TDU; ++u) {
+            const int64_t v = v0 + (int64_t)u * DBLOCK + tid;
+            point(v < T, kk[u], r[u], ((pm >> u) & 1u) ? __longlong_as_double((long long)xb[u]) : 0.0);
+          }
+        };
+        if (T > 0) issue(0, rA, kA);
+        for (int64_t v0 = 0; v0 < T; v0 += 2 * STEP) {
+          batch(v0, rA, kA, rB, kB);
+          if (v0 + STEP >= T) break;
+          batch(v0 + STEP, rB, kB, rA, kA);
+        }
+      } else {
+        int kc[WDU];
+#pragma unroll
+        for (int u = 0; u < WDU; ++u) kc[u] = 0;
+        for (int64_t v0 = 0; v0 < T; v0 += (int64_t)DBLOCK * WDU) {
+          typename H::Reg r[WDU];
+#pragma unroll
+          for (int u = 0; u < WDU; ++u) {
+            const int64_t v = v0 + (int64_t)u * DBLOCK + tid;
+            r[u] = H::zero();
+            if (v < T) {
+              while (v >= sh_tb[kc[u] + 1]) ++kc[u];
+              r[u] = hits.load(sh_tlo[kc[u]] + (v - sh_tb[kc[u]]));
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < WDU; ++u) {
+            const int64_t v = v0 + (int64_t)u * DBLOCK + tid;
+            const uint32_t p = H::pix(r[u]);
+            const double xv = (v < T && !H::dup(r[u]) && R.test(p)) ? ld_agent(&S.vals[R.rank(p)]) : 0.0;
+            point(v < T, kc[u], r[u], xv);
+          }
+        }
+      }
+      flush();
+      __syncthreads();
+      const int nd = min(sh_ctr[2], WIDE_DL);
+      if (nd > 0) {
+        slot_sync();  // the list is complete in L2
+        // sum the listed points per key in the table (all lanes at once: ~one atomic round trip); the lane that
+        // claims an entry lists it
+        for (int j = tid; j < nd; j += DBLOCK) {
+          const uint32_t key = ld_agent(&S.dkey[j]);
+          const double y = ld_agent(&S.dval[j]);
+          uint32_t h = (key * 0x9E3779B1u) >> (32 - WIDE_HT_LOG2);
+          bool own = false, done = false;
+          for (int t = 0; t < WIDE_PROBES; ++t) {
+            const uint32_t old = atomicCAS(&S.hkey[h], WIDE_EMPTY, key);
+            if (old == WIDE_EMPTY || old == key) {
+              atomicAdd(&S.hval[h], y);
+              own = old == WIDE_EMPTY;
+              done = true;
+              break;
+            }
+            h = (h + 1) & (WIDE_HT - 1);
+          }
+          if (!done) sh_ctr[3] = 1;
+          const int idx = wave_append(own, &sh_nown);
+          if (own) S.hown[idx] = h;
+        }
+        slot_sync();  // the table's sums are complete in L2
+        const int no = sh_nown;
+        for (int j = tid; j < no; j += DBLOCK) {  // claimed entries: add their pixels, then release them
+          const uint32_t s = S.hown[j];
+          const uint32_t key = ld_agent(&S.hkey[s]);
+          const double y = ld_agent(&S.hval[s]);
+          const uint32_t k = key / (uint32_t)npx, p = key - k * (uint32_t)npx;
+          const double xv = R.test(p) ? ld_agent(&S.vals[R.rank(p)]) : 0.0;
+          atomicAdd(&kst[0 * MAXK_DENSE + k + 1], xv > 0.0 ? y : 0.0);
+          atomicAdd(&kst[1 * MAXK_DENSE + k + 1], y);
+          atomicAdd(&kst[2 * MAXK_DENSE + k + 1], y * y);
+          atomicAdd(&kst[3 * MAXK_DENSE + k + 1], xv * y);
+          S.hkey[s] = WIDE_EMPTY;
+          S.hval[s] = 0.0;
+        }
+        slot_sync();  // released entries are clean in L2 before the next ion's atomics
+      }
+    }
+    if (sh_ctr[3]) {  // the table overflowed: the pixel-indexed kernel scores this ion
+      if (tid == 0) rej_list[atomicAdd(rej_count, 1u)] = (uint32_t)ion;
+      __syncthreads();
+      continue;
+    }
+
+    STAMP(12);
+    double chaos_raw = NAN;
+    if (chaos_ok) {
+      for (int r0 = tid; r0 < np; r0 += DBLOCK * WDU) {
+        uint64_t vb[WDU];
+#pragma unroll
+        for (int j = 0; j < WDU; ++j) {
+          vb[j] = 0ull;
+          ld8_async_agent(vb[j], &S.vals[(r0 + j * DBLOCK < np) ? r0 + j * DBLOCK : 0]);
+        }
+        vm_wait<0>(vb);
+#pragma unroll
+        for (int j = 0; j < WDU; ++j)
+          if (r0 + j * DBLOCK < np)
+            S.L[r0 + j * DBLOCK] = (uint8_t)level_of(__longlong_as_double((long long)vb[j]), vmax, P);
+      }
+      slot_sync();
+      STAMP(13);
+      // candidates as in ion_dense_kernel: the 4-cross around each principal pixel, owned by the first principal
+      // pixel on its cross, screened over the 3x3 box by presence; the 7x7 level window of a pixel with a
+      // surviving candidate is read by rank (one rank per row, the rest by popcount of the row's bits)
+      for (int i0 = 0; i0 < np; i0 += DBLOCK) {
+        const int i = i0 + tid;
+        const int p = (i < np) ? (int)S.plist[i] : -1;
+        const int r0 = p >= 0 ? p / nc : 0, c0 = p >= 0 ? p - r0 * nc : 0;
+        uint32_t B[7];
+#pragma unroll
+        for (int dr = -3; dr <= 3; ++dr) B[dr + 3] = p >= 0 ? pres.row7(r0 + dr, c0, nr, nc) : 0u;
+        auto bit = [&](int wr, int wc) -> uint32_t { return (B[wr] >> wc) & 1u; };
+        bool cand[5];
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          const int qr = (j == 1) ? -1 : (j == 2) ? 1 : 0, qc = (j == 3) ? -1 : (j == 4) ? 1 : 0;
+          const int r = r0 + qr, c = c0 + qc;
+          bool ok = p >= 0 && r >= 0 && r < nr && c >= 0 && c < nc;
+          const int wr = qr + 3, wc = qc + 3;
+          if (ok) {
+            int orr = 9, occ = 9;
+            if (bit(wr + 1, wc)) orr = 1, occ = 0;
+            if (bit(wr, wc + 1)) orr = 0, occ = 1;
+            if (bit(wr, wc)) orr = 0, occ = 0;
+            if (bit(wr, wc - 1)) orr = 0, occ = -1;
+            if (bit(wr - 1, wc)) orr = -1, occ = 0;
+            ok = (qr + orr == 0 && qc + occ == 0);
+          }
+          if (ok) {
+#pragma unroll
+            for (int a = -1; a <= 1; ++a)
+#pragma unroll
+              for (int b = -1; b <= 1; ++b) {
+                const int rr = r + a, cc = c + b;
+                if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) {
+                  if (!P.erosion_border) ok = false;
+                  continue;
+                }
+                const int ur = wr + a, uc = wc + b;
+                if (!(bit(ur, uc) | bit(ur - 1, uc) | bit(ur + 1, uc) | bit(ur, uc - 1) | bit(ur, uc + 1)))
+                  ok = false;
+              }
+          }
+          cand[j] = ok;
+          any |= ok;
+        }
+        uint64_t WL[7];
+#pragma unroll
+        for (int dr = 0; dr < 7; ++dr) WL[dr] = 0ull;
+        if (any) {
+#pragma unroll
+          for (int dr = -3; dr <= 3; ++dr) {
+            const uint32_t row = B[dr + 3];
+            if (row != 0u) {
+              // the row's present pixels have consecutive ranks: their levels are L[base .. base + popc(row))
+              const uint32_t base = R.rank((uint32_t)((r0 + dr) * nc + max(c0 - 3, 0)));
+              const uint64_t* la = reinterpret_cast<const uint64_t*>(S.L + (base & ~7u));
+              const uint64_t l0 = la[0], l1 = la[1];
+              const uint32_t sh = (base & 7u) * 8u;
+              uint64_t packed = sh ? ((l0 >> sh) | (l1 << (64u - sh))) : l0;
+              uint64_t w = 0ull;
+#pragma unroll
+              for (int j = 0; j < 7; ++j)
+                if ((row >> j) & 1u) {
+                  w |= (packed & 0xFFull) << (8 * j);
+                  packed >>= 8;
+                }
+              WL[dr + 3] = w;
+            }
+          }
+        }
+        auto W = [&](int wr, int wc) -> int { return (int)((WL[wr] >> (8 * wc)) & 0xFFull); };
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          const int qr = (j == 1) ? -1 : (j == 2) ? 1 : 0, qc = (j == 3) ? -1 : (j == 4) ? 1 : 0;
+          const int r = r0 + qr, c = c0 + qc;
+          const int q = cand[j] ? r * nc + c : -1;
+          int e = 0;
+          if (q >= 0) {
+            e = 1 << 20;
+#pragma unroll
+            for (int a = -1; a <= 1; ++a)
+#pragma unroll
+              for (int b = -1; b <= 1; ++b) {
+                const int rr = r + a, cc = c + b;
+                if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) {
+                  if (!P.erosion_border) e = 0;
+                  continue;
+                }
+                const int wr = qr + a + 3, wc = qc + b + 3;
+                const int t = max(max(W(wr, wc), W(wr - 1, wc)), max(max(W(wr + 1, wc), W(wr, wc - 1)), W(wr, wc + 1)));
+                e = min(e, t);
+              }
+            if (e >= (1 << 20)) e = 0;
+          }
+          const int idx = wave_append(e >= 1, &sh_ctr[0]);
+          if (e >= 1) {
+            S.epix[idx] = (uint32_t)q;
+            S.eL[idx] = (uint8_t)e;
+            atomicMax(&sh_ctr[1], e);
+          }
+        }
+      }
+      slot_sync();
+      const int m = sh_ctr[0];
+      const int emax = sh_ctr[1];
+      STAMP(14);
+      double esum = 0.0, wsum = 0.0;
+      for (int i = tid; i < m; i += DBLOCK) esum += (double)S.eL[i];
+      if (m > 0) {  // Kruskal over the candidates, indexed by their rank in a candidate bitmap
+        for (int w = tid; w <= n64; w += DBLOCK) bm[w] = 0ull;
+        __syncthreads();
+        for (int i = tid; i < m; i += DBLOCK) {
+          const uint32_t q = S.epix[i];
+          atomicOr(&bm32[q >> 5], 1u << (q & 31));
+        }
+        __syncthreads();
+        build_rank(bm, pf, sb, n64, sc);
+        for (int i = tid; i < m; i += DBLOCK) {
+          const uint32_t q = S.epix[i];
+          const uint32_t k = R.rank(q);
+          S.epr[k] = q;
+          S.eLr[k] = S.eL[i];
+          S.par[k] = k;
+        }
+        slot_sync();
+        for (int t = emax; t >= 1; --t) {
+          for (int i = tid; i < m; i += DBLOCK) {
+            const int e = S.eLr[i];
+            if (e < t) continue;
+            const int p = (int)S.epr[i];
+            const int r = p / nc, c = p - r * nc;
+            auto edge = [&](int q) {
+              if (!R.test((uint32_t)q)) return;
+              const uint32_t kq = R.rank((uint32_t)q);
+              const int eq = S.eLr[kq];
+              if ((e < eq ? e : eq) == t && guf_unite(S.par, (uint32_t)i, kq)) wsum += (double)t;
+            };
+            if (c + 1 < nc) edge(p + 1);
+            if (r + 1 < nr) {
+              edge(p + nc);
+              if (P.connectivity == 8) {
+                if (c > 0) edge(p + nc - 1);
+                if (c + 1 < nc) edge(p + nc + 1);
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+      double a3[2] = {esum, wsum};
+      dblock_sum<2>(a3, red);
+      chaos_raw = 1.0 - (a3[0] - a3[1]) / (double)P.nlevels / npos;
+    } else {
+      flags |= SMG_ION_CHAOS_NAN;
+    }
+
+    if (tid == 0) {
+      kst[0] = s0;
+      kst[1 * MAXK_DENSE] = kst[2 * MAXK_DENSE] = kst[3 * MAXK_DENSE] = 0.0;
+      finalize_ion(K, theor + w0, kst, sx, sxx, kst + MAXK_DENSE, kst + 2 * MAXK_DENSE, kst + 3 * MAXK_DENSE,
+                   (double)npx, chaos_raw, ion, flags, oc, osp, osc, omsm, oflags);
+    }
+    STAMP(15);
+    __syncthreads();
+  }
+  STAMP_FLUSH();
+}
+
 __global__ void list_all_kernel(uint32_t* list, uint32_t* count, const int64_t* ion_order, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) list[i] = (uint32_t)(ion_order ? ion_order[i] : i);
@@ -2255,6 +2889,7 @@ __global__ void list_all_kernel(uint32_t* list, uint32_t* count, const int64_t* 
 #endif
 static constexpr int DENSE_SLOTS = SMG_DENSE_SLOTS;  // dense-path workgroups (one scratch slot each)
 static constexpr size_t DENSE_BM_LDS_MAX = 152 * 1024;  // dense kernel: LDS presence bitmap up to this size
+static constexpr size_t WIDE_LDS_MAX = 160 * 1024 - 4096;  // wide pass: dynamic LDS (static arrays ~2.3 KB)
 // workspace: header (pass counters at word 0.., per-XCD range counters at word 64..), two ion lists,
 // the ion descriptors, dense scratch slots
 static constexpr size_t WS_HEADER = 2048;
@@ -2271,9 +2906,15 @@ static constexpr int MAIN_BLOCK = MAIN_CFG[0], MAIN_RMAX = MAIN_CFG[1], MAIN_RC 
 static constexpr int BIG_BLOCK = 1024, BIG_RMAX = 8, BIG_RC = 2;
 static constexpr size_t MAIN_LDS = 80 * 1024, BIG_LDS = 160 * 1024 - 512;
 
+// the wide pass and the pixel-indexed kernel run one after the other over the same slots
+static size_t slot_bytes_for(int npx) {
+  const size_t a = dense_slot_bytes(npx), b = wide_slot_bytes(npx);
+  return a > b ? a : b;
+}
+
 static size_t ws_bytes_for(int64_t n_ions, int npx) {
   return WS_HEADER + 2 * al16((size_t)n_ions * 4) + (size_t)n_ions * sizeof(IonDesc) +
-         (size_t)DENSE_SLOTS * dense_slot_bytes(npx);
+         (size_t)DENSE_SLOTS * slot_bytes_for(npx);
 }
 
 using MainLay = Lay<MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX>;
@@ -2283,7 +2924,7 @@ static constexpr int BIG2_RMAX = 4;
 using Main2Lay = Lay2<MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX>;
 using Big2Lay = Lay2<BIG_BLOCK / WAVE, BIG_BLOCK * BIG2_RMAX>;
 static int g_force_two_level = 0;  // smg_debug_force_two_level: two-level passes for every image size
-static int g_force_dense = 0;      // smg_debug_force_dense: every ion on the dense path
+static int g_force_dense = 0;      // smg_debug_force_dense: 1 every ion on the dense path, 2 pixel-indexed only
 // smg_debug_time_main_pass: HIP events recorded on the launch stream around every main-pass launch, so a
 // benchmark measures the dominant kernel itself (not the descriptor kernel and the later passes around it)
 static int g_time_main = 0;
@@ -2304,13 +2945,14 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
                           const double* theor, const int64_t* ion_order, int64_t n_ions, const Params& P,
                           double* oc, double* osp, double* osc, double* omsm, uint32_t* oflags,
                           unsigned char* ws, hipStream_t st) {
-  // header words: [0] count A, [1] cursor A, [2] count B, [3] cursor B, [HDR_XCD + x*CTR_STRIDE] range x
+  // header words: [0] count A, [1] cursor A, [2] count B, [3] cursor B, [4] count / [5] cursor of the wide
+  // pass's rejects (list A again), [HDR_XCD + x*CTR_STRIDE] range x
   uint32_t* hdr = reinterpret_cast<uint32_t*>(ws);
   uint32_t* list_a = reinterpret_cast<uint32_t*>(ws + WS_HEADER);
   uint32_t* list_b = reinterpret_cast<uint32_t*>(ws + WS_HEADER + al16((size_t)n_ions * 4));
   IonDesc* desc = reinterpret_cast<IonDesc*>(ws + WS_HEADER + 2 * al16((size_t)n_ions * 4));
   unsigned char* slots = reinterpret_cast<unsigned char*>(desc) + (size_t)n_ions * sizeof(IonDesc);
-  const size_t slot_bytes = dense_slot_bytes(P.npx);
+  const size_t slot_bytes = slot_bytes_for(P.npx);
   SMG_HIP(hipMemsetAsync(ws, 0, WS_HEADER, st));
   // images above NPX_LDS_MAX pixels (or forced, smg_debug_force_two_level) take the two-level LDS passes
   const bool two = (P.npx > NPX_LDS_MAX || g_force_two_level) && P.npx <= NPX_TWO_MAX;
@@ -2377,17 +3019,34 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
     SMG_LAUNCH_CHECK();
   }
   const int nslots = (int)(n_ions < DENSE_SLOTS ? n_ions : DENSE_SLOTS);
+  // dense path: the rank-indexed wide pass where the image's bitmap + rank prefix fit the LDS (no clip); the
+  // pixel-indexed kernel takes its rejects (or everything)
+  const uint32_t* dlist = list_b;
+  uint32_t* dcount = hdr + 2;
+  uint32_t* dnext = hdr + 3;
+  const size_t wide_lds = wide_lds_bytes(P.npx);
+  if (!P.clip && g_force_dense != 2 && wide_lds <= WIDE_LDS_MAX) {
+    SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ion_wide_kernel<FMT>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)wide_lds));
+    hipLaunchKernelGGL(ion_wide_kernel<FMT>, dim3((unsigned)nslots), dim3(DBLOCK), wide_lds, st, hits, lo, hi, ion_off,
+                       theor, P, list_b, hdr + 2, hdr + 3, list_a, hdr + 4, slots, slot_bytes, oc, osp, osc, omsm,
+                       oflags);
+    SMG_LAUNCH_CHECK();
+    dlist = list_a;
+    dcount = hdr + 4;
+    dnext = hdr + 5;
+  }
   // the principal presence bitmap lives in the LDS when it fits (images up to ~1.2M pixels)
   const size_t bm_bytes = (((size_t)P.npx + 31) / 32 + 1) * 4;
   if (bm_bytes <= DENSE_BM_LDS_MAX) {
     SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ion_dense_kernel<FMT, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)bm_bytes));
     hipLaunchKernelGGL((ion_dense_kernel<FMT, true>), dim3((unsigned)nslots), dim3(DBLOCK), bm_bytes, st, hits, lo,
-                       hi, ion_off, theor, n_ions, P, list_b, hdr + 2, hdr + 3, slots, slot_bytes, oc, osp, osc, omsm,
+                       hi, ion_off, theor, n_ions, P, dlist, dcount, dnext, slots, slot_bytes, oc, osp, osc, omsm,
                        oflags);
   } else {
     hipLaunchKernelGGL((ion_dense_kernel<FMT, false>), dim3((unsigned)nslots), dim3(DBLOCK), 0, st, hits, lo, hi,
-                       ion_off, theor, n_ions, P, list_b, hdr + 2, hdr + 3, slots, slot_bytes, oc, osp, osc, omsm,
+                       ion_off, theor, n_ions, P, dlist, dcount, dnext, slots, slot_bytes, oc, osp, osc, omsm,
                        oflags);
   }
   SMG_LAUNCH_CHECK();
@@ -2444,7 +3103,7 @@ int smg_debug_main_pass_times(double* ms, int32_t cap, int32_t* n) {
 }
 
 int smg_debug_force_dense(int32_t on) {
-  g_force_dense = on ? 1 : 0;
+  g_force_dense = (on == 1 || on == 2) ? on : 0;
   return SMG_OK;
 }
 

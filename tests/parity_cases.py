@@ -173,6 +173,14 @@ def make_case(name: str):
         ints[bright] = rng.lognormal(17.0, 1.0, int(bright.sum())).astype(np.float32)
         ints[~bright] = (ints[~bright] * 1e-3).astype(np.float32)  # background ~0.4, planted blobs ~3
         return syn.SpectraSet(sp_off=ds.sp_off, mz=ds.mz, ints=ints, coords=ds.coords), ions, 100.0, {}
+    if name == "wide_overflow":  # windows beyond the LDS passes whose flagged tail pixels overflow the wide pass's
+        # duplicate table (8192 entries): the pixel-indexed dense kernel takes them over
+        full = syn.make_ion_table(2, seed=161, decoy_seed=162)
+        tgt = np.nonzero(np.isin(full.adducts, list(full.target_adducts)))[0][:3]
+        ions = subset_ions(full, tgt)
+        ds = syn.make_dataset_np(150, 150, 4, seed=163, ions=ions, plant_fraction=1.0, plant_seed=164,
+                                 blob_sigma=(400.0, 500.0))
+        return add_duplicates(ds, 0.7, 165), ions, 20.0, {}
     if name == "boundary":
         ds = syn.make_dataset_np(16, 16, 300, seed=71)
         return ds, boundary_ions(ds, 5.0, 40, 72), 5.0, {}
@@ -181,7 +189,7 @@ def make_case(name: str):
 
 CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels", "nlevels1", "big_window", "huge_window",
          "large_image", "xl_image", "large_blobs", "boundary", "long_tail", "dups_heavy", "kmix", "clip99", "clip_q50_conn8",
-         "wide_range"]
+         "wide_range", "wide_overflow"]
 
 
 def oracle_run(ds, ions, ppm, nlevels=30, connectivity=4, erosion_border=0, q=99.0, do_preprocessing=False):

@@ -137,13 +137,15 @@ def test_forced_two_level_matches_oracle(name):
 
 
 @pytest.mark.parametrize("name", CASES)
-def test_forced_dense_matches_oracle(name):
-    """Every case again with every ion on the dense path (smg_debug_force_dense): sparse scatter into the slot's
-    pixel-sized images, owner lists, candidate-only chaos."""
+@pytest.mark.parametrize("mode", [1, 2])
+def test_forced_dense_matches_oracle(name, mode):
+    """Every case again with every ion on the dense path (smg_debug_force_dense): mode 1 = the rank-indexed wide
+    pass where the image fits it (its rejects and the clip on the pixel-indexed kernel), mode 2 = the pixel-indexed
+    kernel alone (sparse scatter into the slot's pixel-sized images, owner lists, candidate-only chaos)."""
     from sm_distributed_amd import _lib
     ds, ions, ppm, kw, imgs, df, _, _, _, _ = _run_case(name)
     L = _lib.lib()
-    L.smg_debug_force_dense(1)
+    L.smg_debug_force_dense(mode)
     try:
         _, m, _, _ = _device_run(ds, ions, ppm, **kw)
         _, m2, _, _ = _device_run(ds, ions, ppm, **kw)  # a second launch: slots start clean every launch
@@ -151,6 +153,13 @@ def test_forced_dense_matches_oracle(name):
         L.smg_debug_force_dense(0)
     has = (m["flags"] & 1) != 0
     assert ((m["flags"][has] & 2) != 0).all()
+    wide = (m["flags"] & 0x20) != 0
+    if mode == 2 or kw.get("do_preprocessing") or name == "xl_image":
+        assert not wide.any()
+    elif name == "wide_overflow":  # every ion's tail duplicates overflow the wide pass's table
+        assert has.any() and not wide[has].any()
+    else:
+        assert wide[has].all()
     idx = {k: i for i, k in enumerate(zip(ions.sf_ids.tolist(), ions.adducts.tolist()))}
     assert set(zip(ions.sf_ids[has].tolist(), ions.adducts[has].tolist())) == set(df.index.tolist())
     rows = np.array([idx[k] for k in df.index.tolist()], dtype=np.int64)
@@ -186,6 +195,16 @@ def test_duplicate_flags_cover_every_window_duplicate(name):
     assert n_dup > 0 or name == "basic"
     if name == "basic":
         assert flag.mean() < 0.2  # flags stay a small minority on ordinary data
+
+
+def test_wide_pass_reached_without_forcing():
+    """Windows beyond the big-ion pass go to the rank-indexed wide pass; its table overflow to the pixel kernel."""
+    _, _, _, _, _, _, _, m, _, _ = _run_case("huge_window")
+    dense = ((m["flags"] & 1) != 0) & ((m["flags"] & 2) != 0)
+    assert dense.any() and ((m["flags"][dense] & 0x20) != 0).all()
+    _, _, _, _, _, _, _, m, _, _ = _run_case("wide_overflow")
+    has = (m["flags"] & 1) != 0
+    assert has.any() and ((m["flags"][has] & 2) != 0).all() and not ((m["flags"][has] & 0x20) != 0).any()
 
 
 def test_lds_pipeline_paths_exercised():
