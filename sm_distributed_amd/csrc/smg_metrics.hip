@@ -2282,7 +2282,7 @@ struct WideSlot {
   uint8_t* L;       // levels by principal rank
   uint8_t* eL;      // eL in discovery order
   uint8_t* eLr;     // eL by candidate rank
-  uint32_t* hkey;   // tail duplicate table: pixel, summed value, entries claimed in the current window
+  uint32_t* hkey;   // tail duplicate table: (window, pixel) key, Σy, entries claimed for the ion
   double* hval;
   uint32_t* hown;
   uint32_t* dkey;   // flagged tail points of the ion: (window, pixel) key and value
@@ -2378,7 +2378,7 @@ struct RankBits {
 
 template <int FMT>
 __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
-    Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
+    Hits<FMT> hits, const DD4* __restrict__ cum, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
     const int64_t* __restrict__ ion_off, const double* __restrict__ theor, Params P,
     const uint32_t* __restrict__ list, const uint32_t* __restrict__ count, uint32_t* next, uint32_t* rej_list,
     uint32_t* rej_count, unsigned char* scratch, size_t slot_bytes, double* __restrict__ oc,
@@ -2391,6 +2391,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
   __shared__ int sh_ion;
   __shared__ int sh_ctr[4];  // candidates, max eL, listed flagged tail points, list / table overflow
   __shared__ int sh_nown;    // claimed table entries
+  __shared__ double sh_st[5];  // principal sums: x, x^2, x[x > 0], #(x > 0); max
   __shared__ int64_t sh_tb[MAXK_DENSE + 1];  // tail stream: offset of window k at k - 1 (+ the total)
   __shared__ int64_t sh_tlo[MAXK_DENSE];     // first point of window k at k - 1
   const int tid = threadIdx.x;
@@ -2506,14 +2507,23 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     }
     if (np < npx) mx = mx > 0.0 ? mx : 0.0;  // unlisted pixels are zero
     dblock_sum<4>(acc, red);
-    const double sx = acc[0], sxx = acc[1], s0 = acc[2], npos = acc[3];
-    const double vmax = block_max<DNW>(mx, red);
-    const bool chaos_ok = (sx > 0.0) && (npos >= 4.0);
+    {
+      const double vmax = block_max<DNW>(mx, red);
+      if (tid == 0) {  // kept in the LDS until chaos / finalize (frees registers for the tail stream)
+        sh_st[0] = acc[0];
+        sh_st[1] = acc[1];
+        sh_st[2] = acc[2];
+        sh_st[3] = acc[3];
+        sh_st[4] = vmax;
+      }
+    }
 
     STAMP(11);
-    // tail windows joined against x by rank, as one stream over their concatenated points (a lane's window index
-    // only grows along it): each lane sums into the window it is in and adds to the window's LDS row when it
-    // moves on.  Flagged points are summed per (window, pixel) in the duplicate table.
+    // tail windows.  Σy and Σy² per window come from the hit prefix sums (one thread per window; their Σy² covers
+    // the points without the duplicate-candidate flag); Σxy and Σy[x>0] are linear in the points, so one stream
+    // over the windows' concatenated points (a lane's window index only grows along it) adds x·y and [x>0]·y of
+    // every point whose pixel is principal, x gathered by rank.  Flagged points are listed and summed per
+    // (window, pixel) in the table, which adds (Σy)² of each entry to Σy².
     if (tid < 4 * MAXK_DENSE) kst[tid] = 0.0;
     if (tid <= K - 1) {
       int64_t n = 0;
@@ -2522,40 +2532,48 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
       if (tid < K - 1) sh_tlo[tid] = lo[w0 + 1 + tid];
     }
     __syncthreads();
+    if (tid < K - 1) {
+      const double2 ws = window_sums<FMT>(hits, cum, lo[w0 + 1 + tid], hi[w0 + 1 + tid]);
+      kst[1 * MAXK_DENSE + tid + 1] = ws.x;
+      kst[2 * MAXK_DENSE + tid + 1] = ws.y;
+    }
     {
       const int64_t T = (SMG_WIDE_EXP & 4) ? 0 : sh_tb[K - 1];
-      double a2[4] = {0.0, 0.0, 0.0, 0.0};  // s (y[x > 0]), sy, syy, sxy of window kacc
+      double as = 0.0, axy = 0.0;  // Σy[x > 0], Σxy of window kacc
       int kacc = 0;
-      auto flush = [&]() {
-        if (!(SMG_WIDE_EXP & 2) && (a2[1] != 0.0 || a2[2] != 0.0 || a2[3] != 0.0 || a2[0] != 0.0)) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) atomicAdd(&kst[j * MAXK_DENSE + kacc + 1], a2[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a2[j] = 0.0;
-      };
-      // one tail point (stream window kk, hit r, x at its pixel xv when not flagged): into the window's sums, or
-      // (flagged) into the ion's list of flagged points, summed per (window, pixel) after the stream
+      // one tail point (stream window kk, hit r, x at its pixel xv, 0 outside the principal image)
       auto point = [&](bool valid, int kk, typename H::Reg r, double xv) {
-        const bool fl = valid && H::dup(r);
-        if (valid) {
-          if (kk != kacc) {
-            flush();
-            kacc = kk;
+        // a lane moving on to the next window adds its sums to the window's LDS row; when the whole wave moves on
+        // together from one window (the common case: 64 consecutive stream positions), one lane adds the wave's
+        const bool ch = valid && kk != kacc;
+        const uint64_t cm = __ballot(ch);
+        if (cm != 0ull) {
+          const int k0 = __builtin_amdgcn_readfirstlane(kacc);
+          if (cm == __ballot(true) && __all(kacc == k0)) {
+            const double t0 = wave_sum_dpp(as), t1 = wave_sum_dpp(axy);
+            if ((threadIdx.x & 63) == 0 && !(SMG_WIDE_EXP & 2)) {
+              atomicAdd(&kst[0 * MAXK_DENSE + k0 + 1], t0);
+              atomicAdd(&kst[3 * MAXK_DENSE + k0 + 1], t1);
+            }
+            as = axy = 0.0;
+          } else if (ch) {
+            if (!(SMG_WIDE_EXP & 2) && (as != 0.0 || axy != 0.0)) {
+              atomicAdd(&kst[0 * MAXK_DENSE + kacc + 1], as);
+              atomicAdd(&kst[3 * MAXK_DENSE + kacc + 1], axy);
+            }
+            as = axy = 0.0;
           }
-          if (!fl) {
-            const double y = H::val(r);
-            a2[1] += y;
-            a2[2] += y * y;
-            a2[3] += xv * y;
-            if (xv > 0.0) a2[0] += y;
-          }
+          if (ch) kacc = kk;
         }
+        const double y = H::val(r);
+        if (xv > 0.0) as += y;
+        axy += xv * y;
+        const bool fl = valid && H::dup(r);
         const int idx = wave_append(fl, &sh_ctr[2]);
         if (fl) {
           if (idx < WIDE_DL) {
-            S.dkey[idx] = (uint32_t)kacc * (uint32_t)npx + H::pix(r);
-            S.dval[idx] = H::val(r);
+            S.dkey[idx] = (uint32_t)kk * (uint32_t)npx + H::pix(r);
+            S.dval[idx] = y;
           } else {
             sh_ctr[3] = 1;
           }
@@ -2595,7 +2613,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
           for (int u = 0; u < TDU; ++u) {
             const int64_t v = v0 + (int64_t)u * DBLOCK + tid;
             const uint32_t p = H::pix(r[u]);
-            const bool pr = !(SMG_WIDE_EXP & 1) && v < T && !H::dup(r[u]) && R.test(p);
+            const bool pr = !(SMG_WIDE_EXP & 1) && v < T && R.test(p);
             pm |= (uint32_t)pr << u;
             ld8_async_agent(xb[u], pr ? (const void*)&S.vals[R.rank(p)] : (const void*)S.vals);
           }
@@ -2636,12 +2654,15 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
           for (int u = 0; u < WDU; ++u) {
             const int64_t v = v0 + (int64_t)u * DBLOCK + tid;
             const uint32_t p = H::pix(r[u]);
-            const double xv = (v < T && !H::dup(r[u]) && R.test(p)) ? ld_agent(&S.vals[R.rank(p)]) : 0.0;
+            const double xv = (v < T && R.test(p)) ? ld_agent(&S.vals[R.rank(p)]) : 0.0;
             point(v < T, kc[u], r[u], xv);
           }
         }
       }
-      flush();
+      if (!(SMG_WIDE_EXP & 2) && (as != 0.0 || axy != 0.0)) {
+        atomicAdd(&kst[0 * MAXK_DENSE + kacc + 1], as);
+        atomicAdd(&kst[3 * MAXK_DENSE + kacc + 1], axy);
+      }
       __syncthreads();
       const int nd = min(sh_ctr[2], WIDE_DL);
       if (nd > 0) {
@@ -2669,16 +2690,12 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
         }
         slot_sync();  // the table's sums are complete in L2
         const int no = sh_nown;
-        for (int j = tid; j < no; j += DBLOCK) {  // claimed entries: add their pixels, then release them
+        for (int j = tid; j < no; j += DBLOCK) {  // claimed entries: add their pixel's (Σy)², then release them
           const uint32_t s = S.hown[j];
           const uint32_t key = ld_agent(&S.hkey[s]);
           const double y = ld_agent(&S.hval[s]);
-          const uint32_t k = key / (uint32_t)npx, p = key - k * (uint32_t)npx;
-          const double xv = R.test(p) ? ld_agent(&S.vals[R.rank(p)]) : 0.0;
-          atomicAdd(&kst[0 * MAXK_DENSE + k + 1], xv > 0.0 ? y : 0.0);
-          atomicAdd(&kst[1 * MAXK_DENSE + k + 1], y);
+          const uint32_t k = key / (uint32_t)npx;
           atomicAdd(&kst[2 * MAXK_DENSE + k + 1], y * y);
-          atomicAdd(&kst[3 * MAXK_DENSE + k + 1], xv * y);
           S.hkey[s] = WIDE_EMPTY;
           S.hval[s] = 0.0;
         }
@@ -2693,7 +2710,9 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
 
     STAMP(12);
     double chaos_raw = NAN;
-    if (chaos_ok) {
+    const double npos = sh_st[3];
+    if ((sh_st[0] > 0.0) && (npos >= 4.0)) {
+      const double vmax = sh_st[4];
       for (int r0 = tid; r0 < np; r0 += DBLOCK * WDU) {
         uint64_t vb[WDU];
 #pragma unroll
@@ -2867,9 +2886,9 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     }
 
     if (tid == 0) {
-      kst[0] = s0;
+      kst[0] = sh_st[2];
       kst[1 * MAXK_DENSE] = kst[2 * MAXK_DENSE] = kst[3 * MAXK_DENSE] = 0.0;
-      finalize_ion(K, theor + w0, kst, sx, sxx, kst + MAXK_DENSE, kst + 2 * MAXK_DENSE, kst + 3 * MAXK_DENSE,
+      finalize_ion(K, theor + w0, kst, sh_st[0], sh_st[1], kst + MAXK_DENSE, kst + 2 * MAXK_DENSE, kst + 3 * MAXK_DENSE,
                    (double)npx, chaos_raw, ion, flags, oc, osp, osc, omsm, oflags);
     }
     STAMP(15);
@@ -3028,7 +3047,8 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   if (!P.clip && g_force_dense != 2 && wide_lds <= WIDE_LDS_MAX) {
     SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ion_wide_kernel<FMT>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)wide_lds));
-    hipLaunchKernelGGL(ion_wide_kernel<FMT>, dim3((unsigned)nslots), dim3(DBLOCK), wide_lds, st, hits, lo, hi, ion_off,
+    hipLaunchKernelGGL(ion_wide_kernel<FMT>, dim3((unsigned)nslots), dim3(DBLOCK), wide_lds, st, hits,
+                       reinterpret_cast<const DD4*>(hit_cum), lo, hi, ion_off,
                        theor, P, list_b, hdr + 2, hdr + 3, list_a, hdr + 4, slots, slot_bytes, oc, osp, osc, omsm,
                        oflags);
     SMG_LAUNCH_CHECK();
