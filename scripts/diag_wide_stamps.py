@@ -30,8 +30,8 @@ nw = int(((f & 0x20) != 0).sum())
 w = (hi - lo).cpu().numpy()
 print(f"{nrows}x{ncols} P={pk:g}: {dions.n_ions} ions, launch {dt*1e3:.1f} ms, {nw} wide ions, "
       f"mean window points {w.mean():.0f}")
-names = {10: "pass1+rank", 11: "pass2+stats", 12: "tail windows", 13: "levels", 14: "screen+candidates",
-         15: "kruskal+finalize+fetch"}
+names = {10: "pass1+rank", 11: "pass2+stats", 12: "tail windows", 13: "levels", 8: "screen: dilate",
+         9: "screen: erode+list", 14: "candidates exact eL", 15: "kruskal+finalize+fetch"}
 tot = sum(buf[i] for i in names)
 for i, nm in names.items():
     print(f"  {nm:20s} {buf[i]/max(nw,1):10.0f} cycles/ion  {100*buf[i]/max(tot,1):5.1f}%")

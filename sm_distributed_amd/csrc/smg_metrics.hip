@@ -2275,7 +2275,6 @@ constexpr int TDU = SMG_TDU;  // wide pass, pipelined tail stream: points per la
 
 struct WideSlot {
   double* vals;     // principal values by rank
-  uint32_t* plist;  // principal pixels by rank
   uint32_t* epix;   // chaos candidates in discovery order
   uint32_t* epr;    // chaos candidates by rank
   uint32_t* par;    // union-find over candidate ranks
@@ -2287,11 +2286,13 @@ struct WideSlot {
   uint32_t* hown;
   uint32_t* dkey;   // flagged tail points of the ion: (window, pixel) key and value
   double* dval;
+  uint64_t* dmap;   // dilate_cross of the presence bitmap (chaos screen), n64 + 1 words
 };
 
 static inline size_t wide_slot_bytes(int npx) {
-  return al16((size_t)npx * 8) + al16((size_t)npx * 4) * 4 + al16((size_t)npx) * 3 + al16((size_t)WIDE_HT * 4) * 2 +
-         al16((size_t)WIDE_HT * 8) + al16((size_t)WIDE_DL * 4) + al16((size_t)WIDE_DL * 8) + 256;
+  return al16((size_t)npx * 8) + al16((size_t)npx * 4) * 3 + al16((size_t)npx) * 3 + al16((size_t)WIDE_HT * 4) * 2 +
+         al16((size_t)WIDE_HT * 8) + al16((size_t)WIDE_DL * 4) + al16((size_t)WIDE_DL * 8) +
+         al16(((size_t)npx + 63) / 64 * 8 + 8) + 256;
 }
 
 __device__ __forceinline__ WideSlot wide_slot(unsigned char* base, int npx) {
@@ -2300,8 +2301,6 @@ __device__ __forceinline__ WideSlot wide_slot(unsigned char* base, int npx) {
   size_t o = 0;
   S.vals = reinterpret_cast<double*>(base + o);
   o += a16((size_t)npx * 8);
-  S.plist = reinterpret_cast<uint32_t*>(base + o);
-  o += a16((size_t)npx * 4);
   S.epix = reinterpret_cast<uint32_t*>(base + o);
   o += a16((size_t)npx * 4);
   S.epr = reinterpret_cast<uint32_t*>(base + o);
@@ -2323,6 +2322,8 @@ __device__ __forceinline__ WideSlot wide_slot(unsigned char* base, int npx) {
   S.dval = reinterpret_cast<double*>(base + o);
   o += a16((size_t)WIDE_DL * 8);
   S.dkey = reinterpret_cast<uint32_t*>(base + o);
+  o += a16((size_t)WIDE_DL * 4);
+  S.dmap = reinterpret_cast<uint64_t*>(base + o);
   return S;
 }
 
@@ -2365,6 +2366,34 @@ __device__ __forceinline__ void ld8_async_agent(uint64_t& r, const void* addr) {
   asm volatile("global_load_dwordx2 %0, %1, off sc1" : "+v"(r) : "v"(addr) : "memory");
 }
 
+// 64 bits of a flat pixel bitmap at positions off .. off + 63 (0 before position 0 and from word n64 on;
+// words[n64] must be zero)
+__device__ __forceinline__ uint64_t bits_at(const uint64_t* words, int64_t off, int n64) {
+  if (off <= -64) return 0ull;
+  if (off < 0) return words[0] << (uint32_t)(-off);
+  const int64_t wi = off >> 6;
+  if (wi >= n64) return 0ull;
+  const uint32_t sh = (uint32_t)(off & 63);
+  const uint64_t lo = words[wi];
+  return sh ? ((lo >> sh) | (words[wi + 1] << (64u - sh))) : lo;
+}
+
+// bits j of positions base + j (base >= 0) in lo <= base + j < hi
+__device__ __forceinline__ uint64_t range_mask(int64_t base, int64_t lo, int64_t hi) {
+  const int64_t a = lo - base > 0 ? lo - base : 0, b = hi - base < 64 ? hi - base : 64;
+  if (a >= b) return 0ull;
+  const uint64_t upto = (b >= 64) ? ~0ull : ((1ull << b) - 1ull);
+  return upto & ~((1ull << a) - 1ull);
+}
+
+// bits j of positions base + j (base >= 0) in column 0 / column nc - 1 of an nc-column image
+__device__ __forceinline__ void col_masks(int64_t base, int nc, uint64_t& c0, uint64_t& cl) {
+  const int c = (int)(base % nc);
+  c0 = cl = 0ull;
+  for (int j = (c == 0) ? 0 : nc - c; j < 64; j += nc) c0 |= 1ull << j;
+  for (int j = nc - 1 - c; j < 64; j += nc) cl |= 1ull << j;
+}
+
 struct RankBits {
   const uint64_t* bm;
   const uint16_t* pf;
@@ -2391,6 +2420,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
   __shared__ int sh_ion;
   __shared__ int sh_ctr[4];  // candidates, max eL, listed flagged tail points, list / table overflow
   __shared__ int sh_nown;    // claimed table entries
+  __shared__ int sh_ncand;   // screened chaos candidates
   __shared__ double sh_st[5];  // principal sums: x, x^2, x[x > 0], #(x > 0); max
   __shared__ int64_t sh_tb[MAXK_DENSE + 1];  // tail stream: offset of window k at k - 1 (+ the total)
   __shared__ int64_t sh_tlo[MAXK_DENSE];     // first point of window k at k - 1
@@ -2418,6 +2448,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
       sh_ion = (k < total) ? (int)list[k] : -1;
       sh_ctr[0] = sh_ctr[1] = sh_ctr[2] = sh_ctr[3] = 0;
       sh_nown = 0;
+      sh_ncand = 0;
     }
     __syncthreads();
     const int64_t ion = sh_ion;
@@ -2475,7 +2506,6 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
         if (i < b0) {
           const uint32_t p = H::pix(r[u]);
           const uint32_t k = R.rank(p);
-          S.plist[k] = p;
           if (H::dup(r[u])) atomicAdd(&S.vals[k], H::val(r[u]));
           else S.vals[k] = H::val(r[u]);
         }
@@ -2728,107 +2758,111 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
       }
       slot_sync();
       STAMP(13);
-      // candidates as in ion_dense_kernel: the 4-cross around each principal pixel, owned by the first principal
-      // pixel on its cross, screened over the 3x3 box by presence; the 7x7 level window of a pixel with a
-      // surviving candidate is read by rank (one rank per row, the rest by popcount of the row's bits)
-      for (int i0 = 0; i0 < np; i0 += DBLOCK) {
-        const int i = i0 + tid;
-        const int p = (i < np) ? (int)S.plist[i] : -1;
-        const int r0 = p >= 0 ? p / nc : 0, c0 = p >= 0 ? p - r0 * nc : 0;
-        uint32_t B[7];
-#pragma unroll
-        for (int dr = -3; dr <= 3; ++dr) B[dr + 3] = p >= 0 ? pres.row7(r0 + dr, c0, nr, nc) : 0u;
-        auto bit = [&](int wr, int wc) -> uint32_t { return (B[wr] >> wc) & 1u; };
-        bool cand[5];
-        bool any = false;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-          const int qr = (j == 1) ? -1 : (j == 2) ? 1 : 0, qc = (j == 3) ? -1 : (j == 4) ? 1 : 0;
-          const int r = r0 + qr, c = c0 + qc;
-          bool ok = p >= 0 && r >= 0 && r < nr && c >= 0 && c < nc;
-          const int wr = qr + 3, wc = qc + 3;
-          if (ok) {
-            int orr = 9, occ = 9;
-            if (bit(wr + 1, wc)) orr = 1, occ = 0;
-            if (bit(wr, wc + 1)) orr = 0, occ = 1;
-            if (bit(wr, wc)) orr = 0, occ = 0;
-            if (bit(wr, wc - 1)) orr = 0, occ = -1;
-            if (bit(wr - 1, wc)) orr = -1, occ = 0;
-            ok = (qr + orr == 0 && qc + occ == 0);
-          }
-          if (ok) {
-#pragma unroll
-            for (int a = -1; a <= 1; ++a)
-#pragma unroll
-              for (int b = -1; b <= 1; ++b) {
-                const int rr = r + a, cc = c + b;
-                if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) {
-                  if (!P.erosion_border) ok = false;
-                  continue;
-                }
-                const int ur = wr + a, uc = wc + b;
-                if (!(bit(ur, uc) | bit(ur - 1, uc) | bit(ur + 1, uc) | bit(ur, uc - 1) | bit(ur, uc + 1)))
-                  ok = false;
-              }
-          }
-          cand[j] = ok;
-          any |= ok;
+      // candidates: eL = erode_box(dilate_cross(L)) >= 1 only where erode_box(dilate_cross(presence)) is set
+      // (presence is a superset of L >= 1).  That screen is computed 64 pixels at a time on the flat bitmap:
+      // D = dilate_cross(P) into the slot, then E = erode_box(D) with the image border, E's pixels listed; the
+      // exact eL of each listed pixel reads the levels of its 5x5 neighbourhood by rank.
+      const int64_t npx64 = npx;
+      for (int w0 = 0; w0 <= n64; w0 += DBLOCK) {
+        const int w = w0 + tid;
+        if (w < n64) {
+          const int64_t base = (int64_t)w * 64;
+          uint64_t c0m, clm;
+          col_masks(base, nc, c0m, clm);
+          const uint64_t d = bm[w] | (bits_at(bm, base - 1, n64) & ~c0m) | (bits_at(bm, base + 1, n64) & ~clm) |
+                             bits_at(bm, base - nc, n64) | bits_at(bm, base + nc, n64);
+          S.dmap[w] = d & range_mask(base, 0, npx64);
+        } else if (w == n64) {
+          S.dmap[w] = 0ull;
         }
-        uint64_t WL[7];
+      }
+      slot_sync();
+      STAMP(8);
+      for (int w0 = 0; w0 < n64; w0 += DBLOCK) {  // uniform trip count: DPP scan below
+        const int w = w0 + tid;
+        const int64_t base = (int64_t)w * 64;
+        uint64_t e = 0ull;
+        if (w < n64) {
+          uint64_t c0m, clm;
+          col_masks(base, nc, c0m, clm);
+          const uint64_t rf = range_mask(base, 0, nc), rl = range_mask(base, npx64 - nc, npx64);
+          e = range_mask(base, 0, npx64);
 #pragma unroll
-        for (int dr = 0; dr < 7; ++dr) WL[dr] = 0ull;
-        if (any) {
+          for (int a = -1; a <= 1; ++a)
 #pragma unroll
-          for (int dr = -3; dr <= 3; ++dr) {
-            const uint32_t row = B[dr + 3];
+            for (int b = -1; b <= 1; ++b) {
+              uint64_t t = bits_at(S.dmap, base + (int64_t)a * nc + b, n64);
+              const uint64_t oob = (a < 0 ? rf : 0ull) | (a > 0 ? rl : 0ull) | (b < 0 ? c0m : 0ull) |
+                                   (b > 0 ? clm : 0ull);
+              t = P.erosion_border ? (t | oob) : (t & ~oob);
+              e &= t;
+            }
+        }
+        const int cnt = __popcll(e);
+        const int incl = wave_incl_scan_dpp(cnt);
+        int wbase = 0;
+        if ((tid & 63) == 63) wbase = atomicAdd(&sh_ncand, incl);
+        wbase = __shfl(wbase, 63);
+        int idx = wbase + incl - cnt;
+        while (e != 0ull) {
+          const int j = __ffsll((unsigned long long)e) - 1;
+          S.epr[idx++] = (uint32_t)(base + j);
+          e &= e - 1ull;
+        }
+      }
+      slot_sync();
+      STAMP(9);
+      const int nscr = sh_ncand;
+      for (int i0 = 0; i0 < nscr; i0 += DBLOCK) {
+        const int i = i0 + tid;
+        const int q = (i < nscr) ? (int)S.epr[i] : -1;
+        int e = 0;
+        if (q >= 0) {
+          const int r0 = q / nc, c0 = q - r0 * nc;
+          uint64_t WL[7];  // byte (dc + 3) of WL[dr + 3]: level of pixel (r0 + dr, c0 + dc), 0 outside / absent
+          WL[0] = WL[6] = 0ull;
+#pragma unroll
+          for (int dr = -2; dr <= 2; ++dr) {
+            const uint32_t row = pres.row7(r0 + dr, c0, nr, nc);
+            uint64_t wv = 0ull;
             if (row != 0u) {
               // the row's present pixels have consecutive ranks: their levels are L[base .. base + popc(row))
-              const uint32_t base = R.rank((uint32_t)((r0 + dr) * nc + max(c0 - 3, 0)));
-              const uint64_t* la = reinterpret_cast<const uint64_t*>(S.L + (base & ~7u));
+              const uint32_t rb = R.rank((uint32_t)((r0 + dr) * nc + max(c0 - 3, 0)));
+              const uint64_t* la = reinterpret_cast<const uint64_t*>(S.L + (rb & ~7u));
               const uint64_t l0 = la[0], l1 = la[1];
-              const uint32_t sh = (base & 7u) * 8u;
+              const uint32_t sh = (rb & 7u) * 8u;
               uint64_t packed = sh ? ((l0 >> sh) | (l1 << (64u - sh))) : l0;
-              uint64_t w = 0ull;
 #pragma unroll
               for (int j = 0; j < 7; ++j)
                 if ((row >> j) & 1u) {
-                  w |= (packed & 0xFFull) << (8 * j);
+                  wv |= (packed & 0xFFull) << (8 * j);
                   packed >>= 8;
                 }
-              WL[dr + 3] = w;
             }
+            WL[dr + 3] = wv;
           }
-        }
-        auto W = [&](int wr, int wc) -> int { return (int)((WL[wr] >> (8 * wc)) & 0xFFull); };
+          auto W = [&](int wr, int wc) -> int { return (int)((WL[wr] >> (8 * wc)) & 0xFFull); };
+          e = 1 << 20;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) {
-          const int qr = (j == 1) ? -1 : (j == 2) ? 1 : 0, qc = (j == 3) ? -1 : (j == 4) ? 1 : 0;
-          const int r = r0 + qr, c = c0 + qc;
-          const int q = cand[j] ? r * nc + c : -1;
-          int e = 0;
-          if (q >= 0) {
-            e = 1 << 20;
+          for (int a = -1; a <= 1; ++a)
 #pragma unroll
-            for (int a = -1; a <= 1; ++a)
-#pragma unroll
-              for (int b = -1; b <= 1; ++b) {
-                const int rr = r + a, cc = c + b;
-                if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) {
-                  if (!P.erosion_border) e = 0;
-                  continue;
-                }
-                const int wr = qr + a + 3, wc = qc + b + 3;
-                const int t = max(max(W(wr, wc), W(wr - 1, wc)), max(max(W(wr + 1, wc), W(wr, wc - 1)), W(wr, wc + 1)));
-                e = min(e, t);
+            for (int b = -1; b <= 1; ++b) {
+              const int rr = r0 + a, cc = c0 + b;
+              if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) {
+                if (!P.erosion_border) e = 0;
+                continue;
               }
-            if (e >= (1 << 20)) e = 0;
-          }
-          const int idx = wave_append(e >= 1, &sh_ctr[0]);
-          if (e >= 1) {
-            S.epix[idx] = (uint32_t)q;
-            S.eL[idx] = (uint8_t)e;
-            atomicMax(&sh_ctr[1], e);
-          }
+              const int wr = a + 3, wc = b + 3;
+              const int t = max(max(W(wr, wc), W(wr - 1, wc)), max(max(W(wr + 1, wc), W(wr, wc - 1)), W(wr, wc + 1)));
+              e = min(e, t);
+            }
+          if (e >= (1 << 20)) e = 0;
+        }
+        const int idx = wave_append(e >= 1, &sh_ctr[0]);
+        if (e >= 1) {
+          S.epix[idx] = (uint32_t)q;
+          S.eL[idx] = (uint8_t)e;
+          atomicMax(&sh_ctr[1], e);
         }
       }
       slot_sync();
