@@ -16,6 +16,13 @@ if [ -f sm_distributed_amd/libsmg_stamps.so ]; then
   timeout -k 10 300 python3 -u scripts/diag_wide_stamps.py > gpurun_out/$TAG/stamps.txt 2>&1 \
     || { tail -20 gpurun_out/$TAG/stamps.txt; exit 1; }
   grep -v amdgpu.ids gpurun_out/$TAG/stamps.txt
+  for f in sm_distributed_amd/libsmg_stamps_x*.so; do
+    [ -f "$f" ] || continue
+    v=$(basename $f .so)
+    SMG_LIB=$f timeout -k 10 300 python3 -u scripts/diag_wide_stamps.py > gpurun_out/$TAG/stamps_$v.txt 2>&1 \
+      || { tail -20 gpurun_out/$TAG/stamps_$v.txt; exit 1; }
+    echo "== $v"; grep -v amdgpu.ids gpurun_out/$TAG/stamps_$v.txt | tail -9
+  done
 fi
 timeout -k 10 400 python -u scripts/time_paths.py 1000 1000 2100 1000 > gpurun_out/$TAG/time_paths_dense.txt 2>&1 \
   || { tail -20 gpurun_out/$TAG/time_paths_dense.txt; exit 1; }

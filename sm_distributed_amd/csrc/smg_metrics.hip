@@ -21,6 +21,7 @@
 #include <stdarg.h>
 
 #include <mutex>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -2256,13 +2257,11 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
 // candidates get their own bitmap + ranks for Kruskal (the principal bitmap is no longer needed by then).  Nothing
 // is pixel-indexed in global memory, so nothing has to be zeroed per slot; an ion whose flagged tail pixels
 // overflow the table is handed to the pixel-indexed kernel.
-constexpr int WIDE_HT_LOG2 = 14;
+constexpr int WIDE_HT_LOG2 = 13;
 constexpr int WIDE_HT = 1 << WIDE_HT_LOG2;  // tail duplicate table entries per slot
 constexpr int WIDE_PROBES = 64;
-#ifndef SMG_WIDE_EXP
-#define SMG_WIDE_EXP 0  // diagnostic builds only: 1 no x gathers, 2 no window-sum flushes, 4 no tail stream
-#endif
-constexpr int WIDE_DL = 2 * WIDE_HT;        // flagged tail points listed per ion
+constexpr int WIDE_DL = 2 * WIDE_HT;        // flagged tail points listed per ion (beyond the registers)
+constexpr int WIDE_FLR = 3;                 // flagged tail points held in a lane's registers
 constexpr uint32_t WIDE_EMPTY = 0xFFFFFFFFu;
 #ifndef SMG_WDU
 #define SMG_WDU 8
@@ -2286,13 +2285,11 @@ struct WideSlot {
   uint32_t* hown;
   uint32_t* dkey;   // flagged tail points of the ion: (window, pixel) key and value
   double* dval;
-  uint64_t* dmap;   // dilate_cross of the presence bitmap (chaos screen), n64 + 1 words
 };
 
 static inline size_t wide_slot_bytes(int npx) {
   return al16((size_t)npx * 8) + al16((size_t)npx * 4) * 3 + al16((size_t)npx) * 3 + al16((size_t)WIDE_HT * 4) * 2 +
-         al16((size_t)WIDE_HT * 8) + al16((size_t)WIDE_DL * 4) + al16((size_t)WIDE_DL * 8) +
-         al16(((size_t)npx + 63) / 64 * 8 + 8) + 256;
+         al16((size_t)WIDE_HT * 8) + al16((size_t)WIDE_DL * 4) + al16((size_t)WIDE_DL * 8) + 256;
 }
 
 __device__ __forceinline__ WideSlot wide_slot(unsigned char* base, int npx) {
@@ -2322,8 +2319,6 @@ __device__ __forceinline__ WideSlot wide_slot(unsigned char* base, int npx) {
   S.dval = reinterpret_cast<double*>(base + o);
   o += a16((size_t)WIDE_DL * 8);
   S.dkey = reinterpret_cast<uint32_t*>(base + o);
-  o += a16((size_t)WIDE_DL * 4);
-  S.dmap = reinterpret_cast<uint64_t*>(base + o);
   return S;
 }
 
@@ -2336,16 +2331,30 @@ static inline size_t wide_lds_bytes(int npx) {
 // rank structure over the LDS bitmap: #set bits before word w = sb[w >> 10] + pf[w].  A superblock of 1024 words
 // (65536 bits, so pf fits 16 bits) is one wave's: its lanes read consecutive words (no bank conflicts) and scan them
 // 64 at a time with DPP.  Needs n64 <= DNW * 1024.  Returns the bit count.
-__device__ uint32_t build_rank(const uint64_t* bm, uint16_t* pf, uint32_t* sb, int n64, uint32_t* sc) {
+// With list != nullptr the set bits' pixels are also written to list (in no particular order; *lcount = 0 first).
+__device__ uint32_t build_rank(const uint64_t* bm, uint16_t* pf, uint32_t* sb, int n64, uint32_t* sc,
+                               uint32_t* list = nullptr, int* lcount = nullptr) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int w0 = wid * 1024, w1 = min(w0 + 1024, n64);
   uint32_t run = 0;
   for (int c = w0; c < w1; c += 64) {
     const int w = c + lane;
-    const int x = w < w1 ? __popcll(bm[w]) : 0;
+    uint64_t bits = w < w1 ? bm[w] : 0ull;
+    const int x = __popcll(bits);
     const int incl = wave_incl_scan_dpp(x);
     if (w < w1) pf[w] = (uint16_t)(run + (uint32_t)(incl - x));
-    run += (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+    const int tot = __builtin_amdgcn_readlane(incl, 63);
+    run += (uint32_t)tot;
+    if (list != nullptr) {
+      int lb = 0;
+      if (lane == 63) lb = atomicAdd(lcount, tot);
+      lb = __shfl(lb, 63);
+      int idx = lb + incl - x;
+      while (bits != 0ull) {
+        list[idx++] = (uint32_t)w * 64u + (uint32_t)(__ffsll((unsigned long long)bits) - 1);
+        bits &= bits - 1ull;
+      }
+    }
   }
   if (lane == 0) sc[wid] = run;
   __syncthreads();
@@ -2361,37 +2370,14 @@ __device__ uint32_t build_rank(const uint64_t* bm, uint16_t* pf, uint32_t* sb, i
   return tot;
 }
 
-// 8-byte load past L1 (agent scope, like ld_agent) issued asynchronously: waited for with vm_wait
+// 8-byte load past L1 (agent scope, like ld_agent) issued asynchronously: waited for with vm_wait.  No memory
+// clobber (the wide pass's loads read data made visible by an earlier slot_sync, whose asm orders them): the
+// compiler may keep scheduling LDS and address work around them.
 __device__ __forceinline__ void ld8_async_agent(uint64_t& r, const void* addr) {
-  asm volatile("global_load_dwordx2 %0, %1, off sc1" : "+v"(r) : "v"(addr) : "memory");
+  asm volatile("global_load_dwordx2 %0, %1, off sc1" : "+v"(r) : "v"(addr));
 }
-
-// 64 bits of a flat pixel bitmap at positions off .. off + 63 (0 before position 0 and from word n64 on;
-// words[n64] must be zero)
-__device__ __forceinline__ uint64_t bits_at(const uint64_t* words, int64_t off, int n64) {
-  if (off <= -64) return 0ull;
-  if (off < 0) return words[0] << (uint32_t)(-off);
-  const int64_t wi = off >> 6;
-  if (wi >= n64) return 0ull;
-  const uint32_t sh = (uint32_t)(off & 63);
-  const uint64_t lo = words[wi];
-  return sh ? ((lo >> sh) | (words[wi + 1] << (64u - sh))) : lo;
-}
-
-// bits j of positions base + j (base >= 0) in lo <= base + j < hi
-__device__ __forceinline__ uint64_t range_mask(int64_t base, int64_t lo, int64_t hi) {
-  const int64_t a = lo - base > 0 ? lo - base : 0, b = hi - base < 64 ? hi - base : 64;
-  if (a >= b) return 0ull;
-  const uint64_t upto = (b >= 64) ? ~0ull : ((1ull << b) - 1ull);
-  return upto & ~((1ull << a) - 1ull);
-}
-
-// bits j of positions base + j (base >= 0) in column 0 / column nc - 1 of an nc-column image
-__device__ __forceinline__ void col_masks(int64_t base, int nc, uint64_t& c0, uint64_t& cl) {
-  const int c = (int)(base % nc);
-  c0 = cl = 0ull;
-  for (int j = (c == 0) ? 0 : nc - c; j < 64; j += nc) c0 |= 1ull << j;
-  for (int j = nc - 1 - c; j < 64; j += nc) cl |= 1ull << j;
+__device__ __forceinline__ void ld8_async_nm(uint64_t& r, const void* addr) {
+  asm volatile("global_load_dwordx2 %0, %1, off" : "+v"(r) : "v"(addr));
 }
 
 struct RankBits {
@@ -2421,9 +2407,11 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
   __shared__ int sh_ctr[4];  // candidates, max eL, listed flagged tail points, list / table overflow
   __shared__ int sh_nown;    // claimed table entries
   __shared__ int sh_ncand;   // screened chaos candidates
+  __shared__ int sh_anyfl;   // the ion's tail stream met a flagged point
   __shared__ double sh_st[5];  // principal sums: x, x^2, x[x > 0], #(x > 0); max
   __shared__ int64_t sh_tb[MAXK_DENSE + 1];  // tail stream: offset of window k at k - 1 (+ the total)
   __shared__ int64_t sh_tlo[MAXK_DENSE];     // first point of window k at k - 1
+  __shared__ int64_t sh_tn[MAXK_DENSE];      // length of window k at k - 1
   const int tid = threadIdx.x;
   const int npx = P.npx, n64 = (npx + 63) / 64, nsb = (n64 + 1023) / 1024;
   uint64_t* bm = wide_dyn;  // n64 words + one zero word (row7 reads one word past a row's start)
@@ -2449,6 +2437,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
       sh_ctr[0] = sh_ctr[1] = sh_ctr[2] = sh_ctr[3] = 0;
       sh_nown = 0;
       sh_ncand = 0;
+      sh_anyfl = 0;
     }
     __syncthreads();
     const int64_t ion = sh_ion;
@@ -2475,9 +2464,9 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     for (int64_t i0 = a0; i0 < b0; i0 += (int64_t)DBLOCK * WDU) {
       typename H::Reg r[WDU];
 #pragma unroll
-      for (int u = 0; u < WDU; ++u) {
+      for (int u = 0; u < WDU; ++u) {  // unconditional loads (clamped index): counted waits, not vmcnt(0)
         const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
-        r[u] = i < b0 ? hits.load(i) : H::zero();
+        r[u] = hits.load(i < b0 ? i : b0 - 1);
       }
 #pragma unroll
       for (int u = 0; u < WDU; ++u) {
@@ -2489,16 +2478,16 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
       }
     }
     __syncthreads();
-    const int np = (int)build_rank(bm, pf, sb, n64, sc);
+    const int np = (int)build_rank(bm, pf, sb, n64, sc, S.par, &sh_ncand);  // principal pixels listed in par
     STAMP(10);
     for (int r = tid; r < np; r += DBLOCK) S.vals[r] = 0.0;  // flagged points add into their rank
     slot_sync();
     for (int64_t i0 = a0; i0 < b0; i0 += (int64_t)DBLOCK * WDU) {
       typename H::Reg r[WDU];
 #pragma unroll
-      for (int u = 0; u < WDU; ++u) {
+      for (int u = 0; u < WDU; ++u) {  // unconditional loads (clamped index): counted waits, not vmcnt(0)
         const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
-        r[u] = i < b0 ? hits.load(i) : H::zero();
+        r[u] = hits.load(i < b0 ? i : b0 - 1);
       }
 #pragma unroll
       for (int u = 0; u < WDU; ++u) {
@@ -2554,12 +2543,18 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     // over the windows' concatenated points (a lane's window index only grows along it) adds x·y and [x>0]·y of
     // every point whose pixel is principal, x gathered by rank.  Flagged points are listed and summed per
     // (window, pixel) in the table, which adds (Σy)² of each entry to Σy².
+    // the stream runs over the tail windows in batches of TSTEP positions (one per lane and u); each window starts
+    // on a batch boundary (its length padded), so a batch lies in one window: the window index is uniform
+    constexpr int64_t TSTEP = (int64_t)DBLOCK * (FMT == SMG_HITS_PACKED_F32 ? TDU : WDU);
     if (tid < 4 * MAXK_DENSE) kst[tid] = 0.0;
     if (tid <= K - 1) {
       int64_t n = 0;
-      for (int k = 1; k <= tid; ++k) n += hi[w0 + k] - lo[w0 + k];
-      sh_tb[tid] = n;  // sh_tb[k - 1]: stream offset of window k
-      if (tid < K - 1) sh_tlo[tid] = lo[w0 + 1 + tid];
+      for (int k = 1; k <= tid; ++k) n += (hi[w0 + k] - lo[w0 + k] + TSTEP - 1) / TSTEP * TSTEP;
+      sh_tb[tid] = n;  // sh_tb[k - 1]: stream offset of window k (padded lengths before it)
+      if (tid < K - 1) {
+        sh_tlo[tid] = lo[w0 + 1 + tid];
+        sh_tn[tid] = hi[w0 + 1 + tid] - lo[w0 + 1 + tid];
+      }
     }
     __syncthreads();
     if (tid < K - 1) {
@@ -2568,140 +2563,157 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
       kst[2 * MAXK_DENSE + tid + 1] = ws.y;
     }
     {
-      const int64_t T = (SMG_WIDE_EXP & 4) ? 0 : sh_tb[K - 1];
-      double as = 0.0, axy = 0.0;  // Σy[x > 0], Σxy of window kacc
+      const int64_t T = sh_tb[K - 1];
+      double as = 0.0, axy = 0.0;  // the lane's Σy[x > 0], Σxy in window kacc
       int kacc = 0;
-      // one tail point (stream window kk, hit r, x at its pixel xv, 0 outside the principal image)
-      auto point = [&](bool valid, int kk, typename H::Reg r, double xv) {
-        // a lane moving on to the next window adds its sums to the window's LDS row; when the whole wave moves on
-        // together from one window (the common case: 64 consecutive stream positions), one lane adds the wave's
-        const bool ch = valid && kk != kacc;
-        const uint64_t cm = __ballot(ch);
-        if (cm != 0ull) {
-          const int k0 = __builtin_amdgcn_readfirstlane(kacc);
-          if (cm == __ballot(true) && __all(kacc == k0)) {
-            const double t0 = wave_sum_dpp(as), t1 = wave_sum_dpp(axy);
-            if ((threadIdx.x & 63) == 0 && !(SMG_WIDE_EXP & 2)) {
-              atomicAdd(&kst[0 * MAXK_DENSE + k0 + 1], t0);
-              atomicAdd(&kst[3 * MAXK_DENSE + k0 + 1], t1);
-            }
-            as = axy = 0.0;
-          } else if (ch) {
-            if (!(SMG_WIDE_EXP & 2) && (as != 0.0 || axy != 0.0)) {
-              atomicAdd(&kst[0 * MAXK_DENSE + kacc + 1], as);
-              atomicAdd(&kst[3 * MAXK_DENSE + kacc + 1], axy);
-            }
-            as = axy = 0.0;
-          }
-          if (ch) kacc = kk;
+      auto wflush = [&]() {  // uniform: the wave's sums of window kacc into its LDS row
+        const double t0 = wave_sum_dpp(as), t1 = wave_sum_dpp(axy);
+        if ((tid & 63) == 0) {
+          atomicAdd(&kst[0 * MAXK_DENSE + kacc + 1], t0);
+          atomicAdd(&kst[3 * MAXK_DENSE + kacc + 1], t1);
         }
-        const double y = H::val(r);
-        if (xv > 0.0) as += y;
-        axy += xv * y;
-        const bool fl = valid && H::dup(r);
-        const int idx = wave_append(fl, &sh_ctr[2]);
-        if (fl) {
-          if (idx < WIDE_DL) {
-            S.dkey[idx] = (uint32_t)kk * (uint32_t)npx + H::pix(r);
-            S.dval[idx] = y;
-          } else {
-            sh_ctr[3] = 1;
+        as = axy = 0.0;
+      };
+      // the flagged points of a batch (bit u of flm: point u) stay in the lane's registers (WIDE_FLR of them;
+      // ~2% of the points are flagged): no stores in the stream, whose counted waits would then wait for them.
+      // A lane's further flagged points go to the global list (rare).
+      using YT = std::conditional_t<FMT == SMG_HITS_PACKED_F32, float, double>;  // exact: packed values are f32
+      uint32_t fk[WIDE_FLR];
+      YT fv[WIDE_FLR];
+      int fc = 0;
+#pragma unroll
+      for (int j = 0; j < WIDE_FLR; ++j) {
+        fk[j] = 0u;
+        fv[j] = (YT)0;
+      }
+      auto append = [&](uint32_t flm, int kw, const auto& rs, int n) {
+        for (int u = 0; u < n; ++u)
+          if ((flm >> u) & 1u) {
+            const uint32_t key = (uint32_t)kw * (uint32_t)npx + H::pix(rs[u]);
+            const YT y = (YT)H::val(rs[u]);
+            if (fc < WIDE_FLR) {
+#pragma unroll
+              for (int j = 0; j < WIDE_FLR; ++j)
+                if (fc == j) {
+                  fk[j] = key;
+                  fv[j] = y;
+                }
+            } else {
+              const int idx = atomicAdd(&sh_ctr[2], 1);
+              if (idx < WIDE_DL) {
+                S.dkey[idx] = key;
+                S.dval[idx] = (double)y;
+              } else {
+                sh_ctr[3] = 1;
+              }
+            }
+            ++fc;
+            sh_anyfl = 1;
           }
-        }
       };
       if constexpr (FMT == SMG_HITS_PACKED_F32) {
         // software pipeline over batches of TDU points per lane (two register sets): wait for a batch's hits,
         // issue the x gathers of its principal pixels and then the next batch's hits, wait for the gathers only
-        // (all but the TDU youngest operations), accumulate.  Every lane issues every load (a safe address when
-        // it has none) so that the counted waits hold per wave.
-        constexpr int64_t STEP = (int64_t)DBLOCK * TDU;
+        // (all but the TDU youngest operations), accumulate.  Every lane issues every load (a clamped index or
+        // a safe address when it has none) so that the counted waits hold per wave.
         const uint64_t* hb = hits.h;
         uint64_t rA[TDU], rB[TDU], xb[TDU];
-        int kA[TDU], kB[TDU];
 #pragma unroll
-        for (int u = 0; u < TDU; ++u) {
-          rA[u] = rB[u] = xb[u] = 0ull;
-          kA[u] = kB[u] = 0;
-        }
-        auto issue = [&](int64_t v0, uint64_t (&r)[TDU], int (&kk)[TDU]) {
+        for (int u = 0; u < TDU; ++u) rA[u] = rB[u] = xb[u] = 0ull;
+        int ki = 0;  // window of the last batch issued (uniform)
+        auto issue = [&](int64_t v0, uint64_t (&r)[TDU]) -> int {
+          while (v0 >= sh_tb[ki + 1]) ++ki;
+          ki = __builtin_amdgcn_readfirstlane(ki);
+          const int64_t off = v0 - sh_tb[ki], n = sh_tn[ki], a = sh_tlo[ki];
 #pragma unroll
           for (int u = 0; u < TDU; ++u) {
-            const int64_t v = v0 + (int64_t)u * DBLOCK + tid;
-            int64_t i = 0;
-            if (v < T) {
-              while (v >= sh_tb[kk[u] + 1]) ++kk[u];
-              i = sh_tlo[kk[u]] + (v - sh_tb[kk[u]]);
-            }
-            ld8_async_v(r[u], hb + i);
+            const int64_t lv = off + (int64_t)u * DBLOCK + tid;
+            ld8_async_nm(r[u], hb + a + (lv < n ? lv : n - 1));
           }
+          return ki;
         };
-        auto batch = [&](int64_t v0, uint64_t (&r)[TDU], const int (&kk)[TDU], uint64_t (&rn)[TDU],
-                         int (&kn)[TDU]) {
+        auto batch = [&](int64_t v0, uint64_t (&r)[TDU], int kb, uint64_t (&rn)[TDU], int& kn) {
           vm_wait<0>(r);
-          uint32_t pm = 0u;
+          const int64_t off = v0 - sh_tb[kb], n = sh_tn[kb];
+          uint32_t pm = 0u, vm = 0u;
+          uint32_t rk[TDU];
 #pragma unroll
           for (int u = 0; u < TDU; ++u) {
-            const int64_t v = v0 + (int64_t)u * DBLOCK + tid;
+            const bool valid = off + (int64_t)u * DBLOCK + tid < n;
             const uint32_t p = H::pix(r[u]);
-            const bool pr = !(SMG_WIDE_EXP & 1) && v < T && R.test(p);
+            const bool pr = valid && R.test(p);
+            vm |= (uint32_t)valid << u;
             pm |= (uint32_t)pr << u;
-            ld8_async_agent(xb[u], pr ? (const void*)&S.vals[R.rank(p)] : (const void*)S.vals);
+            rk[u] = pr ? R.rank(p) : 0u;
           }
-          if (v0 + STEP < T) {
-            issue(v0 + STEP, rn, kn);
+#pragma unroll
+          for (int u = 0; u < TDU; ++u) ld8_async_agent(xb[u], &S.vals[rk[u]]);
+          if (v0 + TSTEP < T) {
+            kn = issue(v0 + TSTEP, rn);
             vm_wait<TDU>(xb);
           } else {
             vm_wait<0>(xb);
           }
+          if (kb != kacc) {
+            wflush();
+            kacc = kb;
+          }
+          uint32_t flm = 0u;
 #pragma unroll
           for (int u = 0; u < TDU; ++u) {
-            const int64_t v = v0 + (int64_t)u * DBLOCK + tid;
-            point(v < T, kk[u], r[u], ((pm >> u) & 1u) ? __longlong_as_double((long long)xb[u]) : 0.0);
+            const double y = H::val(r[u]);
+            const double xv = ((pm >> u) & 1u) ? __longlong_as_double((long long)xb[u]) : 0.0;
+            if (xv > 0.0) as += y;
+            axy += xv * y;
+            flm |= (uint32_t)(((vm >> u) & 1u) && H::dup(r[u])) << u;
           }
+          append(flm, kb, r, TDU);
         };
-        if (T > 0) issue(0, rA, kA);
-        for (int64_t v0 = 0; v0 < T; v0 += 2 * STEP) {
+        int kA = 0, kB = 0;
+        if (T > 0) kA = issue(0, rA);
+        for (int64_t v0 = 0; v0 < T; v0 += 2 * TSTEP) {
           batch(v0, rA, kA, rB, kB);
-          if (v0 + STEP >= T) break;
-          batch(v0 + STEP, rB, kB, rA, kA);
+          if (v0 + TSTEP >= T) break;
+          batch(v0 + TSTEP, rB, kB, rA, kA);
         }
       } else {
-        int kc[WDU];
-#pragma unroll
-        for (int u = 0; u < WDU; ++u) kc[u] = 0;
-        for (int64_t v0 = 0; v0 < T; v0 += (int64_t)DBLOCK * WDU) {
+        int kb = 0;
+        for (int64_t v0 = 0; v0 < T; v0 += TSTEP) {
+          while (v0 >= sh_tb[kb + 1]) ++kb;
+          kb = __builtin_amdgcn_readfirstlane(kb);
+          if (kb != kacc) {
+            wflush();
+            kacc = kb;
+          }
+          const int64_t off = v0 - sh_tb[kb], n = sh_tn[kb], a = sh_tlo[kb];
           typename H::Reg r[WDU];
 #pragma unroll
           for (int u = 0; u < WDU; ++u) {
-            const int64_t v = v0 + (int64_t)u * DBLOCK + tid;
-            r[u] = H::zero();
-            if (v < T) {
-              while (v >= sh_tb[kc[u] + 1]) ++kc[u];
-              r[u] = hits.load(sh_tlo[kc[u]] + (v - sh_tb[kc[u]]));
-            }
+            const int64_t lv = off + (int64_t)u * DBLOCK + tid;
+            r[u] = hits.load(a + (lv < n ? lv : n - 1));
           }
+          uint32_t flm = 0u;
 #pragma unroll
           for (int u = 0; u < WDU; ++u) {
-            const int64_t v = v0 + (int64_t)u * DBLOCK + tid;
+            const bool valid = off + (int64_t)u * DBLOCK + tid < n;
             const uint32_t p = H::pix(r[u]);
-            const double xv = (v < T && R.test(p)) ? ld_agent(&S.vals[R.rank(p)]) : 0.0;
-            point(v < T, kc[u], r[u], xv);
+            const double xv = (valid && R.test(p)) ? ld_agent(&S.vals[R.rank(p)]) : 0.0;
+            const double y = H::val(r[u]);
+            if (xv > 0.0) as += y;
+            axy += xv * y;
+            flm |= (uint32_t)(valid && H::dup(r[u])) << u;
           }
+          append(flm, kb, r, WDU);
         }
       }
-      if (!(SMG_WIDE_EXP & 2) && (as != 0.0 || axy != 0.0)) {
-        atomicAdd(&kst[0 * MAXK_DENSE + kacc + 1], as);
-        atomicAdd(&kst[3 * MAXK_DENSE + kacc + 1], axy);
-      }
+      wflush();
       __syncthreads();
       const int nd = min(sh_ctr[2], WIDE_DL);
-      if (nd > 0) {
-        slot_sync();  // the list is complete in L2
-        // sum the listed points per key in the table (all lanes at once: ~one atomic round trip); the lane that
-        // claims an entry lists it
-        for (int j = tid; j < nd; j += DBLOCK) {
-          const uint32_t key = ld_agent(&S.dkey[j]);
-          const double y = ld_agent(&S.dval[j]);
+      if (sh_anyfl) {
+        if (nd > 0) slot_sync();  // the overflow list is complete in L2
+        // sum the flagged points per key in the table (all lanes at once: ~one atomic round trip per entry held);
+        // the lane that claims an entry lists it
+        auto insert = [&](uint32_t key, double y) {
           uint32_t h = (key * 0x9E3779B1u) >> (32 - WIDE_HT_LOG2);
           bool own = false, done = false;
           for (int t = 0; t < WIDE_PROBES; ++t) {
@@ -2717,7 +2729,11 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
           if (!done) sh_ctr[3] = 1;
           const int idx = wave_append(own, &sh_nown);
           if (own) S.hown[idx] = h;
-        }
+        };
+#pragma unroll
+        for (int j = 0; j < WIDE_FLR; ++j)
+          if (j < fc) insert(fk[j], (double)fv[j]);
+        for (int j = tid; j < nd; j += DBLOCK) insert(ld_agent(&S.dkey[j]), ld_agent(&S.dval[j]));
         slot_sync();  // the table's sums are complete in L2
         const int no = sh_nown;
         for (int j = tid; j < no; j += DBLOCK) {  // claimed entries: add their pixel's (Σy)², then release them
@@ -2729,7 +2745,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
           S.hkey[s] = WIDE_EMPTY;
           S.hval[s] = 0.0;
         }
-        slot_sync();  // released entries are clean in L2 before the next ion's atomics
+        __syncthreads();  // (released entries reach L2 before the next ion's inserts: slot_syncs lie between)
       }
     }
     if (sh_ctr[3]) {  // the table overflowed: the pixel-indexed kernel scores this ion
@@ -2759,55 +2775,66 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
       slot_sync();
       STAMP(13);
       // candidates: eL = erode_box(dilate_cross(L)) >= 1 only where erode_box(dilate_cross(presence)) is set
-      // (presence is a superset of L >= 1).  That screen is computed 64 pixels at a time on the flat bitmap:
-      // D = dilate_cross(P) into the slot, then E = erode_box(D) with the image border, E's pixels listed; the
-      // exact eL of each listed pixel reads the levels of its 5x5 neighbourhood by rank.
-      const int64_t npx64 = npx;
-      for (int w0 = 0; w0 <= n64; w0 += DBLOCK) {
-        const int w = w0 + tid;
-        if (w < n64) {
-          const int64_t base = (int64_t)w * 64;
-          uint64_t c0m, clm;
-          col_masks(base, nc, c0m, clm);
-          const uint64_t d = bm[w] | (bits_at(bm, base - 1, n64) & ~c0m) | (bits_at(bm, base + 1, n64) & ~clm) |
-                             bits_at(bm, base - nc, n64) | bits_at(bm, base + nc, n64);
-          S.dmap[w] = d & range_mask(base, 0, npx64);
-        } else if (w == n64) {
-          S.dmap[w] = 0ull;
-        }
-      }
-      slot_sync();
+      // (presence is a superset of L >= 1).  That screen is computed 64 pixels at a time on the flat LDS bitmap
+      // (E = erode_box(dilate_cross(P)) with the image border, from presence rows r-2 .. r+2), E's pixels listed;
+      // the exact eL of each listed pixel reads the levels of its 5x5 neighbourhood by rank.
+      // per principal pixel p (listed in par, any order): presence rows r-3 .. r+3 of its 7-column window give
+      // D = dilate_cross and E = erode_box(D) (with the image border) for the five pixels of p's 4-cross by
+      // row-parallel bit operations; each pixel of E is listed once, by the first principal pixel on its cross
       STAMP(8);
-      for (int w0 = 0; w0 < n64; w0 += DBLOCK) {  // uniform trip count: DPP scan below
-        const int w = w0 + tid;
-        const int64_t base = (int64_t)w * 64;
-        uint64_t e = 0ull;
-        if (w < n64) {
-          uint64_t c0m, clm;
-          col_masks(base, nc, c0m, clm);
-          const uint64_t rf = range_mask(base, 0, nc), rl = range_mask(base, npx64 - nc, npx64);
-          e = range_mask(base, 0, npx64);
+      if (tid == 0) sh_ncand = 0;
+      __syncthreads();
+      for (int i0 = 0; i0 < np; i0 += DBLOCK) {  // uniform trip count: DPP scan below
+        const int i = i0 + tid;
+        const int p = (i < np) ? (int)S.par[i] : -1;
+        uint32_t cm = 0u;  // bit j: cross pixel j (0 centre, 1 up, 2 down, 3 left, 4 right) is listed by p
+        int r0 = 0, c0 = 0;
+        if (p >= 0) {
+          r0 = p / nc;
+          c0 = p - r0 * nc;
+          uint32_t B[7], IM[7];
+          uint32_t imc = 0x7Fu;  // columns c0-3 .. c0+3 inside the image
+          if (c0 - 3 < 0) imc &= 0x7Fu << (uint32_t)(3 - c0);
+          if (c0 + 3 >= nc) imc &= 0x7Fu >> (uint32_t)(c0 + 3 - (nc - 1));
 #pragma unroll
-          for (int a = -1; a <= 1; ++a)
+          for (int dr = -3; dr <= 3; ++dr) {
+            B[dr + 3] = pres.row7(r0 + dr, c0, nr, nc);
+            IM[dr + 3] = (r0 + dr >= 0 && r0 + dr < nr) ? imc : 0u;
+          }
+          uint32_t Eh[7];
 #pragma unroll
-            for (int b = -1; b <= 1; ++b) {
-              uint64_t t = bits_at(S.dmap, base + (int64_t)a * nc + b, n64);
-              const uint64_t oob = (a < 0 ? rf : 0ull) | (a > 0 ? rl : 0ull) | (b < 0 ? c0m : 0ull) |
-                                   (b > 0 ? clm : 0ull);
-              t = P.erosion_border ? (t | oob) : (t & ~oob);
-              e &= t;
-            }
+          for (int k = 1; k <= 5; ++k) {
+            const uint32_t d = B[k] | (B[k] << 1) | (B[k] >> 1) | B[k - 1] | B[k + 1];
+            const uint32_t dm = (P.erosion_border ? (d | ~IM[k]) : (d & IM[k])) & 0x7Fu;
+            Eh[k] = dm & (dm << 1) & (dm >> 1);
+          }
+          auto E = [&](int k, int j) -> uint32_t { return (Eh[k - 1] & Eh[k] & Eh[k + 1] & IM[k]) >> j & 1u; };
+          auto pr = [&](int k, int j) -> uint32_t { return (B[k] >> j) & 1u; };
+#pragma unroll
+          for (int t = 0; t < 5; ++t) {
+            const int qr = (t == 1) ? -1 : (t == 2) ? 1 : 0, qc = (t == 3) ? -1 : (t == 4) ? 1 : 0;
+            const int wr = qr + 3, wc = qc + 3;
+            // the first principal pixel among q-nc, q-1, q, q+1, q+nc must be p
+            int orr = 9, occ = 9;
+            if (pr(wr + 1, wc)) orr = 1, occ = 0;
+            if (pr(wr, wc + 1)) orr = 0, occ = 1;
+            if (pr(wr, wc)) orr = 0, occ = 0;
+            if (pr(wr, wc - 1)) orr = 0, occ = -1;
+            if (pr(wr - 1, wc)) orr = -1, occ = 0;
+            if (qr + orr == 0 && qc + occ == 0 && E(wr, wc)) cm |= 1u << t;
+          }
         }
-        const int cnt = __popcll(e);
+        const int cnt = __popc(cm);
         const int incl = wave_incl_scan_dpp(cnt);
         int wbase = 0;
         if ((tid & 63) == 63) wbase = atomicAdd(&sh_ncand, incl);
         wbase = __shfl(wbase, 63);
         int idx = wbase + incl - cnt;
-        while (e != 0ull) {
-          const int j = __ffsll((unsigned long long)e) - 1;
-          S.epr[idx++] = (uint32_t)(base + j);
-          e &= e - 1ull;
+        while (cm != 0u) {
+          const int t = __ffs(cm) - 1;
+          const int qr = (t == 1) ? -1 : (t == 2) ? 1 : 0, qc = (t == 3) ? -1 : (t == 4) ? 1 : 0;
+          S.epr[idx++] = (uint32_t)((r0 + qr) * nc + c0 + qc);
+          cm &= cm - 1u;
         }
       }
       slot_sync();
