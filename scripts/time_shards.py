@@ -1,0 +1,121 @@
+"""Per-rank critical path of the sharded (multi-GPU) step, measured on ONE GPU: every rank's shard of a
+W-way plan (config 3 by default) is scored in turn with the product code (distributed._device_rows), broken into
+slice copy, compute_sf_images and sf_image_metrics rows, plus the rank-0 assembly (rows_to_frame) of all ranks'
+rows.  The N-GPU step is then ~ max over ranks + all-gather + assembly.
+
+usage: time_shards.py [W=8] [nrows ncols peaks n_sf]"""
+import os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+import ctypes
+from sm_distributed_amd import _lib, distributed as D, engine as E, synthetic as syn
+from sm_distributed_amd.dataset import ResidentDataset
+from sm_distributed_amd.formula_imager_segm import compute_sf_images
+from sm_distributed_amd.formula_img_validator import _metrics_device_rows, sf_image_metrics
+from sm_distributed_amd.formulas import FormulasSegm
+
+a = sys.argv[1:]
+W = int(a[0]) if a else 8
+nrows, ncols, pk, n_sf = (int(a[1]), int(a[2]), float(a[3]), int(a[4])) if len(a) >= 5 else (500, 500, 2000.0, 20000)
+ppm = 2.0
+ions = syn.make_ion_table(n_sf, seed=43, decoy_seed=44)
+mz, hits, dims, info = syn.make_dataset_torch(nrows, ncols, pk, seed=42, device="cuda", ions=ions,
+                                              plant_fraction=0.02, plant_seed=45)  # bench.py defaults
+peaks = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
+formulas = FormulasSegm.from_ion_table(ions, ppm)
+conf = {"image_generation": {"ppm": ppm, "nlevels": 30, "q": 99, "do_preprocessing": False}}
+sync = torch.cuda.synchronize
+
+
+def timed(f, reps=3):
+    best, out = 1e9, None
+    for _ in range(reps):
+        sync()
+        t0 = time.perf_counter()
+        out = f()
+        sync()
+        best = min(best, time.perf_counter() - t0)
+    return best * 1e3, out
+
+
+# single-GPU API step for reference
+dds = ResidentDataset(peaks)
+sdf = formulas.get_sf_peak_df()
+t1, df1 = timed(lambda: sf_image_metrics(compute_sf_images(None, dds, sdf, ppm), None, formulas, dds, conf))
+print(f"1 GPU API step {t1:.2f} ms, {len(df1)} rows, {peaks.n_points:,} points, {formulas.n_ions:,} ions", flush=True)
+
+rows_all, worst = [], 0.0
+ONLY = int(os.environ.get("ONLY_RANK", "-1"))
+for r in range(W):
+    if ONLY >= 0 and r != ONLY:
+        continue
+    plan = D.plan_shards(formulas, peaks, ppm, W, r)
+    t_sl, sl = timed(lambda: D.slice_peaks(peaks, plan))
+    sds = ResidentDataset(sl)
+    t_img, ims = timed(lambda: compute_sf_images(None, sds, plan.sf_peak_df, ppm))
+    L = _lib.lib()
+    L.smg_debug_main_pass_times(None, 0, ctypes.byref(ctypes.c_int32(0)))
+    L.smg_debug_time_main_pass(1)
+    t_met, _ = timed(lambda: _metrics_device_rows(ims, plan.formulas.get_sf_peak_ints(), conf["image_generation"]))
+    L.smg_debug_time_main_pass(0)
+    buf = (ctypes.c_double * 16)()
+    nt = ctypes.c_int32(0)
+    L.smg_debug_main_pass_times(buf, 16, ctypes.byref(nt))
+    t_main = min(buf[i] for i in range(nt.value)) if nt.value else float("nan")
+    t_all, (rows, _) = timed(lambda: D._device_rows(plan, peaks, conf))
+    rows_all.append(rows)
+    hist, edges = D.mz_histogram(peaks.mz)
+    wpts = float(((D.ion_costs(plan.formulas.ion_off, plan.formulas.peak_mz, ppm, hist, edges) - D.C_ION)
+                  / D.C_WINDOW_POINT).sum())
+    print(f"FIT rank={r} n_ions={plan.formulas.n_ions} wpts={wpts:.0f} slice={sl.n_points} t_rows={t_all:.3f} "
+          f"t_slice={t_sl:.3f} t_img={t_img:.3f} t_met={t_met:.3f} t_main={t_main:.3f}", flush=True)
+    worst = max(worst, t_all)
+    print(f"rank {r}/{W}: {plan.formulas.n_ions:,} ions, slice {sl.n_points:,} pts [{plan.mz_lo:.2f}, {plan.mz_hi:.2f}] "
+          f"est {plan.est_cost[r]*1e3:.2f} ms | slice {t_sl:.2f} + images {t_img:.2f} + metrics {t_met:.2f} "
+          f"(main kernel {t_main:.2f}); "
+          f"_device_rows {t_all:.2f} ms", flush=True)
+if ONLY >= 0:
+    sys.exit(0)
+n_max = max(x.shape[0] for x in rows_all)
+table = torch.full((W * n_max, 5), -1.0, dtype=torch.float64, device="cuda")
+for r, x in enumerate(rows_all):
+    table[r * n_max:r * n_max + x.shape[0]] = x
+plan0 = D.plan_shards(formulas, peaks, ppm, W, 0)
+t_asm, df = timed(lambda: D.rows_to_frame(table, plan0.global_keys))
+# assembly breakdown
+def asm_parts():
+    out = {}
+    t0 = time.perf_counter()
+    t = table
+    n = len(plan0.global_keys)
+    valid = t[:, 0] >= 0
+    sel = t[valid]
+    gi = sel[:, 0].long()
+    full = torch.zeros(4, n, dtype=t.dtype, device=t.device)
+    full[:, gi] = sel[:, 1:5].T
+    has = torch.zeros(n, dtype=torch.bool, device=t.device)
+    has[gi] = True
+    idx = torch.nonzero(has).flatten()
+    sync(); out["device scatter+nonzero"] = time.perf_counter() - t0; t0 = time.perf_counter()
+    g = full[:, idx]
+    sync(); out["gather cols"] = time.perf_counter() - t0; t0 = time.perf_counter()
+    cols = g.cpu().numpy()
+    out["D2H cols"] = time.perf_counter() - t0; t0 = time.perf_counter()
+    ih = idx.cpu().numpy()
+    out["D2H idx"] = time.perf_counter() - t0; t0 = time.perf_counter()
+    mi = plan0.global_keys.multi_index(ih)
+    out["multi_index"] = time.perf_counter() - t0; t0 = time.perf_counter()
+    import pandas as pd
+    pd.DataFrame(cols.T, index=mi, columns=["chaos", "spatial", "spectral", "msm"], copy=False)
+    out["DataFrame"] = time.perf_counter() - t0
+    return out
+for _ in range(2):
+    parts = asm_parts()
+print("assembly parts (ms): " + ", ".join(f"{k} {v*1e3:.2f}" for k, v in parts.items()))
+same = df.index.equals(df1.index) and np.allclose(df.to_numpy(), df1.to_numpy(), rtol=0, atol=1e-12)
+print(f"assembly (rank 0) {t_asm:.2f} ms; table identical to 1 GPU: {same}")
+gather_est = n_max * 40 / 50e9 * 1e3 + 0.05  # W-1 blocks over W-1 xGMI links into rank 0 at once, ~50 GB/s each
+est = worst + gather_est + t_asm
+print(f"estimated {W}-GPU step {est:.2f} ms = max rank {worst:.2f} + gather ~{gather_est:.2f} + assembly "
+      f"{t_asm:.2f}; strong-scaling efficiency {t1 / (W * est):.2f}")

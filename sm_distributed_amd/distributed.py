@@ -16,8 +16,8 @@ then groups images per ion (:134-138) and collects metric tuples to the driver (
 * ``score_sharded`` (per search): each rank copies its m/z slice of the resident peaks (smg_slice_mz_*, with the
   duplicate flags fused into the copy), so its sort covers ~1/world of the points; runs compute_sf_images +
   sf_image_metrics' device batch on its shard; packs fixed-size rows (global ion index, chaos, spatial,
-  spectral, msm; 40 B) and all-gathers them (one RCCL all_gather_into_tensor over xGMI, ~40 MB at config 3);
-  rank 0 builds the reference DataFrame from codes;
+  spectral, msm; 40 B) and gathers them to rank 0 (one RCCL gather over xGMI: the other ranks send their ~5 MB
+  blocks over their own links to rank 0 at once); rank 0 builds the reference DataFrame from codes;
 * ``search``: MSMBasicSearch.search (msm_basic_search.py:13-20) over the ranks: the table of ``score_sharded``,
   then FDR and the filter on rank 0, the images staying on the rank that made them.
 """
@@ -28,11 +28,12 @@ from dataclasses import dataclass, field
 import numpy as np
 import pandas as pd
 
-# cost model constants (MI355X, config 3, round-1/2 measurements: 42 ms for 6.45e9 window points and 0.98M
-# ions in the ion kernel; 16.4 ms for flag + sort + scan of 5.0e8 points)
-C_WINDOW_POINT = 6.5e-12
-C_ION = 2.0e-9
-C_SLICE_POINT = 33e-12
+# cost model constants (MI355X, config 3): least-squares fit of every rank's measured step over 2-, 4- and 8-way
+# plans scored on one GPU (scripts/time_shards.py, profiles/round2/r2s_time_shards_*.txt): slice copy + flag +
+# sort + scan ~41 ps per slice point, ion stage ~5.4-6.1 ps per window point and a few ns per ion
+C_WINDOW_POINT = 6.0e-12
+C_ION = 3.0e-9
+C_SLICE_POINT = 45e-12
 
 ROW_FIELDS = ("ion", "chaos", "spatial", "spectral", "msm")
 
@@ -171,36 +172,49 @@ def _device_rows(plan, peaks, ds_config):
 
 
 def gather_rows(rows, plan, group=None):
-    """All-gather every rank's row block, padded to the largest shard (one RCCL all_gather_into_tensor);
-    returns the [world * n_max, 5] table on every rank."""
+    """Gather every rank's row block, padded to the largest shard, to rank 0 of ``group`` (one RCCL gather);
+    returns the [world * n_max, 5] table on that rank, None elsewhere."""
     import torch
     import torch.distributed as dist
     n_max = max(plan.counts) if plan.counts else 0
     send = torch.full((n_max, rows.shape[1]), -1.0, dtype=rows.dtype, device=rows.device)
     send[:rows.shape[0]] = rows
+    dst = 0 if group is None else dist.get_global_rank(group, 0)
+    if dist.get_rank(group) != 0:
+        dist.gather(send, None, dst=dst, group=group)
+        return None
     recv = torch.empty(plan.world * n_max, rows.shape[1], dtype=rows.dtype, device=rows.device)
-    dist.all_gather_into_tensor(recv, send, group=group)
+    dist.gather(send, list(recv.view(plan.world, n_max, rows.shape[1]).unbind(0)), dst=dst, group=group)
     return recv
 
 
 def rows_to_frame(table, global_keys):
     """Rank-0 assembly: gathered rows -> the reference DataFrame (index [sf_id, adduct] in table order,
     columns chaos, spatial, spectral, msm), one row per ion with images.  The rows are put in table order by a
-    scatter on the device holding them (no sort), then copied to the host once, column-major."""
+    scatter on the device holding them (no sort; padding rows go to a dummy slot), the metric columns and the
+    index codes are gathered there and copied to pinned host memory together: two host synchronisations."""
     import torch
     t = table if hasattr(table, "device") else torch.as_tensor(np.asarray(table))
     n = len(global_keys)
-    valid = t[:, 0] >= 0
-    sel = t[valid]
-    gi = sel[:, 0].long()
-    full = torch.zeros(4, n, dtype=t.dtype, device=t.device)
-    full[:, gi] = sel[:, 1:5].T
-    has = torch.zeros(n, dtype=torch.bool, device=t.device)
+    gi = t[:, 0].long()
+    gi = torch.where(gi >= 0, gi, torch.full_like(gi, n))
+    full = torch.zeros(4, n + 1, dtype=t.dtype, device=t.device)
+    full[:, gi] = t[:, 1:5].T
+    has = torch.zeros(n + 1, dtype=torch.bool, device=t.device)
     has[gi] = True
-    idx = torch.nonzero(has).flatten()
-    cols = full[:, idx].cpu().numpy()
-    return pd.DataFrame(cols.T, index=global_keys.multi_index(idx.cpu().numpy()),
-                        columns=["chaos", "spatial", "spectral", "msm"], copy=False)
+    idx = torch.nonzero(has[:n]).flatten()
+    sfc, adc = global_keys.codes_dev(t.device)  # the index codes gathered on the device too
+    parts = (full[:, idx], sfc[idx], adc[idx])
+    if t.device.type == "cuda":
+        host = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in parts]
+        for h, x in zip(host, parts):
+            h.copy_(x, non_blocking=True)
+        torch.cuda.current_stream(t.device).synchronize()
+    else:
+        host = parts
+    cols, c_sf, c_ad = (h.numpy() for h in host)
+    index = global_keys.multi_index_from_codes(c_sf, c_ad)
+    return pd.DataFrame(cols.T, index=index, columns=["chaos", "spatial", "spectral", "msm"], copy=False)
 
 
 def score_sharded(plan, peaks, ds_config, group=None, score_local=None):
@@ -210,7 +224,7 @@ def score_sharded(plan, peaks, ds_config, group=None, score_local=None):
     import torch.distributed as dist
     rows, ims = (score_local or _device_rows)(plan, peaks, ds_config)
     table = gather_rows(rows, plan, group)
-    df = rows_to_frame(table, plan.global_keys) if dist.get_rank(group) == 0 else None
+    df = rows_to_frame(table, plan.global_keys) if table is not None else None
     return df, ims
 
 

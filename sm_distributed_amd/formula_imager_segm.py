@@ -100,6 +100,22 @@ class IonKeys:
                 self._codes = (np.asarray(self.sf_levels), sfc.astype(np.int32), adc)
         return self._codes
 
+    def codes_dev(self, device):
+        """level_codes()' sf and adduct codes as device tensors (cached per device)."""
+        import torch
+        cache = self.__dict__.setdefault("_codes_dev", {})
+        key = str(device)
+        if key not in cache:
+            _, sfc, adc = self.level_codes()
+            cache[key] = (torch.from_numpy(sfc).to(device), torch.from_numpy(adc).to(device))
+        return cache[key]
+
+    def multi_index_from_codes(self, sf_codes, ad_codes):
+        """pd.MultiIndex [sf_id, adduct] from already gathered codes (the levels are those of the whole layout)."""
+        sf_lv = self.level_codes()[0]
+        return pd.MultiIndex(levels=[pd.Index(sf_lv), pd.Index(self.adducts, dtype=object)],
+                             codes=[sf_codes, ad_codes], names=["sf_id", "adduct"], verify_integrity=False)
+
     def multi_index(self, idx):
         """pd.MultiIndex [sf_id, adduct] of the ions ``idx`` (ascending positions), built from codes (two
         gathers; the levels are those of the whole layout)."""
