@@ -18,6 +18,8 @@ ion, window m/z in ion-major order, processing orders) is built on the device fr
 """
 from __future__ import annotations
 
+import warnings
+
 import numpy as np
 import pandas as pd
 from scipy.sparse import coo_matrix
@@ -172,7 +174,11 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
     if peak_i.dtype.kind not in "iu" or mz.dtype != np.float64:
         peak_i, mz = peak_i.astype(np.int64), mz.astype(np.float64)
     n_rows = len(sf)
-    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+    def t(a):  # host column -> device (read-only views, e.g. Categorical codes, are only read by the copy)
+        a = np.ascontiguousarray(a)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", UserWarning)
+            return torch.from_numpy(a).to(device)
     with torch.cuda.stream(stream) if stream is not None else _nullctx():
         if n_rows == 0:
             z = torch.zeros(1, dtype=torch.int64, device=device)
