@@ -192,8 +192,11 @@ def rows_to_frame(table, global_keys):
     """Rank-0 assembly: gathered rows -> the reference DataFrame (index [sf_id, adduct] in table order,
     columns chaos, spatial, spectral, msm), one row per ion with images.  The rows are put in table order by a
     scatter on the device holding them (no sort; padding rows go to a dummy slot), the metric columns and the
-    index codes are gathered there and copied to pinned host memory together: two host synchronisations."""
+    index codes are gathered there and copied to pinned host memory together (formula_imager_segm.device_frame):
+    two host synchronisations."""
     import torch
+
+    from .formula_imager_segm import device_frame
     t = table if hasattr(table, "device") else torch.as_tensor(np.asarray(table))
     n = len(global_keys)
     gi = t[:, 0].long()
@@ -203,18 +206,7 @@ def rows_to_frame(table, global_keys):
     has = torch.zeros(n + 1, dtype=torch.bool, device=t.device)
     has[gi] = True
     idx = torch.nonzero(has[:n]).flatten()
-    sfc, adc = global_keys.codes_dev(t.device)  # the index codes gathered on the device too
-    parts = (full[:, idx], sfc[idx], adc[idx])
-    if t.device.type == "cuda":
-        host = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in parts]
-        for h, x in zip(host, parts):
-            h.copy_(x, non_blocking=True)
-        torch.cuda.current_stream(t.device).synchronize()
-    else:
-        host = parts
-    cols, c_sf, c_ad = (h.numpy() for h in host)
-    index = global_keys.multi_index_from_codes(c_sf, c_ad)
-    return pd.DataFrame(cols.T, index=index, columns=["chaos", "spatial", "spectral", "msm"], copy=False)
+    return device_frame(global_keys, full, idx)
 
 
 def score_sharded(plan, peaks, ds_config, group=None, score_local=None):

@@ -34,7 +34,7 @@ class IonKeys:
     ``sf_code`` is the sf_id itself for integer ids (``sf_levels`` None), else its position in the sorted
     ``sf_levels``; ``adducts`` are the sorted adduct strings."""
 
-    def __init__(self, keys: np.ndarray, adducts, sf_levels=None, keys_dev=None, codes=None):
+    def __init__(self, keys: np.ndarray, adducts, sf_levels=None, keys_dev=None, codes=None, codes_dev=None):
         self.keys = keys
         self.keys_dev = keys_dev  # the same keys in HBM (device_layout keeps them)
         self.adducts = list(adducts)
@@ -42,6 +42,9 @@ class IonKeys:
         self.n_cat = max(len(self.adducts), 1)
         self._tuples = None
         self._codes = codes       # (sf level values, sf code, adduct code) per ion, for multi_index
+        self._codes_dev = {}      # device -> (int32 sf codes, int16 adduct codes) tensors
+        if codes_dev is not None:
+            self._codes_dev[str(codes_dev[0].device)] = codes_dev
 
     def __len__(self):
         return len(self.keys)
@@ -105,7 +108,7 @@ class IonKeys:
     def codes_dev(self, device):
         """level_codes()' sf and adduct codes as device tensors (cached per device)."""
         import torch
-        cache = self.__dict__.setdefault("_codes_dev", {})
+        cache = self._codes_dev
         key = str(device)
         if key not in cache:
             _, sfc, adc = self.level_codes()
@@ -223,15 +226,39 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
         new[1:] = sfc[1:] != sfc[:-1]
         sf_code = (torch.cumsum(new.to(torch.int32), 0, dtype=torch.int32) - 1)
         if sf_levels is None:
+            codes_dev = (sf_code, adc)
             codes = (sfc[new].cpu().numpy(), sf_code.cpu().numpy(), adc.cpu().numpy())
         else:
-            codes = (np.asarray(sf_levels), sfc.to(torch.int32).cpu().numpy(), adc.cpu().numpy())
+            codes_dev = (sfc.to(torch.int32), adc)
+            codes = (np.asarray(sf_levels), codes_dev[0].cpu().numpy(), adc.cpu().numpy())
         keys = uniq.cpu().numpy()
         if int(per_slot.max().item()) > 1:
             raise AssertionError("duplicate (sf_id, adduct, peak_i) rows in sf_peak_df")
     ions = DeviceIons(win_off=win_off, peak_mz=peak_mz, theor=None, win_order=win_order, ion_order=ion_order,
                       n_ions=n_ions, n_windows=n_win, max_k=kmax)
-    return IonKeys(keys, cats, sf_levels, keys_dev=uniq, codes=codes), ions, K
+    return IonKeys(keys, cats, sf_levels, keys_dev=uniq, codes=codes, codes_dev=codes_dev), ions, K
+
+
+METRIC_COLUMNS = ["chaos", "spatial", "spectral", "msm"]
+
+
+def device_frame(ion_keys, cols, idx):
+    """The reference metrics DataFrame (index [sf_id, adduct], columns chaos, spatial, spectral, msm) of the ions
+    ``idx`` (device tensor, ascending positions of ``ion_keys``) from device metric columns ``cols`` [4, >n]: the
+    rows and the index codes are gathered on the device and copied to pinned host memory together (one host
+    synchronisation); the DataFrame wraps the column-major block without a copy."""
+    import torch
+    sfc, adc = ion_keys.codes_dev(cols.device)
+    parts = (cols[:, idx], sfc[idx], adc[idx])
+    if cols.device.type == "cuda":
+        host = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in parts]
+        for h, x in zip(host, parts):
+            h.copy_(x, non_blocking=True)
+        torch.cuda.current_stream(cols.device).synchronize()
+    else:
+        host = parts
+    c, c_sf, c_ad = (h.numpy() for h in host)
+    return pd.DataFrame(c.T, index=ion_keys.multi_index_from_codes(c_sf, c_ad), columns=METRIC_COLUMNS, copy=False)
 
 
 class IonImageSet:

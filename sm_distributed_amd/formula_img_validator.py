@@ -198,13 +198,10 @@ def _metrics_device_batch(ims, sf_ints, img_conf):
     """The reference table (index [sf_id, adduct], columns chaos, spatial, spectral, msm) of an IonImageSet:
     one row per ion with images (formula_img_validator.py:115-121), built from codes, not tuples."""
     import torch
+    from .formula_imager_segm import device_frame
     keep, m = _metrics_device_rows(ims, sf_ints, img_conf)
     idx = torch.nonzero(keep).flatten()
-    # one device->host copy of the four columns, column-major: the DataFrame wraps it without a copy
-    cols = torch.stack([m.chaos[idx], m.spatial[idx], m.spectral[idx], m.msm[idx]], 0).cpu().numpy()
-    idx = idx.cpu().numpy()
-    return pd.DataFrame(cols.T, index=ims.ion_keys.multi_index(idx), columns=["chaos", "spatial", "spectral", "msm"],
-                        copy=False)
+    return device_frame(ims.ion_keys, torch.stack([m.chaos, m.spatial, m.spectral, m.msm], 0), idx)
 
 
 def sf_image_metrics_est_fdr(sf_metrics_df, formulas, fdr):
