@@ -737,8 +737,10 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     return prefix_words<NW, CAPC>(W64, Bpf, nwords, wsc);
   };
 
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
+  // tid and lane are laundered at the top of every ion iteration (SMG_LAUNDER): values derived from them are
+  // then recomputed where they are used instead of being hoisted out of the ion loop and spilled to scratch
+  int tid = threadIdx.x;
+  int lane = tid & 63;
   const int wid = uni(tid >> 6);
   const int n64 = (P.npx + 63) / 64;
   const uint32_t big_flag = (SRC == SRC_LIST) ? SMG_ION_BIG : 0u;
@@ -815,6 +817,13 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   int64_t npos = uni(ctr[C_NEXT]);
   int cur = 0;
   while (true) {
+#ifndef SMG_LAUNDER
+#define SMG_LAUNDER 1
+#endif
+    if (SMG_LAUNDER) {
+      asm volatile("" : "+v"(tid));
+      asm volatile("" : "+v"(lane));
+    }
     const IonDesc* D = &dsl[cur];
     IonDesc* DN = &dsl[cur ^ 1];
     // the ticket of the ion after npos: issued now, consumed after phase 1 (wave 0 issues after it exactly one
@@ -864,6 +873,15 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       for (int i = tid; i < P.w32 / 4 + 1; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
       for (int i = tid; i < MAXK * NW * 4; i += BLOCK) part[i] = 0.0;
       if (tid < C_NEXT) ctr[tid] = 0;
+#ifndef SMG_TBL0
+#define SMG_TBL0 1
+#endif
+      if (SMG_TBL0) {  // the duplicate table (free since the previous ion's chaos phase), for phase d
+        for (int i = tid; i < DTBL; i += BLOCK) {
+          tkey[i] = 0xFFFFFFFFu;
+          tval[i] = 0.0;
+        }
+      }
     }
     __syncthreads();
     STAMP(0);
@@ -1009,14 +1027,60 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       double* wdval = dval + wid * DSEG;
       int gnext = uni(D->gs[2]);
       int wend = uni(D->end[1]);
-      // A principal hit (a tail point on a principal pixel: ~0.5% of the points) adds x*y and y[x>0] straight
-      // into this wave's LDS partials of its current window (part[k][wid], zeroed in phase 0): only this wave
-      // writes that slot, in program order, lanes of one instruction in hardware order -- deterministic.  No
-      // per-window wave reduction (it cost two f64 DPP reductions per window change per wave).
+      // Events: a principal hit (a tail point on a principal pixel, ~0.5% of the points: adds x*y and y[x>0] to
+      // its window's partials) or a duplicate candidate (~1%: summed per (pixel, window) before squaring).
+      // The stream only tests for them and parks up to two events per lane in registers (the raw hit and its
+      // window); their LDS lookups, atomics and list appends run after the stream for all lanes at once.  A
+      // lane's third and later events are handled in place (rare).  Partials: part[k][wid] (zeroed in phase 0),
+      // written only by this wave, lanes of one instruction in hardware order -- deterministic.
+#ifndef SMG_STASH
+#define SMG_STASH 1
+#endif
+      Reg ev0 = Hits<FMT>::zero(), ev1 = Hits<FMT>::zero();
+      int evk0 = 0, evk1 = 0, nev = 0;
+      // handles one event per lane (pred); principal membership re-tested from the hit when `in` is unknown
+      auto handle = [&](bool pred, const Reg& h, int k, bool known, bool in_known, uint64_t bwv, int brv) {
+        const uint32_t p = Hits<FMT>::pix(h);
+        const uint64_t bit = 1ull << (p & 63);
+        bool in = false;
+        int r = -1;
+        if (pred) {
+          if (known) {
+            in = in_known;
+            if (in) {
+              if constexpr (TWO) r = (int)Bpf[brv] + __popcll(bwv & (bit - 1ull));
+              else r = (int)pf[p >> 6] + __popcll(bwv & (bit - 1ull));
+            }
+          } else {
+            if constexpr (TWO) r = rank2((int)p);
+            else r = bm_test(Hbm, (int)p) ? bm_rank(Hbm, pf, (int)p) : -1;
+            in = r >= 0;
+          }
+        }
+        in = in && !(SMG_ABL & 16);
+        if (__ballot(in)) {
+          if (in) {
+            const double x = vals[r];
+            const double v = Hits<FMT>::val(h);
+            double* pk = part + ((size_t)k * NW + wid) * 4;
+            atomicAdd(&pk[3], x * v);
+            if (x > 0.0) atomicAdd(&pk[0], v);
+          }
+        }
+        // duplicate candidates: appended to this wave's list segment (ballot compaction, no atomics)
+        const bool dup = pred && Hits<FMT>::dup(h) && !(SMG_ABL & 8);
+        const uint64_t dm = __ballot(dup);
+        if (dm) {
+          const int e = nd + (int)__popcll(dm & ((1ull << lane) - 1ull));
+          if (dup && e < DSEG) {
+            wdkey[e] = (p << 3) | (uint32_t)k;
+            wdval[e] = Hits<FMT>::val(h);
+          }
+          nd += (int)__popcll(dm);
+        }
+      };
       // Lanes past the end of their window hold a copy of its last point (masked by `valid`); groups past the
-      // tail are skipped.  Stage 1 reads the bitmap words of every slot at once; stage 2 handles slot by slot:
-      // window changes (flush), principal hits (rank + value lookups only in waves that have one), duplicate
-      // candidates.
+      // tail are skipped.  Stage 1 reads the bitmap words of every slot at once; stage 2 handles slot by slot.
       auto process = [&](int c, Reg (&buf)[RC]) {
         uint64_t bw[RC];
         int br[RC];  // two-level: index of the slot's word among the non-empty words
@@ -1038,7 +1102,10 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
           }
         } else {
 #pragma unroll
-          for (int j = 0; j < RC; ++j) bw[j] = reinterpret_cast<const uint64_t*>(Hbm)[Hits<FMT>::pix(buf[j]) >> 6];
+          for (int j = 0; j < RC; ++j) {
+            bw[j] = reinterpret_cast<const uint64_t*>(Hbm)[Hits<FMT>::pix(buf[j]) >> 6];
+            br[j] = 0;
+          }
         }
 #pragma unroll
         for (int j = 0; j < RC; ++j) {
@@ -1050,31 +1117,21 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
               wend = uni(D->end[curk]);
             }
             const bool valid = lane < wend - G * 64;
+            const Reg h = buf[j];
             const uint32_t p = Hits<FMT>::pix(buf[j]);
-            const uint64_t bit = 1ull << (p & 63);
-            const bool in = valid && (bw[j] & bit) != 0ull && !(SMG_ABL & 16);
-            if (__ballot(in)) {
-              double x;
-              if constexpr (TWO) x = in ? vals[(int)Bpf[br[j]] + __popcll(bw[j] & (bit - 1ull))] : 0.0;
-              else x = in ? vals[(int)pf[p >> 6] + __popcll(bw[j] & (bit - 1ull))] : 0.0;
-              if (in) {
-                const double v = Hits<FMT>::val(buf[j]);
-                double* pk = part + ((size_t)curk * NW + wid) * 4;
-                atomicAdd(&pk[3], x * v);
-                if (x > 0.0) atomicAdd(&pk[0], v);
-              }
-            }
-            // duplicate candidates are summed per (pixel, window) before squaring: appended to this wave's
-            // list segment (ballot compaction, no atomics)
-            const bool dup = valid && Hits<FMT>::dup(buf[j]) && !(SMG_ABL & 8);
-            const uint64_t dm = __ballot(dup);
-            if (dm) {
-              const int e = nd + (int)__popcll(dm & ((1ull << lane) - 1ull));
-              if (dup && e < DSEG) {
-                wdkey[e] = (p << 3) | (uint32_t)curk;
-                wdval[e] = Hits<FMT>::val(buf[j]);
-              }
-              nd += (int)__popcll(dm);
+            const bool in = valid && (bw[j] & (1ull << (p & 63))) != 0ull;
+            const bool ev = in || (valid && Hits<FMT>::dup(buf[j]));
+            if (SMG_STASH) {
+              const bool s0 = ev && nev == 0, s1 = ev && nev == 1;
+              ev0 = s0 ? h : ev0;
+              evk0 = s0 ? curk : evk0;
+              ev1 = s1 ? h : ev1;
+              evk1 = s1 ? curk : evk1;
+              const bool ovf = ev && nev >= 2;
+              nev += ev ? 1 : 0;
+              if (__ballot(ovf)) handle(ovf, h, curk, true, in, bw[j], br[j]);
+            } else if (__ballot(ev)) {
+              handle(ev, h, curk, true, in, bw[j], br[j]);
             }
           }
         }
@@ -1097,6 +1154,62 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         vm_wait<3 * RC>(pd);
         process(c + 3, pd);
         issue_chunk(D, c + 7, pd);
+      }
+#ifndef SMG_PAIR
+#define SMG_PAIR 1
+#endif
+      if (SMG_STASH && SMG_PAIR) {  // the parked events, both at once: lookups in flight together
+        if (__ballot(nev > 0)) {
+          const uint32_t p0 = Hits<FMT>::pix(ev0), p1 = Hits<FMT>::pix(ev1);
+          int r0 = -1, r1 = -1;
+          if constexpr (TWO) {
+            if (nev > 0) r0 = rank2((int)p0);
+            if (nev > 1) r1 = rank2((int)p1);
+          } else {
+            const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(Hbm);
+            const uint64_t w0 = nev > 0 ? bm64[p0 >> 6] : 0ull, w1 = nev > 1 ? bm64[p1 >> 6] : 0ull;
+            const int f0 = pf[p0 >> 6], f1 = pf[p1 >> 6];
+            const uint64_t b0 = 1ull << (p0 & 63), b1 = 1ull << (p1 & 63);
+            r0 = (w0 & b0) ? f0 + __popcll(w0 & (b0 - 1ull)) : -1;
+            r1 = (w1 & b1) ? f1 + __popcll(w1 & (b1 - 1ull)) : -1;
+          }
+          if (SMG_ABL & 16) r0 = r1 = -1;
+          if (__ballot(r0 >= 0 || r1 >= 0)) {
+            const double x0 = r0 >= 0 ? vals[r0] : 0.0, x1 = r1 >= 0 ? vals[r1] : 0.0;
+            if (r0 >= 0) {
+              const double v = Hits<FMT>::val(ev0);
+              double* pk = part + ((size_t)evk0 * NW + wid) * 4;
+              atomicAdd(&pk[3], x0 * v);
+              if (x0 > 0.0) atomicAdd(&pk[0], v);
+            }
+            if (r1 >= 0) {
+              const double v = Hits<FMT>::val(ev1);
+              double* pk = part + ((size_t)evk1 * NW + wid) * 4;
+              atomicAdd(&pk[3], x1 * v);
+              if (x1 > 0.0) atomicAdd(&pk[0], v);
+            }
+          }
+          const bool d0 = nev > 0 && Hits<FMT>::dup(ev0) && !(SMG_ABL & 8);
+          const bool d1 = nev > 1 && Hits<FMT>::dup(ev1) && !(SMG_ABL & 8);
+          const uint64_t m0 = __ballot(d0), m1 = __ballot(d1);
+          if (m0 | m1) {
+            const uint64_t below = (1ull << lane) - 1ull;
+            const int e0 = nd + (int)__popcll(m0 & below);
+            const int e1 = nd + (int)__popcll(m0) + (int)__popcll(m1 & below);
+            if (d0 && e0 < DSEG) {
+              wdkey[e0] = (p0 << 3) | (uint32_t)evk0;
+              wdval[e0] = Hits<FMT>::val(ev0);
+            }
+            if (d1 && e1 < DSEG) {
+              wdkey[e1] = (p1 << 3) | (uint32_t)evk1;
+              wdval[e1] = Hits<FMT>::val(ev1);
+            }
+            nd += (int)(__popcll(m0) + __popcll(m1));
+          }
+        }
+      } else if (SMG_STASH) {  // the parked events: membership and ranks re-read from the principal set
+        if (__ballot(nev > 0)) handle(nev > 0, ev0, evk0, false, false, 0ull, 0);
+        if (__ballot(nev > 1)) handle(nev > 1, ev1, evk1, false, false, 0ull, 0);
       }
       if (lane == 0) dcnt[wid] = nd;
     } else if (!skip && tid < NW) {
@@ -1125,13 +1238,15 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       if (nd_max > DSEG) {
         reject();
         skip = true;
-      } else if (nd_tot > 0) {
+      } else if (nd_tot > 0 && !(SMG_ABL & 512)) {
         static_assert(NW * DSEG == BLOCK, "one list slot per thread");
-        for (int i = tid; i < DTBL; i += BLOCK) {
-          tkey[i] = 0xFFFFFFFFu;
-          tval[i] = 0.0;
+        if (!SMG_TBL0) {
+          for (int i = tid; i < DTBL; i += BLOCK) {
+            tkey[i] = 0xFFFFFFFFu;
+            tval[i] = 0.0;
+          }
+          __syncthreads();
         }
-        __syncthreads();
         if ((tid % DSEG) < dcnt[tid / DSEG] && !tbl_add<DTBL>(tkey, tval, dkey[tid], dval[tid])) ctr[C_ABORT] = 1;
         __syncthreads();
         if (ctr[C_ABORT]) {
@@ -1224,9 +1339,17 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
             H[d] = bits7(Hbm, rs - 3 + d, cs - 3, cv, P);
           }
         }
-        // isolation pre-filter (erosion border = background only): an eL>0 pixel in the cross of s needs
-        // another principal pixel in s's 7x7, since the 4-cross of s alone cannot cover a 3x3 box
-        const bool isolated = !P.erosion_border && (H[0] | H[1] | H[2] | (H[3] & ~8u) | H[4] | H[5] | H[6]) == 0u;
+        // sparsity pre-filter (erosion border = background only): an eL>0 pixel p in the cross of s has its 3x3
+        // box covered by 4-crosses of principal pixels, which takes at least three of them (one cross meets at
+        // most two corners of the box, and a cross through the centre none), all in p's 5x5, inside s's 7x7
+#ifndef SMG_SCREEN3
+#define SMG_SCREEN3 1
+#endif
+        const bool isolated =
+            !P.erosion_border &&
+            (SMG_SCREEN3 ? (__popc(H[0]) + __popc(H[1]) + __popc(H[2]) + __popc(H[3]) + __popc(H[4]) + __popc(H[5]) +
+                            __popc(H[6])) < 3
+                         : (H[0] | H[1] | H[2] | (H[3] & ~8u) | H[4] | H[5] | H[6]) == 0u);
         uint32_t pass = 0;
         if (oc_i < nnz && !isolated) {
         uint32_t Dl[7];
@@ -2984,7 +3107,11 @@ static constexpr int MAIN_CFG[4] = {SMG_MAIN_CFG};
 static constexpr int MAIN_BLOCK = MAIN_CFG[0], MAIN_RMAX = MAIN_CFG[1], MAIN_RC = MAIN_CFG[2],
                      MAIN_WPE = MAIN_CFG[3];
 static constexpr int BIG_BLOCK = 1024, BIG_RMAX = 8, BIG_RC = 2;
-static constexpr size_t MAIN_LDS = 80 * 1024, BIG_LDS = 160 * 1024 - 512;
+#ifndef SMG_MAIN_WGPCU
+#define SMG_MAIN_WGPCU 2
+#endif
+static constexpr int MAIN_WGPCU = SMG_MAIN_WGPCU;  // main pass: resident workgroups per CU
+static constexpr size_t MAIN_LDS = (160 * 1024) / MAIN_WGPCU, BIG_LDS = 160 * 1024 - 512;
 
 // the wide pass and the pixel-indexed kernel run one after the other over the same slots
 static size_t slot_bytes_for(int npx) {
@@ -3041,7 +3168,10 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   PM.o_pf = two ? Main2Lay::o_pf(P.npx) : MainLay::o_pf(P.npx);
   PB.w32 = two ? Big2Lay::w32(P.npx) : BigLay::w32(P.npx);
   PB.o_pf = two ? Big2Lay::o_pf(P.npx) : BigLay::o_pf(P.npx);
-  const size_t lds_main = two ? Main2Lay::bytes(P.npx) : MainLay::bytes(P.npx);
+  size_t lds_main = two ? Main2Lay::bytes(P.npx) : MainLay::bytes(P.npx);
+#ifdef SMG_MAIN_LDS_MIN  // diagnostic: reserve at least this much LDS per main-pass workgroup (fewer per CU)
+  if (lds_main < (size_t)SMG_MAIN_LDS_MIN) lds_main = SMG_MAIN_LDS_MIN;
+#endif
   const size_t lds_big = two ? Big2Lay::bytes(P.npx) : BigLay::bytes(P.npx);
   // the hot-spot clip needs whole images: every ion takes the dense path
   const bool main_ok = !P.clip && !g_force_dense && (two || P.npx <= NPX_LDS_MAX) && lds_main <= MAIN_LDS;
@@ -3058,8 +3188,8 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
                   : &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, false>;
     SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k1), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_main));
-    // two resident workgroups per CU, a multiple of the XCD count
-    int64_t nwg = (int64_t)cus * 2;
+    // MAIN_WGPCU resident workgroups per CU, a multiple of the XCD count
+    int64_t nwg = (int64_t)cus * MAIN_WGPCU;
     if (nwg > n_ions) nwg = ((n_ions + XCDS - 1) / XCDS) * XCDS;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     if (g_time_main) {

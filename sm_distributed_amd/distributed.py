@@ -52,6 +52,7 @@ class ShardPlan:
     global_keys: object            # IonKeys of the whole table (rank 0 builds the DataFrame from codes)
     est_cost: list = field(default_factory=list)  # estimated seconds per rank
     _sf_peak_df: object = None
+    _glob: object = None           # (shard ion keys, device f64 global index of each): reused while they match
 
     @property
     def sf_peak_df(self):
@@ -157,12 +158,18 @@ def _device_rows(plan, peaks, ds_config):
     # global ion index of each image-set ion: re-encode its (sf_id, adduct) with the whole table's adduct codes
     # (the shard's sf_peak_df may lack some adducts, so its own codes differ)
     ik = ims.ion_keys
-    gk, ok = plan.global_keys.encode_codes(ik.sf_values(), ik.adduct_code, ik.adducts)
-    pos = np.searchsorted(plan.global_keys.keys, gk)
-    if not ok.all() or not (plan.global_keys.keys[np.minimum(pos, len(plan.global_keys.keys) - 1)] == gk).all():
-        raise AssertionError("shard ion missing from the formula table")
-    glob = torch.from_numpy(pos.astype(np.float64)).to(dev)
-    k = len(pos)
+    cached = plan._glob
+    if cached is not None and cached[0] is not ik.keys and np.array_equal(cached[0], ik.keys):
+        cached = (ik.keys, cached[1])  # the same shard layout as the previous step
+    if cached is None or cached[0] is not ik.keys:
+        gk, ok = plan.global_keys.encode_codes(ik.sf_values(), ik.adduct_code, ik.adducts)
+        pos = np.searchsorted(plan.global_keys.keys, gk)
+        if not ok.all() or not (plan.global_keys.keys[np.minimum(pos, len(plan.global_keys.keys) - 1)] == gk).all():
+            raise AssertionError("shard ion missing from the formula table")
+        cached = (ik.keys, torch.from_numpy(pos.astype(np.float64)).to(dev))
+    plan._glob = cached
+    glob = cached[1]
+    k = glob.numel()
     rows[:k, 0] = torch.where(keep, glob, torch.full_like(glob, -1.0))
     rows[:k, 1] = m.chaos
     rows[:k, 2] = m.spatial

@@ -261,6 +261,45 @@ def device_frame(ion_keys, cols, idx):
     return pd.DataFrame(c.T, index=ion_keys.multi_index_from_codes(c_sf, c_ad), columns=METRIC_COLUMNS, copy=False)
 
 
+class FrameIndex:
+    """device_frame in two halves around a kernel launch: ``stage(keep)`` (device bool[n_ion], queued before the
+    launch) gathers the kept ions' index codes into pinned host memory; ``frame(cols)`` (after the launch) builds
+    the MultiIndex on the host -- while the kernel still runs -- then gathers and copies the metric columns."""
+
+    def __init__(self, ion_keys):
+        self.ion_keys = ion_keys
+        self.idx = None
+
+    def stage(self, keep):
+        import torch
+        self.idx = torch.nonzero(keep).flatten()  # one host synchronisation, before the kernel is queued
+        sfc, adc = self.ion_keys.codes_dev(keep.device)
+        parts = (sfc[self.idx], adc[self.idx])
+        if keep.device.type == "cuda":
+            self.codes = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in parts]
+            for h, x in zip(self.codes, parts):
+                h.copy_(x, non_blocking=True)
+            self.ev = torch.cuda.Event()
+            self.ev.record(torch.cuda.current_stream(keep.device))
+        else:
+            self.codes, self.ev = list(parts), None
+
+    def frame(self, cols):
+        import torch
+        if self.ev is not None:
+            self.ev.synchronize()  # the codes were queued before the kernel: ready while it runs
+        c_sf, c_ad = (h.numpy() for h in self.codes)
+        mi = self.ion_keys.multi_index_from_codes(c_sf, c_ad)
+        sel = cols[:, self.idx]
+        if cols.device.type == "cuda":
+            host = torch.empty(sel.shape, dtype=sel.dtype, pin_memory=True)
+            host.copy_(sel, non_blocking=True)
+            torch.cuda.current_stream(cols.device).synchronize()
+        else:
+            host = sel
+        return pd.DataFrame(host.numpy().T, index=mi, columns=METRIC_COLUMNS, copy=False)
+
+
 class IonImageSet:
     """Device-resident ``RDD[((sf_id, adduct), [coo | None, ...])]``."""
 

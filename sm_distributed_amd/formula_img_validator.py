@@ -148,13 +148,17 @@ def _theor_arrays(ims, sf_ints, device):
     return torch.from_numpy(Kt).to(device), torch.from_numpy(flat).to(device)
 
 
-def _metrics_device_rows(ims, sf_ints, img_conf):
+def _metrics_device_rows(ims, sf_ints, img_conf, prelaunch=None):
     """Score every ion of an IonImageSet with one fused launch; returns (device bool[n_ion]: the ion gets a row,
     engine.IonMetrics).
 
     The kernel sees exactly len(sf_ints[key]) windows per ion: compute() pads the image list with empty images
     up to that length (formula_img_validator.py:73-75), and windows of sf_peak_df beyond it do not enter the
-    metrics.  The alignment runs on the side stream (it needs only the layout, not the sorted peaks)."""
+    metrics.  The alignment runs on the side stream (it needs only the layout, not the sorted peaks).
+
+    Which ions get a row is known before the launch (an ion has images and >= 1 of its first min(Kt, 32) scored
+    windows is non-empty: the kernel's SMG_ION_HAS_HITS flag); ``prelaunch(keep)`` is called with it just before
+    the kernel is queued, so a caller can stage the table's index while the kernel runs."""
     import torch
 
     from . import engine as E
@@ -185,23 +189,30 @@ def _metrics_device_rows(ims, sf_ints, img_conf):
     zero = torch.zeros((), dtype=torch.int64, device=dev)
     lo2 = torch.where(valid, ims.lo[src], zero)
     hi2 = torch.where(valid, ims.hi[src], zero)
+    # the kernel's SMG_ION_HAS_HITS: a non-empty window among the ion's first min(Kt, MAXK_DENSE = 32)
+    hit = torch.zeros(n_t + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(((hi2 > lo2) & (k_in < 32)).to(torch.int64), 0, out=hit[1:])
+    keep = has & ((hit[off_t[1:]] - hit[off_t[:-1]]) > 0)
+    if sel_dev is not None:
+        keep &= sel_dev
+    if prelaunch is not None:
+        prelaunch(keep)
     nrows, ncols = ims.dims
     m = E.ion_metrics_raw(SMG_HITS_PACKED_F32, ims.peaks.hits_sorted, None, ims.peaks.sorted_cum(), lo2, hi2,
                           off_t, theor, ims.ions_dev.ion_order, n, nrows, ncols, **opts)
-    keep = has & ((m.flags & 1) != 0)
-    if sel_dev is not None:
-        keep &= sel_dev
     return keep, m
 
 
 def _metrics_device_batch(ims, sf_ints, img_conf):
     """The reference table (index [sf_id, adduct], columns chaos, spatial, spectral, msm) of an IonImageSet:
-    one row per ion with images (formula_img_validator.py:115-121), built from codes, not tuples."""
+    one row per ion with images (formula_img_validator.py:115-121), built from codes, not tuples.  The row set
+    is known before the scoring launch: its index codes are copied to the host and the MultiIndex is built
+    there while the kernel runs; only the metric columns are copied after it."""
     import torch
-    from .formula_imager_segm import device_frame
-    keep, m = _metrics_device_rows(ims, sf_ints, img_conf)
-    idx = torch.nonzero(keep).flatten()
-    return device_frame(ims.ion_keys, torch.stack([m.chaos, m.spatial, m.spectral, m.msm], 0), idx)
+    from .formula_imager_segm import FrameIndex
+    fi = FrameIndex(ims.ion_keys)
+    keep, m = _metrics_device_rows(ims, sf_ints, img_conf, prelaunch=fi.stage)
+    return fi.frame(torch.stack([m.chaos, m.spatial, m.spectral, m.msm], 0))
 
 
 def sf_image_metrics_est_fdr(sf_metrics_df, formulas, fdr):
