@@ -28,12 +28,12 @@ from dataclasses import dataclass, field
 import numpy as np
 import pandas as pd
 
-# cost model constants (MI355X, config 3): least-squares fit of every rank's measured step over 2-, 4- and 8-way
-# plans scored on one GPU (scripts/time_shards.py, profiles/round2/r2s_time_shards_*.txt): slice copy + flag +
-# sort + scan ~41 ps per slice point, ion stage ~5.4-6.1 ps per window point and a few ns per ion
-C_WINDOW_POINT = 6.0e-12
-C_ION = 3.0e-9
-C_SLICE_POINT = 45e-12
+# cost model constants (MI355X, config 3): least-squares fit (no intercept) of every rank's measured step in an
+# 8-way plan scored on one GPU (scripts/time_shards.py, profiles/round2/r2j_time_shards_8.txt): slice copy + flag +
+# sort + scan ~54 ps per slice point, ion stage ~6.2 ps per window point and ~2 ns per ion
+C_WINDOW_POINT = 6.2e-12
+C_ION = 2.0e-9
+C_SLICE_POINT = 54e-12
 
 ROW_FIELDS = ("ion", "chaos", "spatial", "spectral", "msm")
 

@@ -151,6 +151,17 @@ class DevicePeaks:
         out = DevicePeaks(mz=mz, hits=hits, nrows=self.nrows, ncols=self.ncols, sp_off=off, force=self.force)
         out.flags_preset_ppm = float(ppm)
         out._sorted = True
+        # every value of the slice lies in [lo, hi]: positive f32 bit patterns are ordered like the values, so the
+        # bits that vary among them are within those of f32(lo) rounded down and f32(hi) rounded up (no
+        # aminmax + synchronisation per slice)
+        if n and lo > 0.0:
+            a = np.array([lo], np.float32)
+            if float(a[0]) > lo:
+                a = np.nextafter(a, np.float32(0))
+            b = np.array([hi], np.float32)
+            if float(b[0]) < hi:
+                b = np.nextafter(b, np.float32(np.inf))
+            out.sort_key_bits = max(1, (int(a.view(np.int32)[0]) ^ int(b.view(np.int32)[0])).bit_length())
         return out
 
     def sort(self, stream=None) -> "DevicePeaks":

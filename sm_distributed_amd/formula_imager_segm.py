@@ -191,22 +191,22 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
             return IonKeys(np.zeros(0, np.int64), cats, sf_levels), ions, e
         sf_d, code_d, pk_d, mz_d = t(sf).long(), t(codes).long(), t(peak_i).long(), t(mz)
         key_d = sf_d * n_cat + code_d
-        # one synchronisation for the checks: sf range, missing adducts, negative peak_i
-        lims = torch.stack([sf_d.abs().max(), code_d.min(), pk_d.min()]).cpu().tolist()
-        if lims[0] >= (1 << 62) // n_cat:
-            raise ValueError("sf_id out of range")
-        if lims[1] < 0:
-            raise ValueError("sf_peak_df has missing adducts")
-        if lims[2] < 0:
-            raise ValueError("negative peak_i in sf_peak_df")
-        uniq, inv = torch.unique(key_d, sorted=True, return_inverse=True)
+        uniq, inv = torch.unique(key_d, sorted=True, return_inverse=True)  # synchronises (output size)
         n_ions = uniq.numel()
         K = torch.zeros(n_ions, dtype=torch.int64, device=device)
         K.scatter_reduce_(0, inv, pk_d + 1, reduce="amax", include_self=True)
         win_off = torch.zeros(n_ions + 1, dtype=torch.int64, device=device)
         torch.cumsum(K, 0, out=win_off[1:])
+        # one synchronisation for the sizes and the checks: sf range, missing adducts, negative peak_i
+        n_win, kmax, sf_max, code_min, pk_min = (int(v) for v in torch.stack(
+            [win_off[-1], K.max(), sf_d.abs().max(), code_d.min(), pk_d.min()]).cpu().tolist())
+        if sf_max >= (1 << 62) // n_cat:
+            raise ValueError("sf_id out of range")
+        if code_min < 0:
+            raise ValueError("sf_peak_df has missing adducts")
+        if pk_min < 0:
+            raise ValueError("negative peak_i in sf_peak_df")
         slot = win_off[inv] + pk_d
-        n_win, kmax = (int(v) for v in torch.stack([win_off[-1], K.max()]).cpu().tolist())
         # rows per window (atomic adds; torch.bincount runs a slow histogram kernel on ROCm)
         per_slot = torch.zeros(n_win, dtype=torch.int32, device=device)
         per_slot.index_add_(0, slot, torch.ones(1, dtype=torch.int32, device=device).expand(n_rows))
@@ -219,21 +219,23 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
         first = peak_mz[win_off[:-1]]
         first = torch.where(first < 0, torch.full_like(first, float("inf")), first)
         ion_order = torch.sort(first, stable=True).indices
-        # MultiIndex codes of every ion, formed on the device (keys sorted: sf codes nondecreasing)
+        # MultiIndex codes of every ion, formed on the device (keys sorted: sf codes nondecreasing); the host
+        # forms the same codes from the keys when it needs them (IonKeys.level_codes)
         sfc = torch.div(uniq, n_cat, rounding_mode="floor")
         adc = (uniq - sfc * n_cat).to(torch.int16)
-        new = torch.ones(n_ions, dtype=torch.bool, device=device)
-        new[1:] = sfc[1:] != sfc[:-1]
-        sf_code = (torch.cumsum(new.to(torch.int32), 0, dtype=torch.int32) - 1)
         if sf_levels is None:
-            codes_dev = (sf_code, adc)
-            codes = (sfc[new].cpu().numpy(), sf_code.cpu().numpy(), adc.cpu().numpy())
+            new = torch.ones(n_ions, dtype=torch.bool, device=device)
+            new[1:] = sfc[1:] != sfc[:-1]
+            codes_dev = (torch.cumsum(new.to(torch.int32), 0, dtype=torch.int32) - 1, adc)
         else:
             codes_dev = (sfc.to(torch.int32), adc)
-            codes = (np.asarray(sf_levels), codes_dev[0].cpu().numpy(), adc.cpu().numpy())
-        keys = uniq.cpu().numpy()
-        if int(per_slot.max().item()) > 1:
+        # the keys and the duplicate-row check in one copy
+        tail = torch.cat([uniq, (per_slot.max() if n_win else torch.zeros((), dtype=torch.int32, device=device)
+                                 ).to(torch.int64).reshape(1)]).cpu().numpy()
+        keys = tail[:-1]
+        if int(tail[-1]) > 1:
             raise AssertionError("duplicate (sf_id, adduct, peak_i) rows in sf_peak_df")
+        codes = None
     ions = DeviceIons(win_off=win_off, peak_mz=peak_mz, theor=None, win_order=win_order, ion_order=ion_order,
                       n_ions=n_ions, n_windows=n_win, max_k=kmax)
     return IonKeys(keys, cats, sf_levels, keys_dev=uniq, codes=codes, codes_dev=codes_dev), ions, K
