@@ -13,7 +13,7 @@ draws per target as fdr.py does) ~ 0.98M ions, ppm 2, nlevels 30.
 N > 1 (torch.distributed.run, one rank per GPU, RCCL): STRONG scaling of the same config-3 workload.  The
 formula table is sharded once by principal m/z with a cost model (distributed.plan_shards); per step every
 rank selects the m/z slice its windows touch from the replicated resident dataset, runs the same two API
-calls on its shard, and the metric rows are gathered to rank 0 (RCCL all-gather over xGMI), which builds the
+calls on its shard, and the metric rows are gathered to rank 0 (one RCCL gather over xGMI), which builds the
 full table.  ``value`` = rows of rank 0's table / the max-over-ranks step time.
 
 Beside ``value``: ``device_chain`` (the same kernels without the host API layer), per-stage HIP-event times,
@@ -189,7 +189,7 @@ def main():
                 "n_points": info["n_points"], "n_ions": formulas.n_ions, "n_rows_per_step": n_rows,
                 "n_windows": int(formulas.ion_off[-1]), "sum_window_points": sum_hits,
                 "parallelism": (f"formula shards by principal m/z x{world}, dataset replicated, per-rank m/z slice, "
-                                f"RCCL all-gather of metric rows" if sharded else "1 GPU"),
+                                f"RCCL gather of metric rows" if sharded else "1 GPU"),
                 "shard_est_cost_s": plan.est_cost if plan is not None else None,
             },
             "device_chain": chain,

@@ -35,7 +35,7 @@ constexpr int MAXK = 8;              // windows per ion on the LDS path
 constexpr int MAXK_DENSE = 32;       // windows per ion supported at all
 constexpr int NPX_LDS_MAX = 1 << 18; // images up to 262144 pixels use the LDS path
 
-enum { C_NE = 0, C_EMAX, C_ABORT, C_PDUP, C_NEXT, C_NCTR = 8 };
+enum { C_NE = 0, C_EMAX, C_ABORT, C_PDUP, C_NEXT, C_NS, C_NCTR = 8 };
 
 // Diagnostic build only (-DSMG_STAMPS): per-phase wall cycles of the LDS kernel, summed over workgroups
 // into a buffer of their own (read back by smg_debug_stamps); the shipped build executes no stamp.
@@ -872,7 +872,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       uint4* z = reinterpret_cast<uint4*>(smem + LY::o_guard);
       for (int i = tid; i < P.w32 / 4 + 1; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
       for (int i = tid; i < MAXK * NW * 4; i += BLOCK) part[i] = 0.0;
-      if (tid < C_NEXT) ctr[tid] = 0;
+      if (tid < C_NEXT || tid == C_NS) ctr[tid] = 0;
 #ifndef SMG_TBL0
 #define SMG_TBL0 1
 #endif
@@ -1314,15 +1314,12 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         }
         __syncthreads();
       }
-      for (int ob = 0; ob < ((SMG_ABL & 64) ? 0 : nnz); ob += BLOCK) {  // uniform trip count: wave-compacted
-        const int oc_i = ob + tid;
-        const int s = oc_i < nnz ? (int)olist[oc_i] : 0;
-        int rs, cs;
+      // the 7x7 window of principal pixel s: H[d] = columns cs-3..cs+3 of row rs-3+d
+      auto rows7 = [&](int s, int& rs, int& cs, uint32_t& cv, uint32_t (&H)[7]) {
         rowcol(s, P, rs, cs);
         // valid-column mask of columns cs-3..cs+3
         const int clo = 3 - cs > 0 ? 3 - cs : 0, chi = P.ncols - cs + 3 < 7 ? P.ncols - cs + 3 : 7;
-        const uint32_t cv = ((1u << chi) - 1u) & ~((1u << clo) - 1u);
-        uint32_t H[7];
+        cv = ((1u << chi) - 1u) & ~((1u << clo) - 1u);
 #pragma unroll
         for (int d = 0; d < 7; ++d) {
           if constexpr (TWO) {
@@ -1339,19 +1336,62 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
             H[d] = bits7(Hbm, rs - 3 + d, cs - 3, cv, P);
           }
         }
-        // sparsity pre-filter (erosion border = background only): an eL>0 pixel p in the cross of s has its 3x3
-        // box covered by 4-crosses of principal pixels, which takes at least three of them (one cross meets at
-        // most two corners of the box, and a cross through the centre none), all in p's 5x5, inside s's 7x7
+      };
+      // sparsity pre-filter (erosion border = background only): an eL>0 pixel p in the cross of s has its 3x3
+      // box covered by 4-crosses of principal pixels, which takes at least three of them (one cross meets at
+      // most two corners of the box, and a cross through the centre none), all in p's 5x5, inside s's 7x7
 #ifndef SMG_SCREEN3
 #define SMG_SCREEN3 1
 #endif
-        const bool isolated =
-            !P.erosion_border &&
-            (SMG_SCREEN3 ? (__popc(H[0]) + __popc(H[1]) + __popc(H[2]) + __popc(H[3]) + __popc(H[4]) + __popc(H[5]) +
-                            __popc(H[6])) < 3
-                         : (H[0] | H[1] | H[2] | (H[3] & ~8u) | H[4] | H[5] | H[6]) == 0u);
+      auto sparse = [&](const uint32_t (&H)[7]) {
+        return !P.erosion_border &&
+               (SMG_SCREEN3 ? (__popc(H[0]) + __popc(H[1]) + __popc(H[2]) + __popc(H[3]) + __popc(H[4]) +
+                               __popc(H[5]) + __popc(H[6])) < 3
+                            : (H[0] | H[1] | H[2] | (H[3] & ~8u) | H[4] | H[5] | H[6]) == 0u);
+      };
+      // Pass A (erosion border 0): the principal pixels that pass the pre-filter (a few percent of a noise
+      // image) are listed, wave-compacted, from the top of the candidate array down; pass B runs the full
+      // screen over full waves of them only.  Candidates fill the array from the bottom (capacity CAPC - nsurv).
+#ifndef SMG_SCREEN2P
+#define SMG_SCREEN2P 1
+#endif
+      const int nscreen = (SMG_ABL & 64) ? 0 : nnz;
+      int nsurv = nscreen, ccap = CAPC;
+      bool two_pass = SMG_SCREEN2P && !P.erosion_border;
+      if (two_pass) {
+        for (int ob = 0; ob < nscreen; ob += BLOCK) {  // uniform trip count
+          const int oc_i = ob + tid;
+          const int s0p = oc_i < nnz ? (int)olist[oc_i] : 0;
+          int rs, cs;
+          uint32_t cv, H[7];
+          rows7(s0p, rs, cs, cv, H);
+          const bool surv = oc_i < nnz && !sparse(H);
+          const uint64_t m = __ballot(surv);
+          if (m) {
+            int wbase = 0;
+            if (lane == 0) wbase = atomicAdd(&ctr[C_NS], (int)__popcll(m));
+            const int idx = __builtin_amdgcn_readfirstlane(wbase) + (int)__popcll(m & ((1ull << lane) - 1ull));
+            if (surv) epix[CAPC - 1 - idx] = (uint32_t)s0p;
+          }
+        }
+        __syncthreads();
+        nsurv = ctr[C_NS];
+        ccap = CAPC - nsurv;
+        if (nsurv * 4 > CAPC) {  // a dense image: its candidates need the whole array -- screen every pixel
+          two_pass = false;
+          nsurv = nscreen;
+          ccap = CAPC;
+        }
+      }
+      for (int ob = 0; ob < nsurv; ob += BLOCK) {  // uniform trip count: wave-compacted
+        const int oc_i = ob + tid;
+        const int s = oc_i < nsurv ? (int)(two_pass ? epix[CAPC - 1 - oc_i] : olist[oc_i]) : 0;
+        int rs, cs;
+        uint32_t cv, H[7];
+        rows7(s, rs, cs, cv, H);
+        const bool isolated = sparse(H);
         uint32_t pass = 0;
-        if (oc_i < nnz && !isolated) {
+        if (oc_i < nsurv && !isolated) {
         uint32_t Dl[7];
         Dl[0] = Dl[6] = 0;
 #pragma unroll
@@ -1388,7 +1428,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
             const int ci = __ffs(pass) - 1;
             pass &= pass - 1;
             const int p = s + (ci == 1 ? 1 : ci == 2 ? -1 : ci == 3 ? -P.ncols : ci == 4 ? P.ncols : 0);
-            if (idx < CAPC) epix[idx] = (uint32_t)p;
+            if (idx < ccap) epix[idx] = (uint32_t)p;
             ++idx;
           }
         }
@@ -1396,7 +1436,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       __syncthreads();
       STAMP(4);
       const int ncand = (SMG_ABL & 32) ? 0 : ctr[C_NE];
-      if (ncand > CAPC) {
+      if (ncand > ccap) {
         reject();
         skip = true;
       }

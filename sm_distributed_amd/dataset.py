@@ -53,8 +53,8 @@ class DeviceDataset:
         off = np.zeros(len(spectra) + 1, np.int64)
         mzs, its = [], []
         for i, (_, mz, it) in enumerate(spectra):
-            mzs.append(np.asarray(mz, np.float32))
-            its.append(np.asarray(it, np.float32))
+            mzs.append(to_f32(mz, "m/z"))
+            its.append(to_f32(it, "intensity"))
             off[i + 1] = off[i] + len(mzs[-1])
         mz = np.concatenate(mzs) if mzs else np.zeros(0, np.float32)
         it = np.concatenate(its) if its else np.zeros(0, np.float32)
@@ -66,6 +66,23 @@ class DeviceDataset:
         return cls(read_imzml(imzml_path), device=device)
 
 
+_WARNED = set()
+
+
+def to_f32(a, what):
+    """``a`` as float32 (the resident format).  A lossy narrowing (f64 values that are not f32 values) is reported
+    once per quantity: intensities change by <= 6e-8 relative (inside the 1e-6 / 1e-5 tolerances), but an m/z
+    within that distance of a window bound can land on the other side of it."""
+    src = np.asarray(a)
+    out = src.astype(np.float32, copy=False)
+    if src.dtype != np.float32 and what not in _WARNED and src.size and not np.array_equal(out, src):
+        import warnings
+        _WARNED.add(what)
+        warnings.warn(f"{what}: {src.dtype} values rounded to float32 (resident format); relative change <= 6e-8",
+                      RuntimeWarning, stacklevel=3)
+    return out
+
+
 def spectra_from_duck(ds):
     """Collect any reference-style dataset (get_spectra RDD + pixel map + dims) into a SpectraSet-like tuple."""
     items = ds.get_spectra().collect()
@@ -75,8 +92,8 @@ def spectra_from_duck(ds):
     mzs = [np.zeros(0, np.float32)] * n
     its = [np.zeros(0, np.float32)] * n
     for sp_id, mz, it in items:
-        mzs[sp_id] = np.asarray(mz, np.float32)
-        its[sp_id] = np.asarray(it, np.float32)
+        mzs[sp_id] = to_f32(mz, "m/z")
+        its[sp_id] = to_f32(it, "intensity")
     for i in range(n):
         off[i + 1] = off[i] + len(mzs[i])
     mz = np.concatenate(mzs) if n else np.zeros(0, np.float32)

@@ -191,21 +191,32 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
             return IonKeys(np.zeros(0, np.int64), cats, sf_levels), ions, e
         sf_d, code_d, pk_d, mz_d = t(sf).long(), t(codes).long(), t(peak_i).long(), t(mz)
         key_d = sf_d * n_cat + code_d
-        uniq, inv = torch.unique(key_d, sorted=True, return_inverse=True)  # synchronises (output size)
-        n_ions = uniq.numel()
-        K = torch.zeros(n_ions, dtype=torch.int64, device=device)
-        K.scatter_reduce_(0, inv, pk_d + 1, reduce="amax", include_self=True)
-        win_off = torch.zeros(n_ions + 1, dtype=torch.int64, device=device)
-        torch.cumsum(K, 0, out=win_off[1:])
-        # one synchronisation for the sizes and the checks: sf range, missing adducts, negative peak_i
-        n_win, kmax, sf_max, code_min, pk_min = (int(v) for v in torch.stack(
-            [win_off[-1], K.max(), sf_d.abs().max(), code_d.min(), pk_d.min()]).cpu().tolist())
+        # one synchronisation for the key range and the checks: sf range, missing adducts, negative peak_i
+        kmin, kmax_key, sf_max, code_min, pk_min = (int(v) for v in torch.stack(
+            [key_d.min(), key_d.max(), sf_d.abs().max(), code_d.min(), pk_d.min()]).cpu().tolist())
         if sf_max >= (1 << 62) // n_cat:
             raise ValueError("sf_id out of range")
         if code_min < 0:
             raise ValueError("sf_peak_df has missing adducts")
         if pk_min < 0:
             raise ValueError("negative peak_i in sf_peak_df")
+        span = kmax_key - kmin + 1
+        if kmin >= 0 and span <= 8 * n_rows + (1 << 22):
+            # dense key range (integer sf ids): ion index = rank of the key among the present ones, from a
+            # presence table and its prefix sum -- no sort of the rows
+            present = torch.zeros(span, dtype=torch.int32, device=device)
+            present[key_d - kmin] = 1
+            rank = torch.cumsum(present, 0, dtype=torch.int64)
+            inv = rank[key_d - kmin] - 1
+            uniq = torch.nonzero(present).flatten() + kmin  # synchronises (output size)
+        else:
+            uniq, inv = torch.unique(key_d, sorted=True, return_inverse=True)  # synchronises (output size)
+        n_ions = uniq.numel()
+        K = torch.zeros(n_ions, dtype=torch.int64, device=device)
+        K.scatter_reduce_(0, inv, pk_d + 1, reduce="amax", include_self=True)
+        win_off = torch.zeros(n_ions + 1, dtype=torch.int64, device=device)
+        torch.cumsum(K, 0, out=win_off[1:])
+        n_win, kmax = (int(v) for v in torch.stack([win_off[-1], K.max()]).cpu().tolist())
         slot = win_off[inv] + pk_d
         # rows per window (atomic adds; torch.bincount runs a slow histogram kernel on ROCm)
         per_slot = torch.zeros(n_win, dtype=torch.int32, device=device)

@@ -13,6 +13,7 @@ import xml.etree.ElementTree as ET
 
 import numpy as np
 
+from .dataset import to_f32
 from .synthetic import SpectraSet
 
 _DTYPES = {"MS:1000521": np.float32, "MS:1000523": np.float64, "IMS:1000141": np.int32, "IMS:1000142": np.int64,
@@ -67,8 +68,8 @@ def read_imzml(imzml_path: str, ibd_path: str | None = None) -> SpectraSet:
     off = np.zeros(len(arrays) + 1, np.int64)
     mzs, its = [], []
     for i, ((mo, ml, mdt), (io, il, idt)) in enumerate(arrays):
-        mz = np.frombuffer(buf, dtype=mdt, count=ml, offset=mo).astype(np.float32)
-        it = np.frombuffer(buf, dtype=idt, count=il, offset=io).astype(np.float32)
+        mz = to_f32(np.frombuffer(buf, dtype=mdt, count=ml, offset=mo), "m/z")
+        it = to_f32(np.frombuffer(buf, dtype=idt, count=il, offset=io), "intensity")
         mzs.append(mz)
         its.append(it)
         off[i + 1] = off[i] + ml
