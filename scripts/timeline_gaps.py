@@ -28,6 +28,12 @@ ks.sort()
 starts = [i for i, k in enumerate(ks) if a.start in k[2]]
 if len(starts) < 2:
     raise SystemExit(f"fewer than two launches of {a.start}")
+# every step: its window and its longest kernels
+for j, st_i in enumerate(starts):
+    en_i = starts[j + 1] if j + 1 < len(starts) else len(ks)
+    top = sorted(ks[st_i:en_i], key=lambda k: k[0] - k[1])[:4]
+    print(f"step {j}: window {(ks[en_i - 1][1] - ks[st_i][0]) / 1e6:.3f} ms; longest: " +
+          ", ".join(f"{k[2].split('(')[0][-40:]} {(k[1] - k[0]) / 1e3:.0f} us" for k in top))
 s = starts[a.which]
 e = starts[a.which + 1] if a.which + 1 < len(starts) and a.which != -1 else len(ks)
 t0, t1 = ks[s][0], ks[e - 1][1]

@@ -813,6 +813,58 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   STAMP_DECL();
   if (tid == 0) ctr[C_NEXT] = (int)sched_resolve<SRC>(S, sched_issue<SRC>(S));
   __syncthreads();
+#ifndef SMG_LATEFIN
+#define SMG_LATEFIN 1
+#endif
+  static_assert(!SMG_LATEFIN || NW >= 2, "late finalize needs a second wave for the LDS initialisation");
+  struct {
+    double s, sy, syy, sxy, t, sx, sxx, chaos;
+    int K, ion;
+    uint32_t flags;
+    bool pending;
+  } fin;
+  fin.pending = false;
+  // the finalize arithmetic of the ion whose inputs wave 0 gathered (a no-op elsewhere)
+  auto finalize = [&]() {
+    if (!fin.pending) return;
+    fin.pending = false;
+    const int k = lane;
+    const int K = fin.K;
+    const double s = fin.s, sy = fin.sy, syy = fin.syy, sxy = fin.sxy, t = fin.t, sx = fin.sx, sxx = fin.sxx;
+    // isotope_pattern_match
+    const double nt = sqrt(wave_sum_dpp(t * t)), ns = sqrt(wave_sum_dpp(s * s));
+    double spectral = 1.0 - wave_sum_dpp(k < K ? fabs(t / nt - s / ns) : 0.0) / (double)K;
+    if (spectral == 1.0) spectral = 0.0;
+    // isotope_image_correlation: np.corrcoef rows, weights = theor[1:]
+    double spatial = 0.0;
+    if (K >= 2) {
+      const double npx = (double)P.npx, n1 = npx - 1.0;
+      const double sd0 = sqrt((sxx - sx * sx / npx) / n1);
+      double rt = 0.0, tw = 0.0;
+      if (k >= 1 && k < K) {
+        const double syy_c = (syy - sy * sy / npx) / n1;
+        const double sxy_c = (sxy - sx * sy / npx) / n1;
+        double r = sxy_c / sqrt(syy_c) / sd0;
+        if (!isnan(r)) r = r > 1.0 ? 1.0 : (r < -1.0 ? -1.0 : r);
+        if (isinf(r)) r = 0.0;
+        rt = r * t;
+        tw = t;
+      }
+      spatial = wave_sum_dpp(rt) / wave_sum_dpp(tw);
+    }
+    if (lane == 0) {
+      double chaos = fin.chaos;
+      if (!isnan(chaos) && fabs(chaos - 1.0) <= 1e-8 + 1e-5) chaos = 0.0;  // np.isclose(moc, 1.0)
+      chaos = clean(chaos);
+      spatial = clean(spatial);
+      spectral = clean(spectral);
+      oc[fin.ion] = chaos;
+      osp[fin.ion] = spatial;
+      osc[fin.ion] = spectral;
+      omsm[fin.ion] = chaos * spatial * spectral;
+      oflags[fin.ion] = fin.flags;
+    }
+  };
   int64_t pos = -1;  // ion scored in this iteration (-1: none; the first iteration only issues loads)
   int64_t npos = uni(ctr[C_NEXT]);
   int cur = 0;
@@ -868,21 +920,25 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     }
 
     // ---- phase 0: LDS initialisation -------------------------------------------------------------
-    if (!skip) {
+    // wave 0 finishes the previous ion meanwhile (SMG_LATEFIN): the other waves initialise the LDS
+    constexpr int ZW = SMG_LATEFIN ? WAVE : 0;
+    const int zt = tid - ZW;
+    if (!skip && zt >= 0) {
       uint4* z = reinterpret_cast<uint4*>(smem + LY::o_guard);
-      for (int i = tid; i < P.w32 / 4 + 1; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
-      for (int i = tid; i < MAXK * NW * 4; i += BLOCK) part[i] = 0.0;
-      if (tid < C_NEXT || tid == C_NS) ctr[tid] = 0;
+      for (int i = zt; i < P.w32 / 4 + 1; i += BLOCK - ZW) z[i] = make_uint4(0, 0, 0, 0);
+      for (int i = zt; i < MAXK * NW * 4; i += BLOCK - ZW) part[i] = 0.0;
+      if (zt < C_NEXT || zt == C_NS) ctr[zt] = 0;
 #ifndef SMG_TBL0
 #define SMG_TBL0 1
 #endif
       if (SMG_TBL0) {  // the duplicate table (free since the previous ion's chaos phase), for phase d
-        for (int i = tid; i < DTBL; i += BLOCK) {
+        for (int i = zt; i < DTBL; i += BLOCK - ZW) {
           tkey[i] = 0xFFFFFFFFu;
           tval[i] = 0.0;
         }
       }
     }
+    finalize();
     __syncthreads();
     STAMP(0);
 
@@ -1635,61 +1691,40 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     }
 
     // ---- finalize (formula_img_validator.py:78-84 + the restated pyImagingMSpec functions): wave 0,
-    // lane k = window k; sums over lanes in a fixed order
+    // lane k = window k; sums over lanes in a fixed order.  Its inputs are read here; the arithmetic runs
+    // during the next ion's phase 0, which the other waves do alone (SMG_LATEFIN)
     if (!skip && wid == 0) {
       const int k = lane;
-      double s = 0.0, sy = 0.0, syy = 0.0, sxy = 0.0, t = 0.0;
+      fin.s = fin.sy = fin.syy = fin.sxy = fin.t = 0.0;
       if (k < K) {
-        t = D->theor[k];
+        fin.t = D->theor[k];
         if (k == 0) {
-          s = s0;
+          fin.s = s0;
         } else {
-          sy = D->sy[k];
-          syy = D->syy[k];  // + the squared per-pixel sums of duplicate candidates (part[k][*][2])
+          fin.sy = D->sy[k];
+          fin.syy = D->syy[k];  // + the squared per-pixel sums of duplicate candidates (part[k][*][2])
 #pragma unroll
           for (int w = 0; w < NW; ++w) {
             const double* pk = part + ((size_t)k * NW + w) * 4;
-            s += pk[0];
-            syy += pk[2];
-            sxy += pk[3];
+            fin.s += pk[0];
+            fin.syy += pk[2];
+            fin.sxy += pk[3];
           }
         }
       }
-      // isotope_pattern_match
-      const double nt = sqrt(wave_sum_dpp(t * t)), ns = sqrt(wave_sum_dpp(s * s));
-      double spectral = 1.0 - wave_sum_dpp(k < K ? fabs(t / nt - s / ns) : 0.0) / (double)K;
-      if (spectral == 1.0) spectral = 0.0;
-      // isotope_image_correlation: np.corrcoef rows, weights = theor[1:]
-      double spatial = 0.0;
-      if (K >= 2) {
-        const double npx = (double)P.npx, n1 = npx - 1.0;
-        const double sd0 = sqrt((sxx - sx * sx / npx) / n1);
-        double rt = 0.0, tw = 0.0;
-        if (k >= 1 && k < K) {
-          const double syy_c = (syy - sy * sy / npx) / n1;
-          const double sxy_c = (sxy - sx * sy / npx) / n1;
-          double r = sxy_c / sqrt(syy_c) / sd0;
-          if (!isnan(r)) r = r > 1.0 ? 1.0 : (r < -1.0 ? -1.0 : r);
-          if (isinf(r)) r = 0.0;
-          rt = r * t;
-          tw = t;
-        }
-        spatial = wave_sum_dpp(rt) / wave_sum_dpp(tw);
-      }
-      if (lane == 0) {
-        double chaos = chaos_raw;
-        if (!isnan(chaos) && fabs(chaos - 1.0) <= 1e-8 + 1e-5) chaos = 0.0;  // np.isclose(moc, 1.0)
-        chaos = clean(chaos);
-        spatial = clean(spatial);
-        spectral = clean(spectral);
-        oc[ion] = chaos;
-        osp[ion] = spatial;
-        osc[ion] = spectral;
-        omsm[ion] = chaos * spatial * spectral;
-        oflags[ion] = flags | big_flag | (TWO ? SMG_ION_TWO_LEVEL : 0u) | (uint32_t)D->hits;
-      }
+      fin.K = K;
+      fin.ion = ion;
+      fin.sx = sx;
+      fin.sxx = sxx;
+      fin.chaos = chaos_raw;
+      fin.flags = flags | big_flag | (TWO ? SMG_ION_TWO_LEVEL : 0u) | (uint32_t)D->hits;
+      fin.pending = true;
+      if (!SMG_LATEFIN) finalize();
     }
-    if (npos < 0) break;
+    if (npos < 0) {
+      finalize();
+      break;
+    }
     pos = npos;
     npos = n2pos;
     cur ^= 1;
