@@ -568,6 +568,75 @@ __global__ void ion_desc_kernel(Hits<FMT> hits, const int64_t* __restrict__ lo, 
   for (int i = 0; i < 3; ++i) reinterpret_cast<int4*>(d->pad)[i] = make_int4(0, 0, 0, 0);
 }
 
+// The same descriptors with eight lanes per ion, lane k = window k (k >= 8: the has-hits test of windows 8..31):
+// the two partial 64-point blocks of every window are summed in parallel instead of one window after another.
+template <int FMT>
+__global__ void ion_desc8_kernel(Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
+                                 const int64_t* __restrict__ ion_off, const double* __restrict__ theor,
+                                 const DD4* __restrict__ cum, const int64_t* __restrict__ ion_order, int64_t n_ions,
+                                 IonDesc* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t b = t >> 3;
+  const int k = (int)(t & 7);
+  const bool live = b < n_ions;
+  const int64_t ion = live ? (ion_order ? ion_order[b] : b) : 0;
+  const int64_t w0 = live ? ion_off[ion] : 0;
+  const int K = live ? (int)(ion_off[ion + 1] - w0) : 0;
+  int64_t a = 0, n = 0;
+  double wt = 0.0, wy = 0.0, wyy = 0.0;
+  if (k < K) {
+    a = lo[w0 + k];
+    n = hi[w0 + k] - a;
+    wt = theor[w0 + k];
+    const double2 ws = window_sums<FMT>(hits, cum, a, a + n);
+    wy = ws.x;
+    wyy = ws.y;
+  }
+  bool has = n > 0;
+  for (int kk = k + MAXK; kk < K && kk < MAXK_DENSE; kk += MAXK) has |= hi[w0 + kk] > lo[w0 + kk];
+  // groups of the tail windows 1..K-1: exclusive prefix over the eight lanes of this ion
+  const int64_t gk = (k >= 1 && k < K) ? (n + 63) / 64 : 0;
+  int64_t inc = gk;
+#pragma unroll
+  for (int d = 1; d < 8; d <<= 1) {
+    const int64_t v = __shfl_up(inc, d, 8);
+    if (k >= d) inc += v;
+  }
+  const int64_t g = inc - gk;            // first group of window k
+  const int64_t ng_all = __shfl(inc, 7, 8);
+  // any lane of the ion with a point: OR over the eight lanes
+  uint32_t hv = has ? 1u : 0u;
+#pragma unroll
+  for (int d = 1; d < 8; d <<= 1) hv |= __shfl_xor(hv, d, 8);
+  if (!live) return;
+  IonDesc* d = out + b;
+  int64_t wb = 0;
+  int32_t we = 0, wg = 0x7FFFFFFF;
+  if (k < K) {
+    if (k == 0) {
+      wb = a;
+      we = (int32_t)(n < 0x7FFFFFFF ? n : 0x7FFFFFFF);
+      wg = 0;
+    } else {
+      wb = a - 64 * g;
+      we = (int32_t)(64 * g + n < 0x7FFFFFFF ? 64 * g + n : 0x7FFFFFFF);
+      wg = (int32_t)(g < 0x7FFFFFFF ? g : 0x7FFFFFFF);
+    }
+  }
+  d->base[k] = wb;
+  d->end[k] = we;
+  d->gs[k] = wg;
+  d->theor[k] = wt;
+  d->sy[k] = wy;
+  d->syy[k] = wyy;
+  if (k == 0) {
+    const int32_t ng = 64 * ng_all < (1ll << 30) ? (int32_t)ng_all : -1;
+    reinterpret_cast<int4*>(&d->ion)[0] = make_int4((int32_t)ion, K, ng, hv ? (int)SMG_ION_HAS_HITS : 0);
+  } else if (k < 4) {
+    reinterpret_cast<int4*>(d->pad)[k - 1] = make_int4(0, 0, 0, 0);
+  }
+}
+
 // Work sources of the persistent LDS kernel.
 //  SRC_RANGES: positions [0, n) split into 8 contiguous ranges, one per XCD (workgroup w runs on XCD w % 8),
 //    so concurrently scored ions of one XCD are m/z neighbours and share windows in that XCD's L2; a
@@ -3253,8 +3322,15 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   const bool big_ok = !P.clip && !g_force_dense && (two || P.npx <= NPX_LDS_MAX) && lds_big <= BIG_LDS;
   const int cus = device_cus();
   if (main_ok || big_ok) {
-    hipLaunchKernelGGL(ion_desc_kernel<FMT>, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, hits, lo, hi,
-                       ion_off, theor, reinterpret_cast<const DD4*>(hit_cum), ion_order, n_ions, desc);
+#ifndef SMG_DESC8
+#define SMG_DESC8 1
+#endif
+    if (SMG_DESC8)
+      hipLaunchKernelGGL(ion_desc8_kernel<FMT>, dim3((unsigned)((n_ions * 8 + 255) / 256)), dim3(256), 0, st, hits,
+                         lo, hi, ion_off, theor, reinterpret_cast<const DD4*>(hit_cum), ion_order, n_ions, desc);
+    else
+      hipLaunchKernelGGL(ion_desc_kernel<FMT>, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, hits, lo,
+                         hi, ion_off, theor, reinterpret_cast<const DD4*>(hit_cum), ion_order, n_ions, desc);
     SMG_LAUNCH_CHECK();
   }
   if (main_ok) {
