@@ -99,6 +99,16 @@ int smg_slice_mz_copy(const int64_t* sp_off, int64_t n_spectra, const float* mz,
 int smg_window_bounds(const double* peak_mz, const int64_t* order, int64_t n_windows, double ppm,
                       const float* mz_sorted, int64_t n_points, int64_t* lo, int64_t* hi, void* stream);
 
+/* Window alignment for scoring (formula_img_validator.py:73-75 and 115-118): ion i has the layout windows
+ * [win_off[i], win_off[i+1]) (one per peak_i of sf_peak_df) and kt_off[i+1] - kt_off[i] theoretical
+ * intensities (len(sf_peak_ints[(sf_id, adduct)])); compute() pads the image list with empty images up to that
+ * length and ignores images beyond it.  Writes, for every theoretical slot j = kt_off[i] + k, the window run
+ * lo2[j], hi2[j] (layout window k, or the empty run 0, 0 when k is past the layout windows), and keep[i] = 1 if
+ * the ion has a row in the metrics table: some layout window is non-empty, some scored window among the first
+ * 32 is non-empty (the SMG_ION_HAS_HITS of smg_ion_metrics) and sel[i] != 0 (sel optional, NULL = all). */
+int smg_align_windows(const int64_t* lo, const int64_t* hi, const int64_t* win_off, const int64_t* kt_off,
+                      const uint8_t* sel, int64_t n_ions, int64_t* lo2, int64_t* hi2, uint8_t* keep, void* stream);
+
 /* Prefix sums over the m/z-sorted hits at 64-point granularity (exclusive, 4 doubles per entry,
  * ceil(n_points/64)+1 entries): cum64[b] = (sum of intensities of points < 64*b, sum of squared intensities
  * of those points without the duplicate-candidate flag), each as a double-double (hi, lo) pair, so that a

@@ -471,6 +471,40 @@ int smg_window_bounds(const double* peak_mz, const int64_t* order, int64_t n_win
   return SMG_OK;
 }
 
+// one thread per ion: its scored windows' runs (layout window or empty) and its table-row flag
+__global__ void align_windows_kernel(const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
+                                     const int64_t* __restrict__ win_off, const int64_t* __restrict__ kt_off,
+                                     const uint8_t* __restrict__ sel, int64_t n_ions, int64_t* __restrict__ lo2,
+                                     int64_t* __restrict__ hi2, uint8_t* __restrict__ keep) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_ions) return;
+  const int64_t w0 = win_off[i], nw = win_off[i + 1] - w0;
+  const int64_t t0 = kt_off[i], nt = kt_off[i + 1] - t0;
+  bool has = false, hit = false;
+  for (int64_t k = 0; k < nw; ++k) {
+    const int64_t a = lo[w0 + k], b = hi[w0 + k];
+    has |= b > a;
+    if (k < nt) {
+      lo2[t0 + k] = a;
+      hi2[t0 + k] = b;
+      hit |= (k < 32) && (b > a);
+    }
+  }
+  for (int64_t k = nw; k < nt; ++k) lo2[t0 + k] = hi2[t0 + k] = 0;
+  keep[i] = (has && hit && (!sel || sel[i])) ? 1 : 0;
+}
+
+int smg_align_windows(const int64_t* lo, const int64_t* hi, const int64_t* win_off, const int64_t* kt_off,
+                      const uint8_t* sel, int64_t n_ions, int64_t* lo2, int64_t* hi2, uint8_t* keep, void* stream) {
+  SMG_CHECK_ARG(n_ions >= 0, "negative size");
+  if (n_ions == 0) return SMG_OK;
+  SMG_CHECK_ARG(lo && hi && win_off && kt_off && lo2 && hi2 && keep, "null pointer");
+  hipLaunchKernelGGL(align_windows_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, as_stream(stream),
+                     lo, hi, win_off, kt_off, sel, n_ions, lo2, hi2, keep);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
 int smg_sample_spectra(const int64_t* sp_off, const double* mzs, const double* cum_ints, int64_t n_spectra,
                        const double* lower, const double* upper, int64_t n_windows, int64_t* out_window,
                        int64_t* out_spectrum, double* out_value, int64_t capacity, int64_t* count,

@@ -129,10 +129,11 @@ def _theor_arrays(ims, sf_ints, device):
         # (a search per step over the same formula table), without its two synchronisations
         last = cache.get(("last",) + sig)
         if last is not None and len(last[0]) == n and np.array_equal(last[0], ik.keys):
-            return last[1], last[2]
+            return last[1], last[2], last[3]
         ion_key = ik.keys_dev if ik.keys_dev is not None else torch.from_numpy(ik.keys).to(device)
         if n == 0:
-            return torch.zeros(0, dtype=torch.int64, device=device), torch.zeros(0, dtype=torch.float64, device=device)
+            return (torch.zeros(0, dtype=torch.int64, device=device), torch.zeros(0, dtype=torch.float64, device=device),
+                    torch.zeros(1, dtype=torch.int64, device=device))
         if pk_key.numel() == 0:
             raise KeyError(ims.keys[0])
         j = torch.searchsorted(pk_key, ion_key).clamp_(max=pk_key.numel() - 1)
@@ -146,13 +147,15 @@ def _theor_arrays(ims, sf_ints, device):
         n_t = int(off_t[-1].item())
         owner = torch.repeat_interleave(torch.arange(n, device=device), Kt, output_size=n_t)
         k_in = torch.arange(n_t, device=device) - off_t[owner]
-        out = (Kt, pk_val[pk_off[row][owner] + k_in])
+        out = (Kt, pk_val[pk_off[row][owner] + k_in], off_t)
         cache[("last",) + sig] = (np.array(ik.keys, copy=True),) + out
         return out
     vals = [sf_ints[k] for k in ims.keys]
     Kt = np.array([len(v) for v in vals], dtype=np.int64)
     flat = np.concatenate([np.asarray(v, np.float64) for v in vals]) if n else np.zeros(0)
-    return torch.from_numpy(Kt).to(device), torch.from_numpy(flat).to(device)
+    off = np.zeros(n + 1, np.int64)
+    np.cumsum(Kt, out=off[1:])
+    return torch.from_numpy(Kt).to(device), torch.from_numpy(flat).to(device), torch.from_numpy(off).to(device)
 
 
 def _metrics_device_rows(ims, sf_ints, img_conf, prelaunch=None):
@@ -169,7 +172,8 @@ def _metrics_device_rows(ims, sf_ints, img_conf, prelaunch=None):
     import torch
 
     from . import engine as E
-    from ._lib import SMG_HITS_PACKED_F32
+    from ._lib import SMG_HITS_PACKED_F32, check, lib
+    from .engine import _p, _stream
     from .formula_imager_segm import _side_stream
     opts = _chaos_opts(img_conf)
     ims.ensure_current()
@@ -178,30 +182,20 @@ def _metrics_device_rows(ims, sf_ints, img_conf, prelaunch=None):
     main = torch.cuda.current_stream(dev)
     side = _side_stream(dev)
     with torch.cuda.stream(side):
-        Kt, theor = _theor_arrays(ims, sf_ints, dev)
-        K_img = ims.K
-        win_off_img = ims.ions_dev.win_off
-        n_t = theor.numel()
-        off_t = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-        torch.cumsum(Kt, 0, out=off_t[1:])
-        owner = torch.repeat_interleave(torch.arange(n, device=dev), Kt, output_size=n_t)
-        k_in = torch.arange(n_t, device=dev) - off_t[owner]
-        valid = k_in < K_img[owner]
-        src = win_off_img[owner] + torch.minimum(k_in, (K_img[owner] - 1).clamp_(min=0))
-        sel_dev = None if ims._sel is None else torch.from_numpy(ims._sel).to(dev)
+        Kt, theor, off_t = _theor_arrays(ims, sf_ints, dev)
+        sel_dev = None if ims._sel is None else torch.from_numpy(ims._sel.astype(np.uint8)).to(dev)
     main.wait_stream(side)
-    for t in (Kt, theor, off_t, valid, src) + ((sel_dev,) if sel_dev is not None else ()):
+    for t in (Kt, theor, off_t) + ((sel_dev,) if sel_dev is not None else ()):
         t.record_stream(main)
-    has = ims.has_images_device()  # reads lo / hi: on the main stream, after the window search
-    zero = torch.zeros((), dtype=torch.int64, device=dev)
-    lo2 = torch.where(valid, ims.lo[src], zero)
-    hi2 = torch.where(valid, ims.hi[src], zero)
-    # the kernel's SMG_ION_HAS_HITS: a non-empty window among the ion's first min(Kt, MAXK_DENSE = 32)
-    hit = torch.zeros(n_t + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(((hi2 > lo2) & (k_in < 32)).to(torch.int64), 0, out=hit[1:])
-    keep = has & ((hit[off_t[1:]] - hit[off_t[:-1]]) > 0)
-    if sel_dev is not None:
-        keep &= sel_dev
+    # the scored windows (the layout's, padded with empty runs up to len(sf_ints[key])) and the table-row flags
+    # in one launch (smg_align_windows), on the main stream after the window search
+    n_t = theor.numel()
+    lo2 = torch.empty(n_t, dtype=torch.int64, device=dev)
+    hi2 = torch.empty(n_t, dtype=torch.int64, device=dev)
+    keep8 = torch.empty(n, dtype=torch.uint8, device=dev)
+    check(lib().smg_align_windows(_p(ims.lo), _p(ims.hi), _p(ims.ions_dev.win_off), _p(off_t), _p(sel_dev), n,
+                                  _p(lo2), _p(hi2), _p(keep8), _stream(None)), "smg_align_windows")
+    keep = keep8.view(torch.bool)
     if prelaunch is not None:
         prelaunch(keep)
     nrows, ncols = ims.dims
