@@ -15,6 +15,8 @@ ions = syn.make_ion_table(n_sf, seed=43, decoy_seed=44)
 mz, hits, dims, info = syn.make_dataset_torch(nrows, ncols, pk, seed=42, device="cuda", ions=ions)
 peaks = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
 dions = E.DeviceIons.from_arrays(ions.win_off, ions.peak_mz, ions.peak_int)
+if os.environ.get("SMG_FORCE_TWO"):  # diagnostic: the two-level LDS passes for every image size
+    _lib.lib().smg_debug_force_two_level(1)
 m, lo, hi = E.run_hot_path(peaks, dions, 2.0, 30)
 torch.cuda.synchronize()
 ts = []
