@@ -647,6 +647,12 @@ enum { SRC_RANGES = 0, SRC_LIST = 1 };
 #define SMG_XCDS 8  // diagnostic: 1 = one global range (no XCD locality)
 #endif
 constexpr int XCDS = SMG_XCDS;
+#ifndef SMG_SCREEN2P
+#define SMG_SCREEN2P 1  // chaos screen in two passes (pre-filtered survivors, then the full screen over them)
+#endif
+#ifndef SMG_NOB3
+#define SMG_NOB3 1      // no barrier after the duplicate-table reduce when the two-pass screen follows
+#endif
 constexpr int CTR_STRIDE = 32;  // u32 words between counters (one 128-B line each)
 
 struct Sched {
@@ -1385,7 +1391,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
               atomicAdd(&part[(size_t)(key & 7u) * NW * 4 + 2], y * y);
             }
           }
-          __syncthreads();
+          // SMG_NOB3: no barrier -- the chaos phase's first writes into this region (pass A's survivor list at
+          // the bottom of the candidate array) stay below the table, and the partials are read after later ones
+          if (!(SMG_NOB3 && SMG_SCREEN2P && chaos_ok && !P.erosion_border)) __syncthreads();
         }
       }
     }
@@ -1477,11 +1485,12 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       // Pass A (erosion border 0): the principal pixels that pass the pre-filter (a few percent of a noise
       // image) are listed, wave-compacted, from the top of the candidate array down; pass B runs the full
       // screen over full waves of them only.  Candidates fill the array from the bottom (capacity CAPC - nsurv).
-#ifndef SMG_SCREEN2P
-#define SMG_SCREEN2P 1
-#endif
+
+
       const int nscreen = (SMG_ABL & 64) ? 0 : nnz;
-      int nsurv = nscreen, ccap = CAPC;
+      int nsurv = nscreen, ccap = CAPC, cbase = 0;
+      // the survivor list stays below the duplicate table (its last readers may still run, SMG_NOB3)
+      constexpr int SURV_CAP = (int)((LY::o_tkey - LY::o_filt) / 4);
       bool two_pass = SMG_SCREEN2P && !P.erosion_border;
       if (two_pass) {
         for (int ob = 0; ob < nscreen; ob += BLOCK) {  // uniform trip count
@@ -1496,21 +1505,24 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
             int wbase = 0;
             if (lane == 0) wbase = atomicAdd(&ctr[C_NS], (int)__popcll(m));
             const int idx = __builtin_amdgcn_readfirstlane(wbase) + (int)__popcll(m & ((1ull << lane) - 1ull));
-            if (surv) epix[CAPC - 1 - idx] = (uint32_t)s0p;
+            if (surv && idx < SURV_CAP) epix[idx] = (uint32_t)s0p;
           }
         }
         __syncthreads();
         nsurv = ctr[C_NS];
         ccap = CAPC - nsurv;
-        if (nsurv * 4 > CAPC) {  // a dense image: its candidates need the whole array -- screen every pixel
-          two_pass = false;
+        cbase = nsurv;
+        if (nsurv * 4 > CAPC || nsurv > SURV_CAP) {  // a dense image: its candidates need the whole array --
+          two_pass = false;                          // screen every pixel
           nsurv = nscreen;
           ccap = CAPC;
+          cbase = 0;
         }
       }
+      uint32_t* ecand = epix + cbase;  // candidates (behind the survivor list)
       for (int ob = 0; ob < nsurv; ob += BLOCK) {  // uniform trip count: wave-compacted
         const int oc_i = ob + tid;
-        const int s = oc_i < nsurv ? (int)(two_pass ? epix[CAPC - 1 - oc_i] : olist[oc_i]) : 0;
+        const int s = oc_i < nsurv ? (int)(two_pass ? epix[oc_i] : olist[oc_i]) : 0;
         int rs, cs;
         uint32_t cv, H[7];
         rows7(s, rs, cs, cv, H);
@@ -1553,7 +1565,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
             const int ci = __ffs(pass) - 1;
             pass &= pass - 1;
             const int p = s + (ci == 1 ? 1 : ci == 2 ? -1 : ci == 3 ? -P.ncols : ci == 4 ? P.ncols : 0);
-            if (idx < ccap) epix[idx] = (uint32_t)p;
+            if (idx < ccap) ecand[idx] = (uint32_t)p;
             ++idx;
           }
         }
@@ -1580,7 +1592,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         int emax_local = 0;
         const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(Hbm);
         for (int c = tid; c < ncand; c += BLOCK) {
-          const int p = (int)epix[c];
+          const int p = (int)ecand[c];
           int rp, cp;
           rowcol(p, P, rp, cp);
           const int clo = 2 - cp > 0 ? 2 - cp : 0, chi = P.ncols - cp + 2 < 5 ? P.ncols - cp + 2 : 5;
@@ -1656,7 +1668,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
           if (wid == 0) {
             uint32_t* upar = reinterpret_cast<uint32_t*>(red);  // 64 entries (red is free until finalize)
             const bool act = lane < ncand;
-            const int p = act ? (int)epix[lane] : -1;
+            const int p = act ? (int)ecand[lane] : -1;
             const int e = act ? (int)eL8[lane] : 0;
             int rp = 0, cp = 0;
             rowcol(p < 0 ? 0 : p, P, rp, cp);
@@ -1695,17 +1707,17 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
           if constexpr (TWO) {
             m = build2([&](auto&& f) {
               for (int i = tid; i < ncand; i += BLOCK)
-                if (eL8[i]) f(0, epix[i]);
+                if (eL8[i]) f(0, ecand[i]);
             });
           } else {
             for (int i = tid; i < ncand; i += BLOCK)
-              if (eL8[i]) atomicOr(&Hbm[epix[i] >> 5], 1u << (epix[i] & 31));
+              if (eL8[i]) atomicOr(&Hbm[ecand[i] >> 5], 1u << (ecand[i] & 31));
             __syncthreads();
             m = bm_build_prefix<NW>(Hbm, pf, n64, wsc);
           }
           for (int i = tid; i < ncand; i += BLOCK) {
             if (!eL8[i]) continue;
-            const uint32_t p = epix[i];
+            const uint32_t p = ecand[i];
             const int r = TWO ? rank2((int)p) : bm_rank(Hbm, pf, (int)p);
             epix_r[r] = p;
             eLr[r] = eL8[i];
