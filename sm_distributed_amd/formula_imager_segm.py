@@ -192,8 +192,12 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
         sf_d, code_d, pk_d, mz_d = t(sf).long(), t(codes).long(), t(peak_i).long(), t(mz)
         key_d = sf_d * n_cat + code_d
         # one synchronisation for the key range and the checks: sf range, missing adducts, negative peak_i
-        kmin, kmax_key, sf_max, code_min, pk_min = (int(v) for v in torch.stack(
-            [key_d.min(), key_d.max(), sf_d.abs().max(), code_d.min(), pk_d.min()]).cpu().tolist())
+        # and two facts that make later steps cheaper: rows in m/z order, one peak_i = 0 row per ion
+        mz_sorted_rows = (mz_d[1:] >= mz_d[:-1]).all() if n_rows > 1 else torch.ones((), dtype=torch.bool,
+                                                                                      device=device)
+        kmin, kmax_key, sf_max, code_min, pk_min, rows_sorted, n_pk0, mz_pos = (int(v) for v in torch.stack(
+            [key_d.min(), key_d.max(), sf_d.abs().max(), code_d.min(), pk_d.min(), mz_sorted_rows.long(),
+             (pk_d == 0).sum(), (mz_d > 0).all().long()]).cpu().tolist())
         if sf_max >= (1 << 62) // n_cat:
             raise ValueError("sf_id out of range")
         if code_min < 0:
@@ -218,18 +222,30 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
         torch.cumsum(K, 0, out=win_off[1:])
         n_win, kmax = (int(v) for v in torch.stack([win_off[-1], K.max()]).cpu().tolist())
         slot = win_off[inv] + pk_d
-        # rows per window (atomic adds; torch.bincount runs a slow histogram kernel on ROCm)
-        per_slot = torch.zeros(n_win, dtype=torch.int32, device=device)
-        per_slot.index_add_(0, slot, torch.ones(1, dtype=torch.int32, device=device).expand(n_rows))
         peak_mz = torch.full((n_win,), -1.0, dtype=torch.float64, device=device)
         peak_mz.scatter_(0, slot, mz_d)
-        if n_win == n_rows:
+        if n_win == n_rows and mz_pos:
+            # as many rows as windows: a duplicate (sf_id, adduct, peak_i) row would leave a window unfilled
             win_order = slot  # rows come in m/z order (get_sf_peak_df sorts by mz): the search's locality order
+            dup_rows = (peak_mz.min() < 0).to(torch.int64)
         else:
+            # rows per window (atomic adds; torch.bincount runs a slow histogram kernel on ROCm)
+            per_slot = torch.zeros(n_win, dtype=torch.int32, device=device)
+            per_slot.index_add_(0, slot, torch.ones(1, dtype=torch.int32, device=device).expand(n_rows))
             win_order = torch.cat([slot, torch.nonzero(per_slot == 0).flatten()])
-        first = peak_mz[win_off[:-1]]
-        first = torch.where(first < 0, torch.full_like(first, float("inf")), first)
-        ion_order = torch.sort(first, stable=True).indices
+            dup_rows = ((per_slot.max() if n_win else torch.zeros((), dtype=torch.int32, device=device)) > 1
+                        ).to(torch.int64)
+        if rows_sorted and n_pk0 == n_ions:
+            # ions in principal m/z order = the peak_i = 0 rows in row order (a stable compaction, no sort)
+            is0 = pk_d == 0
+            pos = torch.cumsum(is0.to(torch.int64), 0) - 1
+            buf = torch.empty(n_ions + 1, dtype=torch.int64, device=device)
+            buf.scatter_(0, torch.where(is0, pos, torch.full_like(pos, n_ions)), inv)
+            ion_order = buf[:n_ions]
+        else:
+            first = peak_mz[win_off[:-1]]
+            first = torch.where(first < 0, torch.full_like(first, float("inf")), first)
+            ion_order = torch.sort(first, stable=True).indices
         # MultiIndex codes of every ion, formed on the device (keys sorted: sf codes nondecreasing); the host
         # forms the same codes from the keys when it needs them (IonKeys.level_codes)
         sfc = torch.div(uniq, n_cat, rounding_mode="floor")
@@ -241,10 +257,9 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
         else:
             codes_dev = (sfc.to(torch.int32), adc)
         # the keys and the duplicate-row check in one copy
-        tail = torch.cat([uniq, (per_slot.max() if n_win else torch.zeros((), dtype=torch.int32, device=device)
-                                 ).to(torch.int64).reshape(1)]).cpu().numpy()
+        tail = torch.cat([uniq, dup_rows.reshape(1)]).cpu().numpy()
         keys = tail[:-1]
-        if int(tail[-1]) > 1:
+        if int(tail[-1]):
             raise AssertionError("duplicate (sf_id, adduct, peak_i) rows in sf_peak_df")
         codes = None
     ions = DeviceIons(win_off=win_off, peak_mz=peak_mz, theor=None, win_order=win_order, ion_order=ion_order,
