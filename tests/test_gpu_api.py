@@ -216,3 +216,55 @@ def test_image_set_survives_a_later_search_at_another_ppm():
     pd.testing.assert_frame_equal(again, ref)
     _, exp = oracle_run(ds, ions, ppm)
     assert list(ref.index) == list(exp.sort_index().index)
+
+
+def _align_reference(lo, hi, win_off, kt_off, sel):
+    """formula_img_validator.py:73-75 / 115-118 restated: the scored windows of ion i are its first
+    kt_off[i+1] - kt_off[i] layout windows, empty runs past them; a row iff some layout window and some of the
+    first 32 scored windows are non-empty (and sel)."""
+    n = len(win_off) - 1
+    lo2 = np.zeros(kt_off[-1], np.int64)
+    hi2 = np.zeros(kt_off[-1], np.int64)
+    keep = np.zeros(n, bool)
+    for i in range(n):
+        w = np.arange(win_off[i], win_off[i + 1])
+        kt = kt_off[i + 1] - kt_off[i]
+        m = min(kt, len(w))
+        lo2[kt_off[i]:kt_off[i] + m] = lo[w[:m]]
+        hi2[kt_off[i]:kt_off[i] + m] = hi[w[:m]]
+        has = bool((hi[w] > lo[w]).any())
+        hit = bool((hi2[kt_off[i]:kt_off[i] + min(kt, 32)] > lo2[kt_off[i]:kt_off[i] + min(kt, 32)]).any())
+        keep[i] = has and hit and (sel is None or bool(sel[i]))
+    return lo2, hi2, keep
+
+
+@pytest.mark.parametrize("with_sel", [False, True])
+def test_align_windows_matches_reference(with_sel):
+    """smg_align_windows on ragged layouts: more theoretical peaks than layout windows (padding), fewer
+    (truncation), ions without windows, empty windows only, > 32 scored windows."""
+    import torch
+    from sm_distributed_amd import engine as E
+    from sm_distributed_amd._lib import check, lib
+    rng = np.random.default_rng(11)
+    n = 3000
+    k_img = rng.integers(0, 9, n)
+    k_img[:5] = [0, 40, 1, 3, 0]
+    kt = rng.integers(0, 9, n)
+    kt[:5] = [2, 40, 0, 5, 0]
+    win_off = np.concatenate([[0], np.cumsum(k_img)]).astype(np.int64)
+    kt_off = np.concatenate([[0], np.cumsum(kt)]).astype(np.int64)
+    lo = rng.integers(0, 1000, win_off[-1]).astype(np.int64)
+    hi = lo + rng.integers(0, 3, win_off[-1]) * rng.integers(0, 2, win_off[-1])
+    hi[win_off[1]:win_off[2]][:33] = lo[win_off[1]:win_off[2]][:33]  # ion 1: only its 34th+ windows may hit
+    sel = rng.integers(0, 2, n).astype(np.uint8) if with_sel else None
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    lo2 = torch.empty(kt_off[-1], dtype=torch.int64, device="cuda")
+    hi2 = torch.empty_like(lo2)
+    keep = torch.empty(n, dtype=torch.uint8, device="cuda")
+    sel_d = d(sel) if sel is not None else None
+    check(lib().smg_align_windows(E._p(d(lo)), E._p(d(hi)), E._p(d(win_off)), E._p(d(kt_off)), E._p(sel_d), n,
+                                  E._p(lo2), E._p(hi2), E._p(keep), E._stream(None)), "smg_align_windows")
+    torch.cuda.synchronize()
+    rl, rh, rk = _align_reference(lo, hi, win_off, kt_off, sel)
+    assert np.array_equal(lo2.cpu().numpy(), rl) and np.array_equal(hi2.cpu().numpy(), rh)
+    assert np.array_equal(keep.cpu().numpy().astype(bool), rk)

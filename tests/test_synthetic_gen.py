@@ -41,3 +41,30 @@ def test_chunked_generator_layout(monkeypatch, plant):
     assert info["n_planted_ions"] == ref[3]["n_planted_ions"]
     if plant:
         assert info["n_planted_points"] > 0
+
+
+def test_device_layout_fast_paths_match_generic():
+    """device_layout (on CPU tensors): the dense-key, compaction-ordered path for an m/z-sorted sf_peak_df and
+    the sort-based path for a shuffled one (or sparse keys) give the same layout; duplicate rows are refused."""
+    import pandas as pd
+    import pytest as _pt
+    from sm_distributed_amd import formula_imager_segm as FIS
+    from sm_distributed_amd.formulas import FormulasSegm
+    ions = syn.make_ion_table(300, seed=3, decoy_seed=4)
+    df = FormulasSegm.from_ion_table(ions, 2.0).get_sf_peak_df()
+    k1, d1, K1 = FIS.device_layout(df, "cpu")
+    shuffled = df.sample(frac=1.0, random_state=1)
+    sparse = df.copy()
+    sparse["sf_id"] = sparse["sf_id"] * 1000003
+    for other, scale in ((shuffled, 1), (sparse, 1000003)):
+        k2, d2, K2 = FIS.device_layout(other, "cpu")
+        assert np.array_equal(k1.keys // k1.n_cat, k2.keys // k2.n_cat // scale)
+        assert np.array_equal(K1.numpy(), K2.numpy())
+        assert np.array_equal(d1.peak_mz.numpy(), d2.peak_mz.numpy())
+        first = d1.peak_mz[d1.win_off[:-1]].numpy()
+        assert np.array_equal(first[d1.ion_order.numpy()], first[d2.ion_order.numpy()])
+    assert np.all(np.diff(first[d1.ion_order.numpy()]) >= 0)
+    with _pt.raises(AssertionError):
+        FIS.device_layout(pd.concat([df, df.iloc[:1]]), "cpu")
+    with _pt.raises(AssertionError):  # a duplicate that keeps rows == windows: one window left empty
+        FIS.device_layout(pd.concat([df.iloc[:-1], df.iloc[:1]]), "cpu")
