@@ -262,7 +262,8 @@ def test_align_windows_matches_reference(with_sel):
     hi2 = torch.empty_like(lo2)
     keep = torch.empty(n, dtype=torch.uint8, device="cuda")
     sel_d = d(sel) if sel is not None else None
-    check(lib().smg_align_windows(E._p(d(lo)), E._p(d(hi)), E._p(d(win_off)), E._p(d(kt_off)), E._p(sel_d), n,
+    lo_d, hi_d, wo_d, kt_d = d(lo), d(hi), d(win_off), d(kt_off)  # held until the launch has completed
+    check(lib().smg_align_windows(E._p(lo_d), E._p(hi_d), E._p(wo_d), E._p(kt_d), E._p(sel_d), n,
                                   E._p(lo2), E._p(hi2), E._p(keep), E._stream(None)), "smg_align_windows")
     torch.cuda.synchronize()
     rl, rh, rk = _align_reference(lo, hi, win_off, kt_off, sel)
