@@ -208,12 +208,12 @@ def rows_to_frame(table, global_keys):
     n = len(global_keys)
     gi = t[:, 0].long()
     gi = torch.where(gi >= 0, gi, torch.full_like(gi, n))
-    full = torch.zeros(4, n + 1, dtype=t.dtype, device=t.device)
-    full[:, gi] = t[:, 1:5].T
-    has = torch.zeros(n + 1, dtype=torch.bool, device=t.device)
-    has[gi] = True
-    idx = torch.nonzero(has[:n]).flatten()
-    return device_frame(global_keys, full, idx)
+    # the gathered row of every ion (-1: none), then the ions with a row in table order and their rows
+    row = torch.full((n + 1,), -1, dtype=torch.int64, device=t.device)
+    row[gi] = torch.arange(t.shape[0], device=t.device)
+    idx = torch.nonzero(row[:n] >= 0).flatten()
+    cols = t[row[idx], 1:5].T  # [4, rows] in table order
+    return device_frame(global_keys, cols, idx, cols_compact=True)
 
 
 def score_sharded(plan, peaks, ds_config, group=None, score_local=None):

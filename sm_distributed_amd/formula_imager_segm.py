@@ -270,23 +270,31 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
 METRIC_COLUMNS = ["chaos", "spatial", "spectral", "msm"]
 
 
-def device_frame(ion_keys, cols, idx):
+def device_frame(ion_keys, cols, idx, cols_compact=False):
     """The reference metrics DataFrame (index [sf_id, adduct], columns chaos, spatial, spectral, msm) of the ions
-    ``idx`` (device tensor, ascending positions of ``ion_keys``) from device metric columns ``cols`` [4, >n]: the
-    rows and the index codes are gathered on the device and copied to pinned host memory together (one host
-    synchronisation); the DataFrame wraps the column-major block without a copy."""
+    ``idx`` (device tensor, ascending positions of ``ion_keys``) from device metric columns ``cols`` [4, >n] (or
+    [4, len(idx)] already in that order, ``cols_compact``): the rows and the index codes are gathered on the
+    device and copied to pinned host memory, the codes first so that the MultiIndex is built while the columns
+    copy; the DataFrame wraps the column-major block without a copy."""
     import torch
     sfc, adc = ion_keys.codes_dev(cols.device)
-    parts = (cols[:, idx], sfc[idx], adc[idx])
+    parts = (sfc[idx], adc[idx], cols if cols_compact else cols[:, idx])
     if cols.device.type == "cuda":
+        # the codes first: the MultiIndex is built on the host while the metric columns are still copying
+        st = torch.cuda.current_stream(cols.device)
         host = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in parts]
-        for h, x in zip(host, parts):
-            h.copy_(x, non_blocking=True)
-        torch.cuda.current_stream(cols.device).synchronize()
+        host[0].copy_(parts[0], non_blocking=True)
+        host[1].copy_(parts[1], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(st)
+        host[2].copy_(parts[2], non_blocking=True)
+        ev.synchronize()
+        mi = ion_keys.multi_index_from_codes(host[0].numpy(), host[1].numpy())
+        st.synchronize()
     else:
         host = parts
-    c, c_sf, c_ad = (h.numpy() for h in host)
-    return pd.DataFrame(c.T, index=ion_keys.multi_index_from_codes(c_sf, c_ad), columns=METRIC_COLUMNS, copy=False)
+        mi = ion_keys.multi_index_from_codes(host[0].numpy(), host[1].numpy())
+    return pd.DataFrame(host[2].numpy().T, index=mi, columns=METRIC_COLUMNS, copy=False)
 
 
 class FrameIndex:
