@@ -274,9 +274,9 @@ __global__ void __launch_bounds__(256) slice_count_kernel(const int64_t* __restr
   count[s] = u - l;
 }
 
-// one workgroup per spectrum (grid-stride): copies its run [first, first + n) to out at out_off[s], flagging a
-// point when its spectrum neighbour (inside or outside the slice) lies within one window width, or when the
-// spectrum's pixel is shared (force)
+// one wave per spectrum (four per workgroup, grid-stride; a spectrum's run is a few hundred points): copies its
+// run [first, first + n) to out at out_off[s], flagging a point when its spectrum neighbour (inside or outside the
+// slice) lies within one window width, or when the spectrum's pixel is shared (force)
 __global__ void __launch_bounds__(256) slice_copy_kernel(const int64_t* __restrict__ sp_off, int64_t n_spectra,
                                                          const float* __restrict__ mz,
                                                          const uint64_t* __restrict__ hits,
@@ -285,11 +285,13 @@ __global__ void __launch_bounds__(256) slice_copy_kernel(const int64_t* __restri
                                                          const uint8_t* __restrict__ force,
                                                          float* __restrict__ out_mz, uint64_t* __restrict__ out_hits) {
   const double slack = 2.0 * ppm * 1e-6 / (1.0 - ppm * 1e-6) * (1.0 + 1e-9);
-  for (int64_t s = blockIdx.x; s < n_spectra; s += gridDim.x) {
+  constexpr int WPB = 4;  // waves per workgroup
+  const int lane = threadIdx.x & 63;
+  for (int64_t s = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6); s < n_spectra; s += (int64_t)gridDim.x * WPB) {
     const int64_t a = sp_off[s], b = sp_off[s + 1];
     const int64_t f = first[s], o = out_off[s], n = out_off[s + 1] - o;
     const bool all = force && force[s];
-    for (int64_t j = threadIdx.x; j < n; j += blockDim.x) {
+    for (int64_t j = lane; j < n; j += 64) {
       const int64_t i = f + j;
       const double m = (double)mz[i];
       bool fl = all;
@@ -575,7 +577,8 @@ int smg_slice_mz_copy(const int64_t* sp_off, int64_t n_spectra, const float* mz,
   if (n_spectra == 0) return SMG_OK;
   SMG_CHECK_ARG(sp_off && mz && hits && out_sp_off && out_mz && out_hits && workspace, "null pointer");
   const int64_t* first = reinterpret_cast<const int64_t*>(reinterpret_cast<const unsigned char*>(workspace) + 256);
-  const int64_t grid = n_spectra < (1 << 20) ? n_spectra : (1 << 20);
+  const int64_t nwg = (n_spectra + 3) / 4;
+  const int64_t grid = nwg < (1 << 20) ? nwg : (1 << 20);
   hipLaunchKernelGGL(slice_copy_kernel, dim3((unsigned)grid), dim3(256), 0, as_stream(stream), sp_off, n_spectra,
                      mz, hits, first, out_sp_off, ppm, force, out_mz, out_hits);
   SMG_LAUNCH_CHECK();
