@@ -131,8 +131,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    marks = []
     for _ in range(args.steps):
-        df = step_fn()
+        df = step_fn()  # ends with the table on the host (a synchronisation)
+        marks.append(time.perf_counter())
     torch.cuda.synchronize()
     if sharded:
         dist.barrier()
@@ -145,6 +147,10 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_per_step = elapsed / max(args.steps, 1) * 1e3
+    per_step = np.diff([t0] + marks) * 1e3
+    if len(per_step):
+        log(f"[rank {rank}] step ms: min {per_step.min():.2f} median {np.median(per_step):.2f} "
+            f"max {per_step.max():.2f}")
 
     # ---- device chain (the same kernels without the API layer) and per-stage HIP events ----------------------
     chain = device_chain(args, peaks, my_formulas, plan) if args.chain_steps > 0 else None

@@ -317,6 +317,9 @@ class FrameIndex:
                 h.copy_(x, non_blocking=True)
             self.ev = torch.cuda.Event()
             self.ev.record(torch.cuda.current_stream(keep.device))
+            # the columns' pinned buffer too, before the kernel: a pinned allocation while a kernel runs remaps
+            # host memory for the device and was seen to stall the kernel (first calls of a process)
+            self.cols_host = torch.empty((4, self.idx.numel()), dtype=torch.float64, pin_memory=True)
         else:
             self.codes, self.ev = list(parts), None
 
@@ -328,7 +331,7 @@ class FrameIndex:
         mi = self.ion_keys.multi_index_from_codes(c_sf, c_ad)
         sel = cols[:, self.idx]
         if cols.device.type == "cuda":
-            host = torch.empty(sel.shape, dtype=sel.dtype, pin_memory=True)
+            host = self.cols_host
             host.copy_(sel, non_blocking=True)
             torch.cuda.current_stream(cols.device).synchronize()
         else:
