@@ -892,13 +892,22 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
 #define SMG_LATEFIN 1
 #endif
   static_assert(!SMG_LATEFIN || NW >= 2, "late finalize needs a second wave for the LDS initialisation");
+#ifndef SMG_SPLITFIN
+#define SMG_SPLITFIN 1  // wave 0 the spectral score and chaos, wave 1 the spatial score (each about half)
+#endif
+  static_assert(!SMG_SPLITFIN || (SMG_LATEFIN && 8 * NW - 1 >= 32), "split finalize needs the late finalize");
   struct {
-    double s, sy, syy, sxy, t, sx, sxx, chaos;
-    int K, ion;
+    double s, sy, syy, sxy, t, sx, sxx, chaos, cs, csc;
+    int K, ion, msm_ion;
     uint32_t flags;
-    bool pending;
+    bool pending, msm_pending;
   } fin;
   fin.pending = false;
+  fin.msm_pending = false;
+  // wave 1 -> wave 0 across the phase-0 barrier: the last slot of red, which neither the phase-2 sums (5 NW),
+  // block_sum (2 NW) nor wave 0's few-candidate union-find (64 u32) touches -- in the break path wave 1 writes
+  // it while wave 0 may still be in that union-find
+  double* spat_lds = reinterpret_cast<double*>(smem + LY::o_red) + 8 * NW - 1;
   // the finalize arithmetic of the ion whose inputs wave 0 gathered (a no-op elsewhere)
   auto finalize = [&]() {
     if (!fin.pending) return;
@@ -906,13 +915,17 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     const int k = lane;
     const int K = fin.K;
     const double s = fin.s, sy = fin.sy, syy = fin.syy, sxy = fin.sxy, t = fin.t, sx = fin.sx, sxx = fin.sxx;
+    const bool do_spectral = !SMG_SPLITFIN || wid == 0, do_spatial = !SMG_SPLITFIN || wid == 1;
     // isotope_pattern_match
-    const double nt = sqrt(wave_sum_dpp(t * t)), ns = sqrt(wave_sum_dpp(s * s));
-    double spectral = 1.0 - wave_sum_dpp(k < K ? fabs(t / nt - s / ns) : 0.0) / (double)K;
-    if (spectral == 1.0) spectral = 0.0;
+    double spectral = 0.0;
+    if (do_spectral) {
+      const double nt = sqrt(wave_sum_dpp(t * t)), ns = sqrt(wave_sum_dpp(s * s));
+      spectral = 1.0 - wave_sum_dpp(k < K ? fabs(t / nt - s / ns) : 0.0) / (double)K;
+      if (spectral == 1.0) spectral = 0.0;
+    }
     // isotope_image_correlation: np.corrcoef rows, weights = theor[1:]
     double spatial = 0.0;
-    if (K >= 2) {
+    if (do_spatial && K >= 2) {
       const double npx = (double)P.npx, n1 = npx - 1.0;
       const double sd0 = sqrt((sxx - sx * sx / npx) / n1);
       double rt = 0.0, tw = 0.0;
@@ -933,11 +946,28 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       chaos = clean(chaos);
       spatial = clean(spatial);
       spectral = clean(spectral);
-      oc[fin.ion] = chaos;
-      osp[fin.ion] = spatial;
-      osc[fin.ion] = spectral;
-      omsm[fin.ion] = chaos * spatial * spectral;
-      oflags[fin.ion] = fin.flags;
+      if (do_spectral) {
+        oc[fin.ion] = chaos;
+        osc[fin.ion] = spectral;
+        oflags[fin.ion] = fin.flags;
+      }
+      if (do_spatial) osp[fin.ion] = spatial;
+      if (!SMG_SPLITFIN) omsm[fin.ion] = chaos * spatial * spectral;
+      else if (wid == 1) spat_lds[0] = spatial;
+      else {
+        fin.cs = chaos;  // msm = chaos * spatial * spectral, multiplied in the oracle's order
+        fin.csc = spectral;
+      }
+    }
+    if (SMG_SPLITFIN && wid == 0) {  // msm after the next barrier, from wave 1's spatial score
+      fin.msm_ion = fin.ion;
+      fin.msm_pending = true;
+    }
+  };
+  auto finalize_msm = [&]() {
+    if (SMG_SPLITFIN && fin.msm_pending) {
+      if (lane == 0) omsm[fin.msm_ion] = fin.cs * spat_lds[0] * fin.csc;
+      fin.msm_pending = false;
     }
   };
   int64_t pos = -1;  // ion scored in this iteration (-1: none; the first iteration only issues loads)
@@ -996,7 +1026,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
 
     // ---- phase 0: LDS initialisation -------------------------------------------------------------
     // wave 0 finishes the previous ion meanwhile (SMG_LATEFIN): the other waves initialise the LDS
-    constexpr int ZW = SMG_LATEFIN ? WAVE : 0;
+    constexpr int ZW = SMG_LATEFIN ? (SMG_SPLITFIN ? 2 * WAVE : WAVE) : 0;
     const int zt = tid - ZW;
     if (!skip && zt >= 0) {
       uint4* z = reinterpret_cast<uint4*>(smem + LY::o_guard);
@@ -1015,6 +1045,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     }
     finalize();
     __syncthreads();
+    finalize_msm();
     STAMP(0);
 
     // ---- phase 1: principal image -> bitmap, rank prefix, f64 values -----------------------------
@@ -1774,7 +1805,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     // ---- finalize (formula_img_validator.py:78-84 + the restated pyImagingMSpec functions): wave 0,
     // lane k = window k; sums over lanes in a fixed order.  Its inputs are read here; the arithmetic runs
     // during the next ion's phase 0, which the other waves do alone (SMG_LATEFIN)
-    if (!skip && wid == 0) {
+    if (!skip && wid <= (SMG_SPLITFIN ? 1 : 0)) {
       const int k = lane;
       fin.s = fin.sy = fin.syy = fin.sxy = fin.t = 0.0;
       if (k < K) {
@@ -1804,6 +1835,10 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     }
     if (npos < 0) {
       finalize();
+      if (SMG_SPLITFIN) {
+        __syncthreads();
+        finalize_msm();
+      }
       break;
     }
     pos = npos;
