@@ -10,6 +10,15 @@ mz, hits, dims, info = syn.make_dataset_torch(500, 500, 2000, seed=42, device="c
 peaks = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
 peaks.flag_duplicates(2.0)
 kb = peaks.key_bits()
+tf = []
+for _ in range(6):  # repeated passes (the flag-state path a step takes)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    peaks.flag_duplicates(2.0)
+    torch.cuda.synchronize()
+    tf.append(time.perf_counter() - t0)
+print(f"{os.path.basename(_lib.LIB_PATH)}: flag_duplicates min {min(tf[1:])*1e3:.2f} ms median "
+      f"{sorted(tf[1:])[2]*1e3:.2f} ms", flush=True)
 ts = []
 for _ in range(6):
     torch.cuda.synchronize()

@@ -416,9 +416,15 @@ int smg_flag_duplicates(const int64_t* sp_off, int64_t n_spectra, const float* m
 #ifndef SMG_SORT_RANK
 #define SMG_SORT_RANK match
 #endif
+#ifndef SMG_HIST_BLOCK
+#define SMG_HIST_BLOCK 512  // the digit-histogram kernel's tile (reads every key once): 512 x 64 items
+#endif                        // 13.9 -> 12.9-13.1 ms for the whole sort against 512 x 16 (1024x32/1024x64 within
+#ifndef SMG_HIST_IPT          // 0.1 ms of it; 256x32/256x64/512x96/512x128/1024x128 slower; scripts/time_sort.py)
+#define SMG_HIST_IPT 64
+#endif
 using SortConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<SMG_SORT_BLOCK, SMG_SORT_IPT>,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<SMG_HIST_BLOCK, SMG_HIST_IPT>,
                                         rocprim::kernel_config<SMG_SORT_BLOCK, SMG_SORT_IPT>, SMG_SORT_RADIX_BITS,
                                         rocprim::block_radix_rank_algorithm::SMG_SORT_RANK>>;
 
