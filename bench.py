@@ -20,6 +20,10 @@ Beside ``value``: ``device_chain`` (the same kernels without the host API layer)
 ``roofline`` of the dominant kernel (ion_pipe_kernel<512>: 12 B per window point per launch, SURVEY §8d, over
 its own HIP-event time on its launch stream), and ``cpu_baseline`` (the oracle on host cores, rank 0, N = 1).
 
+``python bench.py --gpus N`` without a launcher (WORLD_SIZE unset) starts the N ranks itself: the parent touches
+no GPU, spawns N child processes with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT, relays
+rank 0's JSON line and exits non-zero if any rank fails (``--dry-run`` stops every rank before GPU init).
+
 Run:  python bench.py [--gpus N --steps K --warmup W]
 """
 from __future__ import annotations
@@ -28,7 +32,10 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -60,7 +67,73 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target wall of the CPU baseline sample")
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="cap on CPU-baseline workers (a GPU box's CPU share is 16 cores per GPU)")
-    return ap.parse_args()
+    ap.add_argument("--config", choices=["3", "5"], default="3",
+                    help="workload preset: 3 = BASELINE config 3 (default); 5 = one rank's shard of config 5 "
+                         "(1000x1000 px, Poisson(5000), 40k formulas x 6 adducts both polarities; use --shard-of)")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="score only this rank's shard of an N-way plan on one GPU (N = --shard-of, rank = "
+                         "--shard-rank): one rank of a multi-GPU run measured alone")
+    ap.add_argument("--shard-rank", type=int, default=0)
+    ap.add_argument("--dry-run", action="store_true", help="stop every rank before GPU initialisation")
+    args = ap.parse_args()
+    if args.config == "5":
+        for k, v in CONFIG5.items():
+            if getattr(args, k) == ap.get_default(k):
+                setattr(args, k, v)
+    return args
+
+
+# BASELINE config 5 (stress): 1000x1000 px, ~5k peaks per spectrum, HMDB+ChEBI-sized table (~40k formulas), 6
+# adducts in both polarities (positive +H/+Na/+K, negative -H/+Cl/+Br), decoys as fdr.py draws them
+CONFIG5 = {"nrows": 1000, "ncols": 1000, "peaks": 5000.0, "n_sf": 40000}
+CONFIG5_ADDUCTS = {"+": ("+H", "+Na", "+K"), "-": ("-H", "+Cl", "+Br")}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args):
+    """Start the N ranks of ``--gpus N`` (no launcher in front of this process): one child per GPU with the
+    torch.distributed.run environment; rank 0's stdout (the JSON line) is relayed, the others' go to stderr.
+    This process never initialises a GPU (no torch import), so it may start the children as it likes."""
+    n = args.gpus
+    port = _free_port()
+    argv = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    out0 = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GROUP_RANK="0")
+        procs.append(subprocess.Popen(argv, env=env, stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+    log(f"[launcher] started {n} ranks: pids {[p.pid for p in procs]} (MASTER_PORT {port})")
+    reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    rc = 0
+    live = list(range(n))
+    while live:
+        for r in list(live):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            live.remove(r)
+            if code != 0 and rc == 0:
+                rc = code
+                log(f"[launcher] rank {r} exited with {code}: stopping the other ranks")
+                for q in live:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    reader.join(timeout=30)
+    data = out0[0].decode() if out0 and out0[0] else ""
+    if data:
+        sys.stdout.write(data)
+        sys.stdout.flush()
+    if rc == 0 and not data.strip():
+        log("[launcher] rank 0 printed no result line")
+        rc = 1
+    return 1 if rc < 0 else rc
 
 
 def log(*a):
@@ -69,6 +142,21 @@ def log(*a):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: one rank per GPU")
+    if args.dry_run:
+        log(f"[rank {rank}/{world}] dry run: local rank {local_rank}, master "
+            f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}")
+        if os.environ.get("SMG_BENCH_FAIL_RANK") == str(rank):  # launcher test: a rank that fails
+            raise SystemExit(3)
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "rank": rank, "local_rank": local_rank}), flush=True)
+        return
     # the JSON line is the only thing on stdout: libraries that print at start-up (RCCL's version banner at
     # communicator creation) write to fd 1 directly, so fd 1 points at stderr until the line is printed
     json_out = os.fdopen(os.dup(1), "w")
@@ -85,27 +173,43 @@ def main():
     from sm_distributed_amd.formula_img_validator import sf_image_metrics
     from sm_distributed_amd.formulas import FormulasSegm
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
     sharded = world > 1 or args.sharded
+    rccl_world = None
     if sharded:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", device_id=device, rank=rank, world_size=world)
+        rccl_world = dist.get_world_size()
+        if rccl_world != world:
+            raise SystemExit(f"RCCL reports {rccl_world} ranks, expected {world}")
 
     t_setup = time.perf_counter()
-    ions = syn.make_ion_table(args.n_sf, seed=43, decoy_seed=44)
+    if args.config == "5":
+        ions = syn.make_ion_table_both_polarities(args.n_sf, seed=43, decoy_seed=44)
+    else:
+        ions = syn.make_ion_table(args.n_sf, seed=43, decoy_seed=44)
     mz, hits, dims, info = syn.make_dataset_torch(args.nrows, args.ncols, args.peaks, seed=42, device=device,
                                                   ions=ions, plant_fraction=args.plant_fraction, plant_seed=45)
     peaks = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
     formulas = FormulasSegm.from_ion_table(ions, args.ppm)
     ds_config = {"image_generation": {"ppm": args.ppm, "nlevels": args.nlevels, "q": 99, "do_preprocessing": False}}
+    shard_only = args.shard_of > 1 and not sharded
     if sharded:
         plan = D.plan_shards(formulas, peaks, args.ppm, world, rank)
         step_fn = lambda: D.score_sharded(plan, peaks, ds_config)[0]
+        my_formulas = plan.formulas
+    elif shard_only:
+        # one rank of an N-way plan measured alone on this GPU: its slice, images, scores and row block (the
+        # step every rank runs before the gather); rows = the ions of the shard that get a table row
+        if not 0 <= args.shard_rank < args.shard_of:
+            raise SystemExit("--shard-rank must be in [0, --shard-of)")
+        plan = D.plan_shards(formulas, peaks, args.ppm, args.shard_of, args.shard_rank)
+
+        def step_fn():
+            rows, _ = D._device_rows(plan, peaks, ds_config)
+            return int((rows[:, 0] >= 0).sum().item())
         my_formulas = plan.formulas
     else:
         plan = None
@@ -122,10 +226,13 @@ def main():
 
     # ---- the metric: timed API steps --------------------------------------------------------------------
     L = _lib.lib()
-    for _ in range(max(args.warmup, 1)):
+    t_first = time.perf_counter()
+    df = step_fn()  # the process's first search: library load, workspaces, host caches all cold
+    first_step_ms = (time.perf_counter() - t_first) * 1e3
+    for _ in range(max(args.warmup, 1) - 1):
         df = step_fn()
     torch.cuda.synchronize()
-    L.smg_debug_main_pass_times(None, 0, ctypes.byref(ctypes.c_int32(0)))  # discard
+    _pass_times(L)  # discard
     L.smg_debug_time_main_pass(1)
     if sharded:
         dist.barrier()
@@ -140,8 +247,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     L.smg_debug_time_main_pass(0)
-    main_ms = _main_pass_times(L)
-    n_rows = len(df) if df is not None else 0
+    pass_ms = _pass_times(L)
+    n_rows = df if isinstance(df, int) else (len(df) if df is not None else 0)
     if sharded:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -151,29 +258,33 @@ def main():
     if len(per_step):
         log(f"[rank {rank}] step ms: min {per_step.min():.2f} median {np.median(per_step):.2f} "
             f"max {per_step.max():.2f}")
+    # one more search with the host-side caches dropped (the theoretical-intensity alignment and the shard's
+    # global row index are reused between steps while the ion keys are unchanged): a cold first search of a
+    # new formula table in a warm process
+    cold_ms = cold_step_ms(step_fn, formulas, plan, sharded)
 
     # ---- device chain (the same kernels without the API layer) and per-stage HIP events ----------------------
     chain = device_chain(args, peaks, my_formulas, plan) if args.chain_steps > 0 else None
 
-    # ---- roofline of the dominant kernel: 12 B per window point over its own launch time --------------------
-    sum_hits = chain["sum_window_points"] if chain else None
-    kern_ms = float(np.mean(main_ms)) if len(main_ms) else None
-    roofline = None
-    if sum_hits and kern_ms:
-        ach = ALG_BYTES_PER_POINT * sum_hits / (kern_ms * 1e-3) / 1e9
-        is_c3 = _is_config3(args) and world == 1
-        traffic, src = measured_traffic() if is_c3 else (None, None)
-        roofline = {"bound": "hbm", "kernel": "ion_pipe_kernel<512> (main LDS pass)", "achieved": ach,
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS, "traffic": traffic,
-                    "traffic_source": src, "alg_bytes_per_launch": ALG_BYTES_PER_POINT * sum_hits,
-                    "kernel_ms_avg": kern_ms, "kernel_launches_timed": len(main_ms),
-                    "alg_bytes_8B_per_point_frac": 8.0 * sum_hits / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    # ---- roofline per pass: 12 B per window point of the ions the pass scored over its own launch time --------
+    roofline, passes = pass_roofline(args, pass_ms, chain, world == 1 and not shard_only)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not shard_only and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, ions, peaks, dims)
 
     if rank == 0:
+        if args.config == "5":
+            wl = (f"config5{' shard %d/%d' % (args.shard_rank, args.shard_of) if shard_only else ''}: "
+                  f"{args.nrows}x{args.ncols} px, Poisson({args.peaks:g}) centroids/spectrum, {args.n_sf} formulas x "
+                  f"(+H,+Na,+K positive / -H,+Cl,+Br negative + distinct decoys), ppm {args.ppm:g}, "
+                  f"nlevels {args.nlevels}")
+        else:
+            tag = "config3" if _is_config3(args) else "custom"
+            if shard_only:
+                tag += f" shard {args.shard_rank}/{args.shard_of}"
+            wl = (f"{tag}: {args.nrows}x{args.ncols} px, Poisson({args.peaks:g}) centroids/spectrum, {args.n_sf} "
+                  f"formulas x (+H,+Na,+K + distinct decoys), ppm {args.ppm:g}, nlevels {args.nlevels}")
         line = {
             "metric": METRIC,
             "value": n_rows / (ms_per_step * 1e-3),
@@ -188,18 +299,27 @@ def main():
             "dtype": "f64",
             "data": "synthetic (generated in HBM; HMDB/ChEBI and real imzML are not available offline)",
             "config": {
-                "workload": (f"{'config3' if _is_config3(args) else 'custom'}: {args.nrows}x{args.ncols} px, "
-                             f"Poisson({args.peaks:g}) centroids/spectrum, {args.n_sf} formulas x (+H,+Na,+K + "
-                             f"distinct decoys), ppm {args.ppm:g}, nlevels {args.nlevels}"),
-                "timed_region": "compute_sf_images + sf_image_metrics through the drop-in API, DataFrame included",
-                "n_points": info["n_points"], "n_ions": formulas.n_ions, "n_rows_per_step": n_rows,
-                "n_windows": int(formulas.ion_off[-1]), "sum_window_points": sum_hits,
+                "workload": wl,
+                "timed_region": ("one rank's step of the sharded search (slice + compute_sf_images + "
+                                 "sf_image_metrics' device rows), measured alone" if shard_only else
+                                 "compute_sf_images + sf_image_metrics through the drop-in API, DataFrame included"),
+                "n_points": info["n_points"], "n_ions": formulas.n_ions, "n_ions_this_rank": my_formulas.n_ions,
+                "n_rows_per_step": n_rows, "n_windows": int(formulas.ion_off[-1]),
+                "sum_window_points": chain["sum_window_points"] if chain else None,
                 "parallelism": (f"formula shards by principal m/z x{world}, dataset replicated, per-rank m/z slice, "
-                                f"RCCL gather of metric rows" if sharded else "1 GPU"),
+                                f"RCCL gather of metric rows" if sharded else
+                                (f"1 GPU, rank {args.shard_rank} of a {args.shard_of}-way plan" if shard_only
+                                 else "1 GPU")),
+                "rccl_world_size": rccl_world,
                 "shard_est_cost_s": plan.est_cost if plan is not None else None,
             },
+            "first_step_ms": first_step_ms,
+            "cold_cache_step_ms": cold_ms,
+            "step_ms_min_median_max": ([float(per_step.min()), float(np.median(per_step)), float(per_step.max())]
+                                       if len(per_step) else None),
             "device_chain": chain,
             "roofline": roofline,
+            "passes": passes,
             "cpu_baseline": cpu,
             "lib": _lib.version(),
         }
@@ -208,16 +328,75 @@ def main():
         dist.destroy_process_group()
 
 
+def cold_step_ms(step_fn, formulas, plan, sharded):
+    """Wall time of one search after the host-side caches of the previous searches are dropped."""
+    import torch
+    import torch.distributed as dist
+    pk = formulas.get_sf_peak_ints()
+    pk.__dict__.pop("_dev_cache", None)
+    if plan is not None:
+        plan._glob = None
+        plan.formulas.get_sf_peak_ints().__dict__.pop("_dev_cache", None)
+    if sharded:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    step_fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) * 1e3
+
+
 def _is_config3(args):
     return (args.nrows, args.ncols, args.peaks, args.n_sf, args.ppm, args.nlevels, args.plant_fraction) == \
         (500, 500, 2000.0, 20000, 2.0, 30, 0.02)
 
 
-def _main_pass_times(L):
+def _pass_times(L):
+    """(pass id, ms) of every pass launch recorded since the last call (smg_debug_pass_times)."""
     n = ctypes.c_int32(0)
-    buf = (ctypes.c_double * 4096)()
-    _lib_check(L.smg_debug_main_pass_times(buf, 4096, ctypes.byref(n)))
-    return [buf[i] for i in range(min(n.value, 4096))]
+    cap = 16384
+    ms = (ctypes.c_double * cap)()
+    ps = (ctypes.c_int32 * cap)()
+    _lib_check(L.smg_debug_pass_times(ps, ms, cap, ctypes.byref(n)))
+    return [(int(ps[i]), float(ms[i])) for i in range(min(n.value, cap))]
+
+
+def pass_roofline(args, pass_ms, chain, is_single):
+    """Per pass of smg_ion_metrics: its average launch time (HIP events on the launch stream, timed API steps),
+    the window points of the ions it scored (SMG_ION_* flags of the device chain, same data and ions) and their
+    12-B algorithmic bytes over that time.  ``roofline`` = the scoring pass with the largest time."""
+    from sm_distributed_amd import _lib
+    if not chain or not pass_ms:
+        return None, None
+    by = {}
+    for p, t in pass_ms:
+        by.setdefault(p, []).append(t)
+    passes = {}
+    for p, ts in sorted(by.items()):
+        name = _lib.PASS_NAMES.get(p, str(p))
+        d = {"pass": p, "ms_avg": float(np.mean(ts)), "launches_timed": len(ts)}
+        if p != _lib.SMG_PASS_DESC:
+            pts = chain["pass_window_points"].get(p, 0)
+            d.update({"ions": chain["pass_ions"].get(p, 0), "window_points": pts,
+                      "alg_bytes_per_launch": ALG_BYTES_PER_POINT * pts})
+            if d["ms_avg"] > 0:
+                ach = ALG_BYTES_PER_POINT * pts / (d["ms_avg"] * 1e-3) / 1e9
+                d.update({"achieved_GBps": ach, "frac": ach / HBM_PEAK_GBS})
+        passes[name] = d
+    scoring = [d for d in passes.values() if d["pass"] != _lib.SMG_PASS_DESC and d.get("window_points")]
+    if not scoring:
+        return None, passes
+    dom = max(scoring, key=lambda d: d["ms_avg"])
+    name = _lib.PASS_NAMES[dom["pass"]]
+    key = {1: "ion_pipe_kernel[512]", 2: "ion_pipe_kernel[1024]", 3: "ion_wide_kernel", 4: "ion_dense_kernel"}
+    traffic, src = measured_traffic(key[dom["pass"]], "config5" if args.config == "5" else "config3") \
+        if is_single and (_is_config3(args) or args.config == "5") else (None, None)
+    roofline = {"bound": "hbm", "kernel": name, "achieved": dom["achieved_GBps"], "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": dom["frac"], "traffic": traffic, "traffic_source": src,
+                "alg_bytes_per_launch": dom["alg_bytes_per_launch"], "kernel_ms_avg": dom["ms_avg"],
+                "kernel_launches_timed": dom["launches_timed"], "ions_scored_by_pass": dom["ions"],
+                "alg_bytes_8B_per_point_frac": dom["frac"] * 8.0 / ALG_BYTES_PER_POINT}
+    return roofline, passes
 
 
 def _lib_check(rc):
@@ -263,6 +442,19 @@ def device_chain(args, peaks, formulas, plan):
     torch.cuda.synchronize()
     sum_hits = int((hi - lo).sum().item())
     n_scored = int(((out.flags & 1) != 0).sum().item())
+    # the window points of each ion, attributed to the pass that scored it (SMG_ION_* flags)
+    from sm_distributed_amd import _lib
+    cs = torch.zeros(lo.numel() + 1, dtype=torch.int64, device=lo.device)
+    torch.cumsum(hi - lo, 0, out=cs[1:])
+    pts = (cs[dions.win_off[1:]] - cs[dions.win_off[:-1]]).cpu().numpy()
+    fl = out.flags.cpu().numpy().astype(np.int64)
+    pas = np.full(n, _lib.SMG_PASS_MAIN)
+    pas[(fl & _lib.SMG_ION_BIG) != 0] = _lib.SMG_PASS_BIG
+    pas[(fl & _lib.SMG_ION_DENSE) != 0] = _lib.SMG_PASS_DENSE
+    pas[(fl & _lib.SMG_ION_WIDE) != 0] = _lib.SMG_PASS_WIDE
+    has = (fl & _lib.SMG_ION_HAS_HITS) != 0
+    pass_pts = {int(p): int(pts[has & (pas == p)].sum()) for p in np.unique(pas)}
+    pass_ions = {int(p): int((has & (pas == p)).sum()) for p in np.unique(pas)}
     t0 = time.perf_counter()
     for _ in range(args.chain_steps):
         step(True)
@@ -271,19 +463,22 @@ def device_chain(args, peaks, formulas, plan):
     names = ["flag+sort+scan", "window_search", "ion_metrics"]
     stages = {nm: float(np.mean([e[j].elapsed_time(e[j + 1]) for e in events])) for j, nm in enumerate(names)}
     return {"ms_per_step": ms, "ions_per_s": n_scored / (ms * 1e-3), "n_scored": n_scored, "stages_ms": stages,
-            "sum_window_points": sum_hits, "n_points": pk.n_points}
+            "sum_window_points": sum_hits, "n_points": pk.n_points, "pass_window_points": pass_pts,
+            "pass_ions": pass_ions}
 
 
-def measured_traffic():
-    """HBM bytes per launch of the main ion kernel from the newest committed PMC summary (profiles/*/traffic_*.json,
-    scripts/gpu_traffic.sh: FETCH_SIZE calibrated for the kernel's access width, + WRITE_SIZE).  The counters
-    cannot be read from inside this process; None when no summary exists."""
+def measured_traffic(kernel, workload):
+    """HBM bytes per launch of ``kernel`` on ``workload`` from the newest committed PMC summary
+    (profiles/*/traffic_*.json, scripts/gpu_traffic.sh: FETCH_SIZE calibrated for the kernel's access width, +
+    WRITE_SIZE).  The counters cannot be read from inside this process; None when no summary exists.  Summaries
+    without a "config" field are config-3 summaries of the main ion kernel (rounds 1-2)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic_*.json")))
     best = None
-    for f in files:  # profiles/round<N>/..., newest round last; only summaries of the main ion kernel
+    for f in files:  # profiles/round<N>/..., newest round last
         d = json.load(open(f))
-        if d.get("kernel") == "ion_pipe_kernel[512]":
+        cfg = d.get("config", "config3" if d.get("kernel") == "ion_pipe_kernel[512]" else None)
+        if d.get("kernel") == kernel and cfg == workload:
             best = (float(d["traffic_bytes_per_launch"]), os.path.relpath(f, ROOT))
     return best if best else (None, None)
 

@@ -179,11 +179,20 @@ int smg_debug_force_two_level(int32_t on);
  * returns 0. */
 int smg_debug_force_dense(int32_t on);
 
-/* Diagnostics: on != 0 records HIP events on the launch stream around every main-pass (ion_pipe_kernel<512>)
- * launch of smg_ion_metrics; smg_debug_main_pass_times waits for the recorded launches, writes up to `cap`
- * elapsed times in ms (launch order), the number recorded to *n, and forgets them.  Process-wide. */
+/* passes of smg_ion_metrics, as reported by smg_debug_pass_times */
+#define SMG_PASS_DESC 0   /* ion descriptors (ion_desc8_kernel) */
+#define SMG_PASS_MAIN 1   /* main LDS pass (ion_pipe_kernel<512>, two workgroups per CU) */
+#define SMG_PASS_BIG 2    /* big-ion LDS pass over the main pass's rejects (ion_pipe_kernel<1024>): SMG_ION_BIG */
+#define SMG_PASS_WIDE 3   /* rank-indexed wide pass (ion_wide_kernel): SMG_ION_WIDE */
+#define SMG_PASS_DENSE 4  /* pixel-indexed pass (ion_dense_kernel): SMG_ION_DENSE without SMG_ION_WIDE */
+
+/* Diagnostics: on != 0 records HIP events on the launch stream around every pass launch of smg_ion_metrics.
+ * smg_debug_pass_times waits for the recorded launches, writes up to `cap` (pass id, elapsed ms) pairs in launch
+ * order, the number recorded to *n, and forgets them; smg_debug_main_pass_times does the same for the main-pass
+ * launches only (the other passes' records are dropped).  Process-wide. */
 int smg_debug_time_main_pass(int32_t on);
 int smg_debug_main_pass_times(double* ms, int32_t cap, int32_t* n);
+int smg_debug_pass_times(int32_t* pass, double* ms, int32_t cap, int32_t* n);
 
 #ifdef __cplusplus
 }

@@ -3323,11 +3323,35 @@ using Main2Lay = Lay2<MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX>;
 using Big2Lay = Lay2<BIG_BLOCK / WAVE, BIG_BLOCK * BIG2_RMAX>;
 static int g_force_two_level = 0;  // smg_debug_force_two_level: two-level passes for every image size
 static int g_force_dense = 0;      // smg_debug_force_dense: 1 every ion on the dense path, 2 pixel-indexed only
-// smg_debug_time_main_pass: HIP events recorded on the launch stream around every main-pass launch, so a
-// benchmark measures the dominant kernel itself (not the descriptor kernel and the later passes around it)
+// smg_debug_time_main_pass: HIP events recorded on the launch stream around every pass launch of
+// smg_ion_metrics (descriptors, main LDS pass, big-ion pass, wide pass, pixel-indexed pass), so a benchmark
+// measures each kernel itself and prices each pass's own window points against its own time
 static int g_time_main = 0;
 static std::mutex g_ev_mu;
-static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_main_events;
+struct PassEvents {
+  int pass;
+  hipEvent_t ev0, ev1;
+};
+static std::vector<PassEvents> g_pass_events;
+
+// opens a timed region for one pass launch on `st` (no-op unless smg_debug_time_main_pass is on)
+struct PassTimer {
+  int pass;
+  hipStream_t st;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  PassTimer(int p, hipStream_t s) : pass(p), st(s) {
+    if (!g_time_main) return;
+    if (hipEventCreate(&ev0) != hipSuccess || hipEventCreate(&ev1) != hipSuccess ||
+        hipEventRecord(ev0, st) != hipSuccess)
+      ev0 = ev1 = nullptr;
+  }
+  ~PassTimer() {
+    if (!ev0) return;
+    if (hipEventRecord(ev1, st) != hipSuccess) return;
+    std::lock_guard<std::mutex> g(g_ev_mu);
+    g_pass_events.push_back({pass, ev0, ev1});
+  }
+};
 
 static int device_cus() {
   int dev = 0, cus = 0;
@@ -3372,6 +3396,7 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
 #ifndef SMG_DESC8
 #define SMG_DESC8 1
 #endif
+    PassTimer tm(SMG_PASS_DESC, st);
     if (SMG_DESC8)
       hipLaunchKernelGGL(ion_desc8_kernel<FMT>, dim3((unsigned)((n_ions * 8 + 255) / 256)), dim3(256), 0, st, hits,
                          lo, hi, ion_off, theor, reinterpret_cast<const DD4*>(hit_cum), ion_order, n_ions, desc);
@@ -3389,20 +3414,10 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
     // MAIN_WGPCU resident workgroups per CU, a multiple of the XCD count
     int64_t nwg = (int64_t)cus * MAIN_WGPCU;
     if (nwg > n_ions) nwg = ((n_ions + XCDS - 1) / XCDS) * XCDS;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    if (g_time_main) {
-      SMG_HIP(hipEventCreate(&ev0));
-      SMG_HIP(hipEventCreate(&ev1));
-      SMG_HIP(hipEventRecord(ev0, st));
-    }
+    PassTimer tm(SMG_PASS_MAIN, st);
     hipLaunchKernelGGL(k1, dim3((unsigned)nwg), dim3(MAIN_BLOCK), lds_main, st, hits, desc, SA, PM, oc, osp, osc,
                        omsm, oflags, list_a, hdr + 0);
     SMG_LAUNCH_CHECK();
-    if (g_time_main) {
-      SMG_HIP(hipEventRecord(ev1, st));
-      std::lock_guard<std::mutex> g(g_ev_mu);
-      g_main_events.emplace_back(ev0, ev1);
-    }
   } else if (big_ok) {
     hipLaunchKernelGGL(list_positions_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, list_a,
                        hdr + 0, n_ions);
@@ -3415,6 +3430,7 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
     SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k2), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_big));
     const int nwg2 = (int)(n_ions < cus ? n_ions : cus);
+    PassTimer tm(SMG_PASS_BIG, st);
     hipLaunchKernelGGL(k2, dim3((unsigned)nwg2), dim3(BIG_BLOCK), lds_big, st, hits, desc, SB, PB, oc, osp, osc,
                        omsm, oflags, list_b, hdr + 2);
     SMG_LAUNCH_CHECK();
@@ -3436,6 +3452,7 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   if (!P.clip && g_force_dense != 2 && wide_lds <= WIDE_LDS_MAX) {
     SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ion_wide_kernel<FMT>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)wide_lds));
+    PassTimer tm(SMG_PASS_WIDE, st);
     hipLaunchKernelGGL(ion_wide_kernel<FMT>, dim3((unsigned)nslots), dim3(DBLOCK), wide_lds, st, hits,
                        reinterpret_cast<const DD4*>(hit_cum), lo, hi, ion_off,
                        theor, P, list_b, hdr + 2, hdr + 3, list_a, hdr + 4, slots, slot_bytes, oc, osp, osc, omsm,
@@ -3447,6 +3464,7 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   }
   // the principal presence bitmap lives in the LDS when it fits (images up to ~1.2M pixels)
   const size_t bm_bytes = (((size_t)P.npx + 31) / 32 + 1) * 4;
+  PassTimer tm(SMG_PASS_DENSE, st);
   if (bm_bytes <= DENSE_BM_LDS_MAX) {
     SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ion_dense_kernel<FMT, true>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)bm_bytes));
@@ -3493,22 +3511,41 @@ int smg_debug_time_main_pass(int32_t on) {
   return SMG_OK;
 }
 
-int smg_debug_main_pass_times(double* ms, int32_t cap, int32_t* n) {
-  SMG_CHECK_ARG(n != nullptr && (ms != nullptr || cap == 0), "bad arguments");
+// waits for the recorded launches, hands out those of pass `only` (-1: every pass) and forgets them all
+static int drain_pass_times(int only, int32_t* pass, double* ms, int32_t cap, int32_t* n) {
   std::lock_guard<std::mutex> g(g_ev_mu);
   int32_t k = 0;
-  for (auto& e : g_main_events) {
-    SMG_HIP(hipEventSynchronize(e.second));
+  int rc = SMG_OK;
+  for (auto& e : g_pass_events) {
     float t = 0.0f;
-    SMG_HIP(hipEventElapsedTime(&t, e.first, e.second));
-    if (k < cap) ms[k] = (double)t;
-    ++k;
-    (void)hipEventDestroy(e.first);
-    (void)hipEventDestroy(e.second);
+    if (rc == SMG_OK && (hipEventSynchronize(e.ev1) != hipSuccess ||
+                         hipEventElapsedTime(&t, e.ev0, e.ev1) != hipSuccess)) {
+      set_error("pass timing events failed");
+      rc = SMG_ERR_HIP;
+    }
+    if (only < 0 || e.pass == only) {
+      if (k < cap) {
+        ms[k] = (double)t;
+        if (pass) pass[k] = e.pass;
+      }
+      ++k;
+    }
+    (void)hipEventDestroy(e.ev0);
+    (void)hipEventDestroy(e.ev1);
   }
-  g_main_events.clear();
+  g_pass_events.clear();
   *n = k;
-  return SMG_OK;
+  return rc;
+}
+
+int smg_debug_main_pass_times(double* ms, int32_t cap, int32_t* n) {
+  SMG_CHECK_ARG(n != nullptr && (ms != nullptr || cap == 0), "bad arguments");
+  return drain_pass_times(SMG_PASS_MAIN, nullptr, ms, cap, n);
+}
+
+int smg_debug_pass_times(int32_t* pass, double* ms, int32_t cap, int32_t* n) {
+  SMG_CHECK_ARG(n != nullptr && ((ms != nullptr && pass != nullptr) || cap == 0), "bad arguments");
+  return drain_pass_times(-1, pass, ms, cap, n);
 }
 
 int smg_debug_force_dense(int32_t on) {

@@ -242,6 +242,7 @@ def search(plan, peaks, formulas, fdr, ds_config, group=None, score_local=None):
         out = msm.filter_sf_metrics(sf_image_metrics_est_fdr(df, formulas, fdr))
     # every rank filters its own images by the reported keys (broadcast of the reported index)
     obj = [None if out is None else out.index]
-    dist.broadcast_object_list(obj, src=0, group=group)
+    # src is a global rank: group rank 0's (gather_rows sends the table there)
+    dist.broadcast_object_list(obj, src=0 if group is None else dist.get_global_rank(group, 0), group=group)
     images = msm.filter_sf_images(ims, obj[0]) if ims is not None else None
     return out, images

@@ -133,7 +133,7 @@ class DevicePeaks:
         """The points with lo <= mz <= hi (f64 comparison), in dataset order, as a new DevicePeaks whose
         duplicate-candidate flags for ``ppm`` are set by the copy (smg_slice_mz_count / _copy)."""
         if not self.spectra_sorted():
-            raise ValueError("slice_mz needs m/z-sorted spectra")
+            return self._slice_mz_masked(lo, hi, ppm, stream)
         n_sp = int(self.sp_off.numel()) - 1
         sz = ctypes.c_size_t(0)
         check(lib().smg_slice_mz_workspace_size(n_sp, ctypes.byref(sz)), "smg_slice_mz_workspace_size")
@@ -162,6 +162,25 @@ class DevicePeaks:
             if float(b[0]) < hi:
                 b = np.nextafter(b, np.float32(np.inf))
             out.sort_key_bits = max(1, (int(a.view(np.int32)[0]) ^ int(b.view(np.int32)[0])).bit_length())
+        return out
+
+    def _slice_mz_masked(self, lo: float, hi: float, ppm: float, stream=None) -> "DevicePeaks":
+        """slice_mz for datasets with spectra that are not m/z-sorted (the reference accepts them; the flag pass
+        flags every point of such a spectrum): a masked copy in dataset order (f64 comparison) and a full flag
+        pass over the slice."""
+        with torch.cuda.stream(stream) if stream is not None else _nullctx():
+            m64 = self.mz.to(torch.float64)
+            idx = torch.nonzero((m64 >= float(lo)) & (m64 <= float(hi))).flatten()
+            del m64
+            n_sp = int(self.sp_off.numel()) - 1
+            sp = torch.searchsorted(self.sp_off[1:], idx, right=True)
+            off = torch.zeros(n_sp + 1, dtype=torch.int64, device=self.device)
+            off[1:] = torch.cumsum(torch.bincount(sp, minlength=n_sp)[:n_sp], 0)
+            out = DevicePeaks(mz=self.mz[idx], hits=self.hits[idx], nrows=self.nrows, ncols=self.ncols, sp_off=off,
+                              force=self.force)
+        out.flag_duplicates(ppm, stream)
+        out.flags_preset_ppm = float(ppm)
+        out._sorted = False
         return out
 
     def sort(self, stream=None) -> "DevicePeaks":
@@ -311,6 +330,14 @@ def ion_metrics(peaks: DevicePeaks, ions: DeviceIons, lo, hi, nlevels=30, q=99.0
                            ions.theor,
                            ions.ion_order, ions.n_ions, peaks.nrows, peaks.ncols, nlevels, q, do_preprocessing,
                            connectivity, erosion_border, out, stream)
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def _force_flags(pixel_map, device):

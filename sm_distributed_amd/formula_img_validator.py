@@ -113,7 +113,11 @@ def _theor_arrays(ims, sf_ints, device):
     n = len(ik)
     if isinstance(sf_ints, PeakInts):
         cache = sf_ints.__dict__.setdefault("_dev_cache", {})
+        # keyed by the adduct list and the sf levels object itself: the entry holds a reference to the levels it
+        # was built for and is used only for that same object (an id() alone can be reused after collection)
         sig = (str(device), tuple(ik.adducts), None if ik.sf_levels is None else id(ik.sf_levels))
+        if sig in cache and cache[sig][4] is not ik.sf_levels:
+            cache.clear()
         if sig not in cache:
             k, ok = ik.encode_codes(sf_ints.sf_ids, sf_ints.adduct_codes, sf_ints.adducts)
             rows = np.nonzero(ok)[0]
@@ -123,8 +127,9 @@ def _theor_arrays(ims, sf_ints, device):
                 k, rows = k[o], rows[o]
             t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
             cache.clear()
-            cache[sig] = (t(k), t(rows), t(np.asarray(sf_ints.off, np.int64)), t(np.asarray(sf_ints.values, np.float64)))
-        pk_key, pk_row, pk_off, pk_val = cache[sig]
+            cache[sig] = (t(k), t(rows), t(np.asarray(sf_ints.off, np.int64)), t(np.asarray(sf_ints.values, np.float64)),
+                          ik.sf_levels)
+        pk_key, pk_row, pk_off, pk_val, _ = cache[sig]
         # the alignment is a function of the ion keys only: the last one is reused while they are the same
         # (a search per step over the same formula table), without its two synchronisations
         last = cache.get(("last",) + sig)

@@ -57,9 +57,75 @@ ISOTOPE_SPACING = 1.003355
 TARGET_ADDUCTS = ('+H', '+Na', '+K')
 
 
-def adduct_shift(adduct: str) -> float:
+# BASELINE config 5: 6 target adducts in both polarities (a positive-mode and a negative-mode search over the same
+# molecule table); the charge sign follows the polarity (isocalc_wrapper.py:28-32)
+TARGET_ADDUCTS_POS = ('+H', '+Na', '+K')
+TARGET_ADDUCTS_NEG = ('-H', '+Cl', '+Br')
+
+
+def adduct_shift(adduct: str, charge: int = 1) -> float:
+    """m/z shift of ``sf + adduct`` at charge +-1: the adduct adds ('+X') or removes ('-X') element X, and the
+    ion carries ``charge`` missing electrons (complete_isodist(..., charge), isocalc_wrapper.py:28-40: m/z =
+    (M - z*m_e) / |z|), so a negative ion is one electron mass heavier than its neutral."""
+    if charge not in (1, -1):
+        raise ValueError("synthetic ion tables are singly charged")
     sign = 1.0 if adduct[0] == '+' else -1.0
-    return sign * ELEMENT_MASS[adduct[1:]] - ELECTRON_MASS
+    return sign * ELEMENT_MASS[adduct[1:]] - charge * ELECTRON_MASS
+
+
+@dataclass
+class FormulaSet:
+    """Synthetic sum formulas (CHNOPS compositions): ``sf`` strings, monoisotopic neutral ``mass`` and element
+    ``counts`` [n_sf, len(FORMULA_ELEMENTS)], so negative adducts can be vetted as theor_peaks_gen.py:46-51 does
+    ('-X' needs element X in the formula)."""
+    sf: np.ndarray
+    mass: np.ndarray
+    counts: np.ndarray
+
+    def has_element(self, el: str) -> np.ndarray:
+        if el not in FORMULA_ELEMENTS:
+            return np.zeros(len(self.sf), dtype=bool)
+        return self.counts[:, FORMULA_ELEMENTS.index(el)] > 0
+
+
+FORMULA_ELEMENTS = ('C', 'H', 'N', 'O', 'P', 'S')
+
+
+def make_formulas(n_sf: int, seed: int = 43, mass_range=(150.0, 900.0), no_h_fraction: float = 0.01) -> FormulaSet:
+    """``n_sf`` distinct organic compositions (unique sum formulas, as the reference's agg_formula table) with
+    monoisotopic mass in ``mass_range``: C from the mass, H from a drawn degree of unsaturation (H = 2C + 2 + N -
+    2*DBE), N/P/S sparse, O filling the mass; ``no_h_fraction`` of them carry no hydrogen, so the '-H' adduct is
+    vetted out for those formulas as the reference does."""
+    rng = np.random.default_rng(seed)
+    el_mass = np.array([ELEMENT_MASS[e] for e in FORMULA_ELEMENTS])
+    rows, seen = [], set()
+    while len(rows) < n_sf:
+        k = 2 * (n_sf - len(rows)) + 16
+        m = rng.uniform(mass_range[0], mass_range[1], k)
+        c = np.maximum(1, np.round(m * rng.uniform(0.035, 0.06, k))).astype(np.int64)
+        n = rng.poisson(0.8, k)
+        ph = (rng.random(k) < 0.05).astype(np.int64)
+        su = (rng.random(k) < 0.06).astype(np.int64)
+        dbe = np.floor(rng.random(k) * (c // 2 + 1)).astype(np.int64)
+        h = 2 * c + 2 + n - 2 * dbe
+        h = np.where(rng.random(k) < no_h_fraction, 0, h)
+        rest = m - (c * el_mass[0] + h * el_mass[1] + n * el_mass[2] + ph * el_mass[4] + su * el_mass[5])
+        o = np.round(rest / el_mass[3]).astype(np.int64)
+        cnt = np.stack([c, h, n, o, ph, su], axis=1)
+        mass = cnt @ el_mass
+        ok = (h >= 0) & (o >= 0) & (mass >= mass_range[0]) & (mass <= mass_range[1])
+        for r in cnt[ok].tolist():
+            t = tuple(r)
+            if t not in seen and len(rows) < n_sf:
+                seen.add(t)
+                rows.append(r)
+    counts = np.array(rows, dtype=np.int64).reshape(n_sf, len(FORMULA_ELEMENTS))
+    mass = counts @ el_mass
+
+    def name(row):
+        return ''.join(e + (str(k) if k > 1 else '') for e, k in zip(FORMULA_ELEMENTS, row) if k > 0)
+    sf = np.array([name(r) for r in counts.tolist()], dtype=object)
+    return FormulaSet(sf=sf, mass=mass, counts=counts)
 
 
 @dataclass
@@ -78,6 +144,14 @@ class IonTable:
     target_adducts: tuple = TARGET_ADDUCTS
     decoy_sample_size: int = 20
     td: tuple = field(default=None)   # (sf_id, ta, da) arrays
+    is_target: np.ndarray = None      # bool per ion (None: adduct in target_adducts)
+    charge: np.ndarray = None         # +-1 per ion (None: +1)
+    sf_names: np.ndarray = None       # sum formula string per sf_id - sf_id_offset (FormulaSet tables)
+
+    def target_mask(self):
+        if self.is_target is not None:
+            return self.is_target
+        return np.isin(self.adducts, list(self.target_adducts))
 
     @property
     def n_ions(self):
@@ -103,11 +177,19 @@ class IonTable:
 
 def make_ion_table(n_sf: int, seed: int = 43, decoy_seed: int = 44, target_adducts=TARGET_ADDUCTS,
                    decoy_sample_size: int = 20, mass_range=(150.0, 900.0), k_range=(4, 6),
-                   sf_id_offset: int = 0) -> IonTable:
+                   sf_id_offset: int = 0, formulas: FormulaSet | None = None, charge: int = 1) -> IonTable:
+    """Ion table of one search: ``n_sf`` formulas x target adducts + distinct decoys.  ``formulas`` (a
+    FormulaSet) gives the neutral masses and compositions (else masses are drawn uniformly and every adduct is
+    valid); ``charge`` +-1 is the polarity's (isocalc_wrapper.py:28-32).  A target ion whose '-X' adduct removes
+    an element the formula lacks is not generated (theor_peaks_gen.py:46-51: no theoretical peaks, so no row in
+    sf_df), while its decoy draws stay in the target/decoy table as FDR.decoy_adduct_selection makes them."""
     rng = np.random.default_rng(seed)
     mass = rng.uniform(mass_range[0], mass_range[1], n_sf)
     n_peaks = rng.integers(k_range[0], k_range[1] + 1, n_sf)
     decay = rng.uniform(0.5, 2.5, n_sf)
+    if formulas is not None:
+        assert len(formulas.mass) == n_sf
+        mass = formulas.mass
     sf_ids = np.arange(n_sf, dtype=np.int64) + sf_id_offset
 
     # fdr.py:27-31 / :42-48: per (sf, target adduct) draw decoy_sample_size decoys without replacement
@@ -123,17 +205,26 @@ def make_ion_table(n_sf: int, seed: int = 43, decoy_seed: int = 44, target_adduc
     # ion set = targets + DISTINCT decoys per sf (formulas_segm.py:14-20 SELECT DISTINCT)
     used = np.zeros((n_sf, len(cand)), dtype=bool)
     used[np.repeat(np.arange(n_sf), n_ta * decoy_sample_size), draws.reshape(-1)] = True
-    ion_sf_idx = [np.repeat(np.arange(n_sf), n_ta)]
-    ion_add = [np.tile(np.array(target_adducts, dtype=object), n_sf)]
+    t_sf = np.repeat(np.arange(n_sf), n_ta)
+    t_add = np.tile(np.array(target_adducts, dtype=object), n_sf)
+    if formulas is not None:  # theor_peaks_gen.py:46-51: '-X' needs X in the formula
+        valid = np.ones(t_sf.size, dtype=bool)
+        for j, a in enumerate(target_adducts):
+            if a.startswith('-'):
+                valid[j::n_ta] = formulas.has_element(a[1:])
+        t_sf, t_add = t_sf[valid], t_add[valid]
+    ion_sf_idx = [t_sf]
+    ion_add = [t_add]
     dsf, dc = np.nonzero(used)
     ion_sf_idx.append(dsf)
     ion_add.append(cand_arr[dc])
+    is_tgt = np.concatenate([np.ones(t_sf.size, bool), np.zeros(dsf.size, bool)])
     ion_sf_idx = np.concatenate(ion_sf_idx)
     ion_add = np.concatenate(ion_add)
     order = np.lexsort((ion_add.astype(str), ion_sf_idx))
-    ion_sf_idx, ion_add = ion_sf_idx[order], ion_add[order]
+    ion_sf_idx, ion_add, is_tgt = ion_sf_idx[order], ion_add[order], is_tgt[order]
 
-    shifts = {a: adduct_shift(a) for a in set(ion_add.tolist())}
+    shifts = {a: adduct_shift(a, charge) for a in set(ion_add.tolist())}
     ion_mz0 = mass[ion_sf_idx] + np.array([shifts[a] for a in ion_add])
     K = n_peaks[ion_sf_idx]
     win_off = np.zeros(len(K) + 1, dtype=np.int64)
@@ -147,7 +238,45 @@ def make_ion_table(n_sf: int, seed: int = 43, decoy_seed: int = 44, target_adduc
     peak_int = np.round(peak_int, 6)
     return IonTable(sf_ids=sf_ids[ion_sf_idx], adducts=ion_add, win_off=win_off, peak_mz=peak_mz,
                     peak_int=peak_int, target_adducts=tuple(target_adducts),
-                    decoy_sample_size=decoy_sample_size, td=(td_sf, td_ta, td_da))
+                    decoy_sample_size=decoy_sample_size, td=(td_sf, td_ta, td_da),
+                    is_target=is_tgt if formulas is not None else None,
+                    charge=np.full(len(ion_add), charge, np.int8) if charge != 1 else None,
+                    sf_names=formulas.sf if formulas is not None else None)
+
+
+def concat_ion_tables(tables) -> IonTable:
+    """One ion table from several searches over disjoint sf_id ranges (e.g. both polarities)."""
+    off = [np.zeros(1, np.int64)]
+    base = 0
+    for t in tables:
+        off.append(t.win_off[1:] + base)
+        base += int(t.win_off[-1])
+    cat = lambda f: np.concatenate([f(t) for t in tables])
+    return IonTable(sf_ids=cat(lambda t: t.sf_ids), adducts=cat(lambda t: t.adducts), win_off=np.concatenate(off),
+                    peak_mz=cat(lambda t: t.peak_mz), peak_int=cat(lambda t: t.peak_int),
+                    target_adducts=tuple(a for t in tables for a in t.target_adducts),
+                    decoy_sample_size=tables[0].decoy_sample_size,
+                    td=tuple(np.concatenate([t.td[j] for t in tables]) for j in range(3)),
+                    is_target=cat(lambda t: t.target_mask()),
+                    charge=cat(lambda t: t.charge if t.charge is not None else np.ones(t.n_ions, np.int8)))
+
+
+def make_ion_table_both_polarities(n_sf: int, seed: int = 43, decoy_seed: int = 44,
+                                   pos_adducts=TARGET_ADDUCTS_POS, neg_adducts=TARGET_ADDUCTS_NEG,
+                                   decoy_sample_size: int = 20, mass_range=(150.0, 900.0)) -> IonTable:
+    """BASELINE config 5's table: the same ``n_sf`` formulas searched in positive mode (sf_id 0..n_sf-1, charge
+    +1, ``pos_adducts``) and negative mode (sf_id n_sf..2n_sf-1, charge -1, ``neg_adducts``), each with its own
+    decoys (fdr.py:42-48: candidates = DECOY_ADDUCTS minus that search's targets).  The reference runs one
+    polarity per dataset config; the two searches' ions are kept apart by sf_id so (sf_id, adduct) stays unique
+    (a '+Cl' positive-mode decoy and the '+Cl' negative-mode target are different ions)."""
+    fs = make_formulas(n_sf, seed=seed + 1000, mass_range=mass_range)
+    pos = make_ion_table(n_sf, seed=seed, decoy_seed=decoy_seed, target_adducts=pos_adducts,
+                         decoy_sample_size=decoy_sample_size, formulas=fs, charge=1)
+    neg = make_ion_table(n_sf, seed=seed, decoy_seed=decoy_seed + 1, target_adducts=neg_adducts,
+                         decoy_sample_size=decoy_sample_size, formulas=fs, charge=-1, sf_id_offset=n_sf)
+    out = concat_ion_tables([pos, neg])
+    out.sf_names = fs.sf
+    return out
 
 
 @dataclass
@@ -221,7 +350,7 @@ def make_dataset_np(nrows: int, ncols: int, peaks_per_spectrum: float, seed: int
 
 def _plant_np(ions: IonTable, nrows, ncols, fraction, seed, blob_sigma, mz_range):
     rng = np.random.default_rng(seed)
-    tgt = np.nonzero(np.isin(ions.adducts, list(ions.target_adducts)))[0]
+    tgt = np.nonzero(ions.target_mask())[0]
     n_pl = max(1, int(round(fraction * len(tgt)))) if len(tgt) else 0
     chosen = rng.choice(tgt, size=n_pl, replace=False) if n_pl else np.zeros(0, np.int64)
     sp_l, mz_l, in_l = [], [], []
@@ -329,7 +458,7 @@ def make_dataset_torch(nrows: int, ncols: int, peaks_per_spectrum: float, seed: 
     n_planted = 0
     if ions is not None and plant_fraction > 0:
         rng = np.random.default_rng(plant_seed)
-        tgt = np.nonzero(np.isin(ions.adducts, list(ions.target_adducts)))[0]
+        tgt = np.nonzero(ions.target_mask())[0]
         n_pl = max(1, int(round(plant_fraction * len(tgt)))) if len(tgt) else 0
         chosen = rng.choice(tgt, size=n_pl, replace=False) if n_pl else []
         gp = torch.Generator(device=device)

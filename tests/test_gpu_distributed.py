@@ -99,3 +99,88 @@ def test_score_sharded_world1_rccl():
         assert sorted(k for k, _ in ims.collect()) == sorted(ref.index.tolist())
     finally:
         dist.destroy_process_group()
+
+
+def test_shards_with_an_unsorted_spectrum_equal_single_gpu_table():
+    """A dataset with spectra that are not m/z-sorted (accepted by the reference; every point of such a spectrum is
+    a duplicate candidate): the rank slices take the masked-copy path and the shards still give the single-GPU
+    table (slice_mz used to raise)."""
+    import torch
+    from sm_distributed_amd import distributed as D
+    from sm_distributed_amd import engine as E
+    from sm_distributed_amd.formulas import FormulasSegm
+    ds, ions, ppm, kw = make_case("dups")
+    mz = ds.mz.copy()
+    for s in (3, 17, 40):  # reverse three spectra
+        a, b = ds.sp_off[s], ds.sp_off[s + 1]
+        mz[a:b] = mz[a:b][::-1].copy()
+        ds.ints[a:b] = ds.ints[a:b][::-1].copy()
+    ds.mz = mz
+    pm, dims = ds.pixel_map_dims()
+    peaks = E.DevicePeaks.from_arrays(ds.sp_off, ds.mz, ds.ints, pm, dims)
+    assert not peaks.spectra_sorted()
+    formulas = FormulasSegm.from_ion_table(ions, ppm)
+    conf = {"image_generation": {"ppm": ppm, "nlevels": 30, "q": 99, "do_preprocessing": False}}
+    rows = []
+    for r in range(3):
+        plan = D.plan_shards(formulas, peaks, ppm, 3, r)
+        rr, _ = D._device_rows(plan, peaks, conf)
+        rows.append(rr.cpu())
+    df = D.rows_to_frame(torch.cat(rows), D.plan_shards(formulas, peaks, ppm, 3, 0).global_keys)
+    ref = _api_table(peaks, formulas, ppm)
+    assert list(df.index) == list(ref.index)
+    for c in ("chaos", "spatial", "spectral", "msm"):
+        np.testing.assert_allclose(df[c].values, ref[c].values, rtol=0, atol=1e-12)
+
+
+def _nccl_rank(rank, world, port, out_q):
+    import os
+    import torch
+    import torch.distributed as dist
+    from sm_distributed_amd import distributed as D
+    from sm_distributed_amd import engine as E
+    from sm_distributed_amd.formulas import FormulasSegm
+    torch.cuda.set_device(rank)
+    dev = torch.device("cuda", rank)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            device_id=dev)
+    try:
+        ds, ions, ppm, kw = make_case("basic")
+        pm, dims = ds.pixel_map_dims()
+        peaks = E.DevicePeaks.from_arrays(ds.sp_off, ds.mz, ds.ints, pm, dims, device=dev)
+        formulas = FormulasSegm.from_ion_table(ions, ppm)
+        conf = {"image_generation": {"ppm": ppm, "nlevels": 30, "q": 99, "do_preprocessing": False}}
+        plan = D.plan_shards(formulas, peaks, ppm, world, rank)
+        df, _ = D.score_sharded(plan, peaks, conf)
+        if rank == 0:
+            ref = _api_table(peaks, formulas, ppm)
+            same = df.index.equals(ref.index) and np.allclose(df.to_numpy(), ref.to_numpy(), rtol=0, atol=1e-12)
+            out_q.put(("ok" if same else "mismatch", os.getpid()))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        out_q.put(("error %r" % (e,), rank))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_score_sharded_world2_rccl():
+    """score_sharded over a world-size-2 RCCL group, one process per GPU (skipped on a one-GPU box): the
+    gathered table equals the single-GPU table."""
+    import torch
+    import torch.multiprocessing as mp
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs (the driver's multi-GPU node); gloo world-size 2/3 runs cover the collectives on CPU")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_nccl_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5)[0] == "ok"

@@ -175,3 +175,32 @@ def test_filter_sf_images_keeps_indexed_ions():
                       columns=["sf_id", "adduct", "chaos", "spatial", "spectral", "msm"]).set_index(["sf_id", "adduct"])
     out = MSMBasicSearch(None, None, None, None, None).filter_sf_images(imgs, df).collect()
     assert [k for k, _ in out] == [(0, "+H")]
+
+
+def test_fdr_at_config3_scale_with_zero_ties_matches_oracle():
+    """estimate_fdr (vectorised, fdr.py:70-88) vs the oracle's pandas restatement on a config-3-sized table
+    (0.98M ions, 60k targets, 20 decoy draws per target adduct) whose msm vector has the device table's shape:
+    most ions at exactly 0 (no hits / no signal) and many exact ties elsewhere.  Identical digitised FDR for
+    every target ion, identical annotations at FDR 0.1."""
+    import pandas as pd
+    from oracle import msm_oracle as O
+    from sm_distributed_amd import synthetic as syn
+    from sm_distributed_amd.fdr import FDR
+    from sm_distributed_amd.formulas import FormulasSegm
+    ions = syn.make_ion_table(20000, seed=43, decoy_seed=44)
+    f = FormulasSegm.from_ion_table(ions, 2.0)
+    rng = np.random.default_rng(1)
+    msm = np.where(rng.random(ions.n_ions) < 0.7, 0.0, np.round(0.8 * rng.random(ions.n_ions) ** 3, 3))
+    tgt = ions.target_mask()
+    msm[tgt] = np.where(rng.random(tgt.sum()) < 0.1, np.round(0.75 + 0.25 * rng.random(tgt.sum()), 3), msm[tgt])
+    df = f.get_sf_adduct_sorted_df().copy()
+    df["msm"] = msm
+    fdr = FDR(0, 0, 20, list(ions.target_adducts))
+    sf, ta, da = ions.td
+    fdr.td_df = pd.DataFrame({"sf_id": sf, "ta": ta, "da": da})
+    got = fdr.estimate_fdr(df).sort_index()
+    exp = O.estimate_fdr(df, fdr.td_df, list(ions.target_adducts), 20).sort_index()
+    assert got.index.equals(exp.index) and len(got) == 60000
+    np.testing.assert_array_equal(got.fdr.to_numpy(), exp.fdr.to_numpy())
+    ann = got.index[got.fdr <= 0.1]
+    assert len(ann) > 100 and ann.equals(exp.index[exp.fdr <= 0.1])

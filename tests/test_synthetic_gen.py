@@ -68,3 +68,60 @@ def test_device_layout_fast_paths_match_generic():
         FIS.device_layout(pd.concat([df, df.iloc[:1]]), "cpu")
     with _pt.raises(AssertionError):  # a duplicate that keeps rows == windows: one window left empty
         FIS.device_layout(pd.concat([df.iloc[:-1], df.iloc[:1]]), "cpu")
+
+
+def test_adduct_shift_follows_polarity():
+    """isocalc_wrapper.py:28-32: charge sign from the polarity; m/z = (M - z*m_e)/|z| (the isotope calculator's
+    monoisotopic m/z of the same sum formula agrees)."""
+    from oracle import isocalc_oracle as I
+    M = sum(syn.ELEMENT_MASS[e] * n for e, n in (("C", 6), ("H", 12), ("O", 6)))
+    for add, z in (("+H", 1), ("+Na", 1), ("+K", 1), ("-H", -1), ("+Cl", -1), ("+Br", -1)):
+        got = M + syn.adduct_shift(add, z)
+        exp = I.monoisotopic_mz("C6H12O6" + add, z)
+        assert abs(got - exp) < 2e-5, (add, z, got, exp)
+    assert syn.adduct_shift("-H", -1) == -syn.ELEMENT_MASS["H"] + syn.ELECTRON_MASS
+    assert syn.adduct_shift("+H") == syn.ELEMENT_MASS["H"] - syn.ELECTRON_MASS
+
+
+def test_config5_ion_table_both_polarities():
+    """BASELINE config 5's table: 6 target adducts in both polarities, '-H' only for formulas with hydrogen
+    (theor_peaks_gen.py:46-51), decoys per search from DECOY_ADDUCTS minus its targets (fdr.py:42-48), unique
+    (sf_id, adduct) keys, negative-mode ions two electron masses off the positive-mode m/z of the same adduct."""
+    n = 400
+    t = syn.make_ion_table_both_polarities(n, seed=7, decoy_seed=8)
+    fs = syn.make_formulas(n, seed=7 + 1000)
+    keys = set(zip(t.sf_ids.tolist(), t.adducts.tolist()))
+    assert len(keys) == t.n_ions
+    tgt = t.target_mask()
+    pos, neg = t.sf_ids < n, t.sf_ids >= n
+    assert set(t.adducts[tgt & pos]) == {"+H", "+Na", "+K"} and set(t.adducts[tgt & neg]) == {"-H", "+Cl", "+Br"}
+    # -H only where the formula has hydrogen; every formula has its +Cl / +Br negative targets
+    with_h = fs.has_element("H")
+    assert (~with_h).any(), "the generator must produce some formulas without H"
+    minus_h = t.sf_ids[tgt & (t.adducts == "-H")] - n
+    np.testing.assert_array_equal(np.sort(minus_h), np.nonzero(with_h)[0])
+    assert (tgt & neg & (t.adducts == "+Cl")).sum() == n
+    # decoys: positive-mode decoys never +H/+Na/+K, negative-mode decoys never +Cl/+Br
+    assert not np.isin(t.adducts[~tgt & pos], ["+H", "+Na", "+K"]).any()
+    assert not np.isin(t.adducts[~tgt & neg], ["+Cl", "+Br", "-H"]).any()
+    td_sf, td_ta, td_da = t.td
+    assert len(td_sf) == 2 * n * 3 * 20
+    # principal m/z = neutral mass + shift at the ion's charge
+    first = t.peak_mz[t.win_off[:-1]]
+    i = np.nonzero(tgt & neg & (t.adducts == "+Cl"))[0][0]
+    sf = int(t.sf_ids[i]) - n
+    assert abs(first[i] - round(fs.mass[sf] + syn.ELEMENT_MASS["Cl"] + syn.ELECTRON_MASS, 6)) < 1e-6
+    j = np.nonzero((t.sf_ids == sf) & (t.adducts == "+Cl"))[0]  # the positive-mode '+Cl' decoy, if drawn
+    if len(j):
+        assert abs((first[i] - first[j[0]]) - 2 * syn.ELECTRON_MASS) < 2e-6
+    # the config-3 table is unchanged by the polarity support (same RNG stream, charge +1)
+    c3 = syn.make_ion_table(50, seed=43, decoy_seed=44)
+    assert c3.charge is None and c3.is_target is None
+
+
+def test_formulas_are_unique_compositions_in_range():
+    fs = syn.make_formulas(3000, seed=3)
+    assert len(set(fs.sf.tolist())) == 3000
+    assert fs.mass.min() >= 150.0 and fs.mass.max() <= 900.0
+    el = np.array([syn.ELEMENT_MASS[e] for e in syn.FORMULA_ELEMENTS])
+    np.testing.assert_allclose(fs.counts @ el, fs.mass)
