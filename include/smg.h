@@ -140,6 +140,19 @@ int smg_ion_metrics(int32_t hit_format, const void* hits, const double* hit_vals
                     double* out_chaos, double* out_spatial, double* out_spectral, double* out_msm,
                     uint32_t* out_flags, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Result rows of ion images (search_results.py:88-97, iso_img_row_gen of SearchResults.store_sf_iso_images):
+ * for each window w of the list (the run [lo[w], hi[w]) of the m/z-sorted packed hits = one (ion, peak) image,
+ * duplicate pixels summed as coo.toarray() does), the pixels whose summed intensity is > threshold (the
+ * reference's 0.001), in ascending flattened-pixel order (row * ncols + col), with their intensities, window-major
+ * in out_pix / out_val (window w's rows start at the exclusive prefix sum of out_count), and the min / max over the
+ * whole npx-pixel image (pixels without a point are 0).  total_points = sum(hi - lo) sizes the workspace and is
+ * the capacity out_pix / out_val must have.  Nothing is densified: O(window points) work and memory. */
+int smg_iso_image_rows_workspace_size(int64_t n_windows, int64_t total_points, size_t* bytes);
+int smg_iso_image_rows(const uint64_t* hits, const int64_t* lo, const int64_t* hi, int64_t n_windows,
+                       int64_t total_points, int64_t npx, double threshold, int64_t* out_count, double* out_min,
+                       double* out_max, int32_t* out_pix, double* out_val, void* workspace, size_t workspace_bytes,
+                       void* stream);
+
 /* Legacy imager (formula_imager.py:9-38 _get_nonzero_ints / _sample_spectrum): for every spectrum s and
  * window j, v = cum_ints[searchsorted(mzs, upper_j, 'right')] - cum_ints[searchsorted(mzs, lower_j, 'left')],
  * emitted as (j, s, v) when v > 0.001.  sp_off: int64[n_spectra+1] into mzs; cum_ints has one extra

@@ -50,6 +50,8 @@ PROTOTYPES = {
     "smg_hit_prefix_sums": (ctypes.c_int, [_I32, _P, _P, _I64, _P, _P, _SZ, _P]),
     "smg_ion_metrics": (ctypes.c_int, [_I32, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _I32, _I32, _I32, _D, _I32,
                                        _I32, _I32, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "smg_iso_image_rows_workspace_size": (ctypes.c_int, [_I64, _I64, ctypes.POINTER(_SZ)]),
+    "smg_iso_image_rows": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _I64, _D, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "smg_sample_spectra": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _I64, _P, _P, _P, _I64, _P, _P]),
     "smg_debug_stream_read": (ctypes.c_int, [_P, _I64, _P, _I32, _P]),
     "smg_debug_force_two_level": (ctypes.c_int, [_I32]),

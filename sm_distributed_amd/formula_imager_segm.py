@@ -18,6 +18,7 @@ ion, window m/z in ion-major order, processing orders) is built on the device fr
 """
 from __future__ import annotations
 
+import ctypes
 import warnings
 
 import numpy as np
@@ -339,6 +340,24 @@ class FrameIndex:
         return pd.DataFrame(host.numpy().T, index=mi, columns=METRIC_COLUMNS, copy=False)
 
 
+class ImageRows:
+    """Columnar iso_image rows of an IonImageSet: per listed window (ion ``ion[j]``, peak ``peak[j]``) its
+    ``counts[j]`` pixels above the threshold at ``pix/val[off[j]:off[j+1]]`` (ascending flattened index) and the
+    image's ``vmin/vmax``; ``rows(job_id, db_id)`` yields the reference's tuples (search_results.py:93-95)."""
+
+    def __init__(self, keys, ion, peak, counts, pix, val, vmin, vmax):
+        self.keys, self.ion, self.peak, self.counts = keys, ion, peak, counts
+        self.pix, self.val, self.vmin, self.vmax = pix, val, vmin, vmax
+        self.off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+
+    def rows(self, job_id, db_id):
+        for j in np.nonzero(self.counts > 0)[0].tolist():
+            sf_id, adduct = self.keys[int(self.ion[j])]
+            a, b = self.off[j], self.off[j + 1]
+            yield (job_id, db_id, sf_id, adduct, int(self.peak[j]), self.pix[a:b].tolist(), self.val[a:b].tolist(),
+                   self.vmin[j], self.vmax[j])
+
+
 class IonImageSet:
     """Device-resident ``RDD[((sf_id, adduct), [coo | None, ...])]``."""
 
@@ -470,6 +489,46 @@ class IonImageSet:
             last = max((j for j, m in enumerate(imgs) if m is not None), default=-1)
             res.append((keys[i], imgs[:last + 1]))
         return res
+
+    def image_rows(self, threshold=0.001):
+        """The iso_image rows of every listed ion (search_results.py:88-97) computed on the device
+        (smg_iso_image_rows: duplicates summed, pixels > threshold, ascending flattened index, min / max over the
+        whole image) -- nothing densified.  Returns the columnar ``ImageRows`` (host arrays)."""
+        import torch
+
+        from ._lib import check, lib
+        from .engine import _p, _stream, workspace
+        self.ensure_current()
+        ion_idx = self.ion_indices()
+        win_off = self.win_off
+        Kp = win_off[ion_idx + 1] - win_off[ion_idx]
+        w = (np.repeat(win_off[ion_idx], Kp) + np.arange(Kp.sum()) - np.repeat(np.cumsum(Kp) - Kp, Kp)).astype(np.int64)
+        peak_i = w - np.repeat(win_off[ion_idx], Kp)
+        ion_of = np.repeat(ion_idx, Kp)
+        nrows, ncols = self.dims
+        n = len(w)
+        dev = self.lo.device
+        cnt, _ = self._counts()
+        total = int(cnt[w].sum()) if n else 0
+        out_count = torch.zeros(n, dtype=torch.int64, device=dev)
+        out_min = torch.zeros(n, dtype=torch.float64, device=dev)
+        out_max = torch.zeros(n, dtype=torch.float64, device=dev)
+        out_pix = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+        out_val = torch.empty(max(total, 1), dtype=torch.float64, device=dev)
+        if n:
+            wt = torch.from_numpy(w).to(dev)
+            lo, hi = self.lo[wt].contiguous(), self.hi[wt].contiguous()
+            sz = ctypes.c_size_t(0)
+            check(lib().smg_iso_image_rows_workspace_size(n, total, ctypes.byref(sz)),
+                  "smg_iso_image_rows_workspace_size")
+            ws = workspace(sz.value, dev, "rows")
+            check(lib().smg_iso_image_rows(_p(self.peaks.hits_sorted), _p(lo), _p(hi), n, total, int(nrows * ncols),
+                                           float(threshold), _p(out_count), _p(out_min), _p(out_max), _p(out_pix),
+                                           _p(out_val), _p(ws), ws.numel(), _stream(None)), "smg_iso_image_rows")
+        counts = out_count.cpu().numpy()
+        m = int(counts.sum())
+        return ImageRows(keys=self.keys, ion=ion_of, peak=peak_i, counts=counts, pix=out_pix[:m].cpu().numpy(),
+                         val=out_val[:m].cpu().numpy(), vmin=out_min.cpu().numpy(), vmax=out_max.cpu().numpy())
 
     def _items(self):
         return self.materialize(self.ion_indices())

@@ -34,12 +34,29 @@ def metrics_rows(job_id, db_id, sf_metrics_df, sf_adduct_peaksn, metrics=("chaos
 
 
 def iso_image_rows(job_id, db_id, sf_iso_images, nrows, ncols):
+    """search_results.py:88-97 (iso_img_row_gen) without densifying any image.  A device ``IonImageSet`` (the
+    output of compute_sf_images, possibly filtered) is reduced on the GPU (smg_iso_image_rows); any other iterable
+    of ((sf_id, adduct), [sparse | None]) is reduced per image from its COO entries: duplicates summed
+    (= toarray()), pixels > 0.001 in flattened row-major order, min / max over the nrows*ncols image (pixels without
+    an entry are 0)."""
+    from .formula_imager_segm import IonImageSet
+    if isinstance(sf_iso_images, IonImageSet):
+        yield from sf_iso_images.image_rows().rows(job_id, db_id)
+        return
+    npx = int(nrows) * int(ncols)
     items = sf_iso_images.collect() if hasattr(sf_iso_images, "collect") else sf_iso_images
     for (sf_id, adduct), img_list in items:
         for peak_i, img_sparse in enumerate(img_list):
-            img_ints = np.zeros(int(nrows) * int(ncols)) if img_sparse is None else img_sparse.toarray().flatten()
-            pixel_inds = np.arange(img_ints.shape[0])
-            mask = img_ints > 0.001
+            if img_sparse is None:
+                continue  # np.zeros: no pixel > 0.001
+            c = img_sparse.tocoo(copy=True)
+            c.sum_duplicates()  # sorted by (row, col): flattened index ascending
+            flat = c.row.astype(np.int64) * int(ncols) + c.col.astype(np.int64)
+            v = np.asarray(c.data, dtype=np.float64)
+            mask = v > 0.001
             if mask.sum() > 0:
-                yield (job_id, db_id, sf_id, adduct, peak_i, pixel_inds[mask].tolist(), img_ints[mask].tolist(),
-                       img_ints.min(), img_ints.max())
+                full = len(v) >= npx
+                vmin = v.min() if full else min(0.0, v.min())
+                vmax = v.max() if full else max(0.0, v.max())
+                yield (job_id, db_id, sf_id, adduct, peak_i, flat[mask].tolist(), v[mask].tolist(),
+                       np.float64(vmin), np.float64(vmax))

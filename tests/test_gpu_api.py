@@ -269,3 +269,56 @@ def test_align_windows_matches_reference(with_sel):
     rl, rh, rk = _align_reference(lo, hi, win_off, kt_off, sel)
     assert np.array_equal(lo2.cpu().numpy(), rl) and np.array_equal(hi2.cpu().numpy(), rh)
     assert np.array_equal(keep.cpu().numpy().astype(bool), rk)
+
+
+@pytest.mark.parametrize("name", ["basic", "dups", "zeros_rect", "kmix"])
+def test_device_iso_image_rows_match_dense_rows_of_oracle_images(name):
+    """search_results.iso_image_rows over a device IonImageSet (smg_iso_image_rows: duplicates summed, pixels >
+    0.001 ascending, min / max over the whole image; nothing densified) equals search_results.py:88-97 applied to
+    the oracle's images (densified there, as the reference does); also after filter_sf_images-style selection."""
+    from sm_distributed_amd.dataset import DeviceDataset
+    from sm_distributed_amd.formula_imager_segm import compute_sf_images
+    from sm_distributed_amd.search_results import iso_image_rows
+    from tests.test_reference_kats import _dense_rows
+    ds, ions, ppm, kw = make_case(name)
+    ref, _ = oracle_run(ds, ions, ppm, **kw)
+    nrows, ncols = ds.pixel_map_dims()[1]
+    ims = compute_sf_images(None, DeviceDataset(ds), sf_peak_df(ions), ppm)
+    keys = sorted(ref)
+    for sel in (keys, keys[::3]):
+        sub = ims if sel is keys else ims.filter_by_keys(pd.MultiIndex.from_tuples(sel, names=["sf_id", "adduct"]))
+        got = sorted(iso_image_rows(1, 2, sub, nrows, ncols), key=lambda r: (r[2], r[3], r[4]))
+        exp = sorted(_dense_rows(1, 2, [(k, ref[k]) for k in sel], nrows, ncols), key=lambda r: (r[2], r[3], r[4]))
+        assert [r[:6] for r in got] == [r[:6] for r in exp]
+        assert len(got) > 0
+        for g, e in zip(got, exp):
+            np.testing.assert_allclose(g[6], e[6], rtol=1e-12, atol=0)
+            np.testing.assert_allclose([g[7], g[8]], [e[7], e[8]], rtol=1e-12, atol=0)
+
+
+def test_device_iso_image_rows_reference_kat():
+    """tests/test_search_results.py:59-77 of the reference (2x3 images [[100,0,0],[0,0,0]] and [[0,0,0],[0,0,10]])
+    through the device reducer: rows (.., 0, [0], [100], 0, 100) and (.., 1, [5], [10], 0, 10)."""
+    import torch
+    from sm_distributed_amd import _lib
+    from sm_distributed_amd.engine import _p, workspace
+    import ctypes
+    # packed hits: window 0 = pixel 0 (100), window 1 = pixel 5 (10) split into two duplicates 4 + 6
+    f = lambda x: int(np.array([x], np.float32).view(np.uint32)[0])
+    hits = np.array([0 | (f(100.0) << 32), (5 | 0x80000000) | (f(4.0) << 32), (5 | 0x80000000) | (f(6.0) << 32)],
+                    dtype=np.uint64)
+    d = lambda a, dt: torch.from_numpy(np.asarray(a, dtype=dt)).cuda()
+    h = d(hits.view(np.int64), np.int64)
+    lo, hi = d([0, 1], np.int64), d([1, 3], np.int64)
+    cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+    mn, mx = torch.zeros(2, dtype=torch.float64, device="cuda"), torch.zeros(2, dtype=torch.float64, device="cuda")
+    pix, val = torch.zeros(3, dtype=torch.int32, device="cuda"), torch.zeros(3, dtype=torch.float64, device="cuda")
+    L = _lib.lib()
+    sz = ctypes.c_size_t(0)
+    _lib.check(L.smg_iso_image_rows_workspace_size(2, 3, ctypes.byref(sz)))
+    ws = workspace(sz.value, "cuda", "rows_kat")
+    _lib.check(L.smg_iso_image_rows(_p(h), _p(lo), _p(hi), 2, 3, 6, 0.001, _p(cnt), _p(mn), _p(mx), _p(pix), _p(val),
+                                    _p(ws), ws.numel(), None))
+    torch.cuda.synchronize()
+    assert cnt.tolist() == [1, 1] and pix[:2].tolist() == [0, 5] and val[:2].tolist() == [100.0, 10.0]
+    assert mn.tolist() == [0.0, 0.0] and mx.tolist() == [100.0, 10.0]

@@ -204,3 +204,41 @@ def test_fdr_at_config3_scale_with_zero_ties_matches_oracle():
     np.testing.assert_array_equal(got.fdr.to_numpy(), exp.fdr.to_numpy())
     ann = got.index[got.fdr <= 0.1]
     assert len(ann) > 100 and ann.equals(exp.index[exp.fdr <= 0.1])
+
+
+def _dense_rows(job_id, db_id, items, nrows, ncols):
+    """search_results.py:88-97 verbatim in meaning: densify, mask > 0.001, min/max over the full image."""
+    for (sf_id, adduct), img_list in items:
+        for peak_i, img in enumerate(img_list):
+            ints = np.zeros(nrows * ncols) if img is None else img.toarray().flatten()
+            inds = np.arange(ints.shape[0])
+            m = ints > 0.001
+            if m.sum() > 0:
+                yield (job_id, db_id, sf_id, adduct, peak_i, inds[m].tolist(), ints[m].tolist(), ints.min(),
+                       ints.max())
+
+
+def test_iso_image_rows_sparse_equals_dense_restatement():
+    """The sparse host path (no densifying) gives the reference's rows: duplicates summed, explicit zeros,
+    values at/below the 0.001 threshold, a fully covered image (min > 0), None gaps."""
+    from scipy.sparse import coo_matrix, csr_matrix
+    from sm_distributed_amd.search_results import iso_image_rows
+    rng = np.random.default_rng(9)
+    nr, nc = 7, 9
+    items = []
+    for i in range(30):
+        n = int(rng.integers(0, 40))
+        r, c = rng.integers(0, nr, n), rng.integers(0, nc, n)
+        v = rng.choice([0.0, 0.0005, 0.001, 0.002, 1.0, 37.5], n)
+        imgs = [coo_matrix((v, (r, c)), shape=(nr, nc)), None, csr_matrix(coo_matrix((v[::-1], (r, c)), shape=(nr, nc)))]
+        if i % 5 == 0:  # every pixel covered
+            imgs.append(coo_matrix((rng.uniform(0.5, 2, nr * nc), (np.repeat(np.arange(nr), nc), np.tile(np.arange(nc), nr))),
+                                   shape=(nr, nc)))
+        items.append(((i, "+H"), imgs))
+    got = list(iso_image_rows(3, 4, items, nr, nc))
+    exp = list(_dense_rows(3, 4, items, nr, nc))
+    assert len(got) == len(exp) and len(exp) > 20
+    for g, e in zip(got, exp):
+        assert g[:6] == e[:6]
+        np.testing.assert_allclose(g[6], e[6], rtol=1e-15, atol=0)
+        assert g[7] == e[7] and g[8] == e[8]
