@@ -2636,15 +2636,26 @@ __device__ __forceinline__ WideSlot wide_slot(unsigned char* base, int npx) {
   return S;
 }
 
-// LDS bytes of the wide pass's bitmap (+ one zero word), superblock bases and word prefixes
+// the wide pass's LDS table of flagged tail points (summed per (window, pixel)); entries that find no free slot
+// within WIDE_LT_PROBES go to the slot's global table
+constexpr int WIDE_LT_LOG2 = 10;
+constexpr int WIDE_LT = 1 << WIDE_LT_LOG2;
+constexpr int WIDE_LT_PROBES = 32;
+
+// LDS bytes of the wide pass: the bitmap (+ one zero word, padded to whole 4-word groups), superblock bases, group
+// prefixes (one u16 per 4 words) and the flagged-point table
+__host__ __device__ static inline size_t wide_n64p(int npx) { return ((((size_t)npx + 63) / 64 + 1) + 3) & ~(size_t)3; }
 static inline size_t wide_lds_bytes(int npx) {
-  const size_t n64 = ((size_t)npx + 63) / 64;
-  return (n64 + 1) * 8 + ((n64 + 1023) / 1024) * 4 + ((n64 * 2 + 7) & ~(size_t)7);
+  const size_t n64 = ((size_t)npx + 63) / 64, n64p = wide_n64p(npx);
+  return n64p * 8 + ((((n64 + 1023) / 1024) * 4 + 15) & ~(size_t)15) + (((n64p / 4) * 2 + 15) & ~(size_t)15) +
+         (size_t)WIDE_LT * 4 + (size_t)WIDE_LT * 8;
 }
 
-// rank structure over the LDS bitmap: #set bits before word w = sb[w >> 10] + pf[w].  A superblock of 1024 words
-// (65536 bits, so pf fits 16 bits) is one wave's: its lanes read consecutive words (no bank conflicts) and scan them
-// 64 at a time with DPP.  Needs n64 <= DNW * 1024.  Returns the bit count.
+// rank structure over the LDS bitmap: #set bits before word w = sb[w >> 10] + pf4[w >> 2] + the bits of words
+// (w & ~3) .. w - 1 of its 4-word group.  A superblock of 1024 words (65536 bits, so pf4 fits 16 bits) is one
+// wave's: its lanes read consecutive words (no bank conflicts) and scan them 64 at a time with DPP.  Needs
+// n64 <= DNW * 1024.  Returns the bit count.  One prefix per 4 words (not per word) leaves the LDS room for the
+// flagged-point table.
 // With list != nullptr the set bits' pixels are also written to list (in no particular order; *lcount = 0 first).
 __device__ uint32_t build_rank(const uint64_t* bm, uint16_t* pf, uint32_t* sb, int n64, uint32_t* sc,
                                uint32_t* list = nullptr, int* lcount = nullptr) {
@@ -2656,7 +2667,7 @@ __device__ uint32_t build_rank(const uint64_t* bm, uint16_t* pf, uint32_t* sb, i
     uint64_t bits = w < w1 ? bm[w] : 0ull;
     const int x = __popcll(bits);
     const int incl = wave_incl_scan_dpp(x);
-    if (w < w1) pf[w] = (uint16_t)(run + (uint32_t)(incl - x));
+    if (w < w1 && (w & 3) == 0) pf[w >> 2] = (uint16_t)(run + (uint32_t)(incl - x));
     const int tot = __builtin_amdgcn_readlane(incl, 63);
     run += (uint32_t)tot;
     if (list != nullptr) {
@@ -2696,12 +2707,19 @@ __device__ __forceinline__ void ld8_async_nm(uint64_t& r, const void* addr) {
 
 struct RankBits {
   const uint64_t* bm;
-  const uint16_t* pf;
+  const uint16_t* pf;  // one prefix per 4-word group
   const uint32_t* sb;
   __device__ __forceinline__ bool test(uint32_t p) const { return (bm[p >> 6] >> (p & 63)) & 1ull; }
   __device__ __forceinline__ uint32_t rank(uint32_t p) const {  // number of set bits below pixel p
-    const uint32_t w = p >> 6;
-    return sb[w >> 10] + (uint32_t)pf[w] + (uint32_t)__popcll(bm[w] & ((1ull << (p & 63)) - 1ull));
+    const uint32_t w = p >> 6, j = w & 3u;
+    const ulonglong2* g = reinterpret_cast<const ulonglong2*>(bm + (w & ~3u));
+    const ulonglong2 a = g[0], b = g[1];  // the group's four words (two 16-B reads)
+    const uint64_t m = (1ull << (p & 63)) - 1ull;
+    const uint32_t c = (uint32_t)__popcll(j == 0 ? (a.x & m) : a.x) +
+                       (j >= 1 ? (uint32_t)__popcll(j == 1 ? (a.y & m) : a.y) : 0u) +
+                       (j >= 2 ? (uint32_t)__popcll(j == 2 ? (b.x & m) : b.x) : 0u) +
+                       (j == 3 ? (uint32_t)__popcll(b.y & m) : 0u);
+    return sb[w >> 10] + (uint32_t)pf[w >> 2] + c;
   }
 };
 
@@ -2713,7 +2731,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     uint32_t* rej_count, unsigned char* scratch, size_t slot_bytes, double* __restrict__ oc,
     double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags) {
   using H = Hits<FMT>;
-  extern __shared__ uint64_t wide_dyn[];
+  extern __shared__ __attribute__((aligned(16))) uint64_t wide_dyn[];
   __shared__ double red[8 * DNW];
   __shared__ double kst[4 * MAXK_DENSE];
   __shared__ uint32_t sc[DNW];
@@ -2728,10 +2746,14 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
   __shared__ int64_t sh_tn[MAXK_DENSE];      // length of window k at k - 1
   const int tid = threadIdx.x;
   const int npx = P.npx, n64 = (npx + 63) / 64, nsb = (n64 + 1023) / 1024;
-  uint64_t* bm = wide_dyn;  // n64 words + one zero word (row7 reads one word past a row's start)
+  const int n64p = (int)wide_n64p(npx);  // n64 words + zero words to a whole 4-word group (row7 reads one past)
+  uint64_t* bm = wide_dyn;
   uint32_t* bm32 = reinterpret_cast<uint32_t*>(bm);
-  uint32_t* sb = reinterpret_cast<uint32_t*>(bm + n64 + 1);
-  uint16_t* pf = reinterpret_cast<uint16_t*>(sb + nsb);
+  uint32_t* sb = reinterpret_cast<uint32_t*>(bm + n64p);
+  uint16_t* pf = reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(sb) + (((size_t)nsb * 4 + 15) & ~(size_t)15));
+  uint32_t* ltkey = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(pf) +
+                                                ((((size_t)n64p / 4) * 2 + 15) & ~(size_t)15));
+  double* ltval = reinterpret_cast<double*>(ltkey + WIDE_LT);
   const RankBits R{bm, pf, sb};
   const PresenceBits<true> pres{bm32};
   WideSlot S = wide_slot(scratch + (size_t)blockIdx.x * slot_bytes, npx);
@@ -2739,6 +2761,10 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
   for (int i = tid; i < WIDE_HT; i += DBLOCK) {
     S.hkey[i] = WIDE_EMPTY;
     S.hval[i] = 0.0;
+  }
+  for (int i = tid; i < WIDE_LT; i += DBLOCK) {
+    ltkey[i] = WIDE_EMPTY;
+    ltval[i] = 0.0;
   }
   slot_sync();
   const int nr = P.nrows, nc = P.ncols;
@@ -2772,7 +2798,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
 
     STAMP(15);
     // principal image: presence bits, ranks, then values and pixels at their ranks
-    for (int w = tid; w <= n64; w += DBLOCK) bm[w] = 0ull;
+    for (int w = tid; w < n64p; w += DBLOCK) bm[w] = 0ull;
     __syncthreads();
     const int64_t a0 = lo[w0], b0 = hi[w0];
     for (int64_t i0 = a0; i0 < b0; i0 += (int64_t)DBLOCK * WDU) {
@@ -2785,17 +2811,35 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
 #pragma unroll
       for (int u = 0; u < WDU; ++u) {
         const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
+        bool dup_own = false;
+        uint32_t p = 0u;
         if (i < b0) {
-          const uint32_t p = H::pix(r[u]);
-          atomicOr(&bm32[p >> 5], 1u << (p & 31));
+          p = H::pix(r[u]);
+          const uint32_t bit = 1u << (p & 31);
+          // a flagged point that sets its pixel's bit lists the pixel: one entry per pixel with duplicates
+          dup_own = !(atomicOr(&bm32[p >> 5], bit) & bit) && H::dup(r[u]);
         }
+        const int idx = wave_append(dup_own, &sh_ctr[2]);
+        if (dup_own && idx < WIDE_DL) S.dkey[idx] = p;
       }
     }
     __syncthreads();
     const int np = (int)build_rank(bm, pf, sb, n64, sc, S.par, &sh_ncand);  // principal pixels listed in par
     STAMP(10);
-    for (int r = tid; r < np; r += DBLOCK) S.vals[r] = 0.0;  // flagged points add into their rank
+    // Values by rank.  An unflagged point is the only point of its pixel in the window (smg_flag_duplicates), so it
+    // stores its value and enters the statistics at once; the pixels with flagged points (listed above, ~1-2%) are
+    // zeroed first, summed by atomics and counted after.  (Too many of them for the list: every rank is zeroed and
+    // the statistics re-read all values.)
+    const int ndp = sh_ctr[2];
+    const bool fused = ndp <= WIDE_DL;
+    if (fused) {
+      for (int j = tid; j < ndp; j += DBLOCK) S.vals[R.rank(ld_agent(&S.dkey[j]))] = 0.0;
+    } else {
+      for (int r = tid; r < np; r += DBLOCK) S.vals[r] = 0.0;
+    }
     slot_sync();
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    double mx = -INFINITY;
     for (int64_t i0 = a0; i0 < b0; i0 += (int64_t)DBLOCK * WDU) {
       typename H::Reg r[WDU];
 #pragma unroll
@@ -2809,26 +2853,28 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
         if (i < b0) {
           const uint32_t p = H::pix(r[u]);
           const uint32_t k = R.rank(p);
-          if (H::dup(r[u])) atomicAdd(&S.vals[k], H::val(r[u]));
-          else S.vals[k] = H::val(r[u]);
+          const double v = H::val(r[u]);
+          if (H::dup(r[u])) {
+            atomicAdd(&S.vals[k], v);
+          } else {
+            S.vals[k] = v;
+            if (fused) {
+              acc[0] += v;
+              acc[1] += v * v;
+              if (v > 0.0) {
+                acc[2] += v;
+                acc[3] += 1.0;
+              }
+              mx = v > mx ? v : mx;
+            }
+          }
         }
       }
     }
     slot_sync();
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    double mx = -INFINITY;
-    for (int r0 = tid; r0 < np; r0 += DBLOCK * WDU) {  // WDU loads in flight per lane
-      uint64_t vb[WDU];
-#pragma unroll
-      for (int j = 0; j < WDU; ++j) {
-        vb[j] = 0ull;
-        ld8_async_agent(vb[j], &S.vals[(r0 + j * DBLOCK < np) ? r0 + j * DBLOCK : 0]);
-      }
-      vm_wait<0>(vb);
-#pragma unroll
-      for (int j = 0; j < WDU; ++j) {
-        if (r0 + j * DBLOCK >= np) continue;
-        const double v = __longlong_as_double((long long)vb[j]);
+    if (fused) {  // the summed pixels, once each
+      for (int j = tid; j < ndp; j += DBLOCK) {
+        const double v = ld_agent(&S.vals[R.rank(ld_agent(&S.dkey[j]))]);
         acc[0] += v;
         acc[1] += v * v;
         if (v > 0.0) {
@@ -2837,12 +2883,35 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
         }
         mx = v > mx ? v : mx;
       }
+    } else {
+      for (int r0 = tid; r0 < np; r0 += DBLOCK * WDU) {  // WDU loads in flight per lane
+        uint64_t vb[WDU];
+#pragma unroll
+        for (int j = 0; j < WDU; ++j) {
+          vb[j] = 0ull;
+          ld8_async_agent(vb[j], &S.vals[(r0 + j * DBLOCK < np) ? r0 + j * DBLOCK : 0]);
+        }
+        vm_wait<0>(vb);
+#pragma unroll
+        for (int j = 0; j < WDU; ++j) {
+          if (r0 + j * DBLOCK >= np) continue;
+          const double v = __longlong_as_double((long long)vb[j]);
+          acc[0] += v;
+          acc[1] += v * v;
+          if (v > 0.0) {
+            acc[2] += v;
+            acc[3] += 1.0;
+          }
+          mx = v > mx ? v : mx;
+        }
+      }
     }
     if (np < npx) mx = mx > 0.0 ? mx : 0.0;  // unlisted pixels are zero
     dblock_sum<4>(acc, red);
     {
       const double vmax = block_max<DNW>(mx, red);
       if (tid == 0) {  // kept in the LDS until chaos / finalize (frees registers for the tail stream)
+        sh_ctr[2] = 0;   // the principal's flagged-pixel count: the tail stream's list count from here
         sh_st[0] = acc[0];
         sh_st[1] = acc[1];
         sh_st[2] = acc[2];
@@ -2926,14 +2995,18 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
           }
       };
       if constexpr (FMT == SMG_HITS_PACKED_F32) {
-        // software pipeline over batches of TDU points per lane (two register sets): wait for a batch's hits,
-        // issue the x gathers of its principal pixels and then the next batch's hits, wait for the gathers only
-        // (all but the TDU youngest operations), accumulate.  Every lane issues every load (a clamped index or
-        // a safe address when it has none) so that the counted waits hold per wave.
+        // software pipeline over batches of TDU points per lane, two register sets: a batch first issues the next
+        // batch's loads, then waits for its own (all but the TDU youngest operations).  A batch only tests its
+        // points against the principal bitmap (LDS) and the duplicate flag; a principal hit (~1-2% of the points)
+        // is parked in registers (two per lane, with its window) and its x gathered after the stream, all lanes at
+        // once, so the stream has one memory round trip per batch, not two.  A lane's third and later hits gather
+        // in place (rare).  Every lane issues every load (a clamped index) so that the counted waits hold per wave.
         const uint64_t* hb = hits.h;
-        uint64_t rA[TDU], rB[TDU], xb[TDU];
+        uint64_t rA[TDU], rB[TDU];
 #pragma unroll
-        for (int u = 0; u < TDU; ++u) rA[u] = rB[u] = xb[u] = 0ull;
+        for (int u = 0; u < TDU; ++u) rA[u] = rB[u] = 0ull;
+        uint64_t ev0 = 0ull, ev1 = 0ull;
+        int evk0 = 0, evk1 = 0, nev = 0;
         int ki = 0;  // window of the last batch issued (uniform)
         auto issue = [&](int64_t v0, uint64_t (&r)[TDU]) -> int {
           while (v0 >= sh_tb[ki + 1]) ++ki;
@@ -2947,41 +3020,39 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
           return ki;
         };
         auto batch = [&](int64_t v0, uint64_t (&r)[TDU], int kb, uint64_t (&rn)[TDU], int& kn) {
-          vm_wait<0>(r);
+          if (v0 + TSTEP < T) {
+            kn = issue(v0 + TSTEP, rn);
+            vm_wait<TDU>(r);
+          } else {
+            vm_wait<0>(r);
+          }
           const int64_t off = v0 - sh_tb[kb], n = sh_tn[kb];
-          uint32_t pm = 0u, vm = 0u;
-          uint32_t rk[TDU];
+          uint32_t flm = 0u;
 #pragma unroll
           for (int u = 0; u < TDU; ++u) {
             const bool valid = off + (int64_t)u * DBLOCK + tid < n;
             const uint32_t p = H::pix(r[u]);
             const bool pr = valid && R.test(p);
-            vm |= (uint32_t)valid << u;
-            pm |= (uint32_t)pr << u;
-            rk[u] = pr ? R.rank(p) : 0u;
+            const bool s0 = pr && nev == 0, s1 = pr && nev == 1;
+            ev0 = s0 ? r[u] : ev0;
+            evk0 = s0 ? kb : evk0;
+            ev1 = s1 ? r[u] : ev1;
+            evk1 = s1 ? kb : evk1;
+            nev += pr ? 1 : 0;
+            flm |= (uint32_t)(valid && H::dup(r[u])) << u;
+            flm |= (uint32_t)(pr && nev > 2) << (16 + u);
           }
+          if (__ballot((flm >> 16) != 0u)) {  // rare: a lane's third and later hits gather in place
 #pragma unroll
-          for (int u = 0; u < TDU; ++u) ld8_async_agent(xb[u], &S.vals[rk[u]]);
-          if (v0 + TSTEP < T) {
-            kn = issue(v0 + TSTEP, rn);
-            vm_wait<TDU>(xb);
-          } else {
-            vm_wait<0>(xb);
+            for (int u = 0; u < TDU; ++u)
+              if ((flm >> (16 + u)) & 1u) {
+                const double xv = ld_agent(&S.vals[R.rank(H::pix(r[u]))]);
+                const double y = H::val(r[u]);
+                atomicAdd(&kst[3 * MAXK_DENSE + kb + 1], xv * y);
+                if (xv > 0.0) atomicAdd(&kst[0 * MAXK_DENSE + kb + 1], y);
+              }
           }
-          if (kb != kacc) {
-            wflush();
-            kacc = kb;
-          }
-          uint32_t flm = 0u;
-#pragma unroll
-          for (int u = 0; u < TDU; ++u) {
-            const double y = H::val(r[u]);
-            const double xv = ((pm >> u) & 1u) ? __longlong_as_double((long long)xb[u]) : 0.0;
-            if (xv > 0.0) as += y;
-            axy += xv * y;
-            flm |= (uint32_t)(((vm >> u) & 1u) && H::dup(r[u])) << u;
-          }
-          append(flm, kb, r, TDU);
+          append(flm & 0xFFFFu, kb, r, TDU);
         };
         int kA = 0, kB = 0;
         if (T > 0) kA = issue(0, rA);
@@ -2989,6 +3060,22 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
           batch(v0, rA, kA, rB, kB);
           if (v0 + TSTEP >= T) break;
           batch(v0 + TSTEP, rB, kB, rA, kA);
+        }
+        // the parked principal hits: ranks, both x gathers in flight together, then the window partials
+        if (__ballot(nev > 0)) {
+          const uint32_t p0 = H::pix(ev0), p1 = H::pix(ev1);
+          const double x0 = nev > 0 ? ld_agent(&S.vals[R.rank(p0)]) : 0.0;
+          const double x1 = nev > 1 ? ld_agent(&S.vals[R.rank(p1)]) : 0.0;
+          if (nev > 0) {
+            const double y = H::val(ev0);
+            atomicAdd(&kst[3 * MAXK_DENSE + evk0 + 1], x0 * y);
+            if (x0 > 0.0) atomicAdd(&kst[0 * MAXK_DENSE + evk0 + 1], y);
+          }
+          if (nev > 1) {
+            const double y = H::val(ev1);
+            atomicAdd(&kst[3 * MAXK_DENSE + evk1 + 1], x1 * y);
+            if (x1 > 0.0) atomicAdd(&kst[0 * MAXK_DENSE + evk1 + 1], y);
+          }
         }
       } else {
         int kb = 0;
@@ -3025,9 +3112,10 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
       const int nd = min(sh_ctr[2], WIDE_DL);
       if (sh_anyfl) {
         if (nd > 0) slot_sync();  // the overflow list is complete in L2
-        // sum the flagged points per key in the table (all lanes at once: ~one atomic round trip per entry held);
-        // the lane that claims an entry lists it
-        auto insert = [&](uint32_t key, double y) {
+        // sum the flagged points per key: in the LDS table (LDS atomics), an entry that finds no free slot within
+        // WIDE_LT_PROBES in the slot's global table (one atomic round trip per entry held); the lane that claims a
+        // global entry lists it
+        auto insert_global = [&](uint32_t key, double y) {
           uint32_t h = (key * 0x9E3779B1u) >> (32 - WIDE_HT_LOG2);
           bool own = false, done = false;
           for (int t = 0; t < WIDE_PROBES; ++t) {
@@ -3041,14 +3129,45 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
             h = (h + 1) & (WIDE_HT - 1);
           }
           if (!done) sh_ctr[3] = 1;
-          const int idx = wave_append(own, &sh_nown);
-          if (own) S.hown[idx] = h;
+          return own ? (int)h : -1;
+        };
+        auto insert = [&](bool act, uint32_t key, double y) {  // uniform call: act = this lane has an entry
+          bool placed = !act;
+          if (act) {
+            uint32_t h = (key * 0x9E3779B1u) >> (32 - WIDE_LT_LOG2);
+            for (int t = 0; t < WIDE_LT_PROBES; ++t) {
+              const uint32_t old = atomicCAS(&ltkey[h], WIDE_EMPTY, key);
+              if (old == WIDE_EMPTY || old == key) {
+                atomicAdd(&ltval[h], y);
+                placed = true;
+                break;
+              }
+              h = (h + 1) & (WIDE_LT - 1);
+            }
+          }
+          int gh = -1;
+          if (__ballot(!placed)) {
+            if (!placed) gh = insert_global(key, y);
+          }
+          const int idx = wave_append(gh >= 0, &sh_nown);
+          if (gh >= 0) S.hown[idx] = (uint32_t)gh;
         };
 #pragma unroll
-        for (int j = 0; j < WIDE_FLR; ++j)
-          if (j < fc) insert(fk[j], (double)fv[j]);
-        for (int j = tid; j < nd; j += DBLOCK) insert(ld_agent(&S.dkey[j]), ld_agent(&S.dval[j]));
-        slot_sync();  // the table's sums are complete in L2
+        for (int j = 0; j < WIDE_FLR; ++j) insert(j < fc, fk[j], (double)fv[j]);
+        for (int j0 = 0; j0 < nd; j0 += DBLOCK) {
+          const int j = j0 + tid;
+          insert(j < nd, j < nd ? ld_agent(&S.dkey[j]) : 0u, j < nd ? ld_agent(&S.dval[j]) : 0.0);
+        }
+        slot_sync();  // the tables' sums are complete (LDS; L2 for the global entries)
+        for (int i = tid; i < WIDE_LT; i += DBLOCK) {  // LDS entries: add their pixel's (Σy)², then release them
+          const uint32_t key = ltkey[i];
+          if (key != WIDE_EMPTY) {
+            const double y = ltval[i];
+            atomicAdd(&kst[2 * MAXK_DENSE + key / (uint32_t)npx + 1], y * y);
+            ltkey[i] = WIDE_EMPTY;
+            ltval[i] = 0.0;
+          }
+        }
         const int no = sh_nown;
         for (int j = tid; j < no; j += DBLOCK) {  // claimed entries: add their pixel's (Σy)², then release them
           const uint32_t s = S.hown[j];
@@ -3073,20 +3192,6 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     const double npos = sh_st[3];
     if ((sh_st[0] > 0.0) && (npos >= 4.0)) {
       const double vmax = sh_st[4];
-      for (int r0 = tid; r0 < np; r0 += DBLOCK * WDU) {
-        uint64_t vb[WDU];
-#pragma unroll
-        for (int j = 0; j < WDU; ++j) {
-          vb[j] = 0ull;
-          ld8_async_agent(vb[j], &S.vals[(r0 + j * DBLOCK < np) ? r0 + j * DBLOCK : 0]);
-        }
-        vm_wait<0>(vb);
-#pragma unroll
-        for (int j = 0; j < WDU; ++j)
-          if (r0 + j * DBLOCK < np)
-            S.L[r0 + j * DBLOCK] = (uint8_t)level_of(__longlong_as_double((long long)vb[j]), vmax, P);
-      }
-      slot_sync();
       STAMP(13);
       // candidates: eL = erode_box(dilate_cross(L)) >= 1 only where erode_box(dilate_cross(presence)) is set
       // (presence is a superset of L >= 1).  That screen is computed 64 pixels at a time on the flat LDS bitmap
@@ -3098,14 +3203,18 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
       STAMP(8);
       if (tid == 0) sh_ncand = 0;
       __syncthreads();
+      // the candidate list is staged in the LDS table's space (free until the next ion's tail stream), the rest
+      // in the slot (S.epr); the next iteration's principal pixel is loaded one iteration ahead
+      uint32_t* lcand = ltkey;
+      constexpr int LCAND = WIDE_LT * 3;  // ltkey + ltval: 12 B per table entry
+      int pnext = (tid < np) ? (int)ld_agent(&S.par[tid]) : -1;
       for (int i0 = 0; i0 < np; i0 += DBLOCK) {  // uniform trip count: DPP scan below
-        const int i = i0 + tid;
-        const int p = (i < np) ? (int)S.par[i] : -1;
+        const int p = pnext;
+        pnext = (i0 + DBLOCK + tid < np) ? (int)ld_agent(&S.par[i0 + DBLOCK + tid]) : -1;
         uint32_t cm = 0u;  // bit j: cross pixel j (0 centre, 1 up, 2 down, 3 left, 4 right) is listed by p
         int r0 = 0, c0 = 0;
         if (p >= 0) {
-          r0 = p / nc;
-          c0 = p - r0 * nc;
+          rowcol(p, P, r0, c0);
           uint32_t B[7], IM[7];
           uint32_t imc = 0x7Fu;  // columns c0-3 .. c0+3 inside the image
           if (c0 - 3 < 0) imc &= 0x7Fu << (uint32_t)(3 - c0);
@@ -3115,6 +3224,11 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
             B[dr + 3] = pres.row7(r0 + dr, c0, nr, nc);
             IM[dr + 3] = (r0 + dr >= 0 && r0 + dr < nr) ? imc : 0u;
           }
+          // sparsity pre-filter (erosion border 0): a candidate's 3x3 box is covered by 4-crosses of principal
+          // pixels only if at least three of them lie in its 5x5, inside p's 7x7
+          const bool sparse = !P.erosion_border && (__popc(B[0]) + __popc(B[1]) + __popc(B[2]) + __popc(B[3]) +
+                                                    __popc(B[4]) + __popc(B[5]) + __popc(B[6])) < 3;
+          if (!sparse) {
           uint32_t Eh[7];
 #pragma unroll
           for (int k = 1; k <= 5; ++k) {
@@ -3137,29 +3251,50 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
             if (pr(wr - 1, wc)) orr = -1, occ = 0;
             if (qr + orr == 0 && qc + occ == 0 && E(wr, wc)) cm |= 1u << t;
           }
+          }
         }
         const int cnt = __popc(cm);
         const int incl = wave_incl_scan_dpp(cnt);
         int wbase = 0;
-        if ((tid & 63) == 63) wbase = atomicAdd(&sh_ncand, incl);
+        if ((tid & 63) == 63 && incl > 0) wbase = atomicAdd(&sh_ncand, incl);
         wbase = __shfl(wbase, 63);
         int idx = wbase + incl - cnt;
         while (cm != 0u) {
           const int t = __ffs(cm) - 1;
           const int qr = (t == 1) ? -1 : (t == 2) ? 1 : 0, qc = (t == 3) ? -1 : (t == 4) ? 1 : 0;
-          S.epr[idx++] = (uint32_t)((r0 + qr) * nc + c0 + qc);
+          const uint32_t q = (uint32_t)((r0 + qr) * nc + c0 + qc);
+          if (idx < LCAND) lcand[idx] = q;
+          else S.epr[idx] = q;
+          ++idx;
           cm &= cm - 1u;
         }
       }
       slot_sync();
       STAMP(9);
       const int nscr = sh_ncand;
+      if (nscr > 0) {  // level index per principal pixel, needed only around screened candidates
+        for (int r0 = tid; r0 < np; r0 += DBLOCK * WDU) {
+          uint64_t vb[WDU];
+#pragma unroll
+          for (int j = 0; j < WDU; ++j) {
+            vb[j] = 0ull;
+            ld8_async_agent(vb[j], &S.vals[(r0 + j * DBLOCK < np) ? r0 + j * DBLOCK : 0]);
+          }
+          vm_wait<0>(vb);
+#pragma unroll
+          for (int j = 0; j < WDU; ++j)
+            if (r0 + j * DBLOCK < np)
+              S.L[r0 + j * DBLOCK] = (uint8_t)level_fast(__longlong_as_double((long long)vb[j]), vmax, P);
+        }
+        slot_sync();
+      }
       for (int i0 = 0; i0 < nscr; i0 += DBLOCK) {
         const int i = i0 + tid;
-        const int q = (i < nscr) ? (int)S.epr[i] : -1;
+        const int q = (i < nscr) ? (int)(i < LCAND ? lcand[i] : ld_agent(&S.epr[i])) : -1;
         int e = 0;
         if (q >= 0) {
-          const int r0 = q / nc, c0 = q - r0 * nc;
+          int r0, c0;
+          rowcol(q, P, r0, c0);
           uint64_t WL[7];  // byte (dc + 3) of WL[dr + 3]: level of pixel (r0 + dr, c0 + dc), 0 outside / absent
           WL[0] = WL[6] = 0ull;
 #pragma unroll
@@ -3207,13 +3342,15 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
         }
       }
       slot_sync();
+      // the staged candidates are consumed: the LDS table is empty again for the next ion's tail stream
+      for (int i = tid; i < min(nscr, LCAND); i += DBLOCK) lcand[i] = i < WIDE_LT ? WIDE_EMPTY : 0u;
       const int m = sh_ctr[0];
       const int emax = sh_ctr[1];
       STAMP(14);
       double esum = 0.0, wsum = 0.0;
       for (int i = tid; i < m; i += DBLOCK) esum += (double)S.eL[i];
       if (m > 0) {  // Kruskal over the candidates, indexed by their rank in a candidate bitmap
-        for (int w = tid; w <= n64; w += DBLOCK) bm[w] = 0ull;
+        for (int w = tid; w < n64p; w += DBLOCK) bm[w] = 0ull;
         __syncthreads();
         for (int i = tid; i < m; i += DBLOCK) {
           const uint32_t q = S.epix[i];

@@ -34,6 +34,10 @@ import pandas as pd
 C_WINDOW_POINT = 6.2e-12
 C_ION = 2.0e-9
 C_SLICE_POINT = 54e-12
+# rank 0 alone assembles the gathered rows into the DataFrame (rows_to_frame: device scatter + D2H of the metric
+# columns + MultiIndex), ~1.35 ns per ion of the whole table (profiles/round2/r2end_time_shards_8.txt: 1.28 ms
+# for 0.98M ions); its shard is cut smaller by that much so that every rank ends its step together
+C_ASSEMBLY_ION = 1.35e-9
 
 ROW_FIELDS = ("ion", "chaos", "spatial", "spectral", "msm")
 
@@ -79,15 +83,21 @@ def ion_costs(win_off, peak_mz, ppm, mz_hist=None, mz_edges=None):
     return (cs[win_off[1:]] - cs[win_off[:-1]]) * C_WINDOW_POINT + C_ION
 
 
-def shard_bounds(costs, world):
-    """Contiguous [a, b) ranges with ~equal summed cost (greedy cut on the cost prefix sum)."""
+def shard_bounds(costs, world, head=0.0):
+    """Contiguous [a, b) ranges with ~equal summed cost (greedy cut on the cost prefix sum); ``head`` is work
+    rank 0 does besides its shard (the assembly), so its range is cut that much smaller."""
     costs = np.asarray(costs, dtype=np.float64)
     n = len(costs)
     if world <= 1 or n == 0:
         return [(0, n)] + [(n, n)] * max(0, world - 1)
     pref = np.concatenate([[0.0], np.cumsum(costs)])
     total = pref[-1]
-    cuts = [0] + [int(np.searchsorted(pref, total * r / world)) for r in range(1, world)] + [n]
+    # rank 0's shard a0 and every other rank's share f: a0 + head = f when the head fits one share, else a0 = 0
+    f = (total + head) / world
+    a0 = f - head
+    if a0 < 0.0:
+        a0, f = 0.0, total / (world - 1)
+    cuts = [0] + [int(np.searchsorted(pref, a0 + (r - 1) * f)) for r in range(1, world)] + [n]
     cuts = np.maximum.accumulate(np.array(cuts))
     return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
 
@@ -117,7 +127,8 @@ def plan_shards(formulas, peaks_or_mz, ppm, world, rank, bins=8192):
     pos = np.interp(first[order], edges, cum_pts)
     grow = np.diff(np.concatenate([pos, [cum_pts[-1]]]))
     cost = cost + np.maximum(grow, 0.0) * C_SLICE_POINT
-    bounds = shard_bounds(cost, world)
+    head = C_ASSEMBLY_ION * formulas.n_ions if world > 1 else 0.0
+    bounds = shard_bounds(cost, world, head)
     a, b = bounds[rank]
     mine = np.sort(order[a:b])                        # back to (sf_id, adduct) order
     shard = formulas.subset(mine)
@@ -130,7 +141,8 @@ def plan_shards(formulas, peaks_or_mz, ppm, world, rank, bins=8192):
     keys = formulas.ion_sf.astype(np.int64) * max(len(formulas.adducts), 1) + formulas.ion_adduct_code
     return ShardPlan(rank=rank, world=world, ion_idx=mine, formulas=shard, mz_lo=mz_lo, mz_hi=mz_hi, ppm=ppm,
                      counts=[int(y - x) for x, y in bounds], bounds=bounds,
-                     global_keys=IonKeys(keys, formulas.adducts), est_cost=[float(cost[x:y].sum()) for x, y in bounds])
+                     global_keys=IonKeys(keys, formulas.adducts),
+                     est_cost=[float(cost[x:y].sum()) + (head if r == 0 else 0.0) for r, (x, y) in enumerate(bounds)])
 
 
 def slice_peaks(peaks, plan):

@@ -1,4 +1,4 @@
-"""The LDS kernel's inline-asm prefetch loads obey their discipline in the generated gfx950 ISA: no
+"""The LDS and wide kernels' inline-asm prefetch loads obey their discipline in the generated gfx950 ISA: no
 instruction touches a register with a load in flight before its counted wait, on any control-flow path, and
 no such register is spilled (scripts/check_async_regs.py).  CPU-only: compiles the kernel to assembly."""
 import os
@@ -19,7 +19,7 @@ def test_async_load_registers_are_never_touched_in_flight(tmp_path):
     asm = str(tmp_path / "smg_metrics.s")
     subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "--cuda-device-only",
                     "-S", src, "-o", asm], check=True, capture_output=True)
-    for kern in ("_ZN3smg15ion_pipe_kernelILi0ELi512", "_ZN3smg15ion_pipe_kernelILi0ELi1024"):
+    for kern in ("_ZN3smg15ion_pipe_kernelILi0ELi512", "_ZN3smg15ion_pipe_kernelILi0ELi1024", "_ZN3smg15ion_wide_kernelILi0E"):
         r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "check_async_regs.py"), asm, kern],
                            capture_output=True, text=True)
         assert r.returncode == 0, r.stdout

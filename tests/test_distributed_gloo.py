@@ -90,6 +90,20 @@ def test_shard_bounds_balanced():
     assert max(sums) / min(sums) < 1.1
 
 
+def test_shard_bounds_rank0_head():
+    """Rank 0 also assembles the table: with head = its assembly time, rank 0's shard + head equals every other
+    rank's shard (distributed.C_ASSEMBLY_ION)."""
+    from sm_distributed_amd import distributed as D
+    costs = np.full(8000, 1.0)
+    head = 500.0
+    b = D.shard_bounds(costs, 8, head)
+    sums = [costs[x:y].sum() for x, y in b]
+    assert b[0][0] == 0 and b[-1][1] == 8000 and all(b[i][1] == b[i + 1][0] for i in range(7))
+    loads = [sums[0] + head] + sums[1:]
+    assert max(loads) - min(loads) <= 1.0, loads
+    assert D.shard_bounds(costs, 8, 0.0) == D.shard_bounds(costs, 8)
+
+
 def test_plan_shards_partitions_ions_and_slices_cover_windows():
     from sm_distributed_amd import distributed as D
     from sm_distributed_amd import synthetic as syn
@@ -104,8 +118,9 @@ def test_plan_shards_partitions_ions_and_slices_cover_windows():
         for p in plans:
             pm = p.formulas.peak_mz
             assert (pm - pm * 2e-6 >= p.mz_lo).all() and (pm + pm * 2e-6 <= p.mz_hi).all()
-        cost = plans[0].est_cost
-        assert max(cost) / min(cost) < 1.05, cost
+        cost = plans[0].est_cost  # rank 0's includes its assembly (a whole share on this toy dataset)
+        assert max(cost[1:]) / min(cost[1:]) < 1.05, cost
+        assert cost[0] <= 1.05 * max(cost[1:]) or len(plans[0].ion_idx) == 0, cost  # head > one share: no ions
         # contiguous in principal m/z: slices overlap only by the isotope tails (< 6 Da)
         lo = sorted((p.mz_lo, p.mz_hi) for p in plans)
         assert all(lo[i + 1][0] > lo[i][0] for i in range(world - 1))
