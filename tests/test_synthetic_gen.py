@@ -125,3 +125,29 @@ def test_formulas_are_unique_compositions_in_range():
     assert fs.mass.min() >= 150.0 and fs.mass.max() <= 900.0
     el = np.array([syn.ELEMENT_MASS[e] for e in syn.FORMULA_ELEMENTS])
     np.testing.assert_allclose(fs.counts @ el, fs.mass)
+
+
+def test_theor_alignment_identity_fast_path_matches_generic():
+    """sf_image_metrics' theoretical-intensity alignment (formula_img_validator._theor_arrays, run here on CPU
+    tensors): the identity fast path (layout ions == the table's ions) and the key-search path give the
+    intensities of every ion (formula_img_validator.py:112: sf_peak_ints[(sf_id, adduct)])."""
+    from types import SimpleNamespace
+
+    from sm_distributed_amd.formula_imager_segm import IonKeys
+    from sm_distributed_amd.formula_img_validator import _theor_arrays
+    from sm_distributed_amd.formulas import FormulasSegm
+    ions = syn.make_ion_table(60, seed=3, decoy_seed=4)
+    f = FormulasSegm.from_ion_table(ions)
+    pk = f.get_sf_peak_ints()
+    keys = f.ion_sf.astype(np.int64) * len(f.adducts) + f.ion_adduct_code
+    for sel in (np.arange(f.n_ions), np.arange(0, f.n_ions, 3)):  # identity, then a subset (key search)
+        ims = SimpleNamespace(ion_keys=IonKeys(keys[sel], f.adducts))
+        ims.keys = ims.ion_keys.tuples()
+        Kt, vals, off = _theor_arrays(ims, pk, "cpu")
+        Kt2, vals2, off2 = _theor_arrays(ims, pk, "cpu")  # the cached alignment
+        for (a, b) in ((Kt, Kt2), (vals, vals2), (off, off2)):
+            assert torch.equal(a, b)
+        exp = [pk[k] for k in ims.keys]
+        np.testing.assert_array_equal(Kt.numpy(), [len(e) for e in exp])
+        np.testing.assert_array_equal(vals.numpy(), np.concatenate(exp))
+        np.testing.assert_array_equal(off.numpy(), np.concatenate([[0], np.cumsum([len(e) for e in exp])]))
