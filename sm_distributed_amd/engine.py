@@ -67,6 +67,7 @@ class DevicePeaks:
     version: int = 0                 # bumped by every flag pass / sort: an IonImageSet records the one it used
     flags_preset_ppm: float | None = None  # a slice's copy set the flags for this ppm (no flag pass needed)
     _sorted: bool | None = None      # spectra_sorted() result
+    flag_state: torch.Tensor | None = None  # uint8 mirror of each hit's flag (the flag pass reads it, not the hits)
 
     @property
     def n_points(self) -> int:
@@ -108,8 +109,13 @@ class DevicePeaks:
             return self
         self.flags_preset_ppm = None
         n_sp = int(self.sp_off.numel()) - 1
+        if self.flag_state is None or self.flag_state.numel() != self.n_points:
+            # 1 B per point: the flag pass then reads 5 B per point (m/z + state) instead of 12 B, and a hit only
+            # where its flag changes
+            with torch.cuda.stream(stream) if stream is not None else _nullctx():
+                self.flag_state = ((self.hits >> 31) & 1).to(torch.uint8)
         check(lib().smg_flag_duplicates(_p(self.sp_off), n_sp, _p(self.mz), _p(self.hits), self.n_points,
-                                        float(ppm), _p(self.force), None, _stream(stream)),
+                                        float(ppm), _p(self.force), _p(self.flag_state), _stream(stream)),
               "smg_flag_duplicates")
         self.flag_ppm = float(ppm)
         self.version += 1
