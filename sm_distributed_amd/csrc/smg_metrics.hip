@@ -3525,9 +3525,15 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   if (lds_main < (size_t)SMG_MAIN_LDS_MIN) lds_main = SMG_MAIN_LDS_MIN;
 #endif
   const size_t lds_big = two ? Big2Lay::bytes(P.npx) : BigLay::bytes(P.npx);
-  // the hot-spot clip needs whole images: every ion takes the dense path
-  const bool main_ok = !P.clip && !g_force_dense && (two || P.npx <= NPX_LDS_MAX) && lds_main <= MAIN_LDS;
-  const bool big_ok = !P.clip && !g_force_dense && (two || P.npx <= NPX_LDS_MAX) && lds_big <= BIG_LDS;
+  // the hot-spot clip needs whole images: every ion takes the dense path.  Images above NPX_LDS_MAX pixels go to
+  // the rank-indexed wide pass when its LDS bitmap fits: it outruns the two-level LDS passes on them (config-5
+  // rank shard: the big two-level pass scored 3,958 ions in 18.4 ms, the wide pass 586k in 255 ms, and the main
+  // two-level pass spent 6.7 ms rejecting every ion, profiles/round3/r3c5_*); smg_debug_force_two_level keeps
+  // the two-level passes for the parity suite
+  const bool wide_fits = !P.clip && g_force_dense != 2 && wide_lds_bytes(P.npx) <= WIDE_LDS_MAX;
+  const bool lds_ok = two ? (!wide_fits || g_force_two_level) : P.npx <= NPX_LDS_MAX;
+  const bool main_ok = !P.clip && !g_force_dense && lds_ok && lds_main <= MAIN_LDS;
+  const bool big_ok = !P.clip && !g_force_dense && lds_ok && lds_big <= BIG_LDS;
   const int cus = device_cus();
   if (main_ok || big_ok) {
 #ifndef SMG_DESC8
