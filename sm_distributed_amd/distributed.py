@@ -34,10 +34,9 @@ import pandas as pd
 C_WINDOW_POINT = 6.2e-12
 C_ION = 2.0e-9
 C_SLICE_POINT = 54e-12
-# rank 0 alone assembles the gathered rows into the DataFrame (rows_to_frame: device scatter + D2H of the metric
-# columns + MultiIndex), ~1.35 ns per ion of the whole table (profiles/round2/r2end_time_shards_8.txt: 1.28 ms
-# for 0.98M ions); its shard is cut smaller by that much so that every rank ends its step together
-C_ASSEMBLY_ION = 1.35e-9
+# Rank 0 alone assembles the gathered rows into the DataFrame (rows_to_frame, ~1.3 ms at config 3).  Its shard is
+# NOT cut smaller for it: the assembly needs every rank's rows, so it starts only after the gather, i.e. after the
+# slowest rank -- a smaller rank-0 shard would only make the other shards (and the step) longer.
 
 ROW_FIELDS = ("ion", "chaos", "spatial", "spectral", "msm")
 
@@ -127,8 +126,7 @@ def plan_shards(formulas, peaks_or_mz, ppm, world, rank, bins=8192):
     pos = np.interp(first[order], edges, cum_pts)
     grow = np.diff(np.concatenate([pos, [cum_pts[-1]]]))
     cost = cost + np.maximum(grow, 0.0) * C_SLICE_POINT
-    head = C_ASSEMBLY_ION * formulas.n_ions if world > 1 else 0.0
-    bounds = shard_bounds(cost, world, head)
+    bounds = shard_bounds(cost, world)
     a, b = bounds[rank]
     mine = np.sort(order[a:b])                        # back to (sf_id, adduct) order
     shard = formulas.subset(mine)
@@ -141,8 +139,7 @@ def plan_shards(formulas, peaks_or_mz, ppm, world, rank, bins=8192):
     keys = formulas.ion_sf.astype(np.int64) * max(len(formulas.adducts), 1) + formulas.ion_adduct_code
     return ShardPlan(rank=rank, world=world, ion_idx=mine, formulas=shard, mz_lo=mz_lo, mz_hi=mz_hi, ppm=ppm,
                      counts=[int(y - x) for x, y in bounds], bounds=bounds,
-                     global_keys=IonKeys(keys, formulas.adducts),
-                     est_cost=[float(cost[x:y].sum()) + (head if r == 0 else 0.0) for r, (x, y) in enumerate(bounds)])
+                     global_keys=IonKeys(keys, formulas.adducts), est_cost=[float(cost[x:y].sum()) for x, y in bounds])
 
 
 def slice_peaks(peaks, plan):
