@@ -267,7 +267,10 @@ def main():
     chain = device_chain(args, peaks, my_formulas, plan) if args.chain_steps > 0 else None
 
     # ---- roofline per pass: 12 B per window point of the ions the pass scored over its own launch time --------
-    roofline, passes = pass_roofline(args, pass_ms, chain, world == 1 and not shard_only)
+    # PMC traffic summaries exist for the config-3 single-GPU step and rank 0's shard of the 8-way config-5 plan
+    traffic_ok = world == 1 and ((args.config == "3" and _is_config3(args) and not shard_only) or
+                                 (args.config == "5" and shard_only and args.shard_of == 8 and args.shard_rank == 0))
+    roofline, passes = pass_roofline(args, pass_ms, chain, traffic_ok)
 
     cpu = None
     if rank == 0 and world == 1 and not shard_only and not args.no_cpu_baseline:
@@ -390,7 +393,7 @@ def pass_roofline(args, pass_ms, chain, is_single):
     name = _lib.PASS_NAMES[dom["pass"]]
     key = {1: "ion_pipe_kernel[512]", 2: "ion_pipe_kernel[1024]", 3: "ion_wide_kernel", 4: "ion_dense_kernel"}
     traffic, src = measured_traffic(key[dom["pass"]], "config5" if args.config == "5" else "config3") \
-        if is_single and (_is_config3(args) or args.config == "5") else (None, None)
+        if is_single else (None, None)
     roofline = {"bound": "hbm", "kernel": name, "achieved": dom["achieved_GBps"], "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": dom["frac"], "traffic": traffic, "traffic_source": src,
                 "alg_bytes_per_launch": dom["alg_bytes_per_launch"], "kernel_ms_avg": dom["ms_avg"],
