@@ -191,6 +191,9 @@ int smg_debug_force_two_level(int32_t on);
  * ion to the pixel-indexed slot kernel; so that the parity suite covers both on every case.  Process-wide;
  * returns 0. */
 int smg_debug_force_dense(int32_t on);
+/* main pass kernel: 0 = one wave per ion (ion_wave_kernel, the default for packed hits), 1 = the 512-thread LDS
+ * kernel (ion_pipe_kernel<512>; A/B and parity of the two) */
+int smg_debug_main_kernel(int32_t which);
 
 /* passes of smg_ion_metrics, as reported by smg_debug_pass_times */
 #define SMG_PASS_DESC 0   /* ion descriptors (ion_desc8_kernel) */

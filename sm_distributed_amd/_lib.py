@@ -23,7 +23,7 @@ PIXEL_MASK = 0x7FFFFFFF   # bit 31 of the pixel field = duplicate-candidate flag
 SMG_HITS_SPLIT_F64 = 1
 # pass ids of smg_debug_pass_times
 SMG_PASS_DESC, SMG_PASS_MAIN, SMG_PASS_BIG, SMG_PASS_WIDE, SMG_PASS_DENSE = range(5)
-PASS_NAMES = {0: "ion_desc8_kernel", 1: "ion_pipe_kernel<512> (main LDS pass)",
+PASS_NAMES = {0: "ion_desc8_kernel", 1: "ion_wave_kernel (main pass, one wave per ion)",
               2: "ion_pipe_kernel<1024> (big-ion LDS pass)", 3: "ion_wide_kernel (wide pass)",
               4: "ion_dense_kernel (pixel-indexed pass)"}
 
@@ -56,6 +56,7 @@ PROTOTYPES = {
     "smg_debug_stream_read": (ctypes.c_int, [_P, _I64, _P, _I32, _P]),
     "smg_debug_force_two_level": (ctypes.c_int, [_I32]),
     "smg_debug_force_dense": (ctypes.c_int, [_I32]),
+    "smg_debug_main_kernel": (ctypes.c_int, [_I32]),
     "smg_debug_time_main_pass": (ctypes.c_int, [_I32]),
     "smg_debug_main_pass_times": (ctypes.c_int, [_P, _I32, ctypes.POINTER(_I32)]),
     "smg_debug_pass_times": (ctypes.c_int, [_P, _P, _I32, ctypes.POINTER(_I32)]),

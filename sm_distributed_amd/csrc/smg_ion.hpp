@@ -1,0 +1,288 @@
+// Device-side definitions shared by the ion kernels of libsmg (smg_metrics.hip: the LDS, wide and
+// pixel-indexed passes; smg_wave.hip: the wave-per-ion main pass): kernel parameters, the two hit formats,
+// asynchronous load helpers, level index, ion descriptors, persistent scheduling, LDS union-find.
+#pragma once
+
+#include "smg_common.hpp"
+
+namespace smg {
+
+constexpr int MAXK = 8;              // windows per ion on the LDS path
+constexpr int MAXK_DENSE = 32;       // windows per ion supported at all
+constexpr int NPX_LDS_MAX = 1 << 18; // images up to 262144 pixels use the LDS path
+
+enum { C_NE = 0, C_EMAX, C_ABORT, C_PDUP, C_NEXT, C_NS, C_NCTR = 8 };
+
+struct Params {
+  int32_t nrows, ncols, npx;
+  int32_t nlevels;
+  int32_t connectivity;
+  int32_t erosion_border;
+  double step;      // np.linspace(0, 1, nlevels) step
+  float inv_ncols;  // 1/ncols for the LDS path's row/column split (npx < 2^24)
+  int32_t w32;      // LDS path: bitmap words (Lay::w32)
+  uint32_t o_pf;    // LDS path: byte offset of the rank prefix (Lay::o_pf)
+  double q;         // hot-spot clip percentile (dense path, when clip != 0)
+  int32_t clip;     // image_generation.do_preprocessing
+};
+
+// row and column of pixel p < 2^24 from a float reciprocal: the estimate is off by at most one row
+__device__ __forceinline__ void rowcol(int p, const Params& P, int& r, int& c) {
+  r = (int)((float)p * P.inv_ncols);
+  c = p - r * P.ncols;
+  if (c < 0) {
+    --r;
+    c += P.ncols;
+  } else if (c >= P.ncols) {
+    ++r;
+    c -= P.ncols;
+  }
+}
+
+template <int FMT>
+struct Hits;
+
+template <>
+struct Hits<SMG_HITS_PACKED_F32> {
+  const uint64_t* h;
+  const double* unused;
+  using Reg = uint64_t;
+  __device__ __forceinline__ Reg load(int64_t i) const { return h[i]; }
+  // scalar base + 32-bit lane offset (saddr addressing)
+  __device__ __forceinline__ Reg load(int64_t base, int i) const { return (h + base)[i]; }
+  static __device__ __forceinline__ uint32_t pix(Reg r) { return (uint32_t)r & 0x7FFFFFFFu; }
+  static __device__ __forceinline__ bool dup(Reg r) { return ((uint32_t)r >> 31) != 0u; }
+  static __device__ __forceinline__ double val(Reg r) { return (double)__uint_as_float((uint32_t)(r >> 32)); }
+  static __device__ __forceinline__ Reg zero() { return 0ull; }  // pixel 0, value 0, no flag
+  __device__ __forceinline__ void get(int64_t i, uint32_t& p, double& v) const {
+    const uint64_t x = h[i];
+    p = (uint32_t)x & 0x7FFFFFFFu;
+    v = (double)__uint_as_float((uint32_t)(x >> 32));
+  }
+};
+
+struct PixVal {
+  uint32_t p;
+  double v;
+};
+
+// Asynchronous 8-byte loads for the software pipeline of the LDS kernel.  The compiler's wait-count pass
+// serialises any use of a register loaded before a loop or a branch behind s_waitcnt vmcnt(0), i.e. behind
+// every load issued since, which would expose the latency of each prefetched chunk; these loads are
+// invisible to it and are waited for with counted waits (vm_wait<N>: all but the N youngest vector-memory
+// operations of this wave done).  Vector-memory operations complete in issue order, so operations the
+// compiler issues in between only make a counted wait stricter.  The destination registers are neither
+// read nor copied between issue and wait (the wait takes them as in/out operands).
+// The destination is an in/out operand: its previous value counts as used by the next load into it, so
+// a register with a load in flight is never reallocated to another value, even when that load's data end
+// up unused (a refill past the tail, or an ion that is handed to another pass).
+__device__ __forceinline__ void ld8_async(uint64_t& r, const void* sbase, uint32_t voff) {
+  asm volatile("global_load_dwordx2 %0, %1, %2" : "+v"(r) : "v"(voff), "s"(sbase) : "memory");
+}
+__device__ __forceinline__ void ld8_async_v(uint64_t& r, const void* addr) {  // 64-bit vector address
+  asm volatile("global_load_dwordx2 %0, %1, off" : "+v"(r) : "v"(addr) : "memory");
+}
+__device__ __forceinline__ void ld4_async_v(uint32_t& r, const void* addr) {
+  asm volatile("global_load_dword %0, %1, off" : "+v"(r) : "v"(addr) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait1(uint64_t& r) {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  asm volatile("" : "+v"(r));
+}
+template <int N>
+__device__ __forceinline__ void vm_wait1(uint32_t& r) {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  asm volatile("" : "+v"(r));
+}
+// Returning atomic add issued like the async loads: the compiler would wait for its result with
+// s_waitcnt vmcnt(0) right away -- i.e. for every prefetch load of the wave in flight -- so it is waited
+// for with a counted vm_wait1 where the ticket is consumed.
+__device__ __forceinline__ void atomic_add_rtn_async(uint32_t& r, uint32_t* addr, uint32_t v) {
+  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "+v"(r) : "v"(addr), "v"(v) : "memory");
+}
+template <int N, int M>
+__device__ __forceinline__ void vm_wait(uint64_t (&r)[M]) {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#pragma unroll
+  for (int j = 0; j < M; ++j) asm volatile("" : "+v"(r[j]));
+}
+template <int N, int M>
+__device__ __forceinline__ void vm_wait(PixVal (&)[M]) {}  // split-format hits use compiler-tracked loads
+
+template <>
+struct Hits<SMG_HITS_SPLIT_F64> {
+  const uint32_t* pa;
+  const double* va;
+  using Reg = PixVal;
+  __device__ __forceinline__ Reg load(int64_t i) const { return PixVal{pa[i], va[i]}; }
+  __device__ __forceinline__ Reg load(int64_t base, int i) const { return PixVal{(pa + base)[i], (va + base)[i]}; }
+  static __device__ __forceinline__ uint32_t pix(Reg r) { return r.p & 0x7FFFFFFFu; }
+  static __device__ __forceinline__ bool dup(Reg r) { return (r.p >> 31) != 0u; }
+  static __device__ __forceinline__ double val(Reg r) { return r.v; }
+  static __device__ __forceinline__ Reg zero() { return PixVal{0u, 0.0}; }
+  __device__ __forceinline__ void get(int64_t i, uint32_t& p, double& v) const {
+    p = pa[i] & 0x7FFFFFFFu;
+    v = va[i];
+  }
+};
+
+// level index L = #{i : linspace(0,1,n)[i] < v/vmax}  (measure_of_chaos: bw = im_clean > level)
+// The levels are nondecreasing in i, so L is the lower bound of norm among them (binary search).
+__device__ __forceinline__ int level_of(double v, double vmax, const Params& P) {
+  const double norm = v / vmax;
+  int lo = 0, len = P.nlevels;
+  while (len > 0) {
+    const int half = len >> 1, mid = lo + half;
+    const double lev = (P.nlevels > 1 && mid == P.nlevels - 1) ? 1.0 : (double)mid * P.step;
+    if (lev < norm) {
+      lo = mid + 1;
+      len -= half + 1;
+    } else {
+      len = half;
+    }
+  }
+  return lo;
+}
+
+__device__ __forceinline__ double clean(double v) {  // ImgMeasures._replace_nan
+  return (v == 0.0 || isnan(v) || isinf(v)) ? 0.0 : v;
+}
+
+__device__ __forceinline__ uint32_t uf_load(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ uint32_t uf_find(uint32_t* par, uint32_t x) {
+  while (true) {
+    const uint32_t p = uf_load(&par[x]);
+    if (p == x) return x;
+    const uint32_t g = uf_load(&par[p]);
+    if (g != p) __hip_atomic_store(&par[x], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    x = g;
+  }
+}
+
+// returns true if a and b were in different trees (one successful link)
+__device__ __forceinline__ bool uf_unite(uint32_t* par, uint32_t a, uint32_t b) {
+  while (true) {
+    a = uf_find(par, a);
+    b = uf_find(par, b);
+    if (a == b) return false;
+    if (a < b) {
+      const uint32_t t = a;
+      a = b;
+      b = t;
+    }
+    const uint32_t old = atomicCAS(&par[a], a, b);
+    if (old == a) return true;
+  }
+}
+
+// level index via the closed form of np.linspace(0, 1, n): lev_i = i*step (i < n-1), lev_{n-1} = 1.0;
+// L = #{i : lev_i < norm}; the estimate is corrected with exact comparisons so it equals the loop.
+__device__ __forceinline__ int level_fast(double v, double vmax, const Params& P) {
+  const double norm = v / vmax;
+  const int n = P.nlevels;
+  if (n == 1) return (0.0 < norm) ? 1 : 0;
+  if (!(norm > 0.0)) return 0;
+  int j = (int)(norm * (double)(n - 1));  // candidate count of i*step < norm among i < n-1
+  j = j < 0 ? 0 : (j > n - 1 ? n - 1 : j);
+  while (j > 0 && !((double)(j - 1) * P.step < norm)) --j;
+  while (j < n - 1 && (double)j * P.step < norm) ++j;
+  return j + ((1.0 < norm) ? 1 : 0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Ion descriptors: one 256-B record per position of the processing order (ion_desc_kernel), so that a
+// workgroup reaches an ion's windows with one coalesced read instead of the ion_order -> ion_off -> lo/hi
+// chain.  The tail windows 1..K-1 form one stream of 64-point groups, each window padded to whole groups,
+// so that every group (one wave's share of a chunk slot) lies in a single window.
+// ---------------------------------------------------------------------------------------------
+struct IonDesc {
+  int64_t base[MAXK];  // [0]: lo of the principal window; [k>=1]: lo[k] - 64*gs[k] (padded tail position -> hit)
+  int32_t end[MAXK];   // [0]: principal points; [k>=1]: 64*gs[k] + n[k] (end of window k in the padded tail)
+  int32_t gs[MAXK];    // [k>=1]: first group of window k; INT_MAX for k >= K
+  double theor[MAXK];  // theoretical intensities
+  double sy[MAXK];     // window sums of intensities (prefix-sum differences, smg_hit_prefix_sums)
+  double syy[MAXK];    // window sums of squared intensities over points without the duplicate flag
+  int32_t ion, K, ngroups, hits;  // ngroups < 0: tail too long for 32-bit positions (dense path)
+  int32_t pad[12];
+};
+static_assert(sizeof(IonDesc) == 384, "IonDesc is 384 B");
+constexpr int DESC_QWORDS = (int)(sizeof(IonDesc) / 8);  // 48: one 8-byte load per lane of wave 0
+
+// Work sources of the persistent LDS kernel.
+//  SRC_RANGES: positions [0, n) split into 8 contiguous ranges, one per XCD (workgroup w runs on XCD w % 8),
+//    so concurrently scored ions of one XCD are m/z neighbours and share windows in that XCD's L2; a
+//    workgroup whose range is exhausted steals from the other ranges.
+//  SRC_LIST: a device list of positions (the rejects of the previous pass) with a global cursor.
+enum { SRC_RANGES = 0, SRC_LIST = 1 };
+#ifndef SMG_XCDS
+#define SMG_XCDS 8  // diagnostic: 1 = one global range (no XCD locality)
+#endif
+constexpr int XCDS = SMG_XCDS;
+#ifndef SMG_SCREEN2P
+#define SMG_SCREEN2P 1  // chaos screen in two passes (pre-filtered survivors, then the full screen over them)
+#endif
+#ifndef SMG_NOB3
+#define SMG_NOB3 1      // no barrier after the duplicate-table reduce when the two-pass screen follows
+#endif
+constexpr int CTR_STRIDE = 32;  // u32 words between counters (one 128-B line each)
+
+struct Sched {
+  int64_t n;              // SRC_RANGES: positions
+  uint32_t* ctr;          // SRC_RANGES: XCDS counters; SRC_LIST: cursor
+  const uint32_t* list;   // SRC_LIST
+  const uint32_t* count;  // SRC_LIST
+};
+
+template <int SRC>
+__device__ __forceinline__ uint32_t sched_issue(const Sched& S) {
+  if constexpr (SRC == SRC_RANGES) return atomicAdd(&S.ctr[(blockIdx.x % XCDS) * CTR_STRIDE], 1u);
+  else return atomicAdd(S.ctr, 1u);
+}
+// the same ticket, asynchronously (see atomic_add_rtn_async); valid after the counted wait
+template <int SRC>
+__device__ __forceinline__ void sched_issue_async(const Sched& S, uint32_t& t) {
+  if constexpr (SRC == SRC_RANGES) atomic_add_rtn_async(t, &S.ctr[(blockIdx.x % XCDS) * CTR_STRIDE], 1u);
+  else atomic_add_rtn_async(t, S.ctr, 1u);
+}
+
+// resolves a ticket of sched_issue into a position (-1: no work left)
+template <int SRC>
+__device__ __forceinline__ int64_t sched_resolve(const Sched& S, uint32_t t) {
+  if constexpr (SRC == SRC_RANGES) {
+    const int home = blockIdx.x % XCDS;
+    for (int i = 0; i < XCDS; ++i) {
+      const int x = (home + i) % XCDS;
+      const int64_t a = S.n * x / XCDS, b = S.n * (x + 1) / XCDS;
+      if (i > 0) t = atomicAdd(&S.ctr[x * CTR_STRIDE], 1u);
+      if ((int64_t)t < b - a) return a + (int64_t)t;
+    }
+    return -1;
+  } else {
+    const uint32_t c = *S.count;
+    return t < c ? (int64_t)S.list[t] : -1;
+  }
+}
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+  const int lo = __builtin_amdgcn_readfirstlane((int)v), hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+  return ((int64_t)hi << 32) | (uint32_t)lo;
+}
+
+__device__ __forceinline__ bool desc_lds_ok(const IonDesc* D, int capc) {
+  const int K = D->K;
+  return K >= 1 && K <= MAXK && D->end[0] <= capc && D->ngroups >= 0;
+}
+
+// the wave-per-ion main pass (smg_wave.hip)
+size_t wave_pass_lds_bytes();
+bool wave_pass_supports(int npx);
+int launch_wave_pass(const uint64_t* hits, const IonDesc* desc, int64_t n_ions, const Params& P, uint32_t* xcd_ctr,
+                     double* oc, double* osp, double* osc, double* omsm, uint32_t* oflags, uint32_t* rej_list,
+                     uint32_t* rej_count, int cus, hipStream_t st);
+
+}  // namespace smg

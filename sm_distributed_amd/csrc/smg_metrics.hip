@@ -26,16 +26,12 @@
 #include <vector>
 
 #include "smg_common.hpp"
+#include "smg_ion.hpp"
 
 namespace smg {
 
 constexpr int BLOCK = 256;           // dense (global-scratch) kernel
 constexpr int NW = BLOCK / WAVE;
-constexpr int MAXK = 8;              // windows per ion on the LDS path
-constexpr int MAXK_DENSE = 32;       // windows per ion supported at all
-constexpr int NPX_LDS_MAX = 1 << 18; // images up to 262144 pixels use the LDS path
-
-enum { C_NE = 0, C_EMAX, C_ABORT, C_PDUP, C_NEXT, C_NS, C_NCTR = 8 };
 
 // Diagnostic build only (-DSMG_STAMPS): per-phase wall cycles of the LDS kernel, summed over workgroups
 // into a buffer of their own (read back by smg_debug_stamps); the shipped build executes no stamp.
@@ -70,141 +66,7 @@ __device__ unsigned long long g_stamps[16];
 #define STAMP_FLUSH()
 #endif
 
-struct Params {
-  int32_t nrows, ncols, npx;
-  int32_t nlevels;
-  int32_t connectivity;
-  int32_t erosion_border;
-  double step;      // np.linspace(0, 1, nlevels) step
-  float inv_ncols;  // 1/ncols for the LDS path's row/column split (npx < 2^24)
-  int32_t w32;      // LDS path: bitmap words (Lay::w32)
-  uint32_t o_pf;    // LDS path: byte offset of the rank prefix (Lay::o_pf)
-  double q;         // hot-spot clip percentile (dense path, when clip != 0)
-  int32_t clip;     // image_generation.do_preprocessing
-};
 
-// row and column of pixel p < 2^24 from a float reciprocal: the estimate is off by at most one row
-__device__ __forceinline__ void rowcol(int p, const Params& P, int& r, int& c) {
-  r = (int)((float)p * P.inv_ncols);
-  c = p - r * P.ncols;
-  if (c < 0) {
-    --r;
-    c += P.ncols;
-  } else if (c >= P.ncols) {
-    ++r;
-    c -= P.ncols;
-  }
-}
-
-template <int FMT>
-struct Hits;
-
-template <>
-struct Hits<SMG_HITS_PACKED_F32> {
-  const uint64_t* h;
-  const double* unused;
-  using Reg = uint64_t;
-  __device__ __forceinline__ Reg load(int64_t i) const { return h[i]; }
-  // scalar base + 32-bit lane offset (saddr addressing)
-  __device__ __forceinline__ Reg load(int64_t base, int i) const { return (h + base)[i]; }
-  static __device__ __forceinline__ uint32_t pix(Reg r) { return (uint32_t)r & 0x7FFFFFFFu; }
-  static __device__ __forceinline__ bool dup(Reg r) { return ((uint32_t)r >> 31) != 0u; }
-  static __device__ __forceinline__ double val(Reg r) { return (double)__uint_as_float((uint32_t)(r >> 32)); }
-  static __device__ __forceinline__ Reg zero() { return 0ull; }  // pixel 0, value 0, no flag
-  __device__ __forceinline__ void get(int64_t i, uint32_t& p, double& v) const {
-    const uint64_t x = h[i];
-    p = (uint32_t)x & 0x7FFFFFFFu;
-    v = (double)__uint_as_float((uint32_t)(x >> 32));
-  }
-};
-
-struct PixVal {
-  uint32_t p;
-  double v;
-};
-
-// Asynchronous 8-byte loads for the software pipeline of the LDS kernel.  The compiler's wait-count pass
-// serialises any use of a register loaded before a loop or a branch behind s_waitcnt vmcnt(0), i.e. behind
-// every load issued since, which would expose the latency of each prefetched chunk; these loads are
-// invisible to it and are waited for with counted waits (vm_wait<N>: all but the N youngest vector-memory
-// operations of this wave done).  Vector-memory operations complete in issue order, so operations the
-// compiler issues in between only make a counted wait stricter.  The destination registers are neither
-// read nor copied between issue and wait (the wait takes them as in/out operands).
-// The destination is an in/out operand: its previous value counts as used by the next load into it, so
-// a register with a load in flight is never reallocated to another value, even when that load's data end
-// up unused (a refill past the tail, or an ion that is handed to another pass).
-__device__ __forceinline__ void ld8_async(uint64_t& r, const void* sbase, uint32_t voff) {
-  asm volatile("global_load_dwordx2 %0, %1, %2" : "+v"(r) : "v"(voff), "s"(sbase) : "memory");
-}
-__device__ __forceinline__ void ld8_async_v(uint64_t& r, const void* addr) {  // 64-bit vector address
-  asm volatile("global_load_dwordx2 %0, %1, off" : "+v"(r) : "v"(addr) : "memory");
-}
-__device__ __forceinline__ void ld4_async_v(uint32_t& r, const void* addr) {
-  asm volatile("global_load_dword %0, %1, off" : "+v"(r) : "v"(addr) : "memory");
-}
-template <int N>
-__device__ __forceinline__ void vm_wait1(uint64_t& r) {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-  asm volatile("" : "+v"(r));
-}
-template <int N>
-__device__ __forceinline__ void vm_wait1(uint32_t& r) {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-  asm volatile("" : "+v"(r));
-}
-// Returning atomic add issued like the async loads: the compiler would wait for its result with
-// s_waitcnt vmcnt(0) right away -- i.e. for every prefetch load of the wave in flight -- so it is waited
-// for with a counted vm_wait1 where the ticket is consumed.
-__device__ __forceinline__ void atomic_add_rtn_async(uint32_t& r, uint32_t* addr, uint32_t v) {
-  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "+v"(r) : "v"(addr), "v"(v) : "memory");
-}
-template <int N, int M>
-__device__ __forceinline__ void vm_wait(uint64_t (&r)[M]) {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-#pragma unroll
-  for (int j = 0; j < M; ++j) asm volatile("" : "+v"(r[j]));
-}
-template <int N, int M>
-__device__ __forceinline__ void vm_wait(PixVal (&)[M]) {}  // split-format hits use compiler-tracked loads
-
-template <>
-struct Hits<SMG_HITS_SPLIT_F64> {
-  const uint32_t* pa;
-  const double* va;
-  using Reg = PixVal;
-  __device__ __forceinline__ Reg load(int64_t i) const { return PixVal{pa[i], va[i]}; }
-  __device__ __forceinline__ Reg load(int64_t base, int i) const { return PixVal{(pa + base)[i], (va + base)[i]}; }
-  static __device__ __forceinline__ uint32_t pix(Reg r) { return r.p & 0x7FFFFFFFu; }
-  static __device__ __forceinline__ bool dup(Reg r) { return (r.p >> 31) != 0u; }
-  static __device__ __forceinline__ double val(Reg r) { return r.v; }
-  static __device__ __forceinline__ Reg zero() { return PixVal{0u, 0.0}; }
-  __device__ __forceinline__ void get(int64_t i, uint32_t& p, double& v) const {
-    p = pa[i] & 0x7FFFFFFFu;
-    v = va[i];
-  }
-};
-
-// level index L = #{i : linspace(0,1,n)[i] < v/vmax}  (measure_of_chaos: bw = im_clean > level)
-// The levels are nondecreasing in i, so L is the lower bound of norm among them (binary search).
-__device__ __forceinline__ int level_of(double v, double vmax, const Params& P) {
-  const double norm = v / vmax;
-  int lo = 0, len = P.nlevels;
-  while (len > 0) {
-    const int half = len >> 1, mid = lo + half;
-    const double lev = (P.nlevels > 1 && mid == P.nlevels - 1) ? 1.0 : (double)mid * P.step;
-    if (lev < norm) {
-      lo = mid + 1;
-      len -= half + 1;
-    } else {
-      len = half;
-    }
-  }
-  return lo;
-}
-
-__device__ __forceinline__ double clean(double v) {  // ImgMeasures._replace_nan
-  return (v == 0.0 || isnan(v) || isinf(v)) ? 0.0 : v;
-}
 
 // formula_img_validator.py:78-84 + the restated pyImagingMSpec functions; writes the outputs.
 __device__ void finalize_ion(int K, const double* __restrict__ t, const double* s, double sx, double sxx,
@@ -330,35 +192,6 @@ __device__ __forceinline__ uint32_t bits7(const uint32_t* bm, int row, int c0, u
   return rv ? v : 0u;
 }
 
-__device__ __forceinline__ uint32_t uf_load(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-__device__ __forceinline__ uint32_t uf_find(uint32_t* par, uint32_t x) {
-  while (true) {
-    const uint32_t p = uf_load(&par[x]);
-    if (p == x) return x;
-    const uint32_t g = uf_load(&par[p]);
-    if (g != p) __hip_atomic_store(&par[x], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    x = g;
-  }
-}
-
-// returns true if a and b were in different trees (one successful link)
-__device__ __forceinline__ bool uf_unite(uint32_t* par, uint32_t a, uint32_t b) {
-  while (true) {
-    a = uf_find(par, a);
-    b = uf_find(par, b);
-    if (a == b) return false;
-    if (a < b) {
-      const uint32_t t = a;
-      a = b;
-      b = t;
-    }
-    const uint32_t old = atomicCAS(&par[a], a, b);
-    if (old == a) return true;
-  }
-}
 
 // LDS carve of the persistent kernel.  Everything but the pixel bitmap and its rank prefix has a
 // compile-time offset (immediate ds_* offsets, no offset SGPRs); the bitmap (npx bits, a zero guard word in
@@ -428,38 +261,6 @@ __device__ __forceinline__ bool tbl_add(uint32_t* keys, double* vals, uint32_t k
   return false;
 }
 
-// level index via the closed form of np.linspace(0, 1, n): lev_i = i*step (i < n-1), lev_{n-1} = 1.0;
-// L = #{i : lev_i < norm}; the estimate is corrected with exact comparisons so it equals the loop.
-__device__ __forceinline__ int level_fast(double v, double vmax, const Params& P) {
-  const double norm = v / vmax;
-  const int n = P.nlevels;
-  if (n == 1) return (0.0 < norm) ? 1 : 0;
-  if (!(norm > 0.0)) return 0;
-  int j = (int)(norm * (double)(n - 1));  // candidate count of i*step < norm among i < n-1
-  j = j < 0 ? 0 : (j > n - 1 ? n - 1 : j);
-  while (j > 0 && !((double)(j - 1) * P.step < norm)) --j;
-  while (j < n - 1 && (double)j * P.step < norm) ++j;
-  return j + ((1.0 < norm) ? 1 : 0);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Ion descriptors: one 256-B record per position of the processing order (ion_desc_kernel), so that a
-// workgroup reaches an ion's windows with one coalesced read instead of the ion_order -> ion_off -> lo/hi
-// chain.  The tail windows 1..K-1 form one stream of 64-point groups, each window padded to whole groups,
-// so that every group (one wave's share of a chunk slot) lies in a single window.
-// ---------------------------------------------------------------------------------------------
-struct IonDesc {
-  int64_t base[MAXK];  // [0]: lo of the principal window; [k>=1]: lo[k] - 64*gs[k] (padded tail position -> hit)
-  int32_t end[MAXK];   // [0]: principal points; [k>=1]: 64*gs[k] + n[k] (end of window k in the padded tail)
-  int32_t gs[MAXK];    // [k>=1]: first group of window k; INT_MAX for k >= K
-  double theor[MAXK];  // theoretical intensities
-  double sy[MAXK];     // window sums of intensities (prefix-sum differences, smg_hit_prefix_sums)
-  double syy[MAXK];    // window sums of squared intensities over points without the duplicate flag
-  int32_t ion, K, ngroups, hits;  // ngroups < 0: tail too long for 32-bit positions (dense path)
-  int32_t pad[12];
-};
-static_assert(sizeof(IonDesc) == 384, "IonDesc is 384 B");
-constexpr int DESC_QWORDS = (int)(sizeof(IonDesc) / 8);  // 48: one 8-byte load per lane of wave 0
 
 // (sum v, sum v^2 of unflagged points) over the points [i & ~63, i) of hit i's 64-point block
 template <int FMT>
@@ -637,71 +438,6 @@ __global__ void ion_desc8_kernel(Hits<FMT> hits, const int64_t* __restrict__ lo,
   }
 }
 
-// Work sources of the persistent LDS kernel.
-//  SRC_RANGES: positions [0, n) split into 8 contiguous ranges, one per XCD (workgroup w runs on XCD w % 8),
-//    so concurrently scored ions of one XCD are m/z neighbours and share windows in that XCD's L2; a
-//    workgroup whose range is exhausted steals from the other ranges.
-//  SRC_LIST: a device list of positions (the rejects of the previous pass) with a global cursor.
-enum { SRC_RANGES = 0, SRC_LIST = 1 };
-#ifndef SMG_XCDS
-#define SMG_XCDS 8  // diagnostic: 1 = one global range (no XCD locality)
-#endif
-constexpr int XCDS = SMG_XCDS;
-#ifndef SMG_SCREEN2P
-#define SMG_SCREEN2P 1  // chaos screen in two passes (pre-filtered survivors, then the full screen over them)
-#endif
-#ifndef SMG_NOB3
-#define SMG_NOB3 1      // no barrier after the duplicate-table reduce when the two-pass screen follows
-#endif
-constexpr int CTR_STRIDE = 32;  // u32 words between counters (one 128-B line each)
-
-struct Sched {
-  int64_t n;              // SRC_RANGES: positions
-  uint32_t* ctr;          // SRC_RANGES: XCDS counters; SRC_LIST: cursor
-  const uint32_t* list;   // SRC_LIST
-  const uint32_t* count;  // SRC_LIST
-};
-
-template <int SRC>
-__device__ __forceinline__ uint32_t sched_issue(const Sched& S) {
-  if constexpr (SRC == SRC_RANGES) return atomicAdd(&S.ctr[(blockIdx.x % XCDS) * CTR_STRIDE], 1u);
-  else return atomicAdd(S.ctr, 1u);
-}
-// the same ticket, asynchronously (see atomic_add_rtn_async); valid after the counted wait
-template <int SRC>
-__device__ __forceinline__ void sched_issue_async(const Sched& S, uint32_t& t) {
-  if constexpr (SRC == SRC_RANGES) atomic_add_rtn_async(t, &S.ctr[(blockIdx.x % XCDS) * CTR_STRIDE], 1u);
-  else atomic_add_rtn_async(t, S.ctr, 1u);
-}
-
-// resolves a ticket of sched_issue into a position (-1: no work left)
-template <int SRC>
-__device__ __forceinline__ int64_t sched_resolve(const Sched& S, uint32_t t) {
-  if constexpr (SRC == SRC_RANGES) {
-    const int home = blockIdx.x % XCDS;
-    for (int i = 0; i < XCDS; ++i) {
-      const int x = (home + i) % XCDS;
-      const int64_t a = S.n * x / XCDS, b = S.n * (x + 1) / XCDS;
-      if (i > 0) t = atomicAdd(&S.ctr[x * CTR_STRIDE], 1u);
-      if ((int64_t)t < b - a) return a + (int64_t)t;
-    }
-    return -1;
-  } else {
-    const uint32_t c = *S.count;
-    return t < c ? (int64_t)S.list[t] : -1;
-  }
-}
-
-__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ int64_t uni64(int64_t v) {
-  const int lo = __builtin_amdgcn_readfirstlane((int)v), hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
-  return ((int64_t)hi << 32) | (uint32_t)lo;
-}
-
-__device__ __forceinline__ bool desc_lds_ok(const IonDesc* D, int capc) {
-  const int K = D->K;
-  return K >= 1 && K <= MAXK && D->end[0] <= capc && D->ngroups >= 0;
-}
 
 // ---------------------------------------------------------------------------------------------
 // LDS path: persistent, software-pipelined kernel.  Each workgroup scores a sequence of ions.  Iteration b
@@ -2571,6 +2307,23 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
 // candidates get their own bitmap + ranks for Kruskal (the principal bitmap is no longer needed by then).  Nothing
 // is pixel-indexed in global memory, so nothing has to be zeroed per slot; an ion whose flagged tail pixels
 // overflow the table is handed to the pixel-indexed kernel.
+//
+// Diagnostic build only (-DSMG_WIDE_CHECK): index checks on the wide pass's global and table accesses; a failed
+// check records (code, value) of its first occurrence and a count (smg_debug_wide_check) and the access is
+// clamped, so a bad index is reported instead of faulting.  The shipped build compiles the plain expressions.
+#ifdef SMG_WIDE_CHECK
+__device__ unsigned long long g_wchk[4];  // [0] first code, [1] its value, [2] failures, [3] ions seen
+__device__ __forceinline__ bool wchk(bool ok, int code, long long v) {
+  if (!ok && atomicAdd(&g_wchk[2], 1ull) == 0ull) {
+    g_wchk[0] = (unsigned long long)code;
+    g_wchk[1] = (unsigned long long)v;
+  }
+  return ok;
+}
+#define WCK(ok, code, v) wchk((ok), (code), (long long)(v))
+#else
+#define WCK(ok, code, v) true
+#endif
 constexpr int WIDE_HT_LOG2 = 13;
 constexpr int WIDE_HT = 1 << WIDE_HT_LOG2;  // tail duplicate table entries per slot
 constexpr int WIDE_PROBES = 64;
@@ -2782,6 +2535,13 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     __syncthreads();
     const int64_t ion = sh_ion;
     if (ion < 0) break;
+#ifdef SMG_WIDE_CHECK
+    if (tid == 0) atomicAdd(&g_wchk[3], 1ull);
+    if (!WCK(ion < (int64_t)total, 1, ion)) {
+      __syncthreads();
+      continue;
+    }
+#endif
     const int64_t w0 = ion_off[ion];
     const int K = (int)(ion_off[ion + 1] - w0);
     uint32_t flags = SMG_ION_DENSE | SMG_ION_WIDE;
@@ -2800,7 +2560,9 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     // principal image: presence bits, ranks, then values and pixels at their ranks
     for (int w = tid; w < n64p; w += DBLOCK) bm[w] = 0ull;
     __syncthreads();
-    const int64_t a0 = lo[w0], b0 = hi[w0];
+    const int64_t a0 = lo[w0];
+    int64_t b0 = hi[w0];
+    if (!WCK(a0 >= 0 && a0 <= b0 && b0 < (1ll << 36), 3, b0 - a0)) b0 = a0;
     for (int64_t i0 = a0; i0 < b0; i0 += (int64_t)DBLOCK * WDU) {
       typename H::Reg r[WDU];
 #pragma unroll
@@ -2813,7 +2575,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
         const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
         bool dup_own = false;
         uint32_t p = 0u;
-        if (i < b0) {
+        if (i < b0 && WCK(H::pix(r[u]) < (uint32_t)npx, 4, H::pix(r[u]))) {
           p = H::pix(r[u]);
           const uint32_t bit = 1u << (p & 31);
           // a flagged point that sets its pixel's bit lists the pixel: one entry per pixel with duplicates
@@ -2850,9 +2612,10 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
 #pragma unroll
       for (int u = 0; u < WDU; ++u) {
         const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
-        if (i < b0) {
+        if (i < b0 && WCK(H::pix(r[u]) < (uint32_t)npx, 4, H::pix(r[u]))) {
           const uint32_t p = H::pix(r[u]);
-          const uint32_t k = R.rank(p);
+          uint32_t k = R.rank(p);
+          if (!WCK(k < (uint32_t)np, 5, k)) k = 0;
           const double v = H::val(r[u]);
           if (H::dup(r[u])) {
             atomicAdd(&S.vals[k], v);
@@ -2932,7 +2695,10 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     if (tid < 4 * MAXK_DENSE) kst[tid] = 0.0;
     if (tid <= K - 1) {
       int64_t n = 0;
-      for (int k = 1; k <= tid; ++k) n += (hi[w0 + k] - lo[w0 + k] + TSTEP - 1) / TSTEP * TSTEP;
+      for (int k = 1; k <= tid; ++k) {
+        WCK(hi[w0 + k] >= lo[w0 + k] && lo[w0 + k] >= 0, 6, hi[w0 + k] - lo[w0 + k]);
+        n += (hi[w0 + k] - lo[w0 + k] + TSTEP - 1) / TSTEP * TSTEP;
+      }
       sh_tb[tid] = n;  // sh_tb[k - 1]: stream offset of window k (padded lengths before it)
       if (tid < K - 1) {
         sh_tlo[tid] = lo[w0 + 1 + tid];
@@ -3011,11 +2777,19 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
         auto issue = [&](int64_t v0, uint64_t (&r)[TDU]) -> int {
           while (v0 >= sh_tb[ki + 1]) ++ki;
           ki = __builtin_amdgcn_readfirstlane(ki);
+#ifdef SMG_WIDE_CHECK
+          if (!WCK(ki <= K - 2, 7, ki)) ki = 0;
+#endif
           const int64_t off = v0 - sh_tb[ki], n = sh_tn[ki], a = sh_tlo[ki];
 #pragma unroll
           for (int u = 0; u < TDU; ++u) {
             const int64_t lv = off + (int64_t)u * DBLOCK + tid;
+#ifdef SMG_WIDE_CHECK
+            const int64_t ix = a + (lv < n ? lv : n - 1);
+            ld8_async_nm(r[u], hb + (WCK(ix >= 0 && ix < (1ll << 36), 8, ix) ? ix : 0));
+#else
             ld8_async_nm(r[u], hb + a + (lv < n ? lv : n - 1));
+#endif
           }
           return ki;
         };
@@ -3030,7 +2804,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
           uint32_t flm = 0u;
 #pragma unroll
           for (int u = 0; u < TDU; ++u) {
-            const bool valid = off + (int64_t)u * DBLOCK + tid < n;
+            const bool valid = off + (int64_t)u * DBLOCK + tid < n && WCK(H::pix(r[u]) < (uint32_t)npx, 9, H::pix(r[u]));
             const uint32_t p = H::pix(r[u]);
             const bool pr = valid && R.test(p);
             const bool s0 = pr && nev == 0, s1 = pr && nev == 1;
@@ -3045,7 +2819,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
           if (__ballot((flm >> 16) != 0u)) {  // rare: a lane's third and later hits gather in place
 #pragma unroll
             for (int u = 0; u < TDU; ++u)
-              if ((flm >> (16 + u)) & 1u) {
+              if ((flm >> (16 + u)) & 1u && WCK(R.rank(H::pix(r[u])) < (uint32_t)np, 11, R.rank(H::pix(r[u])))) {
                 const double xv = ld_agent(&S.vals[R.rank(H::pix(r[u]))]);
                 const double y = H::val(r[u]);
                 atomicAdd(&kst[3 * MAXK_DENSE + kb + 1], xv * y);
@@ -3064,8 +2838,15 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
         // the parked principal hits: ranks, both x gathers in flight together, then the window partials
         if (__ballot(nev > 0)) {
           const uint32_t p0 = H::pix(ev0), p1 = H::pix(ev1);
+#ifdef SMG_WIDE_CHECK
+          const uint32_t k0 = nev > 0 && WCK(R.rank(p0) < (uint32_t)np, 10, R.rank(p0)) ? R.rank(p0) : 0u;
+          const uint32_t k1 = nev > 1 && WCK(R.rank(p1) < (uint32_t)np, 10, R.rank(p1)) ? R.rank(p1) : 0u;
+          const double x0 = nev > 0 ? ld_agent(&S.vals[k0]) : 0.0;
+          const double x1 = nev > 1 ? ld_agent(&S.vals[k1]) : 0.0;
+#else
           const double x0 = nev > 0 ? ld_agent(&S.vals[R.rank(p0)]) : 0.0;
           const double x1 = nev > 1 ? ld_agent(&S.vals[R.rank(p1)]) : 0.0;
+#endif
           if (nev > 0) {
             const double y = H::val(ev0);
             atomicAdd(&kst[3 * MAXK_DENSE + evk0 + 1], x0 * y);
@@ -3161,7 +2942,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
         slot_sync();  // the tables' sums are complete (LDS; L2 for the global entries)
         for (int i = tid; i < WIDE_LT; i += DBLOCK) {  // LDS entries: add their pixel's (Σy)², then release them
           const uint32_t key = ltkey[i];
-          if (key != WIDE_EMPTY) {
+          if (key != WIDE_EMPTY && WCK(key / (uint32_t)npx + 1 < (uint32_t)MAXK_DENSE, 12, key)) {
             const double y = ltval[i];
             atomicAdd(&kst[2 * MAXK_DENSE + key / (uint32_t)npx + 1], y * y);
             ltkey[i] = WIDE_EMPTY;
@@ -3174,7 +2955,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
           const uint32_t key = ld_agent(&S.hkey[s]);
           const double y = ld_agent(&S.hval[s]);
           const uint32_t k = key / (uint32_t)npx;
-          atomicAdd(&kst[2 * MAXK_DENSE + k + 1], y * y);
+          if (WCK(k + 1 < (uint32_t)MAXK_DENSE, 12, key)) atomicAdd(&kst[2 * MAXK_DENSE + k + 1], y * y);
           S.hkey[s] = WIDE_EMPTY;
           S.hval[s] = 0.0;
         }
@@ -3264,14 +3045,18 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
           const int qr = (t == 1) ? -1 : (t == 2) ? 1 : 0, qc = (t == 3) ? -1 : (t == 4) ? 1 : 0;
           const uint32_t q = (uint32_t)((r0 + qr) * nc + c0 + qc);
           if (idx < LCAND) lcand[idx] = q;
-          else S.epr[idx] = q;
+          else if (WCK(idx < npx, 13, idx)) S.epr[idx] = q;
           ++idx;
           cm &= cm - 1u;
         }
       }
       slot_sync();
       STAMP(9);
+#ifdef SMG_WIDE_CHECK
+      const int nscr = WCK(sh_ncand <= npx, 14, sh_ncand) ? sh_ncand : 0;
+#else
       const int nscr = sh_ncand;
+#endif
       if (nscr > 0) {  // level index per principal pixel, needed only around screened candidates
         for (int r0 = tid; r0 < np; r0 += DBLOCK * WDU) {
           uint64_t vb[WDU];
@@ -3303,7 +3088,8 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
             uint64_t wv = 0ull;
             if (row != 0u) {
               // the row's present pixels have consecutive ranks: their levels are L[base .. base + popc(row))
-              const uint32_t rb = R.rank((uint32_t)((r0 + dr) * nc + max(c0 - 3, 0)));
+              uint32_t rb = R.rank((uint32_t)((r0 + dr) * nc + max(c0 - 3, 0)));
+              if (!WCK(rb <= (uint32_t)np, 16, rb)) rb = 0;
               const uint64_t* la = reinterpret_cast<const uint64_t*>(S.L + (rb & ~7u));
               const uint64_t l0 = la[0], l1 = la[1];
               const uint32_t sh = (rb & 7u) * 8u;
@@ -3344,7 +3130,11 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
       slot_sync();
       // the staged candidates are consumed: the LDS table is empty again for the next ion's tail stream
       for (int i = tid; i < min(nscr, LCAND); i += DBLOCK) lcand[i] = i < WIDE_LT ? WIDE_EMPTY : 0u;
+#ifdef SMG_WIDE_CHECK
+      const int m = WCK(sh_ctr[0] <= npx, 15, sh_ctr[0]) ? sh_ctr[0] : 0;
+#else
       const int m = sh_ctr[0];
+#endif
       const int emax = sh_ctr[1];
       STAMP(14);
       double esum = 0.0, wsum = 0.0;
@@ -3360,7 +3150,8 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
         build_rank(bm, pf, sb, n64, sc);
         for (int i = tid; i < m; i += DBLOCK) {
           const uint32_t q = S.epix[i];
-          const uint32_t k = R.rank(q);
+          uint32_t k = R.rank(q);
+          if (!WCK(k < (uint32_t)m && q < (uint32_t)npx, 17, k)) k = 0;
           S.epr[k] = q;
           S.eLr[k] = S.eL[i];
           S.par[k] = k;
@@ -3460,6 +3251,7 @@ using Main2Lay = Lay2<MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX>;
 using Big2Lay = Lay2<BIG_BLOCK / WAVE, BIG_BLOCK * BIG2_RMAX>;
 static int g_force_two_level = 0;  // smg_debug_force_two_level: two-level passes for every image size
 static int g_force_dense = 0;      // smg_debug_force_dense: 1 every ion on the dense path, 2 pixel-indexed only
+static int g_main_legacy = 1;      // smg_debug_main_kernel: 1 = the 512-thread LDS kernel as the main pass (default until the wave pass is validated)
 // smg_debug_time_main_pass: HIP events recorded on the launch stream around every pass launch of
 // smg_ion_metrics (descriptors, main LDS pass, big-ion pass, wide pass, pixel-indexed pass), so a benchmark
 // measures each kernel itself and prices each pass's own window points against its own time
@@ -3548,7 +3340,20 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
                          hi, ion_off, theor, reinterpret_cast<const DD4*>(hit_cum), ion_order, n_ions, desc);
     SMG_LAUNCH_CHECK();
   }
-  if (main_ok) {
+  // main pass: one wave per ion (smg_wave.hip) for packed hits, or the legacy 512-thread LDS kernel
+  // (smg_debug_main_kernel(1); the split-f64 hit format always)
+  bool wave = false;
+  if constexpr (FMT == SMG_HITS_PACKED_F32) {
+    wave = main_ok && !two && !g_main_legacy && wave_pass_supports(P.npx);
+    if (wave) {
+      PassTimer tm(SMG_PASS_MAIN, st);
+      const int rc = launch_wave_pass(hits.h, desc, n_ions, P, hdr + HDR_XCD, oc, osp, osc, omsm, oflags, list_a,
+                                      hdr + 0, cus, st);
+      if (rc != SMG_OK) return rc;
+    }
+  }
+  if (wave) {
+  } else if (main_ok) {
     Sched SA{n_ions, hdr + HDR_XCD, nullptr, nullptr};
     auto k1 = two ? &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, true>
                   : &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, false>;
@@ -3644,6 +3449,16 @@ int smg_debug_stamps(unsigned long long* host_out, int n) {
 #endif
 }
 
+#ifdef SMG_WIDE_CHECK
+// diagnostic build only: the wide pass's index checks (first code, its value, failures, ions seen); resets them
+int smg_debug_wide_check(unsigned long long* host_out) {
+  SMG_HIP(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wchk), sizeof(unsigned long long) * 4));
+  unsigned long long z[4] = {0, 0, 0, 0};
+  SMG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wchk), z, sizeof(z)));
+  return SMG_OK;
+}
+#endif
+
 int smg_debug_force_two_level(int32_t on) {
   g_force_two_level = on ? 1 : 0;
   return SMG_OK;
@@ -3689,6 +3504,11 @@ int smg_debug_main_pass_times(double* ms, int32_t cap, int32_t* n) {
 int smg_debug_pass_times(int32_t* pass, double* ms, int32_t cap, int32_t* n) {
   SMG_CHECK_ARG(n != nullptr && ((ms != nullptr && pass != nullptr) || cap == 0), "bad arguments");
   return drain_pass_times(-1, pass, ms, cap, n);
+}
+
+int smg_debug_main_kernel(int32_t which) {
+  g_main_legacy = which == 0 ? 0 : 1;
+  return SMG_OK;
 }
 
 int smg_debug_force_dense(int32_t on) {
