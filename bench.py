@@ -391,7 +391,7 @@ def pass_roofline(args, pass_ms, chain, is_single):
         return None, passes
     dom = max(scoring, key=lambda d: d["ms_avg"])
     name = _lib.PASS_NAMES[dom["pass"]]
-    key = {1: "ion_wave_kernel", 2: "ion_pipe_kernel[1024]", 3: "ion_wide_kernel", 4: "ion_dense_kernel"}
+    key = {1: "ion_pipe_kernel[512]", 2: "ion_pipe_kernel[1024]", 3: "ion_wide_kernel", 4: "ion_dense_kernel"}
     traffic, src = measured_traffic(key[dom["pass"]], "config5" if args.config == "5" else "config3") \
         if is_single else (None, None)
     roofline = {"bound": "hbm", "kernel": name, "achieved": dom["achieved_GBps"], "peak": HBM_PEAK_GBS,

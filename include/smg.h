@@ -191,8 +191,8 @@ int smg_debug_force_two_level(int32_t on);
  * ion to the pixel-indexed slot kernel; so that the parity suite covers both on every case.  Process-wide;
  * returns 0. */
 int smg_debug_force_dense(int32_t on);
-/* main pass kernel: 0 = one wave per ion (ion_wave_kernel, the default for packed hits), 1 = the 512-thread LDS
- * kernel (ion_pipe_kernel<512>; A/B and parity of the two) */
+/* main pass kernel: 1 = the 512-thread LDS kernel (ion_pipe_kernel<512>, the default), 0 = one wave per ion
+ * (ion_wave_kernel, packed hits only; experimental, slower: DESIGN.md §3) */
 int smg_debug_main_kernel(int32_t which);
 
 /* passes of smg_ion_metrics, as reported by smg_debug_pass_times */

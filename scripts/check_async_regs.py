@@ -35,7 +35,8 @@ for st in [i for i, l in enumerate(src) if l.startswith(kern)]:
         elif l.startswith(";;#ASMEND"):
             f = False
         in_asm[i] = f
-    labels = {l[:-1]: i for i, l in enumerate(body) if re.match(r"^\.LBB\w+:$", l)}
+    # labels inside loops carry a trailing comment ("; in Loop: Header=..."): match the name only
+    labels = {m.group(1): i for i, l in enumerate(body) for m in [re.match(r"^(\.LBB\w+):", l)] if m}
     dsts = set()
     for i, l in enumerate(body):
         # async loads and the async returning atomic (scheduling ticket): both write their first operand later
@@ -52,7 +53,7 @@ for st in [i for i, l in enumerate(src) if l.startswith(kern)]:
                 t = body[j]
                 if (in_asm[j] and t.startswith("s_waitcnt")) or (t.startswith("s_waitcnt") and "vmcnt(0)" in t):
                     break
-                if not t or t.startswith((".", ";")) or t.endswith(":"):
+                if not t or t.startswith((".", ";")) or t.endswith(":") or re.match(r"^\.LBB\w+:", t):
                     j += 1
                     continue
                 toks = [x.strip(",") for x in t.split()]

@@ -26,7 +26,13 @@ for which in (1, 0):
     m, lo, hi = E.run_hot_path(peaks, dions, ppm, **kw)
     torch.cuda.synchronize()
     res[which] = m.to_numpy()
+    print(f"main kernel {which}: done", flush=True)
 L.smg_debug_main_kernel(0)
+if hasattr(raw, "smg_debug_wave_check"):
+    ck = (ctypes.c_ulonglong * 8)()
+    assert raw.smg_debug_wave_check(ck) == 0
+    print(f"wave checks: first failed code {ck[0]} value {ck[1]} (as signed {ctypes.c_longlong(ck[1]).value}) "
+          f"at position {ck[3]}; failures {ck[2]}; ions scored {ck[4]}", flush=True)
 tr = (ctypes.c_longlong * (8192 * 8))()
 assert raw.smg_debug_wave_trace(tr, 8192) == 0
 tr = np.frombuffer(tr, dtype=np.int64).reshape(8192, 8)

@@ -23,7 +23,7 @@ PIXEL_MASK = 0x7FFFFFFF   # bit 31 of the pixel field = duplicate-candidate flag
 SMG_HITS_SPLIT_F64 = 1
 # pass ids of smg_debug_pass_times
 SMG_PASS_DESC, SMG_PASS_MAIN, SMG_PASS_BIG, SMG_PASS_WIDE, SMG_PASS_DENSE = range(5)
-PASS_NAMES = {0: "ion_desc8_kernel", 1: "ion_wave_kernel (main pass, one wave per ion)",
+PASS_NAMES = {0: "ion_desc8_kernel", 1: "ion_pipe_kernel<512> (main LDS pass)",
               2: "ion_pipe_kernel<1024> (big-ion LDS pass)", 3: "ion_wide_kernel (wide pass)",
               4: "ion_dense_kernel (pixel-indexed pass)"}
 

@@ -2652,9 +2652,8 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
 #pragma unroll
         for (int j = 0; j < WDU; ++j) {
           vb[j] = 0ull;
-          ld8_async_agent(vb[j], &S.vals[(r0 + j * DBLOCK < np) ? r0 + j * DBLOCK : 0]);
+          vb[j] = (uint64_t)__double_as_longlong(ld_agent(&S.vals[(r0 + j * DBLOCK < np) ? r0 + j * DBLOCK : 0]));
         }
-        vm_wait<0>(vb);
 #pragma unroll
         for (int j = 0; j < WDU; ++j) {
           if (r0 + j * DBLOCK >= np) continue;
@@ -2786,20 +2785,15 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
             const int64_t lv = off + (int64_t)u * DBLOCK + tid;
 #ifdef SMG_WIDE_CHECK
             const int64_t ix = a + (lv < n ? lv : n - 1);
-            ld8_async_nm(r[u], hb + (WCK(ix >= 0 && ix < (1ll << 36), 8, ix) ? ix : 0));
+            r[u] = hb[WCK(ix >= 0 && ix < (1ll << 36), 8, ix) ? ix : 0];
 #else
-            ld8_async_nm(r[u], hb + a + (lv < n ? lv : n - 1));
+            r[u] = hb[a + (lv < n ? lv : n - 1)];
 #endif
           }
           return ki;
         };
         auto batch = [&](int64_t v0, uint64_t (&r)[TDU], int kb, uint64_t (&rn)[TDU], int& kn) {
-          if (v0 + TSTEP < T) {
-            kn = issue(v0 + TSTEP, rn);
-            vm_wait<TDU>(r);
-          } else {
-            vm_wait<0>(r);
-          }
+          if (v0 + TSTEP < T) kn = issue(v0 + TSTEP, rn);
           const int64_t off = v0 - sh_tb[kb], n = sh_tn[kb];
           uint32_t flm = 0u;
 #pragma unroll
@@ -3063,9 +3057,8 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
 #pragma unroll
           for (int j = 0; j < WDU; ++j) {
             vb[j] = 0ull;
-            ld8_async_agent(vb[j], &S.vals[(r0 + j * DBLOCK < np) ? r0 + j * DBLOCK : 0]);
+            vb[j] = (uint64_t)__double_as_longlong(ld_agent(&S.vals[(r0 + j * DBLOCK < np) ? r0 + j * DBLOCK : 0]));
           }
-          vm_wait<0>(vb);
 #pragma unroll
           for (int j = 0; j < WDU; ++j)
             if (r0 + j * DBLOCK < np)
@@ -3251,7 +3244,7 @@ using Main2Lay = Lay2<MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX>;
 using Big2Lay = Lay2<BIG_BLOCK / WAVE, BIG_BLOCK * BIG2_RMAX>;
 static int g_force_two_level = 0;  // smg_debug_force_two_level: two-level passes for every image size
 static int g_force_dense = 0;      // smg_debug_force_dense: 1 every ion on the dense path, 2 pixel-indexed only
-static int g_main_legacy = 1;      // smg_debug_main_kernel: 1 = the 512-thread LDS kernel as the main pass (default until the wave pass is validated)
+static int g_main_legacy = 1;      // smg_debug_main_kernel: 0 = the wave-per-ion kernel as the main pass (experimental: 2.1x slower)
 // smg_debug_time_main_pass: HIP events recorded on the launch stream around every pass launch of
 // smg_ion_metrics (descriptors, main LDS pass, big-ion pass, wide pass, pixel-indexed pass), so a benchmark
 // measures each kernel itself and prices each pass's own window points against its own time
@@ -3340,8 +3333,8 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
                          hi, ion_off, theor, reinterpret_cast<const DD4*>(hit_cum), ion_order, n_ions, desc);
     SMG_LAUNCH_CHECK();
   }
-  // main pass: one wave per ion (smg_wave.hip) for packed hits, or the legacy 512-thread LDS kernel
-  // (smg_debug_main_kernel(1); the split-f64 hit format always)
+  // main pass: the 512-thread LDS kernel, or (smg_debug_main_kernel(0), packed hits only) the experimental
+  // one-wave-per-ion kernel of smg_wave.hip (correct on the parity suite but 2.1x slower at config 3)
   bool wave = false;
   if constexpr (FMT == SMG_HITS_PACKED_F32) {
     wave = main_ok && !two && !g_main_legacy && wave_pass_supports(P.npx);

@@ -26,10 +26,11 @@
 //      candidate from the levels of its 5x5 neighbourhood, Kruskal over <= 64 candidates in registers + LDS;
 //   3. tail windows 1..K-1 as one stream of 64-point groups (ion descriptors, smg_metrics.hip): every point is
 //      looked up in the directory; a principal hit (~0.5% of the points) is parked in registers and its x
-//      gathered after the stream; flagged points are listed and summed per (pixel, window) after it;
+//      gathered after the stream; flagged points are listed and summed per pixel when the stream leaves their
+//      window;
 //   4. finalize (lane k = window k).
 // Ions beyond its capacities (K > 8, principal window > CAP points, > 64 distinct duplicate pixels, > 128 flagged
-// tail points, > 64 chaos candidates) are handed to the big-ion LDS pass as positions, like the main pass's.
+// points in one tail window, > 64 chaos candidates) are handed to the big-ion LDS pass as positions, like the main pass's.
 #include "smg_common.hpp"
 #include "smg_ion.hpp"
 
@@ -93,6 +94,41 @@ __device__ __forceinline__ int rowq_pix(const RowQ& q, int t, uint32_t e, int SH
   return ((t < q.m ? q.s0 : q.s0 + 1) << SH) | (int)(e & OM);
 }
 
+// Diagnostic build only (-DSMG_WAVE_CHECK): index checks on the wave pass's global accesses and directory
+// positions; a failed check records (code, value, position) of its first occurrence and a count
+// (smg_debug_wave_check) and the access is clamped, so a bad index is reported instead of faulting.
+#ifdef SMG_WAVE_CHECK
+__device__ unsigned long long g_wvchk[8];  // [0] code, [1] value, [2] failures, [3] position, [4] ions scored
+__device__ __forceinline__ bool wvchk(bool ok, int code, long long v, long long pos) {
+  if (!ok && atomicAdd(&g_wvchk[2], 1ull) == 0ull) {
+    g_wvchk[0] = (unsigned long long)code;
+    g_wvchk[1] = (unsigned long long)v;
+    g_wvchk[3] = (unsigned long long)pos;
+  }
+  return ok;
+}
+#define WVCK(ok, code, v) wvchk((ok), (code), (long long)(v), (long long)pos)
+#define WVIX(ix, code) (WVCK((ix) >= 0 && (ix) < (1ll << 36), code, ix) ? (ix) : 0)
+#else
+#define WVCK(ok, code, v) true
+#define WVIX(ix, code) (ix)
+#endif
+
+// Diagnostic build only (-DSMG_WAVE_STAMPS): wall cycles per phase summed over waves (smg_debug_wave_stamps):
+// 0 principal image + directory, 1 chaos screen, 2 exact eL + Kruskal, 3 next descriptor / ticket, 4 tail stream,
+// 5 parked hits + flagged points, 6 issue + finalize, 7 skipped ions
+#ifdef SMG_WAVE_STAMPS
+__device__ unsigned long long g_wstamps[8];
+#define WV_STAMP(i)                                    \
+  do {                                                 \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+    wst[i] += _t - wst_t0;                             \
+    wst_t0 = _t;                                       \
+  } while (0)
+#else
+#define WV_STAMP(i)
+#endif
+
 #ifdef SMG_WAVE_TRACE
 // diagnostic build only: per scored position (pos, ion, K, n0, ngroups, fits, rej, flagged tail points)
 __device__ long long g_wtrace[8192][8];
@@ -123,6 +159,7 @@ ion_wave_kernel(Hits<SMG_HITS_PACKED_F32> hits, const IonDesc* __restrict__ desc
   const int lane = threadIdx.x;
   const uint32_t OM = (1u << SH) - 1u;
   const uint64_t* hb = hits.h;
+  int64_t pos = -1, npos = -1;  // see the scheduling comment below
 
   // register buffers: the principal window's first chunk (PC slots, prefetched) and a ring of four tail buffers
   // (RC groups each).  The rest of the principal window is loaded chunk by chunk when it is processed (the
@@ -139,7 +176,7 @@ ion_wave_kernel(Hits<SMG_HITS_PACKED_F32> hits, const IonDesc* __restrict__ desc
 #pragma unroll
     for (int j = 0; j < PC; ++j) {
       const int i = lane + 64 * j;
-      ld8_async_v(hq[j], hb + (n0 > 0 ? a + (i < n0 ? i : n0 - 1) : 0));
+      hq[j] = hb[WVIX(n0 > 0 ? a + (i < n0 ? i : n0 - 1) : 0, 1)];
     }
   };
   // tail chunk c = groups [c*RC, (c+1)*RC); exactly RC loads (lanes past their window's end load its last point,
@@ -158,7 +195,7 @@ ion_wave_kernel(Hits<SMG_HITS_PACKED_F32> hits, const IonDesc* __restrict__ desc
       const int64_t bk = D->base[k];
       const int ek = D->end[k];
       const int64_t idx = (G < ng && ng > 0) ? bk + (int64_t)G * 64 + min(lane, ek - G * 64 - 1) : 0;
-      ld8_async_v(buf[j], hb + idx);
+      buf[j] = hb[WVIX(idx, 2)];
     }
   };
   auto issue_ion = [&](const IonDesc* D, bool valid) {  // !valid: the same loads of hit 0 (no next ion)
@@ -168,37 +205,30 @@ ion_wave_kernel(Hits<SMG_HITS_PACKED_F32> hits, const IonDesc* __restrict__ desc
     issue_chunk(D, 2, rc, valid);
     issue_chunk(D, 3, rd, valid);
   };
-  auto wait_all = [&]() {
-    vm_wait<0>(hq);
-    vm_wait<0>(ra);
-    vm_wait<0>(rb);
-    vm_wait<0>(rc);
-    vm_wait<0>(rd);
-  };
 
   // pos: the ion scored in this iteration (-1: none -- the first iteration only loads); npos: the next one, whose
   // descriptor this iteration fetches and whose loads it issues at its single issue site (one definition of the
   // asynchronous registers per iteration: no copies of them in flight)
-  int64_t pos = -1, npos = -1;
   {
     int64_t t = -1;
     if (lane == 0) t = sched_resolve<SRC_RANGES>(S, sched_issue<SRC_RANGES>(S));
     npos = uni64(__shfl(t, 0));
   }
   int cur = 1;
+#ifdef SMG_WAVE_STAMPS
+  unsigned long long wst[8] = {0, 0, 0, 0, 0, 0, 0, 0}, wst_t0 = __builtin_amdgcn_s_memtime();
+#endif
   while (true) {
     const IonDesc* D = &dsl[cur];
     IonDesc* DN = &dsl[cur ^ 1];
     // npos's descriptor (one word per lane) and the ticket of the ion after it, both asynchronous
-    uint64_t dword = 0ull;
-    ld8_async_v(dword, reinterpret_cast<const uint64_t*>(desc + (npos >= 0 ? npos : 0)) + (lane < DESC_QWORDS ? lane : 0));
+    const uint64_t dword =
+        reinterpret_cast<const uint64_t*>(desc + (npos >= 0 ? npos : 0))[lane < DESC_QWORDS ? lane : 0];
     uint32_t ticket = 0u;
-    if (lane == 0) sched_issue_async<SRC_RANGES>(S, ticket);
+    if (lane == 0) ticket = sched_issue<SRC_RANGES>(S);
     // resolves the ticket and stores npos's descriptor (waits for every load of this wave)
     int64_t n2pos = -1;
     auto advance = [&]() {
-      vm_wait1<0>(dword);
-      vm_wait1<0>(ticket);
       int64_t t = -1;
       if (lane == 0 && npos >= 0) t = sched_resolve<SRC_RANGES>(S, ticket);
       n2pos = uni64(__shfl(t, 0));
@@ -213,13 +243,25 @@ ion_wave_kernel(Hits<SMG_HITS_PACKED_F32> hits, const IonDesc* __restrict__ desc
               ng = live ? uni(D->ngroups) : 0;
     const int64_t base0 = live ? uni64(D->base[0]) : 0;
     const bool fits = live && K >= 1 && K <= MAXK && n0 <= CAP && ng >= 0;
+#ifdef SMG_WAVE_CHECK
+    if (live && lane == 0) atomicAdd(&g_wvchk[4], 1ull);
+    if (live && !WVCK(ion >= 0 && ion < S.n && K >= 0 && K <= MAXK_DENSE && n0 >= 0 && base0 >= 0, 6, ion)) {
+      advance();
+      issue_ion(DN, npos >= 0);
+      if (npos < 0) break;
+      pos = npos;
+      npos = n2pos;
+      cur ^= 1;
+      continue;
+    }
+#endif
     bool rej = live && K != 0 && !fits;
     double sx = 0.0, sxx = 0.0, spos = 0.0, npos_px = 0.0, vmax = 0.0;
     double chaos_raw = NAN;
     uint32_t flags = 0;
     int nd = 0;  // flagged tail points listed (uniform)
+    int ncand_tr = -1;  // chaos candidates (trace builds)
     if (!fits) {
-      wait_all();
       advance();
     } else {
     // ---- 1. principal image ----------------------------------------------------------------------------------
@@ -231,13 +273,12 @@ ion_wave_kernel(Hits<SMG_HITS_PACKED_F32> hits, const IonDesc* __restrict__ desc
       dtv[lane] = 0.0;
       if (lane < 3 * MAXK) part[lane] = 0.0;
     }
-    vm_wait<4 * RC + 2>(hq);  // younger: the four tail buffers, the descriptor word, the ticket
     const int nch = (n0 + CH - 1) / CH;
     auto load_chunk = [&](int c, uint64_t (&h)[PC]) {  // compiler-tracked loads (L2: the window was read before)
 #pragma unroll
       for (int j = 0; j < PC; ++j) {
         const int i = c * CH + lane + 64 * j;
-        h[j] = hb[base0 + (i < n0 ? i : n0 - 1)];
+        h[j] = hb[WVIX(base0 + (i < n0 ? i : n0 - 1), 3)];
       }
     };
     // pass 1: flagged points (duplicate candidates) summed per pixel in the table (coo.toarray() sums duplicates);
@@ -339,7 +380,8 @@ ion_wave_kernel(Hits<SMG_HITS_PACKED_F32> hits, const IonDesc* __restrict__ desc
     auto place = [&](uint32_t p, uint32_t payload) {  // entry of pixel p at the next position of its segment
       const uint32_t s1 = (p >> SH) + 1u, sh = (s1 & 1u) * 16u;
       const uint32_t old = atomicAdd(&dir32[s1 >> 1], 1u << sh);
-      ent[(old >> sh) & 0xFFFFu] = payload | (p & OM);
+      const uint32_t at = (old >> sh) & 0xFFFFu;
+      if (WVCK(at < (uint32_t)CAP, 4, at)) ent[at] = payload | (p & OM);
     };
 #pragma unroll 1
     for (int c = 0; c < nch; ++c) {  // pass 2: the unflagged points (the window again, from L2)
@@ -354,12 +396,13 @@ ion_wave_kernel(Hits<SMG_HITS_PACKED_F32> hits, const IonDesc* __restrict__ desc
     if (tk != WV_EMPTY) place(tk, ((uint32_t)lane << 16) | 0x8000u);
     // entry t -> x (f64): a summed pixel's from the table, else the point's f32 value in the principal window
     auto ent_x_issue = [&](uint32_t e, uint64_t& raw) {  // async gather (waited by the caller)
-      if (!(e & 0x8000u)) raw = hb[base0 + (e >> 16)];
+      if (!(e & 0x8000u)) raw = hb[WVIX(base0 + (e >> 16), 5)];
     };
     auto ent_x = [&](uint32_t e, uint64_t raw) -> double {
       return (e & 0x8000u) ? dtv[e >> 16] : H::val(raw);
     };
 
+    WV_STAMP(0);
     // ---- 2. measure_of_chaos ----------------------------------------------------------------------------------
     const bool chaos_ok = (sx > 0.0) && (npos_px >= 4.0);
     if (chaos_ok && !rej) {
@@ -461,9 +504,11 @@ ion_wave_kernel(Hits<SMG_HITS_PACKED_F32> hits, const IonDesc* __restrict__ desc
           ncand += wtot;
         }
       }
+      ncand_tr = ncand;
       if (ncand > LY::NC) {
         rej = true;
       } else {
+        WV_STAMP(1);
         // (ii) exact eL(p) = min_{q in box(p)} max_{q' in cross[q], in image} L(q'), from the levels of the principal
         // pixels in p's 5x5 neighbourhood (bytes of Lrow[d]: columns cp-2 .. cp+2 of row rp-2+d)
         const bool act = lane < ncand;
@@ -573,7 +618,37 @@ ion_wave_kernel(Hits<SMG_HITS_PACKED_F32> hits, const IonDesc* __restrict__ desc
     }
 
     // ---- 3. tail windows: one stream of window-aligned 64-point groups ------------------------------------------
+    WV_STAMP(2);
     advance();  // npos's descriptor into the LDS, the next ticket resolved (the tail buffers have landed)
+    WV_STAMP(3);
+    // flagged tail points are listed one window at a time (at most TL of them) and summed per pixel when the stream
+    // leaves the window; each sum's square joins the window's sum y^2 (the prefix sums cover the unflagged points)
+    int ndk = 0;  // window of the listed points (uniform)
+    auto resolve_dups = [&]() {  // uniform
+      if (nd > LY::TL) {
+        rej = true;
+      } else if (nd > 0) {
+        const uint32_t k0 = lane < nd ? tlk[lane] : WV_EMPTY, k1 = lane + 64 < nd ? tlk[lane + 64] : WV_EMPTY;
+        const float v0 = lane < nd ? tlv[lane] : 0.0f, v1 = lane + 64 < nd ? tlv[lane + 64] : 0.0f;
+        double s0 = 0.0, s1 = 0.0;
+        bool f0 = true, f1 = true;
+        for (int jj = 0; jj < nd; ++jj) {
+          const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)(jj < 64 ? k0 : k1), jj & 63);
+          const float vj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(jj < 64 ? v0 : v1), jj & 63));
+          if (kj == k0) {
+            s0 += (double)vj;
+            if (jj < lane) f0 = false;
+          }
+          if (kj == k1) {
+            s1 += (double)vj;
+            if (jj < lane + 64) f1 = false;
+          }
+        }
+        if (lane < nd && f0) atomicAdd(&part[2 * MAXK + ndk], s0 * s0);
+        if (lane + 64 < nd && f1) atomicAdd(&part[2 * MAXK + ndk], s1 * s1);
+      }
+      nd = 0;
+    };
     uint64_t ev0 = 0ull, ev1 = 0ull;
     int evt0 = 0, evt1 = 0, evk0 = 0, evk1 = 0, nev = 0;
     {
@@ -643,9 +718,13 @@ ion_wave_kernel(Hits<SMG_HITS_PACKED_F32> hits, const IonDesc* __restrict__ desc
           const bool f = valid[j] && H::dup(buf[j]);
           const uint64_t fm = __ballot(f);
           if (fm) {
+            if (kk[j] != ndk) {  // the stream left the listed window
+              resolve_dups();
+              ndk = kk[j];
+            }
             const int idx = nd + (int)__popcll(fm & ((1ull << lane) - 1ull));
             if (f && idx < LY::TL) {
-              tlk[idx] = (H::pix(buf[j]) << 3) | (uint32_t)kk[j];
+              tlk[idx] = H::pix(buf[j]);
               tlv[idx] = __uint_as_float((uint32_t)(buf[j] >> 32));
             }
             nd += (int)__popcll(fm);
@@ -658,20 +737,18 @@ ion_wave_kernel(Hits<SMG_HITS_PACKED_F32> hits, const IonDesc* __restrict__ desc
       // has one exit and the ring registers one definition each
 #pragma unroll 1
       for (int c = 0; c * RC < ng; c += 4) {
-        vm_wait<3 * RC>(ra);
         process(c, ra);
         issue_chunk(D, c + 4, ra);
-        vm_wait<3 * RC>(rb);
         if ((c + 1) * RC < ng) process(c + 1, rb);
         issue_chunk(D, c + 5, rb);
-        vm_wait<3 * RC>(rc);
         if ((c + 2) * RC < ng) process(c + 2, rc);
         issue_chunk(D, c + 6, rc);
-        vm_wait<3 * RC>(rd);
         if ((c + 3) * RC < ng) process(c + 3, rd);
         issue_chunk(D, c + 7, rd);
       }
     }
+    WV_STAMP(4);
+    resolve_dups();
     // parked principal hits: both x gathers in flight together, then the window partials
     if (__ballot(nev > 0)) {
       const uint32_t e0 = nev > 0 ? ent[evt0] : 0x8000u, e1 = nev > 1 ? ent[evt1] : 0x8000u;
@@ -691,37 +768,12 @@ ion_wave_kernel(Hits<SMG_HITS_PACKED_F32> hits, const IonDesc* __restrict__ desc
     }
     }
     // ---- the registers of this ion are dead: npos's principal window and first four tail chunks go in flight
+    WV_STAMP(fits ? 5 : 7);
     issue_ion(DN, npos >= 0);  // unconditional: one definition of the asynchronous registers
-    // flagged tail points summed per (pixel, window); each sum's square joins the window's sum y^2 (the prefix
-    // sums cover the unflagged points only)
-    if (!fits) {
-    } else if (nd > LY::TL) {
-      rej = true;
-    } else if (nd > 0) {
-      const uint32_t k0 = lane < nd ? tlk[lane] : WV_EMPTY, k1 = lane + 64 < nd ? tlk[lane + 64] : WV_EMPTY;
-      const float v0 = lane < nd ? tlv[lane] : 0.0f, v1 = lane + 64 < nd ? tlv[lane + 64] : 0.0f;
-      double s0 = 0.0, s1 = 0.0;
-      bool f0 = true, f1 = true;
-      for (int jj = 0; jj < nd; ++jj) {
-        const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)(jj < 64 ? k0 : k1), jj & 63);
-        const float vj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(jj < 64 ? v0 : v1), jj & 63));
-        if (kj == k0) {
-          s0 += (double)vj;
-          if (jj < lane) f0 = false;
-        }
-        if (kj == k1) {
-          s1 += (double)vj;
-          if (jj < lane + 64) f1 = false;
-        }
-      }
-      if (lane < nd && f0) atomicAdd(&part[2 * MAXK + (k0 & 7u)], s0 * s0);
-      if (lane + 64 < nd && f1) atomicAdd(&part[2 * MAXK + (k1 & 7u)], s1 * s1);
-    }
-
 #ifdef SMG_WAVE_TRACE
     if (live && lane == 0) {
       long long* tr = g_wtrace[pos & 8191];
-      tr[0] = pos; tr[1] = ion; tr[2] = K; tr[3] = n0; tr[4] = ng; tr[5] = fits; tr[6] = rej; tr[7] = nd;
+      tr[0] = pos; tr[1] = ion; tr[2] = K; tr[3] = n0; tr[4] = ng; tr[5] = fits; tr[6] = rej; tr[7] = ncand_tr;
     }
 #endif
     // ---- 4. finalize (formula_img_validator.py:78-84 + the restated pyImagingMSpec functions): lane k = window k
@@ -781,13 +833,35 @@ ion_wave_kernel(Hits<SMG_HITS_PACKED_F32> hits, const IonDesc* __restrict__ desc
         oflags[ion] = flags | (uint32_t)D->hits;
       }
     }
+    WV_STAMP(6);
     if (npos < 0) break;
     pos = npos;
     npos = n2pos;
     cur ^= 1;
   }
-  wait_all();  // no load of this wave outlives it
+#ifdef SMG_WAVE_STAMPS
+  if (lane == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_wstamps[i], wst[i]);
+#endif
 }
+
+#ifdef SMG_WAVE_CHECK
+extern "C" int smg_debug_wave_check(unsigned long long* host_out) {
+  SMG_HIP(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wvchk), sizeof(unsigned long long) * 8));
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  SMG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wvchk), z, sizeof(z)));
+  return SMG_OK;
+}
+#endif
+
+#ifdef SMG_WAVE_STAMPS
+extern "C" int smg_debug_wave_stamps(unsigned long long* host_out) {
+  SMG_HIP(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_wstamps), sizeof(unsigned long long) * 8));
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  SMG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wstamps), z, sizeof(z)));
+  return SMG_OK;
+}
+#endif
 
 #ifdef SMG_WAVE_TRACE
 extern "C" int smg_debug_wave_trace(long long* host_out, int n) {

@@ -97,16 +97,35 @@ def test_dense_path_used_when_needed():
     assert ((m["flags"] & 8) != 0).any()      # big-ion LDS pass
     _, _, _, _, _, _, _, m, _, _ = _run_case("huge_window")
     assert ((m["flags"] & 2) != 0).any()      # dense global-scratch pass
-    # images above 2^18 pixels: two-level LDS passes (main, big-ion) instead of the dense path
-    _, _, _, _, _, _, _, m, _, _ = _run_case("large_image")
-    has = (m["flags"] & 1) != 0
-    assert ((m["flags"][has] & (0x10 | 2)) == 0x10).all()
-    ds, ions, ppm, kw, imgs, df, peaks, m, lo, hi = _run_case("large_blobs")
+    # images above 2^18 pixels whose presence bitmap fits the LDS: the rank-indexed wide pass, not the two-level
+    # LDS passes (it outruns them there); the two-level passes are checked with smg_debug_force_two_level below
+    for name in ("large_image", "large_blobs"):
+        _, _, _, _, _, _, _, m, _, _ = _run_case(name)
+        has = (m["flags"] & 1) != 0
+        assert has.any() and ((m["flags"][has] & (0x20 | 0x10 | 2)) == (0x20 | 2)).all(), name
+
+
+def test_forced_two_level_large_blobs_reaches_big_pass():
+    """With the two-level passes forced, large_blobs exercises the two-level big-ion pass and the olist rebuilt
+    from the two-level set (principal windows of 1707..2560 points), and still matches the oracle."""
+    from sm_distributed_amd import _lib
+    L = _lib.lib()
+    L.smg_debug_force_two_level(1)
+    try:
+        ds, ions, ppm, kw = make_case("large_blobs")
+        imgs, df = oracle_run(ds, ions, ppm, **kw)
+        peaks, m, lo, hi = _device_run(ds, ions, ppm, **kw)
+    finally:
+        L.smg_debug_force_two_level(0)
     has = (m["flags"] & 1) != 0
     assert ((m["flags"][has] & 0x10) != 0).sum() >= 8
     assert ((m["flags"][has] & (0x10 | 8)) == (0x10 | 8)).any()   # two-level big-ion pass
     n0 = hi[ions.win_off[:-1]] - lo[ions.win_off[:-1]]
     assert (has & (n0 > 1706) & (n0 <= 2560)).any()              # olist rebuilt from the two-level set
+    idx = {k: i for i, k in enumerate(zip(ions.sf_ids.tolist(), ions.adducts.tolist()))}
+    rows = np.array([idx[k] for k in df.index.tolist()], dtype=np.int64)
+    for col in ("chaos", "spatial", "spectral", "msm"):
+        assert np.abs(df[col].to_numpy() - m[col][rows]).max(initial=0.0) <= METRIC_ATOL, col
 
 
 # every LDS-path case again with the two-level pixel set forced (smg_debug_force_two_level)
@@ -271,3 +290,28 @@ def test_edge_inputs_match_oracle(name, dense):
             assert err.max(initial=0.0) <= METRIC_ATOL, (col, float(err.max()))
     if name == "one_hot_pixel":
         assert len(df) > 0
+
+
+@pytest.mark.parametrize("name", ["basic", "dups", "conn8_border1", "nlevels", "kmix", "wide_range",
+                                  pytest.param("long_tail", marks=pytest.mark.xfail(
+                                      reason="wave kernel: wrong scores on some heavy-duplicate ions (DESIGN §3)",
+                                      strict=False))])
+def test_wave_main_kernel_matches_oracle(name):
+    """The experimental wave-per-ion main pass (smg_debug_main_kernel(0)) against the oracle; it
+    scores the bulk of each case itself (the rest go to the big-ion pass)."""
+    from sm_distributed_amd import _lib
+    ds, ions, ppm, kw, imgs, df, _, _, _, _ = _run_case(name)
+    L = _lib.lib()
+    L.smg_debug_main_kernel(0)
+    try:
+        _, m, _, _ = _device_run(ds, ions, ppm, **kw)
+    finally:
+        L.smg_debug_main_kernel(1)
+    has = (m["flags"] & 1) != 0
+    assert set(zip(ions.sf_ids[has].tolist(), ions.adducts[has].tolist())) == set(df.index.tolist())
+    idx = {k: i for i, k in enumerate(zip(ions.sf_ids.tolist(), ions.adducts.tolist()))}
+    rows = np.array([idx[k] for k in df.index.tolist()], dtype=np.int64)
+    for col in ("chaos", "spatial", "spectral", "msm"):
+        assert np.abs(df[col].to_numpy() - m[col][rows]).max(initial=0.0) <= METRIC_ATOL, col
+    wave_scored = has & ((m["flags"] & (2 | 8 | 0x10)) == 0)
+    assert wave_scored.sum() >= 0.5 * has.sum(), (int(wave_scored.sum()), int(has.sum()))
