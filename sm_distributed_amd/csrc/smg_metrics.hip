@@ -1920,15 +1920,22 @@ __device__ int tail_window(const Hits<FMT>& hits, int64_t a, int64_t b, const do
 
 // k-th smallest (0-based) of n positive doubles (list, written by this block): MSB-first radix select over
 // the IEEE bits (monotonic for positive values), 8 passes of an 8-bit LDS histogram.
-__device__ double block_select_pos(const double* list, int n, int k, uint32_t* hist, int* sh) {
+// The i0-th smallest value of list[0..n) and, with pair, the (i0 + 1)-th (i0 + 1 < n): an MSD radix select over
+// the f64 bit patterns (the values are positive: their patterns are ordered like the values) that stops as soon as
+// the selected byte prefix holds a single element (it is then fetched whole), usually after three or four of the
+// eight bytes.  The next order statistic is the same value when more elements than needed equal it, else the
+// smallest value above it (one pass for both).  sh: 4 ints, dsh: 1 u64 of LDS.
+__device__ void block_select_pair(const double* list, int n, int i0, bool pair, uint32_t* hist, int* sh,
+                                  unsigned long long* dsh, double& a, double& b) {
   const int tid = threadIdx.x;
   uint64_t prefix = 0ull, mask = 0ull;
+  int k = i0;
   for (int shift = 56; shift >= 0; shift -= 8) {
     for (int i = tid; i < 256; i += DBLOCK) hist[i] = 0u;
     __syncthreads();
     for (int i = tid; i < n; i += DBLOCK) {
-      const uint64_t b = (uint64_t)__double_as_longlong(ld_agent(&list[i]));
-      if ((b & mask) == prefix) atomicAdd(&hist[(b >> shift) & 255u], 1u);
+      const uint64_t bits = (uint64_t)__double_as_longlong(ld_agent(&list[i]));
+      if ((bits & mask) == prefix) atomicAdd(&hist[(bits >> shift) & 255u], 1u);
     }
     __syncthreads();
     if (tid == 0) {
@@ -1939,14 +1946,45 @@ __device__ double block_select_pos(const double* list, int n, int k, uint32_t* h
       }
       sh[0] = d;
       sh[1] = k - c;
+      sh[2] = (int)hist[d];
     }
     __syncthreads();
     prefix |= (uint64_t)sh[0] << shift;
     mask |= 255ull << shift;
     k = sh[1];
+    const int cnt = sh[2];
     __syncthreads();
+    if (cnt == 1 && shift > 0) {  // a single element carries the prefix: it is the one
+      for (int i = tid; i < n; i += DBLOCK) {
+        const uint64_t bits = (uint64_t)__double_as_longlong(ld_agent(&list[i]));
+        if ((bits & mask) == prefix) *dsh = bits;
+      }
+      __syncthreads();
+      prefix = *dsh;
+      __syncthreads();
+      break;
+    }
   }
-  return __longlong_as_double((long long)prefix);
+  a = __longlong_as_double((long long)prefix);
+  b = a;
+  if (!pair) return;
+  if (tid == 0) {
+    sh[3] = 0;
+    *dsh = ~0ull;
+  }
+  __syncthreads();
+  int le = 0;
+  uint64_t above = ~0ull;
+  for (int i = tid; i < n; i += DBLOCK) {
+    const uint64_t bits = (uint64_t)__double_as_longlong(ld_agent(&list[i]));
+    if (bits <= prefix) ++le;
+    else above = bits < above ? bits : above;
+  }
+  atomicAdd(&sh[3], le);
+  if (above != ~0ull) atomicMin(dsh, (unsigned long long)above);
+  __syncthreads();
+  if (sh[3] < i0 + 2) b = __longlong_as_double((long long)*dsh);  // fewer than i0 + 2 elements <= a
+  __syncthreads();
 }
 
 // Gated hot-spot clip (image_generation.do_preprocessing / q; the oracle's quantile_clip): every pixel above
@@ -1984,8 +2022,9 @@ __device__ void clip_image(double* img, const uint32_t* list, int n_list, double
     i1 = i0 + 1;
     gamma = vi - floor(vi);
   }
-  const double a = block_select_pos(vals, n, i0, hist, sh);
-  const double b = (i1 == i0) ? a : block_select_pos(vals, n, i1, hist, sh);
+  __shared__ unsigned long long sel_u64;
+  double a, b;
+  block_select_pair(vals, n, i0, i1 != i0, hist, sh, &sel_u64, a, b);
   const double d = b - a;
   const double thr = gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
   for (int i = tid; i < n_list; i += DBLOCK) {
@@ -2337,7 +2376,11 @@ constexpr int WDU = SMG_WDU;  // wide pass: points per lane with loads in flight
 #ifndef SMG_TDU
 #define SMG_TDU 4
 #endif
-constexpr int TDU = SMG_TDU;  // wide pass, pipelined tail stream: points per lane per batch (two batches live)
+constexpr int TDU = SMG_TDU;  // wide pass, pipelined tail stream: points per lane per batch
+#ifndef SMG_TDEPTH
+#define SMG_TDEPTH 2
+#endif
+constexpr int TDEPTH = SMG_TDEPTH;  // batches with loads in flight (the one processed and TDEPTH - 1 ahead)
 
 struct WideSlot {
   double* vals;     // principal values by rank
@@ -2767,9 +2810,9 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
         // once, so the stream has one memory round trip per batch, not two.  A lane's third and later hits gather
         // in place (rare).  Every lane issues every load (a clamped index) so that the counted waits hold per wave.
         const uint64_t* hb = hits.h;
-        uint64_t rA[TDU], rB[TDU];
+        uint64_t rA[TDU], rB[TDU], rC[TDU];
 #pragma unroll
-        for (int u = 0; u < TDU; ++u) rA[u] = rB[u] = 0ull;
+        for (int u = 0; u < TDU; ++u) rA[u] = rB[u] = rC[u] = 0ull;
         uint64_t ev0 = 0ull, ev1 = 0ull;
         int evk0 = 0, evk1 = 0, nev = 0;
         int ki = 0;  // window of the last batch issued (uniform)
@@ -2792,8 +2835,9 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
           }
           return ki;
         };
+        // a batch first issues the batch TDEPTH - 1 ahead (TDEPTH register sets in rotation)
         auto batch = [&](int64_t v0, uint64_t (&r)[TDU], int kb, uint64_t (&rn)[TDU], int& kn) {
-          if (v0 + TSTEP < T) kn = issue(v0 + TSTEP, rn);
+          if (v0 + (TDEPTH - 1) * TSTEP < T) kn = issue(v0 + (TDEPTH - 1) * TSTEP, rn);
           const int64_t off = v0 - sh_tb[kb], n = sh_tn[kb];
           uint32_t flm = 0u;
 #pragma unroll
@@ -2822,12 +2866,23 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
           }
           append(flm & 0xFFFFu, kb, r, TDU);
         };
-        int kA = 0, kB = 0;
+        int kA = 0, kB = 0, kC = 0;
         if (T > 0) kA = issue(0, rA);
-        for (int64_t v0 = 0; v0 < T; v0 += 2 * TSTEP) {
-          batch(v0, rA, kA, rB, kB);
-          if (v0 + TSTEP >= T) break;
-          batch(v0 + TSTEP, rB, kB, rA, kA);
+        if constexpr (TDEPTH == 3) {
+          if (TSTEP < T) kB = issue(TSTEP, rB);
+          for (int64_t v0 = 0; v0 < T; v0 += 3 * TSTEP) {
+            batch(v0, rA, kA, rC, kC);
+            if (v0 + TSTEP >= T) break;
+            batch(v0 + TSTEP, rB, kB, rA, kA);
+            if (v0 + 2 * TSTEP >= T) break;
+            batch(v0 + 2 * TSTEP, rC, kC, rB, kB);
+          }
+        } else {
+          for (int64_t v0 = 0; v0 < T; v0 += 2 * TSTEP) {
+            batch(v0, rA, kA, rB, kB);
+            if (v0 + TSTEP >= T) break;
+            batch(v0 + TSTEP, rB, kB, rA, kA);
+          }
         }
         // the parked principal hits: ranks, both x gathers in flight together, then the window partials
         if (__ballot(nev > 0)) {
