@@ -426,8 +426,7 @@ def device_chain(args, peaks, formulas, plan):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
         if ev:
             ev[0].record()
-        p.flag_duplicates(args.ppm)
-        p.sort()
+        p.flag_and_sort(args.ppm)
         p.prefix_sums()
         if ev:
             ev[1].record()

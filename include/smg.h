@@ -71,11 +71,19 @@ int smg_flag_duplicates(const int64_t* sp_off, int64_t n_spectra, const float* m
 /* Global m/z sort of the packed points (the pandas sort_values('mz') of formula_imager_segm.py:73-74,
  * done once over the whole dataset instead of per m/z segment).  Keys are positive float32 m/z; only their
  * low key_bits bits are sorted on (all keys must agree above them: key_bits = 32 - clz(bits(min) ^ bits(max));
- * 0 = all 31 bits). */
+ * 0 = all 31 bits).  Stable (equal m/z keep dataset order); not in place.  A hand-written LSD radix sort
+ * (smg_sort.hip: ceil(key_bits / 9) passes, each one kernel with a look-back over earlier tiles). */
 int smg_sort_points_workspace_size(int64_t n_points, size_t* bytes);
 int smg_sort_points(const float* mz, const uint64_t* hits, int64_t n_points, int32_t key_bits,
                     float* mz_sorted, uint64_t* hits_sorted, void* workspace, size_t workspace_bytes,
                     void* stream);
+/* smg_flag_duplicates + smg_sort_points in one: the sort's first pass sets bit 31 of every output hit from the
+ * point's dataset neighbours that carry the same pixel (the flag pass's rule, the same flags when every spectrum
+ * is m/z-sorted and the pixel map injective -- the caller checks both and otherwise runs the two calls).  The
+ * input hits are not written (their flag bits are ignored). */
+int smg_sort_points_flag(const float* mz, const uint64_t* hits, int64_t n_points, int32_t key_bits, double ppm,
+                         float* mz_sorted, uint64_t* hits_sorted, void* workspace, size_t workspace_bytes,
+                         void* stream);
 
 /* m/z slice of the resident dataset for one rank of a multi-GPU search (the formula list is sharded by m/z,
  * SURVEY.md §8e; the reference instead shuffles every point into m/z segments, formula_imager_segm.py:45-49,
@@ -194,6 +202,9 @@ int smg_debug_force_dense(int32_t on);
 /* main pass kernel: 1 = the 512-thread LDS kernel (ion_pipe_kernel<512>, the default), 0 = one wave per ion
  * (ion_wave_kernel, packed hits only; experimental, slower: DESIGN.md §3) */
 int smg_debug_main_kernel(int32_t which);
+/* smg_sort_points' implementation: 1 = the hand-written sort (default), 0 = rocPRIM's onesweep radix sort (kept for
+ * A/B timing; smg_sort_points_flag always uses the hand-written one).  Process-wide; returns 0. */
+int smg_debug_sort_impl(int32_t which);
 
 /* passes of smg_ion_metrics, as reported by smg_debug_pass_times */
 #define SMG_PASS_DESC 0   /* ion descriptors (ion_desc8_kernel) */

@@ -40,6 +40,7 @@ PROTOTYPES = {
     "smg_flag_duplicates": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _D, _P, _P, _P]),
     "smg_sort_points_workspace_size": (ctypes.c_int, [_I64, ctypes.POINTER(_SZ)]),
     "smg_sort_points": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _SZ, _P]),
+    "smg_sort_points_flag": (ctypes.c_int, [_P, _P, _I64, _I32, _D, _P, _P, _P, _SZ, _P]),
     "smg_window_bounds": (ctypes.c_int, [_P, _P, _I64, _D, _P, _I64, _P, _P, _P]),
     "smg_align_windows": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
     "smg_slice_mz_workspace_size": (ctypes.c_int, [_I64, ctypes.POINTER(_SZ)]),
@@ -57,6 +58,7 @@ PROTOTYPES = {
     "smg_debug_force_two_level": (ctypes.c_int, [_I32]),
     "smg_debug_force_dense": (ctypes.c_int, [_I32]),
     "smg_debug_main_kernel": (ctypes.c_int, [_I32]),
+    "smg_debug_sort_impl": (ctypes.c_int, [_I32]),
     "smg_debug_time_main_pass": (ctypes.c_int, [_I32]),
     "smg_debug_main_pass_times": (ctypes.c_int, [_P, _I32, ctypes.POINTER(_I32)]),
     "smg_debug_pass_times": (ctypes.c_int, [_P, _P, _I32, ctypes.POINTER(_I32)]),

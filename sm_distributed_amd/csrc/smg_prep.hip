@@ -8,7 +8,6 @@
 #include <cstring>
 #include <stdarg.h>
 
-#include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
 #include "smg_common.hpp"
@@ -398,74 +397,7 @@ int smg_flag_duplicates(const int64_t* sp_off, int64_t n_spectra, const float* m
   return SMG_OK;
 }
 
-// Onesweep radix sort of the f32 m/z bit patterns.  Only the low `key_bits` bits vary across a dataset whose
-// m/z lie in [lo, hi] (both bit patterns share everything above the highest bit where they differ), so the
-// sort covers [0, key_bits) (27 bits for m/z in [100, 1000)).  Three 9-bit passes, 512 threads x 16 items per
-// tile: on MI355X (config 3, 5e8 pairs, 27 bits; scripts/sort_ab.sh) 14.0 ms, against 14.8 ms for four 8-bit
-// passes at 1024 x 8 and 16.1-21.9 ms for the other tiles tried (8 bits 512x8/512x12/512x16/256x16, 9 bits
-// 1024x8/256x16).
-#ifndef SMG_SORT_RADIX_BITS
-#define SMG_SORT_RADIX_BITS 9
-#endif
-#ifndef SMG_SORT_BLOCK
-#define SMG_SORT_BLOCK 512
-#endif
-#ifndef SMG_SORT_IPT
-#define SMG_SORT_IPT 16
-#endif
-#ifndef SMG_SORT_RANK
-#define SMG_SORT_RANK match
-#endif
-#ifndef SMG_HIST_BLOCK
-#define SMG_HIST_BLOCK 512  // the digit-histogram kernel's tile (reads every key once): 512 x 64 items
-#endif                        // 13.9 -> 12.9-13.1 ms for the whole sort against 512 x 16 (1024x32/1024x64 within
-#ifndef SMG_HIST_IPT          // 0.1 ms of it; 256x32/256x64/512x96/512x128/1024x128 slower; scripts/time_sort.py)
-#define SMG_HIST_IPT 64
-#endif
-using SortConfig = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<SMG_HIST_BLOCK, SMG_HIST_IPT>,
-                                        rocprim::kernel_config<SMG_SORT_BLOCK, SMG_SORT_IPT>, SMG_SORT_RADIX_BITS,
-                                        rocprim::block_radix_rank_algorithm::SMG_SORT_RANK>>;
-
-int smg_sort_points_workspace_size(int64_t n_points, size_t* bytes) {
-  SMG_CHECK_ARG(bytes != nullptr && n_points >= 0, "bad arguments");
-  size_t tb = 0;
-  const uint32_t* kin = nullptr;
-  uint32_t* kout = nullptr;
-  const uint64_t* vin = nullptr;
-  uint64_t* vout = nullptr;
-  hipError_t e = rocprim::radix_sort_pairs<SortConfig>(nullptr, tb, kin, kout, vin, vout, (size_t)n_points, 0, 31,
-                                                       (hipStream_t)0, false);
-  if (e != hipSuccess) {
-    set_error("rocprim workspace query failed: %s", hipGetErrorString(e));
-    return SMG_ERR_HIP;
-  }
-  *bytes = tb + 256;
-  return SMG_OK;
-}
-
-int smg_sort_points(const float* mz, const uint64_t* hits, int64_t n_points, int32_t key_bits, float* mz_sorted,
-                    uint64_t* hits_sorted, void* workspace, size_t workspace_bytes, void* stream) {
-  SMG_CHECK_ARG(n_points >= 0, "negative n_points");
-  SMG_CHECK_ARG(key_bits >= 0 && key_bits <= 31, "key_bits must be in [0, 31] (0 = all 31)");
-  if (key_bits == 0) key_bits = 31;
-  if (n_points == 0) return SMG_OK;
-  SMG_CHECK_ARG(mz && hits && mz_sorted && hits_sorted && workspace, "null pointer");
-  size_t need = 0;
-  int rc = smg_sort_points_workspace_size(n_points, &need);
-  if (rc) return rc;
-  if (workspace_bytes < need) {
-    set_error("sort workspace too small: %zu < %zu", workspace_bytes, need);
-    return SMG_ERR_WORKSPACE;
-  }
-  size_t tb = need - 256;
-  // positive float32 keys order like their bit patterns; bit 31 (sign) is always 0
-  SMG_HIP(rocprim::radix_sort_pairs<SortConfig>(workspace, tb, reinterpret_cast<const uint32_t*>(mz),
-                                                reinterpret_cast<uint32_t*>(mz_sorted), hits, hits_sorted,
-                                                (size_t)n_points, 0, (unsigned)key_bits, as_stream(stream), false));
-  return SMG_OK;
-}
+// smg_sort_points / smg_sort_points_flag: smg_sort.hip
 
 int smg_window_bounds(const double* peak_mz, const int64_t* order, int64_t n_windows, double ppm,
                       const float* mz_sorted, int64_t n_points, int64_t* lo, int64_t* hi, void* stream) {

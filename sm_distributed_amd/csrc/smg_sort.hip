@@ -1,0 +1,521 @@
+// Global m/z sort of the resident peak list on gfx950: a hand-written stable LSD radix sort of the f32 m/z bit
+// patterns carrying the packed 8-byte hits, with the duplicate-candidate flags fused into its first pass.
+//
+// Reference behaviour (frulo/SM_distributed):
+//   formula_imager_segm.py:73-74  sp_df.sort_values('mz') -- the segment's peaks in m/z order (pandas' sort is
+//                                 stable for equal m/z only by accident of its algorithm; the windows are sums,
+//                                 so only the set of points per window matters; this sort is stable anyway)
+//
+// Design (DESIGN.md "The m/z sort"):
+//   * keys: positive f32 m/z, whose bit patterns order like the values; only the low key_bits bits vary across a
+//     dataset (27 for m/z in [100, 1000)), sorted in ceil(key_bits / 9) passes of <= 9-bit digits;
+//   * one histogram pass reads the keys once for every pass's digit counts, one tiny scan turns them into bin bases;
+//   * each sort pass is a single kernel (a tile of 8192 points per 512-thread workgroup, tiles claimed in order
+//     from a ticket counter): wave-private digit ranking by ballot matching, the tile's digit counts published at
+//     once and the tile's global bin offsets resolved by a look-back over the earlier tiles' published counts
+//     (a tile only waits on tiles with smaller tickets, all of which are resident), then the tile is reordered by
+//     digit in LDS so that the stores come out as contiguous runs per digit;
+//   * 78 KB of LDS per workgroup (one 64 KB exchange buffer, which holds the wave histograms while ranking, the
+//     keys, then the values): two tiles per CU, so one tile's loads overlap the other's ranking and stores;
+//   * the first pass reads the hits in dataset order and sets the duplicate-candidate flag (smg_flag_duplicates)
+//     on the way: a point's spectrum neighbours are its dataset neighbours with the same pixel (spectra are
+//     m/z-sorted and the pixel map injective: the host takes the separate flag pass otherwise).
+// Traffic per pass: 12 B read + 12 B written per point plus 2-8 B of look-back status per 1 KB of tile.
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "smg_common.hpp"
+
+namespace smg {
+
+constexpr int SRT_T = 512;                  // threads per tile
+constexpr int SRT_IPT = 16;                 // points per thread
+constexpr int SRT_TILE = SRT_T * SRT_IPT;   // 8192 points per tile
+constexpr int SRT_WAVES = SRT_T / 64;
+constexpr int SRT_BINS = 512;               // digits of at most 9 bits
+constexpr int SRT_MAXP = 4;                 // passes (31 key bits: 4 x 8)
+constexpr int HST_T = 256;
+
+// look-back status word: flag in the top two bits (1 = this tile's count, 2 = inclusive prefix over tiles <= it),
+// the value below; 32-bit words while every prefix fits in 30 bits
+template <typename S>
+struct StatusBits;
+template <>
+struct StatusBits<uint32_t> {
+  static constexpr int SH = 30;
+};
+template <>
+struct StatusBits<unsigned long long> {
+  static constexpr int SH = 62;
+};
+
+template <typename S>
+__device__ __forceinline__ void status_store(S* p, S v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename S>
+__device__ __forceinline__ S status_load(const S* p) {
+  return __hip_atomic_load(const_cast<S*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// exclusive prefix over the 512 threads of a workgroup (red: SRT_WAVES entries of LDS)
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T v, T* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  T x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const T y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) red[w] = x;
+  __syncthreads();
+  T off = 0;
+#pragma unroll
+  for (int i = 0; i < SRT_WAVES; ++i) off += i < w ? red[i] : (T)0;
+  return off + x - v;
+}
+
+// digit histograms of every pass in one read of the keys: per-workgroup LDS counts, then one global add per bin
+__global__ void __launch_bounds__(HST_T) sort_hist_kernel(const uint32_t* __restrict__ keys, int64_t n, int passes,
+                                                          int dbits, unsigned long long* __restrict__ hist) {
+  __shared__ uint32_t h[SRT_MAXP * SRT_BINS];
+  for (int i = threadIdx.x; i < SRT_MAXP * SRT_BINS; i += HST_T) h[i] = 0;
+  __syncthreads();
+  const uint32_t mask = (1u << dbits) - 1u;
+  auto add = [&](uint32_t k) {
+    for (int p = 0; p < passes; ++p) atomicAdd(&h[p * SRT_BINS + ((k >> (p * dbits)) & mask)], 1u);
+  };
+  const int64_t stride = (int64_t)gridDim.x * HST_T;
+  // 16-byte loads where the keys are 16-byte aligned (a torch allocation is; a view may not be)
+  const int64_t head = (int64_t)((16 - (reinterpret_cast<uintptr_t>(keys) & 15)) & 15) / 4;
+  const int64_t h0 = head < n ? head : n;
+  const int64_t n4 = (n - h0) >> 2;
+  const uint4* k4 = reinterpret_cast<const uint4*>(keys + h0);
+  for (int64_t i = (int64_t)blockIdx.x * HST_T + threadIdx.x; i < n4; i += stride) {
+    const uint4 q = k4[i];
+    add(q.x);
+    add(q.y);
+    add(q.z);
+    add(q.w);
+  }
+  const int64_t t = (int64_t)blockIdx.x * HST_T + threadIdx.x;
+  if (t < h0) add(keys[t]);
+  for (int64_t i = h0 + n4 * 4 + t; i < n; i += stride) add(keys[i]);
+  __syncthreads();
+  for (int i = threadIdx.x; i < passes * SRT_BINS; i += HST_T)
+    if (h[i]) atomicAdd(&hist[i], (unsigned long long)h[i]);
+}
+
+// bin bases: exclusive prefix of each pass's digit counts (one workgroup per pass)
+__global__ void __launch_bounds__(SRT_BINS) sort_scan_kernel(const unsigned long long* __restrict__ hist,
+                                                             int64_t* __restrict__ binbase) {
+  __shared__ int64_t red[SRT_WAVES];
+  const int p = blockIdx.x, d = threadIdx.x;
+  binbase[p * SRT_BINS + d] = block_excl_scan<int64_t>((int64_t)hist[p * SRT_BINS + d], red);
+}
+
+// One LSD pass over digit bits [shift, shift + dbits).  FLAG: the first pass, which also sets the duplicate-
+// candidate flag (bit 31 of the hit) from the dataset-order neighbours.
+template <typename S, bool FLAG>
+__global__ void __launch_bounds__(SRT_T, 4) sort_pass_kernel(const uint32_t* __restrict__ kin,
+                                                          const uint64_t* __restrict__ vin,
+                                                          uint32_t* __restrict__ kout, uint64_t* __restrict__ vout,
+                                                          int64_t n, int shift, int dbits,
+                                                          const int64_t* __restrict__ binbase, S* __restrict__ status,
+                                                          unsigned* __restrict__ ticket, double slack) {
+  // exchange buffer: the wave histograms (u16 [SRT_WAVES][SRT_BINS]) while ranking, then the tile's keys in digit
+  // order, then its values
+  __shared__ __attribute__((aligned(16))) uint64_t xbuf[SRT_TILE];
+  __shared__ int64_t s_gbase[SRT_BINS];   // global position of the tile's first point of each digit, minus its
+  __shared__ uint32_t s_lstart[SRT_BINS]; // local start (so that position = s_gbase[d] + local index)
+  __shared__ int64_t s_red[SRT_WAVES];
+  __shared__ unsigned s_tile;
+  constexpr int SH = StatusBits<S>::SH;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint16_t* wh = reinterpret_cast<uint16_t*>(xbuf);
+  reinterpret_cast<uint4*>(xbuf)[tid] = make_uint4(0u, 0u, 0u, 0u);  // 512 x 16 B: the 8 KB of wave histograms
+  if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const int64_t t = s_tile;
+  const int64_t base = t * SRT_TILE;
+  const int64_t wbase = base + (int64_t)w * (64 * SRT_IPT);  // a wave's points: 16 rows of 64 consecutive points
+  const uint32_t mask = (1u << dbits) - 1u;
+  const int nb = 1 << dbits;
+
+  // keys first; the values are loaded after the ranking (they are not needed before the exchange, and holding
+  // them through it would spill).  Past the end: the last digit, after every real point of the tile (never
+  // stored); the loads of the last tile are clamped to the last point.
+  const bool full = base + SRT_TILE <= n;
+  uint32_t k[SRT_IPT];
+  if (full) {
+#pragma unroll
+    for (int u = 0; u < SRT_IPT; ++u) k[u] = kin[wbase + u * 64 + lane];
+  } else {
+#pragma unroll
+    for (int u = 0; u < SRT_IPT; ++u) {
+      const int64_t i = wbase + u * 64 + lane;
+      k[u] = i < n ? kin[i] : 0xFFFFFFFFu;
+    }
+  }
+
+  uint32_t fmask = 0;  // FLAG: bit u = the duplicate-candidate flag of the thread's point u
+  if constexpr (FLAG) {
+    // the tile's keys and pixels through LDS in dataset order (the exchange buffer is free until ranking); the
+    // points just outside the tile come from memory
+    uint32_t* fk = reinterpret_cast<uint32_t*>(xbuf);
+    uint32_t* fp = fk + SRT_TILE;
+    const uint32_t* vlo = reinterpret_cast<const uint32_t*>(vin);  // the hits' low words: pixel | flag << 31
+    const int64_t ia = base - 1, ib = base + SRT_TILE;
+    uint32_t ka = 0, pa = 0xFFFFFFFFu, kb = 0, pb = 0xFFFFFFFFu;  // 0xFFFFFFFF: no neighbour (pixels are 31-bit)
+    if (ia >= 0) {
+      ka = kin[ia];
+      pa = vlo[2 * ia] & 0x7FFFFFFFu;
+    }
+    if (ib < n) {
+      kb = kin[ib];
+      pb = vlo[2 * ib] & 0x7FFFFFFFu;
+    }
+    uint32_t px[SRT_IPT];
+    if (full) {
+#pragma unroll
+      for (int u = 0; u < SRT_IPT; ++u) px[u] = vlo[2 * (wbase + u * 64 + lane)];
+    } else {
+#pragma unroll
+      for (int u = 0; u < SRT_IPT; ++u) {
+        const int64_t i = wbase + u * 64 + lane;
+        px[u] = i < n ? vlo[2 * i] : 0xFFFFFFFFu;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < SRT_IPT; ++u) {
+      const int p = w * (64 * SRT_IPT) + u * 64 + lane;
+      fk[p] = k[u];
+      fp[p] = px[u] & 0x7FFFFFFFu;
+    }
+    __syncthreads();
+    // (everything from LDS, in a rolled loop: unrolled, the compiler overlaps all sixteen and spills)
+#pragma unroll 2
+    for (int u = 0; u < SRT_IPT; ++u) {
+      const int p = w * (64 * SRT_IPT) + u * 64 + lane;
+      const int64_t i = base + p;
+      const uint32_t pix = fp[p];
+      const uint32_t kp = p > 0 ? fk[p - 1] : ka, pp = p > 0 ? fp[p - 1] : pa;
+      uint32_t kn = p + 1 < SRT_TILE ? fk[p + 1] : kb, pn = p + 1 < SRT_TILE ? fp[p + 1] : pb;
+      if (i + 1 >= n) pn = 0xFFFFFFFFu;
+      // the flag pass's test (smg_prep.hip flag_tile_store), in f64
+      const double m = (double)__uint_as_float(fk[p]);
+      bool f = pp == pix && m - (double)__uint_as_float(kp) <= slack * m;
+      if (pn == pix) {
+        const double m2 = (double)__uint_as_float(kn);
+        f = f || (m2 - m <= slack * m2);
+      }
+      fmask |= (uint32_t)(f && i < n) << u;
+    }
+    __syncthreads();
+    reinterpret_cast<uint4*>(xbuf)[tid] = make_uint4(0u, 0u, 0u, 0u);  // the wave histograms again
+    __syncthreads();
+  }
+
+  // ranking: each wave counts its rows in order (row u, lane) -- the stable order of its points -- into its own
+  // u16 histogram; the lanes of one digit find each other with one ballot per digit bit
+  uint32_t rk[SRT_IPT];
+  uint16_t* myh = wh + w * SRT_BINS;
+  const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int u = 0; u < SRT_IPT; ++u) {
+    const uint32_t d = (k[u] >> shift) & mask;
+    uint64_t peers = ~0ull;
+#pragma unroll
+    for (int b = 0; b < 9; ++b) {  // bits at and above dbits are 0 in every lane: those ballots change nothing
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bal = __ballot(bit);
+      peers &= bit ? bal : ~bal;
+    }
+    const uint32_t below = (uint32_t)__popcll(peers & lt);
+    const uint32_t old = myh[d];
+    if (below == 0) myh[d] = (uint16_t)(old + (uint32_t)__popcll(peers));
+    rk[u] = old + below;
+  }
+  __syncthreads();
+
+  // per digit (one thread each): wave prefixes, the tile's count, published at once for later tiles' look-back
+  const int d = tid;
+  uint32_t cnt = 0;
+  if (d < nb) {
+#pragma unroll
+    for (int ww = 0; ww < SRT_WAVES; ++ww) {
+      const uint32_t c = wh[ww * SRT_BINS + d];
+      wh[ww * SRT_BINS + d] = (uint16_t)cnt;
+      cnt += c;
+    }
+    status_store(status + t * SRT_BINS + d, (S)((t == 0 ? (S)2 : (S)1) << SH) | (S)cnt);
+  }
+  const uint32_t lstart = (uint32_t)block_excl_scan<int64_t>((int64_t)cnt, s_red);
+  if (d < nb) {
+    int64_t excl = 0;
+    if (t > 0) {
+      for (int64_t j = t - 1;;) {
+        const S s = status_load(status + j * SRT_BINS + d);
+        const uint32_t fl = (uint32_t)(s >> SH);
+        if (fl == 0) {
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        excl += (int64_t)(s & (((S)1 << SH) - 1));
+        if (fl == 2) break;
+        --j;
+      }
+      status_store(status + t * SRT_BINS + d, (S)((S)2 << SH) | (S)(excl + cnt));
+    }
+    s_gbase[d] = binbase[d] + excl - (int64_t)lstart;
+    s_lstart[d] = lstart;
+  }
+  __syncthreads();
+
+  // local index of each point in digit order, then the keys through LDS
+#pragma unroll
+  for (int u = 0; u < SRT_IPT; ++u) {
+    const uint32_t dd = (k[u] >> shift) & mask;
+    rk[u] += s_lstart[dd] + wh[w * SRT_BINS + dd];
+  }
+  __syncthreads();  // the wave histograms are overwritten below
+  uint32_t* xk = reinterpret_cast<uint32_t*>(xbuf);
+#pragma unroll
+  for (int u = 0; u < SRT_IPT; ++u) xk[rk[u]] = k[u];
+  __syncthreads();
+  const int64_t left = n - base;
+  const int nvalid = left < SRT_TILE ? (int)left : SRT_TILE;
+#pragma unroll
+  for (int u = 0; u < SRT_IPT; ++u) {
+    const int j = u * SRT_T + tid;
+    k[u] = xk[j];
+    if (j < nvalid) kout[s_gbase[(k[u] >> shift) & mask] + j] = k[u];
+  }
+  // the values (loaded this late: holding them through the ranking and the key exchange would spill)
+  uint64_t v[SRT_IPT];
+  if (full) {
+#pragma unroll
+    for (int u = 0; u < SRT_IPT; ++u) v[u] = vin[wbase + u * 64 + lane];
+  } else {
+#pragma unroll
+    for (int u = 0; u < SRT_IPT; ++u) {
+      const int64_t i = wbase + u * 64 + lane;
+      v[u] = i < n ? vin[i] : 0ull;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < SRT_IPT; ++u) {
+    uint64_t x = v[u];
+    if constexpr (FLAG) x = ((fmask >> u) & 1u) ? (x | 0x80000000ull) : (x & ~0x80000000ull);
+    xbuf[rk[u]] = x;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < SRT_IPT; ++u) {
+    const int j = u * SRT_T + tid;
+    if (j < nvalid) vout[s_gbase[(k[u] >> shift) & mask] + j] = xbuf[j];
+  }
+}
+
+// ---- host side ---------------------------------------------------------------------------------------------
+struct SortPlan {
+  int passes, dbits;
+  int64_t ntiles;
+  bool wide;  // 64-bit look-back words
+  size_t off_hist, off_base, off_status, status_bytes, off_tk, off_tv, total;
+};
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+static SortPlan sort_plan(int64_t n, int key_bits) {
+  SortPlan p;
+  p.passes = (key_bits + 8) / 9;
+  if (p.passes < 1) p.passes = 1;
+  p.dbits = (key_bits + p.passes - 1) / p.passes;
+  if (p.dbits < 1) p.dbits = 1;
+  p.ntiles = (n + SRT_TILE - 1) / SRT_TILE;
+  p.wide = n >= (int64_t(1) << 30);
+  const size_t sw = p.wide ? 8 : 4;
+  p.off_hist = 256;  // [0, 256): the passes' ticket counters
+  p.off_base = p.off_hist + SRT_MAXP * SRT_BINS * 8;
+  p.off_status = p.off_base + SRT_MAXP * SRT_BINS * 8;
+  p.status_bytes = (size_t)p.passes * (size_t)p.ntiles * SRT_BINS * sw;
+  p.off_tk = align_up(p.off_status + p.status_bytes, 256);
+  p.off_tv = align_up(p.off_tk + (size_t)n * 4, 256);
+  p.total = p.off_tv + (size_t)n * 8;
+  return p;
+}
+
+// 0 = rocPRIM onesweep (A/B reference), 1 = the hand-written sort (default)
+static int g_sort_impl = 1;
+
+#ifndef SMG_SORT_RADIX_BITS
+#define SMG_SORT_RADIX_BITS 9
+#endif
+#ifndef SMG_SORT_BLOCK
+#define SMG_SORT_BLOCK 512
+#endif
+#ifndef SMG_SORT_IPT
+#define SMG_SORT_IPT 16
+#endif
+#ifndef SMG_HIST_BLOCK
+#define SMG_HIST_BLOCK 512
+#endif
+#ifndef SMG_HIST_IPT
+#define SMG_HIST_IPT 64
+#endif
+// the library sort kept for A/B timing (smg_debug_sort_impl(0)): onesweep, three 9-bit passes, 512 x 16 tiles
+// (its best configuration on MI355X, scripts/sort_ab.sh)
+using RocSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<SMG_HIST_BLOCK, SMG_HIST_IPT>,
+                                        rocprim::kernel_config<SMG_SORT_BLOCK, SMG_SORT_IPT>, SMG_SORT_RADIX_BITS,
+                                        rocprim::block_radix_rank_algorithm::match>>;
+
+static int roc_workspace(int64_t n, size_t* bytes) {
+  size_t tb = 0;
+  const uint32_t* kin = nullptr;
+  uint32_t* kout = nullptr;
+  const uint64_t* vin = nullptr;
+  uint64_t* vout = nullptr;
+  hipError_t e = rocprim::radix_sort_pairs<RocSortConfig>(nullptr, tb, kin, kout, vin, vout, (size_t)n, 0, 31,
+                                                          (hipStream_t)0, false);
+  if (e != hipSuccess) {
+    set_error("rocprim workspace query failed: %s", hipGetErrorString(e));
+    return SMG_ERR_HIP;
+  }
+  *bytes = tb;
+  return SMG_OK;
+}
+
+template <typename S>
+static int run_passes(const SortPlan& P, const uint32_t* mz, const uint64_t* hits, int64_t n, uint32_t* ko,
+                      uint64_t* vo, unsigned char* ws, bool flag, double slack, hipStream_t st) {
+  unsigned* tickets = reinterpret_cast<unsigned*>(ws);
+  const int64_t* binbase = reinterpret_cast<const int64_t*>(ws + P.off_base);
+  S* status = reinterpret_cast<S*>(ws + P.off_status);
+  uint32_t* tk = reinterpret_cast<uint32_t*>(ws + P.off_tk);
+  uint64_t* tv = reinterpret_cast<uint64_t*>(ws + P.off_tv);
+  const uint32_t* ki = mz;
+  const uint64_t* vi = hits;
+  for (int p = 0; p < P.passes; ++p) {
+    // the last pass writes the caller's arrays, the ones before alternate with the workspace copy
+    const bool to_out = ((P.passes - 1 - p) & 1) == 0;
+    uint32_t* kdst = to_out ? ko : tk;
+    uint64_t* vdst = to_out ? vo : tv;
+    S* sp = status + (size_t)p * P.ntiles * SRT_BINS;
+    if (flag && p == 0)
+      hipLaunchKernelGGL((sort_pass_kernel<S, true>), dim3((unsigned)P.ntiles), dim3(SRT_T), 0, st, ki, vi, kdst,
+                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, slack);
+    else
+      hipLaunchKernelGGL((sort_pass_kernel<S, false>), dim3((unsigned)P.ntiles), dim3(SRT_T), 0, st, ki, vi, kdst,
+                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, slack);
+    SMG_LAUNCH_CHECK();
+    ki = kdst;
+    vi = vdst;
+  }
+  return SMG_OK;
+}
+
+static int native_sort(const float* mz, const uint64_t* hits, int64_t n, int key_bits, float* mz_sorted,
+                       uint64_t* hits_sorted, void* workspace, size_t workspace_bytes, bool flag, double ppm,
+                       hipStream_t st) {
+  const SortPlan P = sort_plan(n, key_bits);
+  if (workspace_bytes < P.total) {
+    set_error("sort workspace too small: %zu < %zu", workspace_bytes, P.total);
+    return SMG_ERR_WORKSPACE;
+  }
+  if (P.ntiles > 0x7FFFFFFF) {
+    set_error("too many points for one sort: %lld", (long long)n);
+    return SMG_ERR_UNSUPPORTED;
+  }
+  unsigned char* ws = reinterpret_cast<unsigned char*>(workspace);
+  // tickets, histograms and every pass's look-back words start at zero
+  SMG_HIP(hipMemsetAsync(ws, 0, P.off_status + P.status_bytes, st));
+  const uint32_t* keys = reinterpret_cast<const uint32_t*>(mz);
+  int64_t hb = (n + (int64_t)HST_T * 16 - 1) / ((int64_t)HST_T * 16);
+  if (hb > 2048) hb = 2048;
+  hipLaunchKernelGGL(sort_hist_kernel, dim3((unsigned)hb), dim3(HST_T), 0, st, keys, n, P.passes, P.dbits,
+                     reinterpret_cast<unsigned long long*>(ws + P.off_hist));
+  SMG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sort_scan_kernel, dim3((unsigned)P.passes), dim3(SRT_BINS), 0, st,
+                     reinterpret_cast<const unsigned long long*>(ws + P.off_hist),
+                     reinterpret_cast<int64_t*>(ws + P.off_base));
+  SMG_LAUNCH_CHECK();
+  const double slack = 2.0 * ppm * 1e-6 / (1.0 - ppm * 1e-6) * (1.0 + 1e-9);
+  uint32_t* ko = reinterpret_cast<uint32_t*>(mz_sorted);
+  return P.wide ? run_passes<unsigned long long>(P, keys, hits, n, ko, hits_sorted, ws, flag, slack, st)
+                : run_passes<uint32_t>(P, keys, hits, n, ko, hits_sorted, ws, flag, slack, st);
+}
+
+}  // namespace smg
+
+using namespace smg;
+
+extern "C" {
+
+int smg_sort_points_workspace_size(int64_t n_points, size_t* bytes) {
+  SMG_CHECK_ARG(bytes != nullptr && n_points >= 0, "bad arguments");
+  size_t roc = 0;
+  int rc = roc_workspace(n_points, &roc);
+  if (rc) return rc;
+  const size_t mine = sort_plan(n_points, 31).total;  // the most passes any key width takes
+  *bytes = (roc > mine ? roc : mine) + 256;
+  return SMG_OK;
+}
+
+static int sort_args(const float* mz, const uint64_t* hits, int64_t n_points, int32_t* key_bits, float* mz_sorted,
+                     uint64_t* hits_sorted, void* workspace, size_t workspace_bytes, size_t* need) {
+  SMG_CHECK_ARG(n_points >= 0, "negative n_points");
+  SMG_CHECK_ARG(*key_bits >= 0 && *key_bits <= 31, "key_bits must be in [0, 31] (0 = all 31)");
+  if (*key_bits == 0) *key_bits = 31;
+  if (n_points == 0) return SMG_OK;
+  SMG_CHECK_ARG(mz && hits && mz_sorted && hits_sorted && workspace, "null pointer");
+  SMG_CHECK_ARG((const void*)mz != (const void*)mz_sorted && (const void*)hits != (const void*)hits_sorted,
+                "the sort is not in place");
+  int rc = smg_sort_points_workspace_size(n_points, need);
+  if (rc) return rc;
+  if (workspace_bytes < *need) {
+    set_error("sort workspace too small: %zu < %zu", workspace_bytes, *need);
+    return SMG_ERR_WORKSPACE;
+  }
+  return SMG_OK;
+}
+
+int smg_sort_points(const float* mz, const uint64_t* hits, int64_t n_points, int32_t key_bits, float* mz_sorted,
+                    uint64_t* hits_sorted, void* workspace, size_t workspace_bytes, void* stream) {
+  size_t need = 0;
+  int rc = sort_args(mz, hits, n_points, &key_bits, mz_sorted, hits_sorted, workspace, workspace_bytes, &need);
+  if (rc || n_points == 0) return rc;
+  if (g_sort_impl == 0) {
+    size_t tb = need - 256;
+    // positive float32 keys order like their bit patterns; bit 31 (sign) is always 0
+    SMG_HIP(rocprim::radix_sort_pairs<RocSortConfig>(workspace, tb, reinterpret_cast<const uint32_t*>(mz),
+                                                     reinterpret_cast<uint32_t*>(mz_sorted), hits, hits_sorted,
+                                                     (size_t)n_points, 0, (unsigned)key_bits, as_stream(stream),
+                                                     false));
+    return SMG_OK;
+  }
+  return native_sort(mz, hits, n_points, key_bits, mz_sorted, hits_sorted, workspace, workspace_bytes, false, 0.0,
+                     as_stream(stream));
+}
+
+int smg_sort_points_flag(const float* mz, const uint64_t* hits, int64_t n_points, int32_t key_bits, double ppm,
+                         float* mz_sorted, uint64_t* hits_sorted, void* workspace, size_t workspace_bytes,
+                         void* stream) {
+  SMG_CHECK_ARG(ppm >= 0 && ppm < 1e6, "bad ppm");
+  size_t need = 0;
+  int rc = sort_args(mz, hits, n_points, &key_bits, mz_sorted, hits_sorted, workspace, workspace_bytes, &need);
+  if (rc || n_points == 0) return rc;
+  return native_sort(mz, hits, n_points, key_bits, mz_sorted, hits_sorted, workspace, workspace_bytes, true, ppm,
+                     as_stream(stream));
+}
+
+int smg_debug_sort_impl(int32_t which) {
+  SMG_CHECK_ARG(which == 0 || which == 1, "which: 0 = rocPRIM, 1 = hand-written");
+  g_sort_impl = which;
+  return SMG_OK;
+}
+
+}  // extern "C"

@@ -190,6 +190,13 @@ class DevicePeaks:
         return out
 
     def sort(self, stream=None) -> "DevicePeaks":
+        """Stable m/z sort of the points (smg_sort_points), flags as the hits carry them."""
+        self._sort_into(lambda ws: lib().smg_sort_points(
+            _p(self.mz), _p(self.hits), self.n_points, self.key_bits(), _p(self.mz_sorted), _p(self.hits_sorted),
+            _p(ws), ws.numel(), _stream(stream)), "smg_sort_points", stream)
+        return self
+
+    def _sort_into(self, call, name, stream=None):
         n = self.n_points
         if self.mz_sorted is None or self.mz_sorted.numel() != n:
             self.mz_sorted = torch.empty_like(self.mz)
@@ -197,12 +204,25 @@ class DevicePeaks:
         self.cum_valid = False
         self.version += 1
         if n == 0:
-            return self
+            return
         sz = ctypes.c_size_t(0)
         check(lib().smg_sort_points_workspace_size(n, ctypes.byref(sz)), "smg_sort_points_workspace_size")
         ws = workspace(sz.value, self.device, "sort")
-        check(lib().smg_sort_points(_p(self.mz), _p(self.hits), n, self.key_bits(), _p(self.mz_sorted),
-                                    _p(self.hits_sorted), _p(ws), ws.numel(), _stream(stream)), "smg_sort_points")
+        check(call(ws), name)
+
+    def flag_and_sort(self, ppm: float, stream=None) -> "DevicePeaks":
+        """flag_duplicates(ppm) then sort(), as one pass less: the sort's first pass sets the flags from each
+        point's dataset neighbours with the same pixel (smg_sort_points_flag), which are its spectrum neighbours
+        when every spectrum is m/z-sorted and no pixel is shared.  Otherwise (and on a slice whose copy set the
+        flags) the separate flag pass, then the sort."""
+        preset = self.flags_preset_ppm is not None and float(ppm) == self.flags_preset_ppm
+        if self.sp_off is None or self.force is not None or preset or not self.spectra_sorted():
+            self.flag_duplicates(ppm, stream)
+            return self.sort(stream)
+        self._sort_into(lambda ws: lib().smg_sort_points_flag(
+            _p(self.mz), _p(self.hits), self.n_points, self.key_bits(), float(ppm), _p(self.mz_sorted),
+            _p(self.hits_sorted), _p(ws), ws.numel(), _stream(stream)), "smg_sort_points_flag", stream)
+        self.flag_ppm = float(ppm)
         return self
 
     def prefix_sums(self, stream=None) -> "DevicePeaks":
@@ -359,8 +379,7 @@ def _force_flags(pixel_map, device):
 
 def run_hot_path(peaks: DevicePeaks, ions: DeviceIons, ppm: float, nlevels: int = 30, **kw):
     """One full pass: duplicate flags -> sort -> window search -> fused metrics (all on the current stream)."""
-    peaks.flag_duplicates(ppm)
-    peaks.sort()
+    peaks.flag_and_sort(ppm)
     peaks.prefix_sums()
     lo, hi = window_bounds(peaks, ions, ppm)
     return ion_metrics(peaks, ions, lo, hi, nlevels=nlevels, **kw), lo, hi

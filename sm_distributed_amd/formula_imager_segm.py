@@ -398,8 +398,7 @@ class IonImageSet:
         stable and keyed by m/z only, so re-flagging at this ppm and re-sorting gives back the same positions."""
         p = self.peaks
         if p is not None and (p.version != self.peaks_version or p.flag_ppm != self.ppm):
-            p.flag_duplicates(self.ppm)
-            p.sort()
+            p.flag_and_sort(self.ppm)
             p.prefix_sums()
             self.peaks_version = p.version
         return self
@@ -597,8 +596,7 @@ def compute_sf_images(sc, ds, sf_peak_df, ppm):
     main = torch.cuda.current_stream(peaks.device)
     side = _side_stream(peaks.device)
     side.wait_stream(main)  # the side stream may reuse memory the main stream released
-    peaks.flag_duplicates(ppm)
-    peaks.sort()
+    peaks.flag_and_sort(ppm)
     peaks.prefix_sums()
     keys, dions, K = device_layout(sf_peak_df, peaks.device, side)
     main.wait_stream(side)
