@@ -77,13 +77,14 @@ int smg_sort_points_workspace_size(int64_t n_points, size_t* bytes);
 int smg_sort_points(const float* mz, const uint64_t* hits, int64_t n_points, int32_t key_bits,
                     float* mz_sorted, uint64_t* hits_sorted, void* workspace, size_t workspace_bytes,
                     void* stream);
-/* smg_flag_duplicates + smg_sort_points in one: the sort's first pass sets bit 31 of every output hit from the
- * point's dataset neighbours that carry the same pixel (the flag pass's rule, the same flags when every spectrum
- * is m/z-sorted and the pixel map injective -- the caller checks both and otherwise runs the two calls).  The
- * input hits are not written (their flag bits are ignored). */
-int smg_sort_points_flag(const float* mz, const uint64_t* hits, int64_t n_points, int32_t key_bits, double ppm,
-                         float* mz_sorted, uint64_t* hits_sorted, void* workspace, size_t workspace_bytes,
-                         void* stream);
+/* smg_flag_duplicates + smg_sort_points in one: the sort's first pass sets bit 31 of every output hit by the
+ * flag pass's rule (a spectrum neighbour within one window width; spectra from sp_off[0..n_spectra]).  The same
+ * flags as smg_flag_duplicates when every spectrum is m/z-sorted and no pixel is shared (force all zero) -- the
+ * caller checks both and otherwise runs the two calls.  The input hits are not written (their flag bits are
+ * ignored). */
+int smg_sort_points_flag(const int64_t* sp_off, int64_t n_spectra, const float* mz, const uint64_t* hits,
+                         int64_t n_points, int32_t key_bits, double ppm, float* mz_sorted, uint64_t* hits_sorted,
+                         void* workspace, size_t workspace_bytes, void* stream);
 
 /* m/z slice of the resident dataset for one rank of a multi-GPU search (the formula list is sharded by m/z,
  * SURVEY.md §8e; the reference instead shuffles every point into m/z segments, formula_imager_segm.py:45-49,

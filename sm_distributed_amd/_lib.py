@@ -40,7 +40,7 @@ PROTOTYPES = {
     "smg_flag_duplicates": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _D, _P, _P, _P]),
     "smg_sort_points_workspace_size": (ctypes.c_int, [_I64, ctypes.POINTER(_SZ)]),
     "smg_sort_points": (ctypes.c_int, [_P, _P, _I64, _I32, _P, _P, _P, _SZ, _P]),
-    "smg_sort_points_flag": (ctypes.c_int, [_P, _P, _I64, _I32, _D, _P, _P, _P, _SZ, _P]),
+    "smg_sort_points_flag": (ctypes.c_int, [_P, _I64, _P, _P, _I64, _I32, _D, _P, _P, _P, _SZ, _P]),
     "smg_window_bounds": (ctypes.c_int, [_P, _P, _I64, _D, _P, _I64, _P, _P, _P]),
     "smg_align_windows": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64, _P, _P, _P, _P]),
     "smg_slice_mz_workspace_size": (ctypes.c_int, [_I64, ctypes.POINTER(_SZ)]),

@@ -17,9 +17,10 @@
 //     digit in LDS so that the stores come out as contiguous runs per digit;
 //   * 78 KB of LDS per workgroup (one 64 KB exchange buffer, which holds the wave histograms while ranking, the
 //     keys, then the values): two tiles per CU, so one tile's loads overlap the other's ranking and stores;
-//   * the first pass reads the hits in dataset order and sets the duplicate-candidate flag (smg_flag_duplicates)
-//     on the way: a point's spectrum neighbours are its dataset neighbours with the same pixel (spectra are
-//     m/z-sorted and the pixel map injective: the host takes the separate flag pass otherwise).
+//   * the first pass reads the keys in dataset order and sets the duplicate-candidate flag (smg_flag_duplicates)
+//     on the way: a bit per position marks the spectrum starts (from sp_off, one small kernel), so a point's
+//     spectrum neighbours are its dataset neighbours across no start (spectra must be m/z-sorted and no pixel
+//     shared: the host takes the separate flag pass otherwise); no pixel is read.
 // Traffic per pass: 12 B read + 12 B written per point plus 2-8 B of look-back status per 1 KB of tile.
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -27,8 +28,20 @@
 
 namespace smg {
 
+#ifndef SMG_SRT_IPT
+#define SMG_SRT_IPT 16
+#endif
+#ifndef SMG_SRT_VLOAD  // where the values are loaded: 0 after the keys' stores, 1 before them, 2 after the ranking
+#define SMG_SRT_VLOAD 0
+#endif
+#ifndef SMG_SRT_WPE
+#define SMG_SRT_WPE 4
+#endif
+#ifndef SMG_SRT_LB  // look-back words per round trip
+#define SMG_SRT_LB 4
+#endif
 constexpr int SRT_T = 512;                  // threads per tile
-constexpr int SRT_IPT = 16;                 // points per thread
+constexpr int SRT_IPT = SMG_SRT_IPT;        // points per thread
 constexpr int SRT_TILE = SRT_T * SRT_IPT;   // 8192 points per tile
 constexpr int SRT_WAVES = SRT_T / 64;
 constexpr int SRT_BINS = 512;               // digits of at most 9 bits
@@ -83,7 +96,40 @@ __global__ void __launch_bounds__(HST_T) sort_hist_kernel(const uint32_t* __rest
   __syncthreads();
   const uint32_t mask = (1u << dbits) - 1u;
   auto add = [&](uint32_t k) {
-    for (int p = 0; p < passes; ++p) atomicAdd(&h[p * SRT_BINS + ((k >> (p * dbits)) & mask)], 1u);
+#pragma unroll
+    for (int p = 0; p < SRT_MAXP; ++p)
+      if (p < passes) atomicAdd(&h[p * SRT_BINS + ((k >> (p * dbits)) & mask)], 1u);
+  };
+  // the top digit of consecutive points of an m/z-sorted spectrum repeats: for it, a lane's four keys and then
+  // a run of lanes with one digit are added at once (LDS atomics on one address serialise)
+  const int lane = threadIdx.x & 63;
+  const int top = passes - 1;
+  auto add4 = [&](const uint4 q) {  // wave-uniform
+#pragma unroll
+    for (int p = 0; p < SRT_MAXP - 1; ++p) {
+      if (p < top) {
+        atomicAdd(&h[p * SRT_BINS + ((q.x >> (p * dbits)) & mask)], 1u);
+        atomicAdd(&h[p * SRT_BINS + ((q.y >> (p * dbits)) & mask)], 1u);
+        atomicAdd(&h[p * SRT_BINS + ((q.z >> (p * dbits)) & mask)], 1u);
+        atomicAdd(&h[p * SRT_BINS + ((q.w >> (p * dbits)) & mask)], 1u);
+      }
+    }
+    const int sh = top * dbits;
+    const int d0 = (q.x >> sh) & mask, d1 = (q.y >> sh) & mask, d2 = (q.z >> sh) & mask, d3 = (q.w >> sh) & mask;
+    const bool same = d0 == d1 && d1 == d2 && d2 == d3;
+    if (!same) {
+      atomicAdd(&h[top * SRT_BINS + d0], 1u);
+      atomicAdd(&h[top * SRT_BINS + d1], 1u);
+      atomicAdd(&h[top * SRT_BINS + d2], 1u);
+      atomicAdd(&h[top * SRT_BINS + d3], 1u);
+    }
+    const int sd = same ? d0 : -1;
+    const int prev = __shfl_up(sd, 1, 64);
+    const bool bound = lane == 0 || prev != sd;
+    const uint64_t heads = __ballot(bound);
+    const uint64_t later = lane == 63 ? 0ull : heads & ~((2ull << lane) - 1ull);
+    const int next = later ? __ffsll((unsigned long long)later) - 1 : 64;
+    if (same && bound) atomicAdd(&h[top * SRT_BINS + sd], 4u * (uint32_t)(next - lane));
   };
   const int64_t stride = (int64_t)gridDim.x * HST_T;
   // 16-byte loads where the keys are 16-byte aligned (a torch allocation is; a view may not be)
@@ -91,16 +137,20 @@ __global__ void __launch_bounds__(HST_T) sort_hist_kernel(const uint32_t* __rest
   const int64_t h0 = head < n ? head : n;
   const int64_t n4 = (n - h0) >> 2;
   const uint4* k4 = reinterpret_cast<const uint4*>(keys + h0);
-  for (int64_t i = (int64_t)blockIdx.x * HST_T + threadIdx.x; i < n4; i += stride) {
-    const uint4 q = k4[i];
-    add(q.x);
-    add(q.y);
-    add(q.z);
-    add(q.w);
+  // whole waves over chunks of 64 quads (wave-uniform loop bounds), four chunks' loads in flight per round
+  const int64_t nw = stride >> 6, nchunk = n4 >> 6;
+  int64_t c = ((int64_t)blockIdx.x * HST_T + threadIdx.x) >> 6;
+  for (; c + 3 * nw < nchunk; c += 4 * nw) {
+    uint4 q[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) q[r] = k4[(c + r * nw) * 64 + lane];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) add4(q[r]);
   }
+  for (; c < nchunk; c += nw) add4(k4[c * 64 + lane]);
   const int64_t t = (int64_t)blockIdx.x * HST_T + threadIdx.x;
   if (t < h0) add(keys[t]);
-  for (int64_t i = h0 + n4 * 4 + t; i < n; i += stride) add(keys[i]);
+  for (int64_t i = h0 + nchunk * 256 + t; i < n; i += stride) add(keys[i]);
   __syncthreads();
   for (int i = threadIdx.x; i < passes * SRT_BINS; i += HST_T)
     if (h[i]) atomicAdd(&hist[i], (unsigned long long)h[i]);
@@ -114,38 +164,56 @@ __global__ void __launch_bounds__(SRT_BINS) sort_scan_kernel(const unsigned long
   binbase[p * SRT_BINS + d] = block_excl_scan<int64_t>((int64_t)hist[p * SRT_BINS + d], red);
 }
 
+// FLAG pass: one bit per point position marking the first point of a spectrum (sp_off; an empty spectrum marks
+// its successor's start, which that one marks anyway)
+__global__ void __launch_bounds__(256) sort_mark_starts_kernel(const int64_t* __restrict__ sp_off, int64_t n_spectra,
+                                                               int64_t n, uint32_t* __restrict__ bits) {
+  for (int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x; s < n_spectra; s += (int64_t)gridDim.x * 256) {
+    const int64_t o = sp_off[s];
+    if (o < n) atomicOr(&bits[o >> 5], 1u << (o & 31));
+  }
+}
+
 // One LSD pass over digit bits [shift, shift + dbits).  FLAG: the first pass, which also sets the duplicate-
 // candidate flag (bit 31 of the hit) from the dataset-order neighbours.
+// Values go through LDS whole (8-byte words) when a tile's values fit the 64 KB exchange buffer, else as two
+// rounds of 4-byte halves (SPLIT; the second round's loads hit the lines the first one brought into L2).
 template <typename S, bool FLAG>
-__global__ void __launch_bounds__(SRT_T, 4) sort_pass_kernel(const uint32_t* __restrict__ kin,
-                                                          const uint64_t* __restrict__ vin,
-                                                          uint32_t* __restrict__ kout, uint64_t* __restrict__ vout,
-                                                          int64_t n, int shift, int dbits,
-                                                          const int64_t* __restrict__ binbase, S* __restrict__ status,
-                                                          unsigned* __restrict__ ticket, double slack) {
+__global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uint32_t* __restrict__ kin,
+                                                                    const uint64_t* __restrict__ vin,
+                                                                    uint32_t* __restrict__ kout,
+                                                                    uint64_t* __restrict__ vout, int64_t n, int shift,
+                                                                    int dbits, const int64_t* __restrict__ binbase,
+                                                                    S* __restrict__ status,
+                                                                    unsigned* __restrict__ ticket, double slack,
+                                                                    const uint32_t* __restrict__ starts) {
+  constexpr bool SPLIT = SRT_TILE * 8 > 65536;
+  constexpr int XWORDS = 65536 / 8;
   // exchange buffer: the wave histograms (u16 [SRT_WAVES][SRT_BINS]) while ranking, then the tile's keys in digit
-  // order, then its values
-  __shared__ __attribute__((aligned(16))) uint64_t xbuf[SRT_TILE];
+  // order, then its values (or value halves)
+  __shared__ __attribute__((aligned(16))) uint64_t xbuf[XWORDS];
   __shared__ int64_t s_gbase[SRT_BINS];   // global position of the tile's first point of each digit, minus its
   __shared__ uint32_t s_lstart[SRT_BINS]; // local start (so that position = s_gbase[d] + local index)
   __shared__ int64_t s_red[SRT_WAVES];
   __shared__ unsigned s_tile;
+  static_assert(SRT_TILE * 4 <= 65536, "the keys of a tile must fit the exchange buffer");
+  static_assert(SRT_TILE <= 65536, "wave ranks are packed in 16 bits");
   constexpr int SH = StatusBits<S>::SH;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   uint16_t* wh = reinterpret_cast<uint16_t*>(xbuf);
+  uint32_t* xk = reinterpret_cast<uint32_t*>(xbuf);
   reinterpret_cast<uint4*>(xbuf)[tid] = make_uint4(0u, 0u, 0u, 0u);  // 512 x 16 B: the 8 KB of wave histograms
   if (tid == 0) s_tile = atomicAdd(ticket, 1u);
   __syncthreads();
   const int64_t t = s_tile;
   const int64_t base = t * SRT_TILE;
-  const int64_t wbase = base + (int64_t)w * (64 * SRT_IPT);  // a wave's points: 16 rows of 64 consecutive points
+  const int64_t wbase = base + (int64_t)w * (64 * SRT_IPT);  // a wave's points: SRT_IPT rows of 64 consecutive
   const uint32_t mask = (1u << dbits) - 1u;
   const int nb = 1 << dbits;
-
-  // keys first; the values are loaded after the ranking (they are not needed before the exchange, and holding
-  // them through it would spill).  Past the end: the last digit, after every real point of the tile (never
-  // stored); the loads of the last tile are clamped to the last point.
   const bool full = base + SRT_TILE <= n;
+
+  // keys first; the values are loaded after the ranking (held through it with the keys, they would spill).  Past
+  // the end: the last digit, after every real point of the tile (never stored).
   uint32_t k[SRT_IPT];
   if (full) {
 #pragma unroll
@@ -160,56 +228,36 @@ __global__ void __launch_bounds__(SRT_T, 4) sort_pass_kernel(const uint32_t* __r
 
   uint32_t fmask = 0;  // FLAG: bit u = the duplicate-candidate flag of the thread's point u
   if constexpr (FLAG) {
-    // the tile's keys and pixels through LDS in dataset order (the exchange buffer is free until ranking); the
-    // points just outside the tile come from memory
-    uint32_t* fk = reinterpret_cast<uint32_t*>(xbuf);
-    uint32_t* fp = fk + SRT_TILE;
-    const uint32_t* vlo = reinterpret_cast<const uint32_t*>(vin);  // the hits' low words: pixel | flag << 31
+    static_assert(SRT_IPT <= 32, "one flag bit per point in a 32-bit mask");
+    static_assert(SRT_TILE * 4 + (SRT_TILE / 32 + 1) * 4 <= 65536, "keys and spectrum-start bits share the buffer");
+    // the tile's keys in dataset order and its spectrum-start bits for positions [0, SRT_TILE] (tiles start on
+    // a word boundary); the points just outside the tile from memory
+    uint32_t* sb = xk + SRT_TILE;
     const int64_t ia = base - 1, ib = base + SRT_TILE;
-    uint32_t ka = 0, pa = 0xFFFFFFFFu, kb = 0, pb = 0xFFFFFFFFu;  // 0xFFFFFFFF: no neighbour (pixels are 31-bit)
-    if (ia >= 0) {
-      ka = kin[ia];
-      pa = vlo[2 * ia] & 0x7FFFFFFFu;
-    }
-    if (ib < n) {
-      kb = kin[ib];
-      pb = vlo[2 * ib] & 0x7FFFFFFFu;
-    }
-    uint32_t px[SRT_IPT];
-    if (full) {
-#pragma unroll
-      for (int u = 0; u < SRT_IPT; ++u) px[u] = vlo[2 * (wbase + u * 64 + lane)];
-    } else {
-#pragma unroll
-      for (int u = 0; u < SRT_IPT; ++u) {
-        const int64_t i = wbase + u * 64 + lane;
-        px[u] = i < n ? vlo[2 * i] : 0xFFFFFFFFu;
-      }
+    uint32_t ka = 0, kb = 0;
+    if (ia >= 0) ka = kin[ia];
+    if (ib < n) kb = kin[ib];
+    const int64_t nwords = (n + 31) >> 5;
+    for (int i = tid; i <= SRT_TILE / 32; i += SRT_T) {
+      const int64_t wi = (base >> 5) + i;
+      sb[i] = wi < nwords ? starts[wi] : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < SRT_IPT; ++u) {
-      const int p = w * (64 * SRT_IPT) + u * 64 + lane;
-      fk[p] = k[u];
-      fp[p] = px[u] & 0x7FFFFFFFu;
-    }
+    for (int u = 0; u < SRT_IPT; ++u) xk[w * (64 * SRT_IPT) + u * 64 + lane] = k[u];
     __syncthreads();
-    // (everything from LDS, in a rolled loop: unrolled, the compiler overlaps all sixteen and spills)
+    auto start = [&](int p) { return (sb[p >> 5] >> (p & 31)) & 1u; };
+    // in a rolled loop reading everything from LDS (unrolled, the compiler overlaps all the points and spills)
 #pragma unroll 2
     for (int u = 0; u < SRT_IPT; ++u) {
       const int p = w * (64 * SRT_IPT) + u * 64 + lane;
       const int64_t i = base + p;
-      const uint32_t pix = fp[p];
-      const uint32_t kp = p > 0 ? fk[p - 1] : ka, pp = p > 0 ? fp[p - 1] : pa;
-      uint32_t kn = p + 1 < SRT_TILE ? fk[p + 1] : kb, pn = p + 1 < SRT_TILE ? fp[p + 1] : pb;
-      if (i + 1 >= n) pn = 0xFFFFFFFFu;
-      // the flag pass's test (smg_prep.hip flag_tile_store), in f64
-      const double m = (double)__uint_as_float(fk[p]);
-      bool f = pp == pix && m - (double)__uint_as_float(kp) <= slack * m;
-      if (pn == pix) {
-        const double m2 = (double)__uint_as_float(kn);
-        f = f || (m2 - m <= slack * m2);
-      }
-      fmask |= (uint32_t)(f && i < n) << u;
+      const uint32_t kp = p > 0 ? xk[p - 1] : ka, kn = p + 1 < SRT_TILE ? xk[p + 1] : kb;
+      // the flag pass's test (smg_prep.hip flag_tile_store): the spectrum's previous / next point within one
+      // window width, in f64
+      const double m = (double)__uint_as_float(xk[p]), m2 = (double)__uint_as_float(kn);
+      const bool fp = i > 0 && !start(p) && m - (double)__uint_as_float(kp) <= slack * m;
+      const bool fn = i + 1 < n && !start(p + 1) && m2 - m <= slack * m2;
+      fmask |= (uint32_t)((fp || fn) && i < n) << u;
     }
     __syncthreads();
     reinterpret_cast<uint4*>(xbuf)[tid] = make_uint4(0u, 0u, 0u, 0u);  // the wave histograms again
@@ -234,7 +282,7 @@ __global__ void __launch_bounds__(SRT_T, 4) sort_pass_kernel(const uint32_t* __r
     const uint32_t below = (uint32_t)__popcll(peers & lt);
     const uint32_t old = myh[d];
     if (below == 0) myh[d] = (uint16_t)(old + (uint32_t)__popcll(peers));
-    rk[u] = old + below;
+    rk[u] = (old + below) | (d << 16);  // the digit rides along (one register per point, not two)
   }
   __syncthreads();
 
@@ -254,16 +302,29 @@ __global__ void __launch_bounds__(SRT_T, 4) sort_pass_kernel(const uint32_t* __r
   if (d < nb) {
     int64_t excl = 0;
     if (t > 0) {
+      // SMG_SRT_LB earlier tiles' words loaded together per round trip, consumed newest first until an inclusive
+      // prefix; a word not yet published ends the round (the ones before it are kept, the walk resumes there)
       for (int64_t j = t - 1;;) {
-        const S s = status_load(status + j * SRT_BINS + d);
-        const uint32_t fl = (uint32_t)(s >> SH);
-        if (fl == 0) {
-          __builtin_amdgcn_s_sleep(1);
-          continue;
+        S sw[SMG_SRT_LB];
+#pragma unroll
+        for (int q = 0; q < SMG_SRT_LB; ++q)
+          sw[q] = j - q >= 0 ? status_load(status + (j - q) * SRT_BINS + d) : (S)((S)2 << SH);
+        int used = SMG_SRT_LB;
+        bool done = false;
+#pragma unroll
+        for (int q = 0; q < SMG_SRT_LB; ++q) {
+          if (done || used < SMG_SRT_LB) continue;
+          const uint32_t fl = (uint32_t)(sw[q] >> SH);
+          if (fl == 0) {
+            used = q;
+            continue;
+          }
+          excl += (int64_t)(sw[q] & (((S)1 << SH) - 1));
+          if (fl == 2) done = true;
         }
-        excl += (int64_t)(s & (((S)1 << SH) - 1));
-        if (fl == 2) break;
-        --j;
+        if (done) break;
+        j -= used;
+        if (used < SMG_SRT_LB) __builtin_amdgcn_s_sleep(1);
       }
       status_store(status + t * SRT_BINS + d, (S)((S)2 << SH) | (S)(excl + cnt));
     }
@@ -275,46 +336,85 @@ __global__ void __launch_bounds__(SRT_T, 4) sort_pass_kernel(const uint32_t* __r
   // local index of each point in digit order, then the keys through LDS
 #pragma unroll
   for (int u = 0; u < SRT_IPT; ++u) {
-    const uint32_t dd = (k[u] >> shift) & mask;
-    rk[u] += s_lstart[dd] + wh[w * SRT_BINS + dd];
+    const uint32_t dd = rk[u] >> 16;
+    rk[u] = (rk[u] & 0xFFFFu) + s_lstart[dd] + wh[w * SRT_BINS + dd];
   }
   __syncthreads();  // the wave histograms are overwritten below
-  uint32_t* xk = reinterpret_cast<uint32_t*>(xbuf);
 #pragma unroll
   for (int u = 0; u < SRT_IPT; ++u) xk[rk[u]] = k[u];
   __syncthreads();
   const int64_t left = n - base;
   const int nvalid = left < SRT_TILE ? (int)left : SRT_TILE;
+  uint32_t dj[(SRT_IPT + 1) / 2];  // the digit of each slot this thread stores, two per word
 #pragma unroll
   for (int u = 0; u < SRT_IPT; ++u) {
     const int j = u * SRT_T + tid;
-    k[u] = xk[j];
-    if (j < nvalid) kout[s_gbase[(k[u] >> shift) & mask] + j] = k[u];
+    const uint32_t kk = xk[j];
+    const uint32_t dd = (kk >> shift) & mask;
+    if (u & 1)
+      dj[u >> 1] |= dd << 16;
+    else
+      dj[u >> 1] = dd;
+    if (j < nvalid) kout[s_gbase[dd] + j] = kk;
   }
-  // the values (loaded this late: holding them through the ranking and the key exchange would spill)
-  uint64_t v[SRT_IPT];
-  if (full) {
+  auto slot_digit = [&](int u) { return (dj[u >> 1] >> ((u & 1) * 16)) & 0xFFFFu; };
+
+  if constexpr (!SPLIT) {
+    // the values (not loaded before: with the keys they would spill)
+    uint64_t v[SRT_IPT];
+    if (full) {
 #pragma unroll
-    for (int u = 0; u < SRT_IPT; ++u) v[u] = vin[wbase + u * 64 + lane];
-  } else {
+      for (int u = 0; u < SRT_IPT; ++u) v[u] = vin[wbase + u * 64 + lane];
+    } else {
+#pragma unroll
+      for (int u = 0; u < SRT_IPT; ++u) {
+        const int64_t i = wbase + u * 64 + lane;
+        v[u] = i < n ? vin[i] : 0ull;
+      }
+    }
+    __syncthreads();
 #pragma unroll
     for (int u = 0; u < SRT_IPT; ++u) {
-      const int64_t i = wbase + u * 64 + lane;
-      v[u] = i < n ? vin[i] : 0ull;
+      uint64_t x = v[u];
+      if constexpr (FLAG) x = ((fmask >> u) & 1u) ? (x | 0x80000000ull) : (x & ~0x80000000ull);
+      xbuf[rk[u]] = x;
     }
-  }
-  __syncthreads();
+    __syncthreads();
 #pragma unroll
-  for (int u = 0; u < SRT_IPT; ++u) {
-    uint64_t x = v[u];
-    if constexpr (FLAG) x = ((fmask >> u) & 1u) ? (x | 0x80000000ull) : (x & ~0x80000000ull);
-    xbuf[rk[u]] = x;
-  }
-  __syncthreads();
+    for (int u = 0; u < SRT_IPT; ++u) {
+      const int j = u * SRT_T + tid;
+      if (j < nvalid) vout[s_gbase[slot_digit(u)] + j] = xbuf[j];
+    }
+  } else {
+    const uint32_t* vw = reinterpret_cast<const uint32_t*>(vin);
+    uint32_t* ow = reinterpret_cast<uint32_t*>(vout);
 #pragma unroll
-  for (int u = 0; u < SRT_IPT; ++u) {
-    const int j = u * SRT_T + tid;
-    if (j < nvalid) vout[s_gbase[(k[u] >> shift) & mask] + j] = xbuf[j];
+    for (int half = 0; half < 2; ++half) {
+      uint32_t v[SRT_IPT];
+      if (full) {
+#pragma unroll
+        for (int u = 0; u < SRT_IPT; ++u) v[u] = vw[2 * (wbase + u * 64 + lane) + half];
+      } else {
+#pragma unroll
+        for (int u = 0; u < SRT_IPT; ++u) {
+          const int64_t i = wbase + u * 64 + lane;
+          v[u] = i < n ? vw[2 * i + half] : 0u;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < SRT_IPT; ++u) {
+        uint32_t x = v[u];
+        if (FLAG && half == 0) x = ((fmask >> u) & 1u) ? (x | 0x80000000u) : (x & ~0x80000000u);
+        xk[rk[u]] = x;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < SRT_IPT; ++u) {
+        const int j = u * SRT_T + tid;
+        if (j < nvalid) ow[2 * (s_gbase[slot_digit(u)] + j) + half] = xk[j];
+      }
+    }
   }
 }
 
@@ -323,7 +423,7 @@ struct SortPlan {
   int passes, dbits;
   int64_t ntiles;
   bool wide;  // 64-bit look-back words
-  size_t off_hist, off_base, off_status, status_bytes, off_tk, off_tv, total;
+  size_t off_hist, off_base, off_status, status_bytes, off_s0, start_bytes, off_tk, off_tv, total;
 };
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -341,7 +441,9 @@ static SortPlan sort_plan(int64_t n, int key_bits) {
   p.off_base = p.off_hist + SRT_MAXP * SRT_BINS * 8;
   p.off_status = p.off_base + SRT_MAXP * SRT_BINS * 8;
   p.status_bytes = (size_t)p.passes * (size_t)p.ntiles * SRT_BINS * sw;
-  p.off_tk = align_up(p.off_status + p.status_bytes, 256);
+  p.off_s0 = align_up(p.off_status + p.status_bytes, 256);  // FLAG pass: spectrum-start bits
+  p.start_bytes = (size_t)((n + 31) / 32 + 2) * 4;
+  p.off_tk = align_up(p.off_s0 + p.start_bytes, 256);
   p.off_tv = align_up(p.off_tk + (size_t)n * 4, 256);
   p.total = p.off_tv + (size_t)n * 8;
   return p;
@@ -392,6 +494,7 @@ static int roc_workspace(int64_t n, size_t* bytes) {
 template <typename S>
 static int run_passes(const SortPlan& P, const uint32_t* mz, const uint64_t* hits, int64_t n, uint32_t* ko,
                       uint64_t* vo, unsigned char* ws, bool flag, double slack, hipStream_t st) {
+  const uint32_t* starts = reinterpret_cast<const uint32_t*>(ws + P.off_s0);
   unsigned* tickets = reinterpret_cast<unsigned*>(ws);
   const int64_t* binbase = reinterpret_cast<const int64_t*>(ws + P.off_base);
   S* status = reinterpret_cast<S*>(ws + P.off_status);
@@ -407,10 +510,10 @@ static int run_passes(const SortPlan& P, const uint32_t* mz, const uint64_t* hit
     S* sp = status + (size_t)p * P.ntiles * SRT_BINS;
     if (flag && p == 0)
       hipLaunchKernelGGL((sort_pass_kernel<S, true>), dim3((unsigned)P.ntiles), dim3(SRT_T), 0, st, ki, vi, kdst,
-                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, slack);
+                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, slack, starts);
     else
       hipLaunchKernelGGL((sort_pass_kernel<S, false>), dim3((unsigned)P.ntiles), dim3(SRT_T), 0, st, ki, vi, kdst,
-                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, slack);
+                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, slack, nullptr);
     SMG_LAUNCH_CHECK();
     ki = kdst;
     vi = vdst;
@@ -420,7 +523,7 @@ static int run_passes(const SortPlan& P, const uint32_t* mz, const uint64_t* hit
 
 static int native_sort(const float* mz, const uint64_t* hits, int64_t n, int key_bits, float* mz_sorted,
                        uint64_t* hits_sorted, void* workspace, size_t workspace_bytes, bool flag, double ppm,
-                       hipStream_t st) {
+                       const int64_t* sp_off, int64_t n_spectra, hipStream_t st) {
   const SortPlan P = sort_plan(n, key_bits);
   if (workspace_bytes < P.total) {
     set_error("sort workspace too small: %zu < %zu", workspace_bytes, P.total);
@@ -443,6 +546,14 @@ static int native_sort(const float* mz, const uint64_t* hits, int64_t n, int key
                      reinterpret_cast<const unsigned long long*>(ws + P.off_hist),
                      reinterpret_cast<int64_t*>(ws + P.off_base));
   SMG_LAUNCH_CHECK();
+  if (flag) {
+    SMG_HIP(hipMemsetAsync(ws + P.off_s0, 0, P.start_bytes, st));
+    int64_t g = (n_spectra + 255) / 256;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(sort_mark_starts_kernel, dim3((unsigned)g), dim3(256), 0, st, sp_off, n_spectra, n,
+                       reinterpret_cast<uint32_t*>(ws + P.off_s0));
+    SMG_LAUNCH_CHECK();
+  }
   const double slack = 2.0 * ppm * 1e-6 / (1.0 - ppm * 1e-6) * (1.0 + 1e-9);
   uint32_t* ko = reinterpret_cast<uint32_t*>(mz_sorted);
   return P.wide ? run_passes<unsigned long long>(P, keys, hits, n, ko, hits_sorted, ws, flag, slack, st)
@@ -498,18 +609,20 @@ int smg_sort_points(const float* mz, const uint64_t* hits, int64_t n_points, int
     return SMG_OK;
   }
   return native_sort(mz, hits, n_points, key_bits, mz_sorted, hits_sorted, workspace, workspace_bytes, false, 0.0,
-                     as_stream(stream));
+                     nullptr, 0, as_stream(stream));
 }
 
-int smg_sort_points_flag(const float* mz, const uint64_t* hits, int64_t n_points, int32_t key_bits, double ppm,
-                         float* mz_sorted, uint64_t* hits_sorted, void* workspace, size_t workspace_bytes,
-                         void* stream) {
+int smg_sort_points_flag(const int64_t* sp_off, int64_t n_spectra, const float* mz, const uint64_t* hits,
+                         int64_t n_points, int32_t key_bits, double ppm, float* mz_sorted, uint64_t* hits_sorted,
+                         void* workspace, size_t workspace_bytes, void* stream) {
   SMG_CHECK_ARG(ppm >= 0 && ppm < 1e6, "bad ppm");
+  SMG_CHECK_ARG(n_spectra >= 1 || n_points == 0, "a dataset with points has spectra");
+  SMG_CHECK_ARG(sp_off != nullptr || n_points == 0, "null sp_off");
   size_t need = 0;
   int rc = sort_args(mz, hits, n_points, &key_bits, mz_sorted, hits_sorted, workspace, workspace_bytes, &need);
   if (rc || n_points == 0) return rc;
   return native_sort(mz, hits, n_points, key_bits, mz_sorted, hits_sorted, workspace, workspace_bytes, true, ppm,
-                     as_stream(stream));
+                     sp_off, n_spectra, as_stream(stream));
 }
 
 int smg_debug_sort_impl(int32_t which) {

@@ -211,17 +211,19 @@ class DevicePeaks:
         check(call(ws), name)
 
     def flag_and_sort(self, ppm: float, stream=None) -> "DevicePeaks":
-        """flag_duplicates(ppm) then sort(), as one pass less: the sort's first pass sets the flags from each
-        point's dataset neighbours with the same pixel (smg_sort_points_flag), which are its spectrum neighbours
-        when every spectrum is m/z-sorted and no pixel is shared.  Otherwise (and on a slice whose copy set the
-        flags) the separate flag pass, then the sort."""
+        """flag_duplicates(ppm) then sort(), with one pass less: the sort's first pass sets the flags from each
+        point's spectrum neighbours (smg_sort_points_flag), the same flags as the flag pass when every spectrum is
+        m/z-sorted and no pixel is shared.  Otherwise (and on a slice whose copy set the flags) the separate flag
+        pass, then the sort."""
         preset = self.flags_preset_ppm is not None and float(ppm) == self.flags_preset_ppm
         if self.sp_off is None or self.force is not None or preset or not self.spectra_sorted():
             self.flag_duplicates(ppm, stream)
             return self.sort(stream)
+        n_sp = int(self.sp_off.numel()) - 1
         self._sort_into(lambda ws: lib().smg_sort_points_flag(
-            _p(self.mz), _p(self.hits), self.n_points, self.key_bits(), float(ppm), _p(self.mz_sorted),
-            _p(self.hits_sorted), _p(ws), ws.numel(), _stream(stream)), "smg_sort_points_flag", stream)
+            _p(self.sp_off), n_sp, _p(self.mz), _p(self.hits), self.n_points, self.key_bits(), float(ppm),
+            _p(self.mz_sorted), _p(self.hits_sorted), _p(ws), ws.numel(), _stream(stream)), "smg_sort_points_flag",
+            stream)
         self.flag_ppm = float(ppm)
         return self
 

@@ -160,3 +160,35 @@ def test_unsorted_spectrum_takes_flag_pass():
     h = p.hits_sorted.cpu().numpy()
     pix = h & 0x7FFFFFFF
     assert ((h[pix == 1] >> 31) & 1).all()
+
+
+@pytest.mark.parametrize("sizes", ["ragged", "long"])
+def test_fused_flags_ragged_spectra(sizes):
+    """Spectrum starts marked per tile from sp_off: empty spectra, one-point spectra, many spectra per 8192-point
+    tile, and spectra longer than a tile; flags identical to the flag pass."""
+    import torch
+    from sm_distributed_amd import engine as E
+    rng = np.random.default_rng(17)
+    if sizes == "ragged":
+        cnt = rng.choice([0, 0, 1, 2, 3, 7, 40, 300], size=60_000)
+    else:
+        cnt = rng.integers(5_000, 30_000, size=40)
+    sp_off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+    n = int(sp_off[-1])
+    mz = rng.uniform(100.0, 100.4 if sizes == "ragged" else 1000.0, n)  # both flagged and unflagged points
+    for s in range(len(cnt)):
+        mz[sp_off[s]:sp_off[s + 1]].sort()
+    ints = rng.uniform(1, 10, n).astype(np.float32)
+    pm = np.arange(len(cnt), dtype=np.int32)
+    dims = (1, len(cnt))
+    p = E.DevicePeaks.from_arrays(sp_off, mz.astype(np.float32), ints, pm, dims)
+    assert p.force is None and p.spectra_sorted()
+    p.flag_and_sort(50.0)
+    torch.cuda.synchronize()
+    fused = p.hits_sorted.clone()
+    p.flag_duplicates(50.0)
+    p.sort()
+    torch.cuda.synchronize()
+    assert torch.equal(fused, p.hits_sorted)
+    flagged = int(((fused >> 31) & 1).sum().item())
+    assert 0 < flagged < n
