@@ -258,6 +258,9 @@ def main():
     if len(per_step):
         log(f"[rank {rank}] step ms: min {per_step.min():.2f} median {np.median(per_step):.2f} "
             f"max {per_step.max():.2f}")
+        if os.environ.get("SMG_BENCH_VERBOSE"):
+            log(f"[rank {rank}] steps: " + " ".join(f"{x:.1f}" for x in per_step))
+            log(f"[rank {rank}] pass launches (pass:ms): " + " ".join(f"{p}:{t:.2f}" for p, t in pass_ms))
     # one more search with the host-side caches dropped (the theoretical-intensity alignment and the shard's
     # global row index are reused between steps while the ion keys are unchanged): a cold first search of a
     # new formula table in a warm process

@@ -324,40 +324,135 @@ __global__ void stream_read_kernel(const uint64_t* __restrict__ p, int64_t n, ui
 // points without the duplicate-candidate flag: a flagged point may share its pixel with another point of the
 // window and is squared after the per-pixel sum (ion kernel).  One wave per block: a coalesced 512-B read, a
 // fixed-order DPP reduction (plain f64: its error is relative to the block's own 64 points).
-// Each wave takes BS_PER_WAVE consecutive 64-point blocks and has all their loads in flight at once.
+// Each wave takes BS_PER_WAVE consecutive 64-point blocks and has all their loads in flight at once
+// (chunk_sums_kernel below).
 constexpr int BS_PER_WAVE = 8;
 
+
+// Prefix sums of the block sums without a library scan (reduce, then scan): the 64-point blocks in chunks of
+// PS_CHUNK; chunk_sums_kernel writes every block's sums (one wave per block, as described above) and each chunk's
+// double-double total, chunk_base_kernel scans the chunk totals, chunk_scan_kernel scans each chunk from its
+// base.  Every sum is formed in one fixed order: the result does not depend on scheduling.
+constexpr int PS_CHUNK = 2048;            // 64-point blocks per chunk
+constexpr int PS_T = 256;                 // threads per chunk workgroup
+constexpr int PS_BPT = PS_CHUNK / PS_T;   // blocks per thread in the scan
+static_assert(PS_CHUNK % (4 * BS_PER_WAVE) == 0, "waves take whole groups of blocks");
+
+__device__ __forceinline__ DD4 dd4_add(const DD4& a, const DD4& b) { return DD4Add()(a, b); }
+__device__ __forceinline__ DD4 dd4_shfl_up(const DD4& v, int o) {
+  return DD4{__shfl_up(v.xh, o, 64), __shfl_up(v.xl, o, 64), __shfl_up(v.yh, o, 64), __shfl_up(v.yl, o, 64)};
+}
+
 template <int FMT>
-__global__ void __launch_bounds__(256) block_sums64_kernel(const void* __restrict__ hits,
-                                                           const double* __restrict__ hit_vals, int64_t n,
-                                                           DD4* __restrict__ out) {
-  const int64_t blk0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * BS_PER_WAVE;
-  const int lane = threadIdx.x & 63;
+__global__ void __launch_bounds__(PS_T) chunk_sums_kernel(const void* __restrict__ hits,
+                                                          const double* __restrict__ hit_vals, int64_t n,
+                                                          DD4* __restrict__ bs, DD4* __restrict__ ctot) {
+  __shared__ DD4 wt[PS_T / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t nblk = (n + 63) >> 6;
-  if (blk0 >= nblk) return;  // whole waves exit together
-  double v[BS_PER_WAVE];
-  bool dup[BS_PER_WAVE];
+  const int64_t c0 = (int64_t)blockIdx.x * PS_CHUNK;
+  DD4 acc{0.0, 0.0, 0.0, 0.0};  // lane 0: this wave's blocks, in order
+  constexpr int PER_WAVE = PS_CHUNK / (PS_T / 64);
+  for (int g = 0; g < PER_WAVE; g += BS_PER_WAVE) {
+    const int64_t blk0 = c0 + (int64_t)w * PER_WAVE + g;
+    if (blk0 >= nblk) break;  // wave-uniform
+    double v[BS_PER_WAVE];
+    bool dup[BS_PER_WAVE];
 #pragma unroll
-  for (int j = 0; j < BS_PER_WAVE; ++j) {
-    const int64_t i = (blk0 + j) * 64 + lane;
-    v[j] = 0.0;
-    dup[j] = false;
-    if (i < n) {
-      if constexpr (FMT == SMG_HITS_PACKED_F32) {
-        const uint64_t h = reinterpret_cast<const uint64_t*>(hits)[i];
-        v[j] = (double)__uint_as_float((uint32_t)(h >> 32));
-        dup[j] = ((uint32_t)h >> 31) != 0u;
-      } else {
-        v[j] = hit_vals[i];
-        dup[j] = (reinterpret_cast<const uint32_t*>(hits)[i] >> 31) != 0u;
+    for (int j = 0; j < BS_PER_WAVE; ++j) {
+      const int64_t i = (blk0 + j) * 64 + lane;
+      v[j] = 0.0;
+      dup[j] = false;
+      if (i < n) {
+        if constexpr (FMT == SMG_HITS_PACKED_F32) {
+          const uint64_t h = reinterpret_cast<const uint64_t*>(hits)[i];
+          v[j] = (double)__uint_as_float((uint32_t)(h >> 32));
+          dup[j] = ((uint32_t)h >> 31) != 0u;
+        } else {
+          v[j] = hit_vals[i];
+          dup[j] = (reinterpret_cast<const uint32_t*>(hits)[i] >> 31) != 0u;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < BS_PER_WAVE; ++j) {
+      const double a = wave_sum_dpp(v[j]), b = wave_sum_dpp(dup[j] ? 0.0 : v[j] * v[j]);
+      if (lane == 0 && blk0 + j < nblk) {
+        const DD4 d{a, 0.0, b, 0.0};
+        bs[blk0 + j] = d;
+        acc = dd4_add(acc, d);
       }
     }
   }
+  if (lane == 0) wt[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    DD4 t = wt[0];
 #pragma unroll
-  for (int j = 0; j < BS_PER_WAVE; ++j) {
-    const double a = wave_sum_dpp(v[j]), b = wave_sum_dpp(dup[j] ? 0.0 : v[j] * v[j]);
-    if (lane == 0 && blk0 + j < nblk) out[blk0 + j] = DD4{a, 0.0, b, 0.0};
+    for (int i = 1; i < PS_T / 64; ++i) t = dd4_add(t, wt[i]);
+    ctot[blockIdx.x] = t;
   }
+}
+
+// exclusive scan of the chunk totals in one workgroup: each thread a run of chunks, then the thread totals
+constexpr int PSB_T = 1024;
+__global__ void __launch_bounds__(PSB_T) chunk_base_kernel(const DD4* __restrict__ ctot, int64_t nch,
+                                                           DD4* __restrict__ cbase) {
+  __shared__ DD4 tt[PSB_T];
+  const int t = threadIdx.x;
+  const int64_t per = (nch + PSB_T - 1) / PSB_T;
+  const int64_t a = t * per, b = a + per < nch ? a + per : nch;
+  DD4 s{0.0, 0.0, 0.0, 0.0};
+  for (int64_t i = a; i < b; ++i) s = dd4_add(s, ctot[i]);
+  tt[t] = s;
+  __syncthreads();
+  if (t == 0) {  // exclusive prefix of the thread totals, in order
+    DD4 run{0.0, 0.0, 0.0, 0.0};
+    for (int i = 0; i < PSB_T; ++i) {
+      const DD4 x = tt[i];
+      tt[i] = run;
+      run = dd4_add(run, x);
+    }
+  }
+  __syncthreads();
+  DD4 run = tt[t];
+  for (int64_t i = a; i < b; ++i) {
+    cbase[i] = run;
+    run = dd4_add(run, ctot[i]);
+  }
+}
+
+// each chunk's inclusive prefixes from its base: a thread scans PS_BPT consecutive blocks, the thread totals are
+// combined in order through the waves and the LDS; out[b] = sums over blocks [0, b]
+__global__ void __launch_bounds__(PS_T) chunk_scan_kernel(const DD4* __restrict__ bs, const DD4* __restrict__ cbase,
+                                                          int64_t nblk, DD4* __restrict__ out) {
+  __shared__ DD4 wt[PS_T / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b0 = (int64_t)blockIdx.x * PS_CHUNK + (int64_t)threadIdx.x * PS_BPT;
+  DD4 loc[PS_BPT];
+  DD4 s{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int j = 0; j < PS_BPT; ++j) {
+    const DD4 x = b0 + j < nblk ? bs[b0 + j] : DD4{0.0, 0.0, 0.0, 0.0};
+    s = dd4_add(s, x);
+    loc[j] = s;
+  }
+  // exclusive prefix of the thread totals within the wave (in lane order), then across the waves
+  DD4 incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const DD4 y = dd4_shfl_up(incl, o);
+    if (lane >= o) incl = dd4_add(y, incl);
+  }
+  if (lane == 63) wt[w] = incl;
+  __syncthreads();
+  DD4 base = cbase[blockIdx.x];
+  for (int i = 0; i < w; ++i) base = dd4_add(base, wt[i]);
+  DD4 ex = dd4_shfl_up(incl, 1);
+  if (lane > 0) base = dd4_add(base, ex);
+#pragma unroll
+  for (int j = 0; j < PS_BPT; ++j)
+    if (b0 + j < nblk) out[b0 + j] = dd4_add(base, loc[j]);
 }
 
 }  // namespace smg
@@ -532,20 +627,11 @@ int smg_debug_stream_read(const uint64_t* data, int64_t n_words, uint64_t* out, 
   return SMG_OK;
 }
 
-static hipError_t block_scan(void* tmp, size_t& bytes, const DD4* in, DD4* out, int64_t nblk, hipStream_t st) {
-  return rocprim::inclusive_scan(tmp, bytes, in, out, (size_t)nblk, DD4Add(), st, false);
-}
-
 int smg_hit_prefix_sums_workspace_size(int64_t n_points, size_t* bytes) {
   SMG_CHECK_ARG(bytes != nullptr && n_points >= 0, "bad arguments");
-  const int64_t nblk = (n_points + 63) / 64;
-  size_t b0 = 0;
-  hipError_t e = block_scan(nullptr, b0, nullptr, nullptr, nblk > 0 ? nblk : 1, 0);
-  if (e != hipSuccess) {
-    set_error("rocprim scan workspace query failed: %s", hipGetErrorString(e));
-    return SMG_ERR_HIP;
-  }
-  *bytes = 256 + ((size_t)(nblk > 0 ? nblk : 1) * sizeof(DD4) + 255) / 256 * 256 + b0;
+  const int64_t nblk = (n_points + 63) / 64 > 0 ? (n_points + 63) / 64 : 1;
+  const int64_t nch = (nblk + PS_CHUNK - 1) / PS_CHUNK;
+  *bytes = 256 + ((size_t)nblk * sizeof(DD4) + 255) / 256 * 256 + 2 * (((size_t)nch * sizeof(DD4) + 255) / 256 * 256);
   return SMG_OK;
 }
 
@@ -566,19 +652,29 @@ int smg_hit_prefix_sums(int32_t hit_format, const void* hits, const double* hit_
     return SMG_ERR_WORKSPACE;
   }
   const int64_t nblk = (n_points + 63) / 64;
-  DD4* bs = reinterpret_cast<DD4*>(reinterpret_cast<unsigned char*>(workspace) + 256);
-  unsigned char* tmp = reinterpret_cast<unsigned char*>(bs) + ((size_t)nblk * sizeof(DD4) + 255) / 256 * 256;
-  size_t tb = need - (size_t)(tmp - reinterpret_cast<unsigned char*>(workspace));
-  const int64_t nwaves = (nblk + BS_PER_WAVE - 1) / BS_PER_WAVE;
-  const int64_t grid = (nwaves * 64 + 255) / 256;
+  const int64_t nch = (nblk + PS_CHUNK - 1) / PS_CHUNK;
+  if (nch > 0x7FFFFFFF) {
+    set_error("too many points for one prefix sum: %lld", (long long)n_points);
+    return SMG_ERR_UNSUPPORTED;
+  }
+  unsigned char* p = reinterpret_cast<unsigned char*>(workspace) + 256;
+  DD4* bs = reinterpret_cast<DD4*>(p);
+  p += ((size_t)nblk * sizeof(DD4) + 255) / 256 * 256;
+  DD4* ctot = reinterpret_cast<DD4*>(p);
+  p += ((size_t)nch * sizeof(DD4) + 255) / 256 * 256;
+  DD4* cbase = reinterpret_cast<DD4*>(p);
   if (hit_format == SMG_HITS_PACKED_F32)
-    hipLaunchKernelGGL(block_sums64_kernel<SMG_HITS_PACKED_F32>, dim3((unsigned)grid), dim3(256), 0, st, hits,
-                       hit_vals, n_points, bs);
+    hipLaunchKernelGGL(chunk_sums_kernel<SMG_HITS_PACKED_F32>, dim3((unsigned)nch), dim3(PS_T), 0, st, hits,
+                       hit_vals, n_points, bs, ctot);
   else
-    hipLaunchKernelGGL(block_sums64_kernel<SMG_HITS_SPLIT_F64>, dim3((unsigned)grid), dim3(256), 0, st, hits,
-                       hit_vals, n_points, bs);
+    hipLaunchKernelGGL(chunk_sums_kernel<SMG_HITS_SPLIT_F64>, dim3((unsigned)nch), dim3(PS_T), 0, st, hits,
+                       hit_vals, n_points, bs, ctot);
   SMG_LAUNCH_CHECK();
-  SMG_HIP(block_scan(tmp, tb, bs, reinterpret_cast<DD4*>(cum64) + 1, nblk, st));
+  hipLaunchKernelGGL(chunk_base_kernel, dim3(1), dim3(PSB_T), 0, st, ctot, nch, cbase);
+  SMG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(chunk_scan_kernel, dim3((unsigned)nch), dim3(PS_T), 0, st, bs, cbase, nblk,
+                     reinterpret_cast<DD4*>(cum64) + 1);
+  SMG_LAUNCH_CHECK();
   return SMG_OK;
 }
 

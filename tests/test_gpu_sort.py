@@ -192,3 +192,31 @@ def test_fused_flags_ragged_spectra(sizes):
     assert torch.equal(fused, p.hits_sorted)
     flagged = int(((fused >> 31) & 1).sum().item())
     assert 0 < flagged < n
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 131072 * 3 + 77, 5_000_000])
+def test_prefix_sums_match_exact_sums(n):
+    """smg_hit_prefix_sums (chunked double-double scan): every block prefix (sum v, sum v^2 of unflagged points)
+    equals the exactly rounded sum over the points before it (math.fsum) to ~1e-15 relative, whatever the
+    chunk boundaries and a dynamic range of 1e-3..1e9."""
+    import math
+
+    import torch
+    from sm_distributed_amd import _lib
+    from sm_distributed_amd import engine as E
+    rng = np.random.default_rng(n)
+    v = (10.0 ** rng.uniform(-3, 9, n)).astype(np.float32)
+    flag = rng.random(n) < 0.1
+    hits = (v.view(np.uint32).astype(np.uint64) << np.uint64(32)) | (flag.astype(np.uint64) << np.uint64(31))
+    d_hits = torch.from_numpy(hits.view(np.int64)).cuda()
+    cum = E.hit_prefix_sums(_lib.SMG_HITS_PACKED_F32, d_hits, None, n).cpu().numpy()
+    nb = (n + 63) // 64
+    assert cum.shape == (nb + 1, 4)
+    vd = v.astype(np.float64)
+    check = sorted({0, 1, nb // 2, nb - 1, nb} | {b for b in (2048, 2049, 4096) if b <= nb})
+    for b in check:
+        x = math.fsum(vd[:64 * b])
+        y = math.fsum((vd[:64 * b] ** 2)[~flag[:64 * b]])
+        gx, gy = cum[b, 0] + cum[b, 1], cum[b, 2] + cum[b, 3]
+        assert abs(gx - x) <= 1e-14 * max(abs(x), 1e-300), (b, gx, x)
+        assert abs(gy - y) <= 1e-14 * max(abs(y), 1e-300), (b, gy, y)
