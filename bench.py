@@ -236,6 +236,10 @@ def main():
     L.smg_debug_time_main_pass(1)
     if sharded:
         dist.barrier()
+    if os.environ.get("SMG_BENCH_GC_FREEZE"):  # A/B: collector pauses over the setup's objects
+        import gc
+        gc.collect()
+        gc.freeze()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     marks = []
