@@ -243,9 +243,13 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     marks = []
+    verbose = bool(os.environ.get("SMG_BENCH_VERBOSE"))
+    host_allocs = []
     for _ in range(args.steps):
         df = step_fn()  # ends with the table on the host (a synchronisation)
         marks.append(time.perf_counter())
+        if verbose:  # pinned host allocations so far (diagnostic: step-time outliers)
+            host_allocs.append(torch.cuda.host_memory_stats().get("num_host_alloc", -1))
     torch.cuda.synchronize()
     if sharded:
         dist.barrier()
@@ -265,6 +269,8 @@ def main():
         if os.environ.get("SMG_BENCH_VERBOSE"):
             log(f"[rank {rank}] steps: " + " ".join(f"{x:.1f}" for x in per_step))
             log(f"[rank {rank}] pass launches (pass:ms): " + " ".join(f"{p}:{t:.2f}" for p, t in pass_ms))
+            log(f"[rank {rank}] pinned host allocations after each step: {host_allocs}")
+            log(f"[rank {rank}] host allocator stats: {dict(torch.cuda.host_memory_stats())}")
     # one more search with the host-side caches dropped (the theoretical-intensity alignment and the shard's
     # global row index are reused between steps while the ion keys are unchanged): a cold first search of a
     # new formula table in a warm process
