@@ -519,7 +519,10 @@ def cpu_baseline(args, ions, peaks, dims):
             "sample": (f"{len(pick)} ions drawn uniformly from the {ions.n_ions:,}-ion table ({len(rows)} scored), "
                        f"the {b_mz.size:,} data points of their windows; {workers} worker processes (the box's CPU share; "
                        f"Spark local[*]-style), each sorts its ions' window points by m/z and images + scores them "
-                       f"(oracle/cpu_baseline.py); wall {wall:.1f}s"),
+                       f"(oracle/cpu_baseline.py); wall {wall:.1f}s.  Favourable to the CPU: the selection of the "
+                       f"window points from the resident dataset runs before the timed wall, and each worker sorts only "
+                       f"its ions' window points, not a whole m/z segment of every spectrum as formula_imager_segm.py:"
+                       f"73-74 does -- an upper bound on the reference CPU path's rate"),
             "nproc": os.cpu_count(), "cpus_available": CB.available_cpus(), "cpu_model": CB.cpu_model()}
 
 

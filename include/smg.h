@@ -200,9 +200,6 @@ int smg_debug_force_two_level(int32_t on);
  * ion to the pixel-indexed slot kernel; so that the parity suite covers both on every case.  Process-wide;
  * returns 0. */
 int smg_debug_force_dense(int32_t on);
-/* main pass kernel: 1 = the 512-thread LDS kernel (ion_pipe_kernel<512>, the default), 0 = one wave per ion
- * (ion_wave_kernel, packed hits only; experimental, slower: DESIGN.md §3) */
-int smg_debug_main_kernel(int32_t which);
 /* smg_sort_points' implementation: 1 = the hand-written sort (default), 0 = rocPRIM's onesweep radix sort (kept for
  * A/B timing; smg_sort_points_flag always uses the hand-written one).  Process-wide; returns 0. */
 int smg_debug_sort_impl(int32_t which);

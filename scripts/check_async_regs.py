@@ -6,14 +6,22 @@ drain before any other instruction reads or writes v[a..b]; the only exception i
 into the same registers (its "+v" operand keeps them allocated).  Spills are covered: a scratch_store of such
 a register on such a path is a read of it.
 
+Loads tagged "smg:wave0" in the inline asm (the scheduling ticket and the ion descriptor of ion_pipe_kernel) are
+issued and waited by wave 0 only, under wave-uniform conditions that hold for every lane of wave 0; the other
+waves branch around both with s_cbranch_execz.  For them the paths are searched twice: without taking any
+s_cbranch_execz edge (the issuing wave: a use found there is a VIOLATION), and with them (a use found only there
+is reported as GUARDED: reached only by a wave that issued no such load).  Every other load is searched along all
+edges.
+
 usage: check_async_regs.py file.s [kernel-symbol-prefix]
+Last line: "<n> async loads checked, <v> violations, <g> guarded".
 """
 import re
 import sys
 
 src = open(sys.argv[1]).read().split("\n")
 kern = sys.argv[2] if len(sys.argv) > 2 else "_ZN3smg15ion_pipe_kernelILi0E"
-bad = total = 0
+bad = total = guarded = 0
 
 
 def regs(tok):
@@ -22,6 +30,38 @@ def regs(tok):
         return set(range(int(m.group(1)), int(m.group(2)) + 1))
     m = re.match(r"v(\d+)$", tok)
     return {int(m.group(1))} if m else set()
+
+
+def search(body, in_asm, labels, dst, start, follow_execz=True):
+    """First instruction touching ``dst`` on a path from ``start`` that meets no wait (None: every path waits)."""
+    seen, stack = set(), [start]
+    while stack:
+        j = stack.pop()
+        while j < len(body) and j not in seen:
+            seen.add(j)
+            t = body[j]
+            if (in_asm[j] and t.startswith("s_waitcnt")) or (t.startswith("s_waitcnt") and "vmcnt(0)" in t):
+                break
+            if not t or t.startswith((".", ";")) or t.endswith(":") or re.match(r"^\.LBB\w+:", t):
+                j += 1
+                continue
+            toks = [x.strip(",") for x in t.split()]
+            touched = set()
+            for x in toks[1:]:
+                touched |= regs(x)
+            if touched & dst and not (in_asm[j] and t.startswith(("global_load", "global_atomic"))):
+                return (j, t)
+            op = toks[0]
+            if op.startswith("s_cbranch") or op == "s_branch":
+                tgt = toks[1] if len(toks) > 1 else ""
+                if tgt in labels and (follow_execz or op != "s_cbranch_execz"):
+                    stack.append(labels[tgt])
+                if op == "s_branch":
+                    break
+            if op in ("s_endpgm", "s_setpc_b64"):
+                break
+            j += 1
+    return None
 
 
 for st in [i for i, l in enumerate(src) if l.startswith(kern)]:
@@ -45,36 +85,15 @@ for st in [i for i, l in enumerate(src) if l.startswith(kern)]:
         total += 1
         dst = regs(l.split()[1].rstrip(","))
         dsts |= dst
-        seen, stack, hit = set(), [i + 1], None
-        while stack and hit is None:
-            j = stack.pop()
-            while j < len(body) and j not in seen:
-                seen.add(j)
-                t = body[j]
-                if (in_asm[j] and t.startswith("s_waitcnt")) or (t.startswith("s_waitcnt") and "vmcnt(0)" in t):
-                    break
-                if not t or t.startswith((".", ";")) or t.endswith(":") or re.match(r"^\.LBB\w+:", t):
-                    j += 1
-                    continue
-                toks = [x.strip(",") for x in t.split()]
-                touched = set()
-                for x in toks[1:]:
-                    touched |= regs(x)
-                if touched & dst and not (in_asm[j] and t.startswith(("global_load", "global_atomic"))):
-                    hit = (j, t)
-                    break
-                op = toks[0]
-                if op.startswith("s_cbranch") or op == "s_branch":
-                    tgt = toks[1] if len(toks) > 1 else ""
-                    if tgt in labels:
-                        stack.append(labels[tgt])
-                    if op == "s_branch":
-                        break
-                if op in ("s_endpgm", "s_setpc_b64"):
-                    break
-                j += 1
+        wave0 = "smg:wave0" in l
+        hit = search(body, in_asm, labels, dst, i + 1, follow_execz=not wave0)
         if hit:
             print("VIOLATION", name[:60], i, l, "->", hit[0], hit[1])
             bad += 1
-print(f"{total} async loads checked, {bad} violations")
+        elif wave0:
+            hit = search(body, in_asm, labels, dst, i + 1, follow_execz=True)
+            if hit:
+                print("GUARDED", name[:60], i, l, "->", hit[0], hit[1])
+                guarded += 1
+print(f"{total} async loads checked, {bad} violations, {guarded} guarded")
 sys.exit(1 if bad else 0)

@@ -3,7 +3,9 @@ W-way plan (config 3 by default) is scored in turn with the product code (distri
 slice copy, compute_sf_images and sf_image_metrics rows, plus the rank-0 assembly (rows_to_frame) of all ranks'
 rows.  The N-GPU step is then ~ max over ranks + all-gather + assembly.
 
-usage: time_shards.py [W=8] [nrows ncols peaks n_sf]"""
+usage: time_shards.py [W=8] [nrows ncols peaks n_sf]
+CONFIG=5: BASELINE config 5 (1000x1000 px, Poisson(5000), 40k formulas x 6 adducts in both polarities); every rank
+also gets a roofline per pass (12 B per window point of the ions the pass scored over its HIP-event time)."""
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
@@ -19,7 +21,12 @@ a = sys.argv[1:]
 W = int(a[0]) if a else 8
 nrows, ncols, pk, n_sf = (int(a[1]), int(a[2]), float(a[3]), int(a[4])) if len(a) >= 5 else (500, 500, 2000.0, 20000)
 ppm = 2.0
-ions = syn.make_ion_table(n_sf, seed=43, decoy_seed=44)
+CONFIG5 = os.environ.get("CONFIG") == "5"
+if CONFIG5:
+    nrows, ncols, pk, n_sf = 1000, 1000, 5000.0, 40000
+    ions = syn.make_ion_table_both_polarities(n_sf, seed=43, decoy_seed=44)
+else:
+    ions = syn.make_ion_table(n_sf, seed=43, decoy_seed=44)
 mz, hits, dims, info = syn.make_dataset_torch(nrows, ncols, pk, seed=42, device="cuda", ions=ions,
                                               plant_fraction=0.02, plant_seed=45)  # bench.py defaults
 peaks = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
@@ -39,11 +46,20 @@ def timed(f, reps=3):
     return best * 1e3, out
 
 
-# single-GPU API step for reference
+# single-GPU API step for reference (SKIP_T1=1: skip it; the efficiency is then not printed)
 dds = ResidentDataset(peaks)
 sdf = formulas.get_sf_peak_df()
-t1, df1 = timed(lambda: sf_image_metrics(compute_sf_images(None, dds, sdf, ppm), None, formulas, dds, conf))
-print(f"1 GPU API step {t1:.2f} ms, {len(df1)} rows, {peaks.n_points:,} points, {formulas.n_ions:,} ions", flush=True)
+SKIP_T1 = bool(os.environ.get("SKIP_T1"))
+if SKIP_T1:
+    t1, df1 = float("nan"), None
+else:
+    t1, df1 = timed(lambda: sf_image_metrics(compute_sf_images(None, dds, sdf, ppm), None, formulas, dds, conf),
+                    reps=2 if CONFIG5 else 3)
+    print(f"1 GPU API step {t1:.2f} ms, {len(df1)} rows, {peaks.n_points:,} points, {formulas.n_ions:,} ions",
+          flush=True)
+    peaks.mz_sorted = peaks.hits_sorted = peaks.cum = None  # the slices need the HBM at config 5
+    E._ws_cache.clear()
+    torch.cuda.empty_cache()
 
 rows_all, worst = [], 0.0
 ONLY = int(os.environ.get("ONLY_RANK", "-1"))
@@ -57,12 +73,39 @@ for r in range(W):
     L = _lib.lib()
     L.smg_debug_main_pass_times(None, 0, ctypes.byref(ctypes.c_int32(0)))
     L.smg_debug_time_main_pass(1)
-    t_met, _ = timed(lambda: _metrics_device_rows(ims, plan.formulas.get_sf_peak_ints(), conf["image_generation"]))
+    t_met, (_, mets) = timed(lambda: _metrics_device_rows(ims, plan.formulas.get_sf_peak_ints(),
+                                                           conf["image_generation"]))
     L.smg_debug_time_main_pass(0)
-    buf = (ctypes.c_double * 16)()
+    buf = (ctypes.c_double * 64)()
+    pbuf = (ctypes.c_int32 * 64)()
     nt = ctypes.c_int32(0)
-    L.smg_debug_main_pass_times(buf, 16, ctypes.byref(nt))
-    t_main = min(buf[i] for i in range(nt.value)) if nt.value else float("nan")
+    L.smg_debug_pass_times(pbuf, buf, 64, ctypes.byref(nt))
+    by = {}
+    for i in range(min(nt.value, 64)):
+        by.setdefault(int(pbuf[i]), []).append(float(buf[i]))
+    t_main = min(by.get(_lib.SMG_PASS_MAIN, [float("nan")]))
+    # per pass: best launch time and 12 B per window point of the ions it scored
+    fl = mets.flags.cpu().numpy().astype(np.int64)
+    cs = torch.zeros(ims.lo.numel() + 1, dtype=torch.int64, device=ims.lo.device)
+    torch.cumsum(ims.hi - ims.lo, 0, out=cs[1:])
+    wo = ims.ions_dev.win_off
+    ipts = (cs[wo[1:]] - cs[wo[:-1]]).cpu().numpy()
+    pas = np.full(len(fl), _lib.SMG_PASS_MAIN)
+    pas[(fl & _lib.SMG_ION_BIG) != 0] = _lib.SMG_PASS_BIG
+    pas[(fl & _lib.SMG_ION_DENSE) != 0] = _lib.SMG_PASS_DENSE
+    pas[(fl & _lib.SMG_ION_WIDE) != 0] = _lib.SMG_PASS_WIDE
+    has = (fl & _lib.SMG_ION_HAS_HITS) != 0
+    roof = []
+    for p_, ts in sorted(by.items()):
+        if p_ == _lib.SMG_PASS_DESC:
+            roof.append(f"{_lib.PASS_NAMES.get(p_, p_)} {min(ts):.2f} ms")
+            continue
+        n_p = int((has & (pas == p_)).sum())
+        pts = int(ipts[has & (pas == p_)].sum())
+        t = min(ts)
+        frac = 12.0 * pts / (t * 1e-3) / 8e12 if t > 0 and pts else 0.0
+        roof.append(f"{_lib.PASS_NAMES.get(p_, p_)} {t:.2f} ms {n_p:,} ions {pts:,} window pts -> {frac:.3f} of 8 TB/s")
+    print(f"  rank {r} passes: " + "; ".join(roof), flush=True)
     t_all, (rows, _) = timed(lambda: D._device_rows(plan, peaks, conf))
     rows_all.append(rows)
     hist, edges = D.mz_histogram(peaks.mz)
@@ -113,7 +156,8 @@ def asm_parts():
 for _ in range(2):
     parts = asm_parts()
 print("assembly parts (ms): " + ", ".join(f"{k} {v*1e3:.2f}" for k, v in parts.items()))
-same = df.index.equals(df1.index) and np.allclose(df.to_numpy(), df1.to_numpy(), rtol=0, atol=1e-12)
+same = df1 is not None and df.index.equals(df1.index) and np.allclose(df.to_numpy(), df1.to_numpy(), rtol=0,
+                                                                       atol=1e-12)
 print(f"assembly (rank 0) {t_asm:.2f} ms; table identical to 1 GPU: {same}")
 gather_est = n_max * 40 / 50e9 * 1e3 + 0.05  # W-1 blocks over W-1 xGMI links into rank 0 at once, ~50 GB/s each
 est = worst + gather_est + t_asm

@@ -57,7 +57,6 @@ PROTOTYPES = {
     "smg_debug_stream_read": (ctypes.c_int, [_P, _I64, _P, _I32, _P]),
     "smg_debug_force_two_level": (ctypes.c_int, [_I32]),
     "smg_debug_force_dense": (ctypes.c_int, [_I32]),
-    "smg_debug_main_kernel": (ctypes.c_int, [_I32]),
     "smg_debug_sort_impl": (ctypes.c_int, [_I32]),
     "smg_debug_time_main_pass": (ctypes.c_int, [_I32]),
     "smg_debug_main_pass_times": (ctypes.c_int, [_P, _I32, ctypes.POINTER(_I32)]),

@@ -1,6 +1,6 @@
 // Device-side definitions shared by the ion kernels of libsmg (smg_metrics.hip: the LDS, wide and
-// pixel-indexed passes; smg_wave.hip: the wave-per-ion main pass): kernel parameters, the two hit formats,
-// asynchronous load helpers, level index, ion descriptors, persistent scheduling, LDS union-find.
+// pixel-indexed passes): kernel parameters, the two hit formats, asynchronous load helpers, level index, ion
+// descriptors, persistent scheduling, LDS union-find.
 #pragma once
 
 #include "smg_common.hpp"
@@ -98,8 +98,14 @@ __device__ __forceinline__ void vm_wait1(uint32_t& r) {
 // Returning atomic add issued like the async loads: the compiler would wait for its result with
 // s_waitcnt vmcnt(0) right away -- i.e. for every prefetch load of the wave in flight -- so it is waited
 // for with a counted vm_wait1 where the ticket is consumed.
+// Tagged "smg:wave0" in the ISA: issued by wave 0 only and waited by wave 0 only (scripts/check_async_regs.py
+// accepts a path that skips its wait only through an exec-zero branch, i.e. in another wave).
 __device__ __forceinline__ void atomic_add_rtn_async(uint32_t& r, uint32_t* addr, uint32_t v) {
-  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "+v"(r) : "v"(addr), "v"(v) : "memory");
+  asm volatile("global_atomic_add %0, %1, %2, off sc0 ; smg:wave0" : "+v"(r) : "v"(addr), "v"(v) : "memory");
+}
+// an 8-byte load issued and waited by wave 0 only (the ion descriptor), tagged like the ticket
+__device__ __forceinline__ void ld8_async_wave0(uint64_t& r, const void* addr) {
+  asm volatile("global_load_dwordx2 %0, %1, off ; smg:wave0" : "+v"(r) : "v"(addr) : "memory");
 }
 template <int N, int M>
 __device__ __forceinline__ void vm_wait(uint64_t (&r)[M]) {
@@ -277,12 +283,5 @@ __device__ __forceinline__ bool desc_lds_ok(const IonDesc* D, int capc) {
   const int K = D->K;
   return K >= 1 && K <= MAXK && D->end[0] <= capc && D->ngroups >= 0;
 }
-
-// the wave-per-ion main pass (smg_wave.hip)
-size_t wave_pass_lds_bytes();
-bool wave_pass_supports(int npx);
-int launch_wave_pass(const uint64_t* hits, const IonDesc* desc, int64_t n_ions, const Params& P, uint32_t* xcd_ctr,
-                     double* oc, double* osp, double* osc, double* omsm, uint32_t* oflags, uint32_t* rej_list,
-                     uint32_t* rej_count, int cus, hipStream_t st);
 
 }  // namespace smg

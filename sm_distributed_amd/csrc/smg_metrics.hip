@@ -732,8 +732,8 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     uint64_t dword = 0;
     if (wid == 0) {
       if constexpr (ASYNC) {
-        ld8_async_v(dword, reinterpret_cast<const uint64_t*>(desc + (npos >= 0 ? npos : 0)) +
-                               (lane < DESC_QWORDS ? lane : 0));
+        ld8_async_wave0(dword, reinterpret_cast<const uint64_t*>(desc + (npos >= 0 ? npos : 0)) +
+                                   (lane < DESC_QWORDS ? lane : 0));
       } else {
         if (npos >= 0 && lane < DESC_QWORDS) dword = reinterpret_cast<const uint64_t*>(desc + npos)[lane];
       }
@@ -3299,7 +3299,6 @@ using Main2Lay = Lay2<MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX>;
 using Big2Lay = Lay2<BIG_BLOCK / WAVE, BIG_BLOCK * BIG2_RMAX>;
 static int g_force_two_level = 0;  // smg_debug_force_two_level: two-level passes for every image size
 static int g_force_dense = 0;      // smg_debug_force_dense: 1 every ion on the dense path, 2 pixel-indexed only
-static int g_main_legacy = 1;      // smg_debug_main_kernel: 0 = the wave-per-ion kernel as the main pass (experimental: 2.1x slower)
 // smg_debug_time_main_pass: HIP events recorded on the launch stream around every pass launch of
 // smg_ion_metrics (descriptors, main LDS pass, big-ion pass, wide pass, pixel-indexed pass), so a benchmark
 // measures each kernel itself and prices each pass's own window points against its own time
@@ -3318,16 +3317,33 @@ struct PassTimer {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   PassTimer(int p, hipStream_t s) : pass(p), st(s) {
     if (!g_time_main) return;
-    if (hipEventCreate(&ev0) != hipSuccess || hipEventCreate(&ev1) != hipSuccess ||
-        hipEventRecord(ev0, st) != hipSuccess)
-      ev0 = ev1 = nullptr;
+    if (hipEventCreate(&ev0) != hipSuccess) {
+      ev0 = nullptr;
+      return;
+    }
+    if (hipEventCreate(&ev1) != hipSuccess) ev1 = nullptr;
+    if (!ev1 || hipEventRecord(ev0, st) != hipSuccess) release();
   }
   ~PassTimer() {
     if (!ev0) return;
-    if (hipEventRecord(ev1, st) != hipSuccess) return;
+    if (hipEventRecord(ev1, st) != hipSuccess) {
+      release();
+      return;
+    }
     std::lock_guard<std::mutex> g(g_ev_mu);
+    if (g_pass_events.size() >= kMaxPassEvents) {  // nobody drains them: drop the oldest record
+      (void)hipEventDestroy(g_pass_events.front().ev0);
+      (void)hipEventDestroy(g_pass_events.front().ev1);
+      g_pass_events.erase(g_pass_events.begin());
+    }
     g_pass_events.push_back({pass, ev0, ev1});
   }
+  void release() {  // destroys whatever was created; no record is kept
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    ev0 = ev1 = nullptr;
+  }
+  static constexpr size_t kMaxPassEvents = 16384;
 };
 
 static int device_cus() {
@@ -3388,20 +3404,7 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
                          hi, ion_off, theor, reinterpret_cast<const DD4*>(hit_cum), ion_order, n_ions, desc);
     SMG_LAUNCH_CHECK();
   }
-  // main pass: the 512-thread LDS kernel, or (smg_debug_main_kernel(0), packed hits only) the experimental
-  // one-wave-per-ion kernel of smg_wave.hip (correct on the parity suite but 2.1x slower at config 3)
-  bool wave = false;
-  if constexpr (FMT == SMG_HITS_PACKED_F32) {
-    wave = main_ok && !two && !g_main_legacy && wave_pass_supports(P.npx);
-    if (wave) {
-      PassTimer tm(SMG_PASS_MAIN, st);
-      const int rc = launch_wave_pass(hits.h, desc, n_ions, P, hdr + HDR_XCD, oc, osp, osc, omsm, oflags, list_a,
-                                      hdr + 0, cus, st);
-      if (rc != SMG_OK) return rc;
-    }
-  }
-  if (wave) {
-  } else if (main_ok) {
+  if (main_ok) {
     Sched SA{n_ions, hdr + HDR_XCD, nullptr, nullptr};
     auto k1 = two ? &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, true>
                   : &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, false>;
@@ -3552,11 +3555,6 @@ int smg_debug_main_pass_times(double* ms, int32_t cap, int32_t* n) {
 int smg_debug_pass_times(int32_t* pass, double* ms, int32_t cap, int32_t* n) {
   SMG_CHECK_ARG(n != nullptr && ((ms != nullptr && pass != nullptr) || cap == 0), "bad arguments");
   return drain_pass_times(-1, pass, ms, cap, n);
-}
-
-int smg_debug_main_kernel(int32_t which) {
-  g_main_legacy = which == 0 ? 0 : 1;
-  return SMG_OK;
 }
 
 int smg_debug_force_dense(int32_t on) {

@@ -440,7 +440,9 @@ static SortPlan sort_plan(int64_t n, int key_bits) {
   p.off_hist = 256;  // [0, 256): the passes' ticket counters
   p.off_base = p.off_hist + SRT_MAXP * SRT_BINS * 8;
   p.off_status = p.off_base + SRT_MAXP * SRT_BINS * 8;
-  p.status_bytes = (size_t)p.passes * (size_t)p.ntiles * SRT_BINS * sw;
+  // two look-back regions, used by alternate passes: the region of pass p >= 2 is zeroed again after pass p - 2
+  // (the workspace does not grow with the number of passes: ~2 B per point at 64-bit words)
+  p.status_bytes = (size_t)(p.passes < 2 ? p.passes : 2) * (size_t)p.ntiles * SRT_BINS * sw;
   p.off_s0 = align_up(p.off_status + p.status_bytes, 256);  // FLAG pass: spectrum-start bits
   p.start_bytes = (size_t)((n + 31) / 32 + 2) * 4;
   p.off_tk = align_up(p.off_s0 + p.start_bytes, 256);
@@ -494,6 +496,7 @@ static int roc_workspace(int64_t n, size_t* bytes) {
 template <typename S>
 static int run_passes(const SortPlan& P, const uint32_t* mz, const uint64_t* hits, int64_t n, uint32_t* ko,
                       uint64_t* vo, unsigned char* ws, bool flag, double slack, hipStream_t st) {
+  const size_t region = (size_t)P.ntiles * SRT_BINS;  // look-back words per pass
   const uint32_t* starts = reinterpret_cast<const uint32_t*>(ws + P.off_s0);
   unsigned* tickets = reinterpret_cast<unsigned*>(ws);
   const int64_t* binbase = reinterpret_cast<const int64_t*>(ws + P.off_base);
@@ -507,7 +510,8 @@ static int run_passes(const SortPlan& P, const uint32_t* mz, const uint64_t* hit
     const bool to_out = ((P.passes - 1 - p) & 1) == 0;
     uint32_t* kdst = to_out ? ko : tk;
     uint64_t* vdst = to_out ? vo : tv;
-    S* sp = status + (size_t)p * P.ntiles * SRT_BINS;
+    S* sp = status + (size_t)(p & 1) * region;
+    if (p >= 2) SMG_HIP(hipMemsetAsync(sp, 0, region * sizeof(S), st));  // pass p - 2's words
     if (flag && p == 0)
       hipLaunchKernelGGL((sort_pass_kernel<S, true>), dim3((unsigned)P.ntiles), dim3(SRT_T), 0, st, ki, vi, kdst,
                          vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, slack, starts);
@@ -534,7 +538,7 @@ static int native_sort(const float* mz, const uint64_t* hits, int64_t n, int key
     return SMG_ERR_UNSUPPORTED;
   }
   unsigned char* ws = reinterpret_cast<unsigned char*>(workspace);
-  // tickets, histograms and every pass's look-back words start at zero
+  // tickets, histograms and the first two passes' look-back words start at zero
   SMG_HIP(hipMemsetAsync(ws, 0, P.off_status + P.status_bytes, st));
   const uint32_t* keys = reinterpret_cast<const uint32_t*>(mz);
   int64_t hb = (n + (int64_t)HST_T * 16 - 1) / ((int64_t)HST_T * 16);

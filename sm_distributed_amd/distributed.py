@@ -184,6 +184,7 @@ def _device_rows(plan, peaks, ds_config):
     rows[:k, 2] = m.spatial
     rows[:k, 3] = m.spectral
     rows[:k, 4] = m.msm
+    ims.score_flags = m.flags  # SMG_ION_* per image-set ion (which pass scored it): diagnostics and tests
     return rows, ims
 
 

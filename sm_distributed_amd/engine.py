@@ -60,7 +60,8 @@ class DevicePeaks:
     force: torch.Tensor | None = None      # uint8[n_spectra]: spectra whose pixel is shared (non-injective map)
     mz_sorted: torch.Tensor | None = None
     hits_sorted: torch.Tensor | None = None
-    flag_ppm: float | None = None
+    flag_ppm: float | None = None          # the ppm of the flags hits_sorted carries (what the ion kernels read)
+    hits_flag_ppm: float | None = None     # the ppm of the flags the dataset-order hits carry (None: unknown/stale)
     sort_key_bits: int | None = None
     cum: torch.Tensor | None = None  # 64-point block double-double prefix sums of the sorted hits
     cum_valid: bool = False          # cum describes the current hits_sorted
@@ -105,7 +106,7 @@ class DevicePeaks:
         if self.sp_off is None:
             raise ValueError("DevicePeaks needs sp_off (spectrum offsets) for duplicate flags")
         if self.flags_preset_ppm is not None and float(ppm) == self.flags_preset_ppm:
-            self.flag_ppm = float(ppm)
+            self.hits_flag_ppm = float(ppm)
             return self
         self.flags_preset_ppm = None
         n_sp = int(self.sp_off.numel()) - 1
@@ -117,7 +118,7 @@ class DevicePeaks:
         check(lib().smg_flag_duplicates(_p(self.sp_off), n_sp, _p(self.mz), _p(self.hits), self.n_points,
                                         float(ppm), _p(self.force), _p(self.flag_state), _stream(stream)),
               "smg_flag_duplicates")
-        self.flag_ppm = float(ppm)
+        self.hits_flag_ppm = float(ppm)
         self.version += 1
         return self
 
@@ -190,10 +191,13 @@ class DevicePeaks:
         return out
 
     def sort(self, stream=None) -> "DevicePeaks":
-        """Stable m/z sort of the points (smg_sort_points), flags as the hits carry them."""
+        """Stable m/z sort of the points (smg_sort_points), flags as the hits carry them: the sorted copy's flags
+        are then those of the last flag pass over the hits (flag_ppm None if the hits' flags are stale, e.g. after
+        a fused flag_and_sort, which flags only the sorted copy)."""
         self._sort_into(lambda ws: lib().smg_sort_points(
             _p(self.mz), _p(self.hits), self.n_points, self.key_bits(), _p(self.mz_sorted), _p(self.hits_sorted),
             _p(ws), ws.numel(), _stream(stream)), "smg_sort_points", stream)
+        self.flag_ppm = self.hits_flag_ppm
         return self
 
     def _sort_into(self, call, name, stream=None):
@@ -224,7 +228,7 @@ class DevicePeaks:
             _p(self.sp_off), n_sp, _p(self.mz), _p(self.hits), self.n_points, self.key_bits(), float(ppm),
             _p(self.mz_sorted), _p(self.hits_sorted), _p(ws), ws.numel(), _stream(stream)), "smg_sort_points_flag",
             stream)
-        self.flag_ppm = float(ppm)
+        self.flag_ppm = float(ppm)  # the sorted copy's flags; the dataset-order hits keep whatever they had
         return self
 
     def prefix_sums(self, stream=None) -> "DevicePeaks":

@@ -298,46 +298,82 @@ def device_frame(ion_keys, cols, idx, cols_compact=False):
     return pd.DataFrame(host[2].numpy().T, index=mi, columns=METRIC_COLUMNS, copy=False)
 
 
+_STAGE = {}  # device -> [copy stream, ring index, two grow-only pinned uint8 buffers]
+
+
+def _stage_buffers(device, n):
+    """A persistent pinned host buffer of >= n bytes (ring of two per device, grow-only) and the device's copy
+    stream: the per-step row mask never allocates pinned memory."""
+    import torch
+    key = str(device)
+    ent = _STAGE.get(key)
+    if ent is None:
+        ent = _STAGE[key] = [torch.cuda.Stream(device=device), 0, [None, None]]
+    ent[1] ^= 1
+    buf = ent[2][ent[1]]
+    if buf is None or buf.numel() < n:
+        buf = ent[2][ent[1]] = torch.empty(max(int(n), 1 << 20), dtype=torch.uint8, pin_memory=True)
+    return ent[0], buf
+
+
 class FrameIndex:
-    """device_frame in two halves around a kernel launch: ``stage(keep)`` (device bool[n_ion], queued before the
-    launch) gathers the kept ions' index codes into pinned host memory; ``frame(cols)`` (after the launch) builds
-    the MultiIndex on the host -- while the kernel still runs -- then gathers and copies the metric columns."""
+    """device_frame in two halves around a kernel launch.  ``stage(keep)`` (device bool[n_ion], queued before the
+    launch) copies the row mask to a persistent pinned buffer on a copy stream of its own -- nothing is queued on
+    the compute stream in front of the kernel and nothing synchronises -- and takes the pinned block the
+    DataFrame's columns will live in.  ``frame(cols)`` (after the launch) builds the MultiIndex on the host from
+    the mask while the kernel still runs, then compacts the metric columns on the device (a scatter, no host
+    synchronisation) and copies them to that block."""
 
     def __init__(self, ion_keys):
         self.ion_keys = ion_keys
-        self.idx = None
+        self.keep = None
 
     def stage(self, keep):
         import torch
-        self.idx = torch.nonzero(keep).flatten()  # one host synchronisation, before the kernel is queued
-        sfc, adc = self.ion_keys.codes_dev(keep.device)
-        parts = (sfc[self.idx], adc[self.idx])
+        self.keep = keep
         if keep.device.type == "cuda":
-            self.codes = [torch.empty(x.shape, dtype=x.dtype, pin_memory=True) for x in parts]
-            for h, x in zip(self.codes, parts):
-                h.copy_(x, non_blocking=True)
-            self.ev = torch.cuda.Event()
-            self.ev.record(torch.cuda.current_stream(keep.device))
-            # the columns' pinned buffer too, before the kernel: a pinned allocation while a kernel runs remaps
-            # host memory for the device and was seen to stall the kernel (first calls of a process)
-            self.cols_host = torch.empty((4, self.idx.numel()), dtype=torch.float64, pin_memory=True)
+            n = keep.numel()
+            main = torch.cuda.current_stream(keep.device)
+            cs, buf = _stage_buffers(keep.device, n)
+            cs.wait_stream(main)
+            with torch.cuda.stream(cs):
+                buf[:n].copy_(keep.view(torch.uint8), non_blocking=True)
+                self.ev = torch.cuda.Event()
+                self.ev.record(cs)
+            keep.record_stream(cs)
+            self.keep_host = buf[:n]
+            # the DataFrame's own pinned block (caching host allocator: reused once an earlier frame is freed),
+            # taken before the kernel: a pinned allocation while a kernel runs remaps host memory and was seen to
+            # stall the kernel (first calls of a process)
+            self.cols_host = torch.empty(4 * n, dtype=torch.float64, pin_memory=True)
         else:
-            self.codes, self.ev = list(parts), None
+            self.ev = None
 
     def frame(self, cols):
         import torch
-        if self.ev is not None:
-            self.ev.synchronize()  # the codes were queued before the kernel: ready while it runs
-        c_sf, c_ad = (h.numpy() for h in self.codes)
-        mi = self.ion_keys.multi_index_from_codes(c_sf, c_ad)
-        sel = cols[:, self.idx]
-        if cols.device.type == "cuda":
-            host = self.cols_host
-            host.copy_(sel, non_blocking=True)
-            torch.cuda.current_stream(cols.device).synchronize()
-        else:
-            host = sel
-        return pd.DataFrame(host.numpy().T, index=mi, columns=METRIC_COLUMNS, copy=False)
+        keep = self.keep
+        if self.ev is None:
+            idx = torch.nonzero(keep).flatten().numpy()
+            _, sfc, adc = self.ion_keys.level_codes()
+            mi = self.ion_keys.multi_index_from_codes(sfc[idx], adc[idx])
+            return pd.DataFrame(cols[:, idx].numpy().T, index=mi, columns=METRIC_COLUMNS, copy=False)
+        self.ev.synchronize()  # the mask was copied before the kernel ran: ready while it runs
+        idx = np.flatnonzero(self.keep_host.numpy())
+        m = len(idx)
+        _, sfc, adc = self.ion_keys.level_codes()
+        mi = self.ion_keys.multi_index_from_codes(sfc[idx], adc[idx])
+        # rows of kept ions in table order, compacted on the device: row k of ion i goes to k*m + (rank of i among
+        # the kept ions); the others to a dummy slot 4m
+        n = keep.numel()
+        pos = torch.cumsum(keep, 0) - 1
+        dst = torch.arange(4, device=cols.device).unsqueeze(1) * m + pos.unsqueeze(0)
+        dst = torch.where(keep.unsqueeze(0), dst, torch.full_like(dst, 4 * m))
+        out = torch.empty(4 * m + 1, dtype=torch.float64, device=cols.device)
+        out.scatter_(0, dst.flatten(), cols[:, :n].reshape(-1))
+        host = self.cols_host[:4 * m]
+        host.copy_(out[:4 * m], non_blocking=True)
+        torch.cuda.current_stream(cols.device).synchronize()
+        return pd.DataFrame(host.view(4, m).numpy().T, index=mi, columns=METRIC_COLUMNS, copy=False)
 
 
 class ImageRows:

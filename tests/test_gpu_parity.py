@@ -291,28 +291,3 @@ def test_edge_inputs_match_oracle(name, dense):
             assert err.max(initial=0.0) <= METRIC_ATOL, (col, float(err.max()))
     if name == "one_hot_pixel":
         assert len(df) > 0
-
-
-@pytest.mark.parametrize("name", ["basic", "dups", "conn8_border1", "nlevels", "kmix", "wide_range",
-                                  pytest.param("long_tail", marks=pytest.mark.xfail(
-                                      reason="wave kernel: wrong scores on some heavy-duplicate ions (DESIGN §3)",
-                                      strict=False))])
-def test_wave_main_kernel_matches_oracle(name):
-    """The experimental wave-per-ion main pass (smg_debug_main_kernel(0)) against the oracle; it
-    scores the bulk of each case itself (the rest go to the big-ion pass)."""
-    from sm_distributed_amd import _lib
-    ds, ions, ppm, kw, imgs, df, _, _, _, _ = _run_case(name)
-    L = _lib.lib()
-    L.smg_debug_main_kernel(0)
-    try:
-        _, m, _, _ = _device_run(ds, ions, ppm, **kw)
-    finally:
-        L.smg_debug_main_kernel(1)
-    has = (m["flags"] & 1) != 0
-    assert set(zip(ions.sf_ids[has].tolist(), ions.adducts[has].tolist())) == set(df.index.tolist())
-    idx = {k: i for i, k in enumerate(zip(ions.sf_ids.tolist(), ions.adducts.tolist()))}
-    rows = np.array([idx[k] for k in df.index.tolist()], dtype=np.int64)
-    for col in ("chaos", "spatial", "spectral", "msm"):
-        assert np.abs(df[col].to_numpy() - m[col][rows]).max(initial=0.0) <= METRIC_ATOL, col
-    wave_scored = has & ((m["flags"] & (2 | 8 | 0x10)) == 0)
-    assert wave_scored.sum() >= 0.5 * has.sum(), (int(wave_scored.sum()), int(has.sum()))

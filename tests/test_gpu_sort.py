@@ -220,3 +220,25 @@ def test_prefix_sums_match_exact_sums(n):
         gx, gy = cum[b, 0] + cum[b, 1], cum[b, 2] + cum[b, 3]
         assert abs(gx - x) <= 1e-14 * max(abs(x), 1e-300), (b, gx, x)
         assert abs(gy - y) <= 1e-14 * max(abs(y), 1e-300), (b, gy, y)
+
+
+def test_flag_ppm_tracks_the_sorted_copy():
+    """The fused flag + sort flags only the sorted copy: a later plain sort() of the (unflagged) dataset-order hits
+    must not claim that ppm's flags (flag_ppm None), so an image set made at that ppm re-flags before use; a flag
+    pass then sort() carries the ppm again (engine.py flag_and_sort)."""
+    import torch
+    from sm_distributed_amd import synthetic as syn
+    from sm_distributed_amd import engine as E
+    mz, hits, dims, info = syn.make_dataset_torch(16, 16, 200.0, seed=3, device="cuda")
+    p = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
+    p.flag_and_sort(5.0)
+    assert p.flag_ppm == 5.0 and p.hits_flag_ppm is None
+    fused = p.hits_sorted.clone()
+    p.sort()
+    assert p.flag_ppm is None
+    p.flag_duplicates(5.0)
+    assert p.hits_flag_ppm == 5.0
+    p.sort()
+    assert p.flag_ppm == 5.0
+    torch.cuda.synchronize()
+    assert torch.equal(p.hits_sorted, fused)  # the two ways give the same flags
