@@ -210,6 +210,7 @@ int smg_debug_sort_impl(int32_t which);
 #define SMG_PASS_BIG 2    /* big-ion LDS pass over the main pass's rejects (ion_pipe_kernel<1024>): SMG_ION_BIG */
 #define SMG_PASS_WIDE 3   /* rank-indexed wide pass (ion_wide_kernel): SMG_ION_WIDE */
 #define SMG_PASS_DENSE 4  /* pixel-indexed pass (ion_dense_kernel): SMG_ION_DENSE without SMG_ION_WIDE */
+#define SMG_PASS_FINALIZE 5 /* scores of the ions the LDS passes scored, from their recorded sums (ion_finalize_kernel) */
 
 /* Diagnostics: on != 0 records HIP events on the launch stream around every pass launch of smg_ion_metrics.
  * smg_debug_pass_times waits for the recorded launches, writes up to `cap` (pass id, elapsed ms) pairs in launch

@@ -8,9 +8,10 @@ a register on such a path is a read of it.
 
 Loads tagged "smg:wave0" in the inline asm (the scheduling ticket and the ion descriptor of ion_pipe_kernel) are
 issued and waited by wave 0 only, under wave-uniform conditions that hold for every lane of wave 0; the other
-waves branch around both with s_cbranch_execz.  For them the paths are searched twice: without taking any
-s_cbranch_execz edge (the issuing wave: a use found there is a VIOLATION), and with them (a use found only there
-is reported as GUARDED: reached only by a wave that issued no such load).  Every other load is searched along all
+waves branch around both with an exec-zero edge (the taken edge of s_cbranch_execz, or the fall-through of
+s_cbranch_execnz).  For them the paths are searched twice: without any exec-zero edge (the issuing wave: a use
+found there is a VIOLATION), and with them (a use found only there is reported as GUARDED: reached only by a wave
+that issued no such load).  Every other load is searched along all
 edges.
 
 usage: check_async_regs.py file.s [kernel-symbol-prefix]
@@ -54,9 +55,10 @@ def search(body, in_asm, labels, dst, start, follow_execz=True):
             op = toks[0]
             if op.startswith("s_cbranch") or op == "s_branch":
                 tgt = toks[1] if len(toks) > 1 else ""
+                # exec-zero edges: the taken edge of s_cbranch_execz, the fall-through of s_cbranch_execnz
                 if tgt in labels and (follow_execz or op != "s_cbranch_execz"):
                     stack.append(labels[tgt])
-                if op == "s_branch":
+                if op == "s_branch" or (op == "s_cbranch_execnz" and not follow_execz):
                     break
             if op in ("s_endpgm", "s_setpc_b64"):
                 break

@@ -12,9 +12,9 @@ for s in $STEPS; do
   echo "## $s $(date +%T)"
   case $s in
     tests)
-      timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider \
+      timeout -k 10 1000 python -u -m pytest ${TESTS:-tests} -m gpu -x -v -s --timeout 600 --timeout-method thread -p no:cacheprovider \
         ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/$TAG/pytest_gpu.log 2>&1 || { tail -60 gpurun_out/$TAG/pytest_gpu.log; exit 1; }
-      tail -3 gpurun_out/$TAG/pytest_gpu.log; grep -h "config 5\|rank [0-9]/8\|config 3 API\|8-way" gpurun_out/$TAG/pytest_gpu.log | head -20 ;;
+      tail -3 gpurun_out/$TAG/pytest_gpu.log; grep -h "config 5\|rank [0-9]/8:\|config 3 API\|8-way\|steady-state" gpurun_out/$TAG/pytest_gpu.log | head -30 ;;
     bench)
       SMG_BENCH_VERBOSE=1 timeout -k 10 400 python -u bench.py --steps ${BENCH_STEPS:-100} --warmup 3 ${BENCH_ARGS} \
         > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err || { tail -30 gpurun_out/$TAG/bench.err; exit 1; }

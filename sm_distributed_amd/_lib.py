@@ -22,10 +22,10 @@ SMG_HITS_PACKED_F32 = 0
 PIXEL_MASK = 0x7FFFFFFF   # bit 31 of the pixel field = duplicate-candidate flag
 SMG_HITS_SPLIT_F64 = 1
 # pass ids of smg_debug_pass_times
-SMG_PASS_DESC, SMG_PASS_MAIN, SMG_PASS_BIG, SMG_PASS_WIDE, SMG_PASS_DENSE = range(5)
+SMG_PASS_DESC, SMG_PASS_MAIN, SMG_PASS_BIG, SMG_PASS_WIDE, SMG_PASS_DENSE, SMG_PASS_FINALIZE = range(6)
 PASS_NAMES = {0: "ion_desc8_kernel", 1: "ion_pipe_kernel<512> (main LDS pass)",
               2: "ion_pipe_kernel<1024> (big-ion LDS pass)", 3: "ion_wide_kernel (wide pass)",
-              4: "ion_dense_kernel (pixel-indexed pass)"}
+              4: "ion_dense_kernel (pixel-indexed pass)", 5: "ion_finalize_kernel (LDS passes' scores)"}
 
 # every symbol include/smg.h declares, with its ctypes prototype
 _P = ctypes.c_void_p

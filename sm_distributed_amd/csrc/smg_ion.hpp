@@ -218,6 +218,24 @@ struct IonDesc {
 static_assert(sizeof(IonDesc) == 384, "IonDesc is 384 B");
 constexpr int DESC_QWORDS = (int)(sizeof(IonDesc) / 8);  // 48: one 8-byte load per lane of wave 0
 
+// The same 384 B once an LDS pass has scored the position: the consumed window fields (base, end, gs, pad) hold the
+// ion's sums, and ion_finalize_kernel computes the scores from them (state == 1) after the pass.
+struct IonRec {
+  double s[MAXK];      // over base[]: s[0] = Σx[x>0] of the principal image, s[k>=1] = Σy_k[x>0]
+  double sxy[MAXK];    // over end[], gs[]: Σ x·y_k
+  double theor[MAXK];  // unchanged
+  double sy[MAXK];     // unchanged: Σy_k
+  double syy[MAXK];    // Σy_k² + the squared per-pixel sums of duplicate candidates
+  int32_t ion, K, ngroups, hits;
+  double sx, sxx, chaos;  // over pad[]: Σx, Σx², raw measure_of_chaos
+  uint32_t flags, state;
+  int32_t pad[4];
+};
+static_assert(sizeof(IonRec) == sizeof(IonDesc) && offsetof(IonRec, theor) == offsetof(IonDesc, theor) &&
+                  offsetof(IonRec, syy) == offsetof(IonDesc, syy) && offsetof(IonRec, ion) == offsetof(IonDesc, ion) &&
+                  offsetof(IonRec, sx) == offsetof(IonDesc, pad),
+              "IonRec overlays IonDesc");
+
 // Work sources of the persistent LDS kernel.
 //  SRC_RANGES: positions [0, n) split into 8 contiguous ranges, one per XCD (workgroup w runs on XCD w % 8),
 //    so concurrently scored ions of one XCD are m/z neighbours and share windows in that XCD's L2; a

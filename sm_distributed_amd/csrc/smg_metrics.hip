@@ -464,7 +464,7 @@ __global__ void ion_desc8_kernel(Hits<FMT> hits, const int64_t* __restrict__ lo,
 // ---------------------------------------------------------------------------------------------
 template <int FMT, int LB, int LRMAX, int LRC, int WPE, int SRC, bool TWO>
 __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
-    Hits<FMT> hits, const IonDesc* __restrict__ desc, Sched S, Params P, double* __restrict__ oc,
+    Hits<FMT> hits, IonDesc* __restrict__ desc, Sched S, Params P, double* __restrict__ oc,
     double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags,
     uint32_t* __restrict__ rej_list, uint32_t* __restrict__ rej_count) {
   constexpr int BLOCK = LB;
@@ -569,7 +569,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
 #pragma unroll
   for (int j = 0; j < RE; ++j) pe[j] = Hits<FMT>::zero();
   auto hs = [&](int j) -> Reg& { return j < RC ? pc[j] : (j < 2 * RC ? pd[j - RC] : pe[j - 2 * RC]); };
-  constexpr bool ASYNC = (FMT == SMG_HITS_PACKED_F32);
+  // Asynchronous (inline-asm, counted-wait) loads in the main pass only; the big-ion pass (~1% of the ions at
+  // config 3) uses compiler-tracked loads: its 8-deep principal slots made the compiler copy in-flight registers
+  constexpr bool ASYNC = (FMT == SMG_HITS_PACKED_F32) && LB <= 512;
   // principal window (<= CAPC points, RMAX per thread).  Async form: every slot issues exactly one load
   // (clamped to the window's last point, or to hit 0 for an empty window) so that the counted waits hold.
   auto issue_principal = [&](const IonDesc* D) {
@@ -624,88 +626,6 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   STAMP_DECL();
   if (tid == 0) ctr[C_NEXT] = (int)sched_resolve<SRC>(S, sched_issue<SRC>(S));
   __syncthreads();
-#ifndef SMG_LATEFIN
-#define SMG_LATEFIN 1
-#endif
-  static_assert(!SMG_LATEFIN || NW >= 2, "late finalize needs a second wave for the LDS initialisation");
-#ifndef SMG_SPLITFIN
-#define SMG_SPLITFIN 1  // wave 0 the spectral score and chaos, wave 1 the spatial score (each about half)
-#endif
-  static_assert(!SMG_SPLITFIN || (SMG_LATEFIN && 8 * NW - 1 >= 32), "split finalize needs the late finalize");
-  struct {
-    double s, sy, syy, sxy, t, sx, sxx, chaos, cs, csc;
-    int K, ion, msm_ion;
-    uint32_t flags;
-    bool pending, msm_pending;
-  } fin;
-  fin.pending = false;
-  fin.msm_pending = false;
-  // wave 1 -> wave 0 across the phase-0 barrier: the last slot of red, which neither the phase-2 sums (5 NW),
-  // block_sum (2 NW) nor wave 0's few-candidate union-find (64 u32) touches -- in the break path wave 1 writes
-  // it while wave 0 may still be in that union-find
-  double* spat_lds = reinterpret_cast<double*>(smem + LY::o_red) + 8 * NW - 1;
-  // the finalize arithmetic of the ion whose inputs wave 0 gathered (a no-op elsewhere)
-  auto finalize = [&]() {
-    if (!fin.pending) return;
-    fin.pending = false;
-    const int k = lane;
-    const int K = fin.K;
-    const double s = fin.s, sy = fin.sy, syy = fin.syy, sxy = fin.sxy, t = fin.t, sx = fin.sx, sxx = fin.sxx;
-    const bool do_spectral = !SMG_SPLITFIN || wid == 0, do_spatial = !SMG_SPLITFIN || wid == 1;
-    // isotope_pattern_match
-    double spectral = 0.0;
-    if (do_spectral) {
-      const double nt = sqrt(wave_sum_dpp(t * t)), ns = sqrt(wave_sum_dpp(s * s));
-      spectral = 1.0 - wave_sum_dpp(k < K ? fabs(t / nt - s / ns) : 0.0) / (double)K;
-      if (spectral == 1.0) spectral = 0.0;
-    }
-    // isotope_image_correlation: np.corrcoef rows, weights = theor[1:]
-    double spatial = 0.0;
-    if (do_spatial && K >= 2) {
-      const double npx = (double)P.npx, n1 = npx - 1.0;
-      const double sd0 = sqrt((sxx - sx * sx / npx) / n1);
-      double rt = 0.0, tw = 0.0;
-      if (k >= 1 && k < K) {
-        const double syy_c = (syy - sy * sy / npx) / n1;
-        const double sxy_c = (sxy - sx * sy / npx) / n1;
-        double r = sxy_c / sqrt(syy_c) / sd0;
-        if (!isnan(r)) r = r > 1.0 ? 1.0 : (r < -1.0 ? -1.0 : r);
-        if (isinf(r)) r = 0.0;
-        rt = r * t;
-        tw = t;
-      }
-      spatial = wave_sum_dpp(rt) / wave_sum_dpp(tw);
-    }
-    if (lane == 0) {
-      double chaos = fin.chaos;
-      if (!isnan(chaos) && fabs(chaos - 1.0) <= 1e-8 + 1e-5) chaos = 0.0;  // np.isclose(moc, 1.0)
-      chaos = clean(chaos);
-      spatial = clean(spatial);
-      spectral = clean(spectral);
-      if (do_spectral) {
-        oc[fin.ion] = chaos;
-        osc[fin.ion] = spectral;
-        oflags[fin.ion] = fin.flags;
-      }
-      if (do_spatial) osp[fin.ion] = spatial;
-      if (!SMG_SPLITFIN) omsm[fin.ion] = chaos * spatial * spectral;
-      else if (wid == 1) spat_lds[0] = spatial;
-      else {
-        fin.cs = chaos;  // msm = chaos * spatial * spectral, multiplied in the oracle's order
-        fin.csc = spectral;
-      }
-    }
-    if (SMG_SPLITFIN && wid == 0) {  // msm after the next barrier, from wave 1's spatial score
-      fin.msm_ion = fin.ion;
-      fin.msm_pending = true;
-    }
-  };
-  auto finalize_msm = [&]() {
-    if (SMG_SPLITFIN && fin.msm_pending) {
-      if (lane == 0) omsm[fin.msm_ion] = fin.cs * spat_lds[0] * fin.csc;
-      fin.msm_pending = false;
-    }
-  };
   int64_t pos = -1;  // ion scored in this iteration (-1: none; the first iteration only issues loads)
   int64_t npos = uni(ctr[C_NEXT]);
   int cur = 0;
@@ -730,7 +650,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     // npos's descriptor: one async word per lane of wave 0 (exactly one load per lane, clamped), waited in
     // phase 2 behind the 2*RC loads of tail chunks 2 and 3
     uint64_t dword = 0;
-    if (wid == 0) {
+    if ((tid >> 6) == 0) {
       if constexpr (ASYNC) {
         ld8_async_wave0(dword, reinterpret_cast<const uint64_t*>(desc + (npos >= 0 ? npos : 0)) +
                                    (lane < DESC_QWORDS ? lane : 0));
@@ -761,27 +681,22 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     }
 
     // ---- phase 0: LDS initialisation -------------------------------------------------------------
-    // wave 0 finishes the previous ion meanwhile (SMG_LATEFIN): the other waves initialise the LDS
-    constexpr int ZW = SMG_LATEFIN ? (SMG_SPLITFIN ? 2 * WAVE : WAVE) : 0;
-    const int zt = tid - ZW;
-    if (!skip && zt >= 0) {
+    if (!skip) {
       uint4* z = reinterpret_cast<uint4*>(smem + LY::o_guard);
-      for (int i = zt; i < P.w32 / 4 + 1; i += BLOCK - ZW) z[i] = make_uint4(0, 0, 0, 0);
-      for (int i = zt; i < MAXK * NW * 4; i += BLOCK - ZW) part[i] = 0.0;
-      if (zt < C_NEXT || zt == C_NS) ctr[zt] = 0;
+      for (int i = tid; i < P.w32 / 4 + 1; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
+      for (int i = tid; i < MAXK * NW * 4; i += BLOCK) part[i] = 0.0;
+      if (tid < C_NEXT || tid == C_NS) ctr[tid] = 0;
 #ifndef SMG_TBL0
 #define SMG_TBL0 1
 #endif
       if (SMG_TBL0) {  // the duplicate table (free since the previous ion's chaos phase), for phase d
-        for (int i = zt; i < DTBL; i += BLOCK - ZW) {
+        for (int i = tid; i < DTBL; i += BLOCK) {
           tkey[i] = 0xFFFFFFFFu;
           tval[i] = 0.0;
         }
       }
     }
-    finalize();
     __syncthreads();
-    finalize_msm();
     STAMP(0);
 
     // ---- phase 1: principal image -> bitmap, rank prefix, f64 values -----------------------------
@@ -844,12 +759,19 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     if (!skip) {  // the principal registers are consumed: tail chunks 2 and 3 go in flight
       issue_chunk(D, 2, pc);
       issue_chunk(D, 3, pd);
+    } else if constexpr (ASYNC) {
+      // the same number of loads (into the same registers, which the next principal overwrites): the waits for
+      // the ticket and the descriptor below count 2*RC younger loads on every path
+#pragma unroll
+      for (int j = 0; j < RC; ++j) {
+        ld8_async_v(pc[j], hits.h);
+        ld8_async_v(pd[j], hits.h);
+      }
     }
     if constexpr (ASYNC) {
-      if (wid == 0) {  // counted waits are per wave: wave 0 waits, lane 0 uses the ticket
-        if (skip) vm_wait1<1>(ticket);
-        else vm_wait1<1 + 2 * RC>(ticket);
-      }
+      // counted waits are per wave: wave 0 waits, lane 0 uses the ticket.  The test is on the laundered tid (an
+      // exec-masked branch, not a scalar one), the form scripts/check_async_regs.py recognises as wave-0 only
+      if ((tid >> 6) == 0) vm_wait1<1 + 2 * RC>(ticket);
     }
     if (tid == 0) ctr[C_NEXT] = (int)sched_resolve<SRC>(S, ticket);
     __syncthreads();
@@ -879,11 +801,8 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
           for (int q = 0; q < 5; ++q) red[q * NW + wid] = acc[q];
         }
       }
-      if (wid == 0) {
-        if constexpr (ASYNC) {  // chunks 2 and 3 were issued after it only if this ion is being scored
-          if (skip) vm_wait1<0>(dword);
-          else vm_wait1<2 * RC>(dword);
-        }
+      if ((tid >> 6) == 0) {  // wave 0 (exec-masked branch, see the ticket's wait)
+        if constexpr (ASYNC) vm_wait1<2 * RC>(dword);  // chunks 2 and 3 (or their stand-ins) were issued after it
         if (npos >= 0 && lane < DESC_QWORDS) reinterpret_cast<uint64_t*>(DN)[lane] = dword;
       }
       __syncthreads();
@@ -1538,45 +1457,38 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       flags |= SMG_ION_CHAOS_NAN;
     }
 
-    // ---- finalize (formula_img_validator.py:78-84 + the restated pyImagingMSpec functions): wave 0,
-    // lane k = window k; sums over lanes in a fixed order.  Its inputs are read here; the arithmetic runs
-    // during the next ion's phase 0, which the other waves do alone (SMG_LATEFIN)
-    if (!skip && wid <= (SMG_SPLITFIN ? 1 : 0)) {
+    // ---- the ion's sums -> its record (the descriptor's consumed fields, IonRec): ion_finalize_kernel turns them
+    // into the scores after the pass (formula_img_validator.py:78-84 + the restated pyImagingMSpec functions), so
+    // the f64 divisions and square roots stay out of this kernel.  Wave 0, lane k = window k.
+    if (!skip && wid == 0) {
+      IonRec* G = reinterpret_cast<IonRec*>(desc + pos);
       const int k = lane;
-      fin.s = fin.sy = fin.syy = fin.sxy = fin.t = 0.0;
       if (k < K) {
-        fin.t = D->theor[k];
+        double sk = 0.0, syy = D->syy[k], sxy = 0.0;  // Σy² + the squared per-pixel sums of duplicate candidates
         if (k == 0) {
-          fin.s = s0;
+          sk = s0;
         } else {
-          fin.sy = D->sy[k];
-          fin.syy = D->syy[k];  // + the squared per-pixel sums of duplicate candidates (part[k][*][2])
 #pragma unroll
           for (int w = 0; w < NW; ++w) {
             const double* pk = part + ((size_t)k * NW + w) * 4;
-            fin.s += pk[0];
-            fin.syy += pk[2];
-            fin.sxy += pk[3];
+            sk += pk[0];
+            syy += pk[2];
+            sxy += pk[3];
           }
         }
+        G->s[k] = sk;
+        G->sxy[k] = sxy;
+        G->syy[k] = syy;
       }
-      fin.K = K;
-      fin.ion = ion;
-      fin.sx = sx;
-      fin.sxx = sxx;
-      fin.chaos = chaos_raw;
-      fin.flags = flags | big_flag | (TWO ? SMG_ION_TWO_LEVEL : 0u) | (uint32_t)D->hits;
-      fin.pending = true;
-      if (!SMG_LATEFIN) finalize();
-    }
-    if (npos < 0) {
-      finalize();
-      if (SMG_SPLITFIN) {
-        __syncthreads();
-        finalize_msm();
+      if (lane == 0) {
+        G->sx = sx;
+        G->sxx = sxx;
+        G->chaos = chaos_raw;
+        G->flags = flags | big_flag | (TWO ? SMG_ION_TWO_LEVEL : 0u) | (uint32_t)D->hits;
+        G->state = 1u;
       }
-      break;
     }
+    if (npos < 0) break;
     pos = npos;
     npos = n2pos;
     cur ^= 1;
@@ -1590,6 +1502,19 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   vm_wait<0>(pc);
   vm_wait<0>(pd);
   vm_wait<0>(pe);
+}
+
+// Scores of the positions the LDS passes scored (IonRec state 1), from the sums they recorded: one thread per
+// position, formula_img_validator.py:78-84 via finalize_ion (the dense passes call it themselves).
+__global__ void ion_finalize_kernel(const IonRec* __restrict__ rec, int64_t n, double npx, double* __restrict__ oc,
+                                    double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm,
+                                    uint32_t* __restrict__ oflags) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const IonRec* R = rec + i;
+  if (R->state != 1u) return;
+  finalize_ion(R->K, R->theor, R->s, R->sx, R->sxx, R->sy, R->syy, R->sxy, npx, R->chaos, R->ion, R->flags, oc, osp,
+               osc, omsm, oflags);
 }
 
 // position list -> ion list (when the big-ion pass is skipped, the dense kernel reads ion indices)
@@ -3439,6 +3364,12 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   } else {
     hipLaunchKernelGGL(list_all_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, list_b, hdr + 2,
                        ion_order, n_ions);
+    SMG_LAUNCH_CHECK();
+  }
+  if (main_ok || big_ok) {  // the scores of every position the LDS passes scored
+    PassTimer tm(SMG_PASS_FINALIZE, st);
+    hipLaunchKernelGGL(ion_finalize_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st,
+                       reinterpret_cast<const IonRec*>(desc), n_ions, (double)P.npx, oc, osp, osc, omsm, oflags);
     SMG_LAUNCH_CHECK();
   }
   const int nslots = (int)(n_ions < DENSE_SLOTS ? n_ions : DENSE_SLOTS);

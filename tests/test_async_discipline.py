@@ -2,8 +2,9 @@
 register with a load in flight before its counted wait, on any control-flow path, and no such register is spilled
 (scripts/check_async_regs.py).  CPU-only: compiles the kernels to assembly.
 
-* ion_wide_kernel uses compiler-tracked loads only: no asynchronous load at all.
-* ion_pipe_kernel (the main pass and the big-ion pass) keeps its asynchronous loads: zero violations.  Its two
+* ion_wide_kernel and the big-ion pass (ion_pipe_kernel<1024>) use compiler-tracked loads only: no asynchronous
+  load at all.
+* the main pass (ion_pipe_kernel<512>) keeps its asynchronous loads: zero violations.  Its two
   wave-0 loads (scheduling ticket, ion descriptor; tagged "smg:wave0") are waited by wave 0 only; paths that skip
   that wait through an exec-zero branch (the other waves, which issued no such load) are reported as guarded, and
   only for tagged loads -- an untagged load, or a tagged one whose wait is skipped on a path without an exec-zero
@@ -35,15 +36,15 @@ def test_async_load_registers_are_never_touched_in_flight(tmp_path):
     asm = str(tmp_path / "smg_metrics.s")
     subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "--cuda-device-only",
                     "-S", src, "-o", asm], check=True, capture_output=True)
-    n_loads, n_bad, n_guarded, out = _check(asm, "_ZN3smg15ion_wide_kernelILi0E")
-    assert (n_loads, n_bad, n_guarded) == (0, 0, 0), out
-    for kern in ("_ZN3smg15ion_pipe_kernelILi0ELi512", "_ZN3smg15ion_pipe_kernelILi0ELi1024"):
+    for kern in ("_ZN3smg15ion_wide_kernelILi0E", "_ZN3smg15ion_pipe_kernelILi0ELi1024"):
         n_loads, n_bad, n_guarded, out = _check(asm, kern)
-        assert n_loads > 0 and n_bad == 0, out
-        # every guarded report is one of the tagged wave-0 loads (two per instantiation at most)
-        guarded = [l for l in out.split("\n") if l.startswith("GUARDED")]
-        assert all("smg:wave0" in l for l in guarded), out
-        assert n_guarded <= 4, out
+        assert (n_loads, n_bad, n_guarded) == (0, 0, 0), out
+    n_loads, n_bad, n_guarded, out = _check(asm, "_ZN3smg15ion_pipe_kernelILi0ELi512")
+    assert n_loads > 0 and n_bad == 0, out
+    # every guarded report is one of the tagged wave-0 loads (two per instantiation at most)
+    guarded = [l for l in out.split("\n") if l.startswith("GUARDED")]
+    assert all("smg:wave0" in l for l in guarded), out
+    assert n_guarded <= 4, out
 
 
 def _kernel(tmp_path, lines):
@@ -74,3 +75,14 @@ def test_checker_execz_paths(tmp_path):
                            "v_mov_b32_e32 v5, 1"] + body)
     n_loads, n_bad, n_guarded, out = _check(s, "_ZN3smg4testE")
     assert (n_loads, n_bad) == (1, 1), out
+
+
+def test_checker_execnz_fallthrough_is_exec_zero(tmp_path):
+    """s_cbranch_execnz jumps to the wave-0 block that waits; its fall-through (exec zero) reaches the use: guarded
+    for a tagged load, a violation for an untagged one."""
+    body = ["s_cbranch_execnz .LBB0_3", ".LBB0_2:", "v_mov_b32_e32 v4, 0", "s_endpgm", ".LBB0_3:", ";;#ASMSTART",
+            "s_waitcnt vmcnt(0)", ";;#ASMEND", "s_branch .LBB0_2"]
+    for tag, bad, guarded in (("", 1, 0), (" ; smg:wave0", 0, 1)):
+        s = _kernel(tmp_path, [";;#ASMSTART", "global_load_dwordx2 v[4:5], v[8:9], off" + tag, ";;#ASMEND"] + body)
+        n_loads, n_bad, n_guarded, out = _check(s, "_ZN3smg4testE")
+        assert (n_loads, n_bad, n_guarded) == (1, bad, guarded), out
