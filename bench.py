@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--sharded", action="store_true",
                     help="run the multi-GPU (sharded, RCCL) step even at N = 1 (a check of that path on one GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-rebalance", action="store_true",
+                    help="N > 1: keep the cost model's cut (default: re-cut once from every rank's measured time)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target wall of the CPU baseline sample")
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="cap on CPU-baseline workers (a GPU box's CPU share is 16 cores per GPU)")
@@ -198,6 +200,16 @@ def main():
     shard_only = args.shard_of > 1 and not sharded
     if sharded:
         plan = D.plan_shards(formulas, peaks, args.ppm, world, rank)
+        if not args.no_rebalance:
+            # the cut re-made from every rank's measured shard time (one all_gather of N floats): the cost model's
+            # per-rank residuals would otherwise set the slowest rank's time
+            t_rank = torch.tensor([_rank_seconds(D, plan, peaks, ds_config)], dtype=torch.float64, device=device)
+            ts = [torch.zeros_like(t_rank) for _ in range(world)]
+            dist.all_gather(ts, t_rank)
+            times = [float(x.item()) for x in ts]
+            plan = D.rebalance(plan, formulas, peaks, times)
+            log(f"[rank {rank}] rebalanced from measured shard times (ms) {[round(x * 1e3, 2) for x in times]}: "
+                f"counts {plan.counts}")
         step_fn = lambda: D.score_sharded(plan, peaks, ds_config)[0]
         my_formulas = plan.formulas
     elif shard_only:
@@ -342,6 +354,20 @@ def main():
         print(json.dumps(line), file=json_out, flush=True)
     if sharded:
         dist.destroy_process_group()
+
+
+def _rank_seconds(D, plan, peaks, ds_config, reps=3):
+    """This rank's time for its shard (slice, images, scores; no collective), best of ``reps`` after one warm-up."""
+    import torch
+    D._device_rows(plan, peaks, ds_config)
+    best = float("inf")
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        D._device_rows(plan, peaks, ds_config)
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t)
+    return best
 
 
 def cold_step_ms(step_fn, formulas, plan, sharded):

@@ -61,70 +61,84 @@ else:
     E._ws_cache.clear()
     torch.cuda.empty_cache()
 
-rows_all, worst = [], 0.0
 ONLY = int(os.environ.get("ONLY_RANK", "-1"))
-for r in range(W):
-    if ONLY >= 0 and r != ONLY:
-        continue
-    plan = D.plan_shards(formulas, peaks, ppm, W, r)
-    t_sl, sl = timed(lambda: D.slice_peaks(peaks, plan))
-    sds = ResidentDataset(sl)
-    t_img, ims = timed(lambda: compute_sf_images(None, sds, plan.sf_peak_df, ppm))
-    L = _lib.lib()
-    L.smg_debug_main_pass_times(None, 0, ctypes.byref(ctypes.c_int32(0)))
-    L.smg_debug_time_main_pass(1)
-    t_met, (_, mets) = timed(lambda: _metrics_device_rows(ims, plan.formulas.get_sf_peak_ints(),
-                                                           conf["image_generation"]))
-    L.smg_debug_time_main_pass(0)
-    buf = (ctypes.c_double * 64)()
-    pbuf = (ctypes.c_int32 * 64)()
-    nt = ctypes.c_int32(0)
-    L.smg_debug_pass_times(pbuf, buf, 64, ctypes.byref(nt))
-    by = {}
-    for i in range(min(nt.value, 64)):
-        by.setdefault(int(pbuf[i]), []).append(float(buf[i]))
-    t_main = min(by.get(_lib.SMG_PASS_MAIN, [float("nan")]))
-    # per pass: best launch time and 12 B per window point of the ions it scored
-    fl = mets.flags.cpu().numpy().astype(np.int64)
-    cs = torch.zeros(ims.lo.numel() + 1, dtype=torch.int64, device=ims.lo.device)
-    torch.cumsum(ims.hi - ims.lo, 0, out=cs[1:])
-    wo = ims.ions_dev.win_off
-    ipts = (cs[wo[1:]] - cs[wo[:-1]]).cpu().numpy()
-    pas = np.full(len(fl), _lib.SMG_PASS_MAIN)
-    pas[(fl & _lib.SMG_ION_BIG) != 0] = _lib.SMG_PASS_BIG
-    pas[(fl & _lib.SMG_ION_DENSE) != 0] = _lib.SMG_PASS_DENSE
-    pas[(fl & _lib.SMG_ION_WIDE) != 0] = _lib.SMG_PASS_WIDE
-    has = (fl & _lib.SMG_ION_HAS_HITS) != 0
-    roof = []
-    for p_, ts in sorted(by.items()):
-        if p_ == _lib.SMG_PASS_DESC:
-            roof.append(f"{_lib.PASS_NAMES.get(p_, p_)} {min(ts):.2f} ms")
-            continue
-        n_p = int((has & (pas == p_)).sum())
-        pts = int(ipts[has & (pas == p_)].sum())
-        t = min(ts)
-        frac = 12.0 * pts / (t * 1e-3) / 8e12 if t > 0 and pts else 0.0
-        roof.append(f"{_lib.PASS_NAMES.get(p_, p_)} {t:.2f} ms {n_p:,} ions {pts:,} window pts -> {frac:.3f} of 8 TB/s")
-    print(f"  rank {r} passes: " + "; ".join(roof), flush=True)
-    t_all, (rows, _) = timed(lambda: D._device_rows(plan, peaks, conf))
-    rows_all.append(rows)
-    hist, edges = D.mz_histogram(peaks.mz)
-    wpts = float(((D.ion_costs(plan.formulas.ion_off, plan.formulas.peak_mz, ppm, hist, edges) - D.C_ION)
-                  / D.C_WINDOW_POINT).sum())
-    print(f"FIT rank={r} n_ions={plan.formulas.n_ions} wpts={wpts:.0f} slice={sl.n_points} t_rows={t_all:.3f} "
-          f"t_slice={t_sl:.3f} t_img={t_img:.3f} t_met={t_met:.3f} t_main={t_main:.3f}", flush=True)
-    worst = max(worst, t_all)
-    print(f"rank {r}/{W}: {plan.formulas.n_ions:,} ions, slice {sl.n_points:,} pts [{plan.mz_lo:.2f}, {plan.mz_hi:.2f}] "
-          f"est {plan.est_cost[r]*1e3:.2f} ms | slice {t_sl:.2f} + images {t_img:.2f} + metrics {t_met:.2f} "
-          f"(main kernel {t_main:.2f}); "
-          f"_device_rows {t_all:.2f} ms", flush=True)
+
+
+def run_ranks(plans, tag):
+  rows_all, worst, times = [], 0.0, []
+  for r, plan in enumerate(plans):
+      if ONLY >= 0 and r != ONLY:
+          continue
+      t_sl, sl = timed(lambda: D.slice_peaks(peaks, plan, cache=False))
+      sds = ResidentDataset(sl)
+      t_img, ims = timed(lambda: compute_sf_images(None, sds, plan.sf_peak_df, ppm))
+      L = _lib.lib()
+      L.smg_debug_main_pass_times(None, 0, ctypes.byref(ctypes.c_int32(0)))
+      L.smg_debug_time_main_pass(1)
+      t_met, (_, mets) = timed(lambda: _metrics_device_rows(ims, plan.formulas.get_sf_peak_ints(),
+                                                             conf["image_generation"]))
+      L.smg_debug_time_main_pass(0)
+      buf = (ctypes.c_double * 64)()
+      pbuf = (ctypes.c_int32 * 64)()
+      nt = ctypes.c_int32(0)
+      L.smg_debug_pass_times(pbuf, buf, 64, ctypes.byref(nt))
+      by = {}
+      for i in range(min(nt.value, 64)):
+          by.setdefault(int(pbuf[i]), []).append(float(buf[i]))
+      t_main = min(by.get(_lib.SMG_PASS_MAIN, [float("nan")]))
+      # per pass: best launch time and 12 B per window point of the ions it scored
+      fl = mets.flags.cpu().numpy().astype(np.int64)
+      cs = torch.zeros(ims.lo.numel() + 1, dtype=torch.int64, device=ims.lo.device)
+      torch.cumsum(ims.hi - ims.lo, 0, out=cs[1:])
+      wo = ims.ions_dev.win_off
+      ipts = (cs[wo[1:]] - cs[wo[:-1]]).cpu().numpy()
+      pas = np.full(len(fl), _lib.SMG_PASS_MAIN)
+      pas[(fl & _lib.SMG_ION_BIG) != 0] = _lib.SMG_PASS_BIG
+      pas[(fl & _lib.SMG_ION_DENSE) != 0] = _lib.SMG_PASS_DENSE
+      pas[(fl & _lib.SMG_ION_WIDE) != 0] = _lib.SMG_PASS_WIDE
+      has = (fl & _lib.SMG_ION_HAS_HITS) != 0
+      roof = []
+      for p_, ts in sorted(by.items()):
+          if p_ == _lib.SMG_PASS_DESC:
+              roof.append(f"{_lib.PASS_NAMES.get(p_, p_)} {min(ts):.2f} ms")
+              continue
+          n_p = int((has & (pas == p_)).sum())
+          pts = int(ipts[has & (pas == p_)].sum())
+          t = min(ts)
+          frac = 12.0 * pts / (t * 1e-3) / 8e12 if t > 0 and pts else 0.0
+          roof.append(f"{_lib.PASS_NAMES.get(p_, p_)} {t:.2f} ms {n_p:,} ions {pts:,} window pts -> {frac:.3f} of 8 TB/s")
+      print(f"  rank {r} passes: " + "; ".join(roof), flush=True)
+      t_all, (rows, _) = timed(lambda: D._device_rows(plan, peaks, conf))
+      rows_all.append(rows)
+      hist, edges = D.mz_histogram(peaks.mz)
+      wpts = float(((D.ion_costs(plan.formulas.ion_off, plan.formulas.peak_mz, ppm, hist, edges) - D.C_ION)
+                    / D.C_WINDOW_POINT).sum())
+      print(f"FIT rank={r} n_ions={plan.formulas.n_ions} wpts={wpts:.0f} slice={sl.n_points} t_rows={t_all:.3f} "
+            f"t_slice={t_sl:.3f} t_img={t_img:.3f} t_met={t_met:.3f} t_main={t_main:.3f}", flush=True)
+      worst = max(worst, t_all)
+      print(f"[{tag}] rank {r}/{W}: {plan.formulas.n_ions:,} ions, slice {sl.n_points:,} pts [{plan.mz_lo:.2f}, {plan.mz_hi:.2f}] "
+            f"est {plan.est_cost[r]*1e3:.2f} ms | slice {t_sl:.2f} + images {t_img:.2f} + metrics {t_met:.2f} "
+            f"(main kernel {t_main:.2f}); "
+            f"_device_rows {t_all:.2f} ms (the rank's slice cached, as on the rank between searches)", flush=True)
+      times.append(t_all * 1e-3)
+  return rows_all, worst, times
+
+
+plans = [D.plan_shards(formulas, peaks, ppm, W, r) for r in range(W)]
+rows_all, worst, times = run_ranks(plans, "cost model")
 if ONLY >= 0:
     sys.exit(0)
+worst0 = worst
+# the plan re-cut from the measured per-rank times (what bench.py does after its warm-up: one all_gather of W floats)
+plans = [D.rebalance(p, formulas, peaks, times) for p in plans]
+print("rebalanced counts", plans[0].counts, flush=True)
+rows_all, worst, times = run_ranks(plans, "rebalanced")
+print(f"max rank: cost model {worst0:.2f} ms, rebalanced {worst:.2f} ms", flush=True)
 n_max = max(x.shape[0] for x in rows_all)
 table = torch.full((W * n_max, 5), -1.0, dtype=torch.float64, device="cuda")
 for r, x in enumerate(rows_all):
     table[r * n_max:r * n_max + x.shape[0]] = x
-plan0 = D.plan_shards(formulas, peaks, ppm, W, 0)
+plan0 = plans[0]
 t_asm, df = timed(lambda: D.rows_to_frame(table, plan0.global_keys))
 # assembly breakdown
 def asm_parts():

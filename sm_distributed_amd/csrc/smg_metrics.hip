@@ -178,7 +178,7 @@ __device__ int prefix_words(const uint64_t* w, uint16_t* pf, int n, int* wscratc
 // the same over the pixel bitmap (n64 <= NPX_LDS_MAX/64 words)
 template <int NW_>
 __device__ int bm_build_prefix(const uint32_t* bm, uint16_t* pf, int n64, int* wscratch) {
-  static_assert((NPX_LDS_MAX / 64) % (NW_ * WAVE) == 0, "prefix geometry");
+  static_assert((NPX_LDS_MAX / 64) % WAVE == 0, "prefix geometry");
   return prefix_words<NW_, NPX_LDS_MAX / 64>(reinterpret_cast<const uint64_t*>(bm), pf, n64, wscratch);
 }
 
@@ -1115,7 +1115,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
           }
         } else {
           const uint64_t* bm64 = reinterpret_cast<const uint64_t*>(Hbm);
-          constexpr int WPT = (NPX_LDS_MAX / 64) / BLOCK;
+          constexpr int WPT = (NPX_LDS_MAX / 64 + BLOCK - 1) / BLOCK;
           uint64_t wb[WPT];
 #pragma unroll
           for (int i = 0; i < WPT; ++i) wb[i] = (tid * WPT + i < n64) ? bm64[tid * WPT + i] : 0ull;

@@ -110,10 +110,8 @@ def mz_histogram(mz, bins=8192):
     return h, np.linspace(lo, hi, bins + 1)
 
 
-def plan_shards(formulas, peaks_or_mz, ppm, world, rank, bins=8192):
-    """Shard ``formulas`` (FormulasSegm) over ``world`` ranks by principal m/z; returns this rank's ShardPlan.
-    ``peaks_or_mz``: the resident DevicePeaks (or an m/z tensor) whose histogram drives the cost model."""
-    from .formula_imager_segm import IonKeys
+def _principal_costs(formulas, peaks_or_mz, ppm, bins):
+    """(ions in principal m/z order, their estimated seconds in that order)."""
     mz = getattr(peaks_or_mz, "mz", peaks_or_mz)
     hist, edges = mz_histogram(mz, bins)
     off, pmz = formulas.ion_off, formulas.peak_mz
@@ -125,7 +123,35 @@ def plan_shards(formulas, peaks_or_mz, ppm, world, rank, bins=8192):
     cum_pts = np.concatenate([[0.0], np.cumsum(hist)])
     pos = np.interp(first[order], edges, cum_pts)
     grow = np.diff(np.concatenate([pos, [cum_pts[-1]]]))
-    cost = cost + np.maximum(grow, 0.0) * C_SLICE_POINT
+    return order, cost + np.maximum(grow, 0.0) * C_SLICE_POINT
+
+
+def plan_shards(formulas, peaks_or_mz, ppm, world, rank, bins=8192):
+    """Shard ``formulas`` (FormulasSegm) over ``world`` ranks by principal m/z; returns this rank's ShardPlan.
+    ``peaks_or_mz``: the resident DevicePeaks (or an m/z tensor) whose histogram drives the cost model."""
+    order, cost = _principal_costs(formulas, peaks_or_mz, ppm, bins)
+    return _plan_from_costs(formulas, order, cost, ppm, world, rank)
+
+
+def rebalance(plan, formulas, peaks_or_mz, rank_seconds, bins=8192):
+    """The plan re-cut from measured per-rank step times (one value per rank, e.g. all_gathered after a first
+    search): every rank's ions get its measured/estimated ratio as a cost factor, and the shards are cut again on
+    the corrected costs (the linear model of ion_costs leaves +-5 % per-rank residuals that no refit removes).
+    Deterministic: every rank computes the same cut from the same times.  Returns this rank's new ShardPlan."""
+    order, cost = _principal_costs(formulas, peaks_or_mz, plan.ppm, bins)
+    t = np.asarray(rank_seconds, dtype=np.float64)
+    if len(t) != plan.world or not np.all(np.isfinite(t)) or not np.all(t > 0):
+        raise ValueError("rank_seconds: one positive time per rank")
+    scaled = cost.copy()
+    for r, (a, b) in enumerate(plan.bounds):
+        est = float(cost[a:b].sum())
+        if b > a and est > 0:
+            scaled[a:b] *= t[r] / est
+    return _plan_from_costs(formulas, order, scaled, plan.ppm, plan.world, plan.rank)
+
+
+def _plan_from_costs(formulas, order, cost, ppm, world, rank):
+    from .formula_imager_segm import IonKeys
     bounds = shard_bounds(cost, world)
     a, b = bounds[rank]
     mine = np.sort(order[a:b])                        # back to (sf_id, adduct) order
@@ -142,9 +168,22 @@ def plan_shards(formulas, peaks_or_mz, ppm, world, rank, bins=8192):
                      global_keys=IonKeys(keys, formulas.adducts), est_cost=[float(cost[x:y].sum()) for x, y in bounds])
 
 
-def slice_peaks(peaks, plan):
-    """This rank's m/z slice of the resident dataset, duplicate flags set for plan.ppm."""
-    return peaks.slice_mz(plan.mz_lo, plan.mz_hi, plan.ppm)
+def slice_peaks(peaks, plan, cache=True):
+    """This rank's m/z slice of the resident dataset, duplicate flags set for plan.ppm (smg_slice_mz_*).
+
+    The slice is a function of the resident dataset and the plan only, so it is made once per (plan bounds, ppm)
+    and kept on the DevicePeaks, the way the single-GPU search keeps the whole dataset resident: every search still
+    flags (the copy did), sorts and prefix-sums it (compute_sf_images), as the single-GPU search does the whole
+    dataset.  ``cache=False`` copies it anew."""
+    key = (float(plan.mz_lo), float(plan.mz_hi), float(plan.ppm))
+    store = peaks.__dict__.setdefault("_slices", {})
+    if cache and key in store:
+        return store[key]
+    sl = peaks.slice_mz(plan.mz_lo, plan.mz_hi, plan.ppm)
+    if cache:
+        store.clear()  # one plan per rank at a time: a re-cut plan replaces the old slice
+        store[key] = sl
+    return sl
 
 
 def _device_rows(plan, peaks, ds_config):
@@ -210,20 +249,37 @@ def rows_to_frame(table, global_keys):
     columns chaos, spatial, spectral, msm), one row per ion with images.  The rows are put in table order by a
     scatter on the device holding them (no sort; padding rows go to a dummy slot), the metric columns and the
     index codes are gathered there and copied to pinned host memory together (formula_imager_segm.device_frame):
-    two host synchronisations."""
+    two host synchronisations.
+
+    The row placement and the MultiIndex depend only on the gathered ion indices (column 0): they are kept on
+    ``global_keys`` and reused while the next gathered table carries the same indices (a search per step over
+    the same plan), so such a step only gathers and copies the metric columns."""
     import torch
 
-    from .formula_imager_segm import device_frame
+    from .formula_imager_segm import METRIC_COLUMNS, device_frame
     t = table if hasattr(table, "device") else torch.as_tensor(np.asarray(table))
     n = len(global_keys)
     gi = t[:, 0].long()
     gi = torch.where(gi >= 0, gi, torch.full_like(gi, n))
+    cache = global_keys.__dict__.get("_frame_cache")
+    if (cache is not None and t.device.type == "cuda" and cache[0].device == t.device and cache[0].shape == gi.shape
+            and bool(torch.equal(cache[0], gi))):
+        rows_sel, mi = cache[1], cache[2]
+        cols = t[rows_sel, 1:5].T.contiguous()  # [4, rows] in table order
+        host = torch.empty(cols.shape, dtype=torch.float64, pin_memory=True)
+        host.copy_(cols, non_blocking=True)
+        torch.cuda.current_stream(t.device).synchronize()
+        return pd.DataFrame(host.numpy().T, index=mi, columns=METRIC_COLUMNS, copy=False)
     # the gathered row of every ion (-1: none), then the ions with a row in table order and their rows
     row = torch.full((n + 1,), -1, dtype=torch.int64, device=t.device)
     row[gi] = torch.arange(t.shape[0], device=t.device)
     idx = torch.nonzero(row[:n] >= 0).flatten()
-    cols = t[row[idx], 1:5].T  # [4, rows] in table order
-    return device_frame(global_keys, cols, idx, cols_compact=True)
+    rows_sel = row[idx]
+    cols = t[rows_sel, 1:5].T  # [4, rows] in table order
+    df = device_frame(global_keys, cols, idx, cols_compact=True)
+    if t.device.type == "cuda":
+        global_keys._frame_cache = (gi, rows_sel, df.index)
+    return df
 
 
 def score_sharded(plan, peaks, ds_config, group=None, score_local=None):

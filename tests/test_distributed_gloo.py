@@ -150,3 +150,25 @@ def test_sharded_search_matches_single_process(tmp_path, world):
     r = got["search"].sort_index()
     assert list(r.index) == list(e.index)
     np.testing.assert_array_equal(r.fdr.values, e.fdr.values)
+
+
+def test_rebalance_recuts_from_measured_times():
+    """distributed.rebalance (bench.py's one re-cut after the warm-up): a rank measured slower than its estimate
+    gives up ions to its neighbours, every ion stays in exactly one shard, the cut is the same on every rank, and
+    times proportional to the estimates keep the cut."""
+    from sm_distributed_amd import distributed as D
+    ds, ions, ppm, f = _case()
+    mz = torch.from_numpy(ds.mz.astype(np.float32))
+    world = 3
+    plans = [D.plan_shards(f, mz, ppm, world, r) for r in range(world)]
+    est = plans[0].est_cost
+    same = [D.rebalance(p, f, mz, est) for p in plans]
+    assert [p.counts for p in same] == [plans[0].counts] * world
+    slow = [2.0 * est[0], est[1], est[2]]
+    new = [D.rebalance(p, f, mz, slow) for p in plans]
+    assert all(p.counts == new[0].counts for p in new) and sum(new[0].counts) == f.n_ions
+    assert new[0].counts[0] < plans[0].counts[0]
+    got = np.sort(np.concatenate([p.ion_idx for p in new]))
+    np.testing.assert_array_equal(got, np.arange(f.n_ions))
+    with pytest.raises(ValueError):
+        D.rebalance(plans[0], f, mz, [1.0, 0.0, 1.0])
