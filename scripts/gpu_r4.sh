@@ -33,6 +33,9 @@ for s in $STEPS; do
     variants)
       timeout -k 10 900 bash scripts/variants.sh > gpurun_out/$TAG/variants.log 2>&1 || { tail -30 gpurun_out/$TAG/variants.log; exit 1; }
       cp gpurun_out/variants.log gpurun_out/$TAG/variants_summary.log 2>/dev/null; grep "ion_metrics" gpurun_out/$TAG/variants.log ;;
+    stamps)
+      timeout -k 10 300 python3 -u scripts/diag_stamps.py > gpurun_out/$TAG/stamps.txt 2>&1 || { tail -30 gpurun_out/$TAG/stamps.txt; exit 1; }
+      grep -v amdgpu.ids gpurun_out/$TAG/stamps.txt ;;
     c3shards)
       timeout -k 10 400 python3 -u scripts/time_shards.py 8 > gpurun_out/$TAG/c3_time_shards_8.txt 2>&1 \
         || { tail -30 gpurun_out/$TAG/c3_time_shards_8.txt; exit 1; }

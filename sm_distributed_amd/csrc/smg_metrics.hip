@@ -1504,17 +1504,75 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   vm_wait<0>(pe);
 }
 
-// Scores of the positions the LDS passes scored (IonRec state 1), from the sums they recorded: one thread per
-// position, formula_img_validator.py:78-84 via finalize_ion (the dense passes call it themselves).
-__global__ void ion_finalize_kernel(const IonRec* __restrict__ rec, int64_t n, double npx, double* __restrict__ oc,
-                                    double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm,
-                                    uint32_t* __restrict__ oflags) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const IonRec* R = rec + i;
-  if (R->state != 1u) return;
-  finalize_ion(R->K, R->theor, R->s, R->sx, R->sxx, R->sy, R->syy, R->sxy, npx, R->chaos, R->ion, R->flags, oc, osp,
-               osc, omsm, oflags);
+// Scores of the positions the LDS passes scored (IonRec state 1), from the sums they recorded (formula_img_validator.py
+// :78-84 + the restated pyImagingMSpec functions, the arithmetic of finalize_ion): eight lanes per position, lane k
+// = window k, so that a record's fields are read as coalesced 64-B runs; the sums over windows are taken in window
+// order (lane 0 gathers them), as finalize_ion does.
+__global__ void __launch_bounds__(256) ion_finalize_kernel(const IonRec* __restrict__ rec, int64_t n, double npx,
+                                                           double* __restrict__ oc, double* __restrict__ osp,
+                                                           double* __restrict__ osc, double* __restrict__ omsm,
+                                                           uint32_t* __restrict__ oflags) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = t >> 3;
+  const int k = (int)(t & 7);
+  const bool live = i < n && rec[i].state == 1u;
+  const IonRec* R = rec + (live ? i : 0);
+  const int K = live ? R->K : 0;
+  const bool act = live && k < K;
+  const double tk = act ? R->theor[k] : 0.0, sk = act ? R->s[k] : 0.0;
+  double rt = 0.0;  // r_k * t_k of isotope_image_correlation (k >= 1)
+  if (act && k >= 1 && K >= 2) {
+    const double sx = R->sx, n1 = npx - 1.0;
+    const double sd0 = sqrt((R->sxx - sx * sx / npx) / n1);
+    const double sy = R->sy[k];
+    const double syy_c = (R->syy[k] - sy * sy / npx) / n1;
+    const double sxy_c = (R->sxy[k] - sx * sy / npx) / n1;
+    double r = sxy_c / sqrt(syy_c) / sd0;
+    if (!isnan(r)) r = r > 1.0 ? 1.0 : (r < -1.0 ? -1.0 : r);
+    if (isinf(r)) r = 0.0;
+    rt = r * tk;
+  }
+  // gather the eight lanes' terms in lane 0 of the group (window order)
+  const int g0 = (threadIdx.x & 63) & ~7;
+  double T[MAXK], S[MAXK], RT[MAXK];
+#pragma unroll
+  for (int j = 0; j < MAXK; ++j) {
+    T[j] = __shfl(tk, g0 + j, 64);
+    S[j] = __shfl(sk, g0 + j, 64);
+    RT[j] = __shfl(rt, g0 + j, 64);
+  }
+  if (!live || k != 0) return;
+  // isotope_pattern_match
+  double tt = 0.0, ss = 0.0;
+  for (int j = 0; j < K; ++j) {
+    tt += T[j] * T[j];
+    ss += S[j] * S[j];
+  }
+  const double nt = sqrt(tt), ns = sqrt(ss);
+  double acc = 0.0;
+  for (int j = 0; j < K; ++j) acc += fabs(T[j] / nt - S[j] / ns);
+  double spectral = 1.0 - acc / (double)K;
+  if (spectral == 1.0) spectral = 0.0;
+  double spatial = 0.0;
+  if (K >= 2) {
+    double num = 0.0, den = 0.0;
+    for (int j = 1; j < K; ++j) {
+      num += RT[j];
+      den += T[j];
+    }
+    spatial = num / den;
+  }
+  double chaos = R->chaos;
+  if (!isnan(chaos) && fabs(chaos - 1.0) <= 1e-8 + 1e-5) chaos = 0.0;  // np.isclose(moc, 1.0)
+  chaos = clean(chaos);
+  spatial = clean(spatial);
+  spectral = clean(spectral);
+  const int64_t ion = R->ion;
+  oc[ion] = chaos;
+  osp[ion] = spatial;
+  osc[ion] = spectral;
+  omsm[ion] = chaos * spatial * spectral;
+  oflags[ion] = R->flags;
 }
 
 // position list -> ion list (when the big-ion pass is skipped, the dense kernel reads ion indices)
@@ -3368,7 +3426,7 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   }
   if (main_ok || big_ok) {  // the scores of every position the LDS passes scored
     PassTimer tm(SMG_PASS_FINALIZE, st);
-    hipLaunchKernelGGL(ion_finalize_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(ion_finalize_kernel, dim3((unsigned)((n_ions * 8 + 255) / 256)), dim3(256), 0, st,
                        reinterpret_cast<const IonRec*>(desc), n_ions, (double)P.npx, oc, osp, osc, omsm, oflags);
     SMG_LAUNCH_CHECK();
   }
