@@ -624,6 +624,23 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   // scheduling runs one ion further ahead than the loads: iteration b scores pos, loads npos's descriptor and
   // data, and takes the ticket of the ion after npos
   STAMP_DECL();
+  // The LDS structures start zeroed: the pixel set and the values here, then at the end of every ion that used
+  // them (by the waves other than wave 0, while it writes the ion's record), so that no ion starts with a barrier of
+  // its own; the window partials and the counters are zeroed in phase 1 before its first barrier, the duplicate
+  // table before the tail stream's closing barrier.
+  auto clear_set_vals = [&](int t0, int nt) {
+    uint4* z = reinterpret_cast<uint4*>(smem + LY::o_guard);
+    for (int i = t0; i < P.w32 / 4 + 1; i += nt) z[i] = make_uint4(0, 0, 0, 0);
+    uint4* zv = reinterpret_cast<uint4*>(smem + LY::o_vals);
+    for (int i = t0; i < CAPC / 2; i += nt) zv[i] = make_uint4(0, 0, 0, 0);
+  };
+  auto clear_table = [&]() {
+    for (int i = tid; i < DTBL; i += BLOCK) {
+      tkey[i] = 0xFFFFFFFFu;
+      tval[i] = 0.0;
+    }
+  };
+  clear_set_vals(tid, BLOCK);
   if (tid == 0) ctr[C_NEXT] = (int)sched_resolve<SRC>(S, sched_issue<SRC>(S));
   __syncthreads();
   int64_t pos = -1;  // ion scored in this iteration (-1: none; the first iteration only issues loads)
@@ -680,29 +697,17 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       }
     }
 
-    // ---- phase 0: LDS initialisation -------------------------------------------------------------
-    if (!skip) {
-      uint4* z = reinterpret_cast<uint4*>(smem + LY::o_guard);
-      for (int i = tid; i < P.w32 / 4 + 1; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
-      for (int i = tid; i < MAXK * NW * 4; i += BLOCK) part[i] = 0.0;
-      if (tid < C_NEXT || tid == C_NS) ctr[tid] = 0;
-#ifndef SMG_TBL0
-#define SMG_TBL0 1
-#endif
-      if (SMG_TBL0) {  // the duplicate table (free since the previous ion's chaos phase), for phase d
-        for (int i = tid; i < DTBL; i += BLOCK) {
-          tkey[i] = 0xFFFFFFFFu;
-          tval[i] = 0.0;
-        }
-      }
-    }
-    __syncthreads();
+    const bool began = !skip;  // this ion uses the LDS structures (cleared again at its end)
     STAMP(0);
 
     // ---- phase 1: principal image -> bitmap, rank prefix, f64 values -----------------------------
     int nnz = 0;
     uint32_t* olist = nullptr;
     if (!skip) {
+      // the window partials (first added to in the tail stream) and the counters (dup table, chaos), ordered before
+      // their uses by phase 1's first barrier
+      for (int i = tid; i < MAXK * NW * 4; i += BLOCK) part[i] = 0.0;
+      if (tid < C_NEXT || tid == C_NS) ctr[tid] = 0;
       vm_wait<2 * RC>(pc);  // the principal window was issued before this ion's tail chunks 0 and 1
       vm_wait<2 * RC>(pd);
       vm_wait<2 * RC>(pe);
@@ -731,28 +736,16 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       olist = reinterpret_cast<uint32_t*>(vals) + (nnz <= OL_MAX ? ((2 * nnz + 3) & ~3) : 0);
       // A point without the duplicate-candidate flag is the only point of its pixel in this window
       // (smg_flag_duplicates), so it stores its value; flagged points (true duplicates and a few false
-      // positives) zero the slot here and add atomically after a barrier (coo.toarray() sums duplicates).
-      bool any_dup = false;
+      // positives) add theirs atomically into the slot, zeroed in phase 0 (coo.toarray() sums duplicates).  The
+      // pixel list behind the values (olist) lies past slot nnz - 1: no store of it meets a slot being summed.
 #pragma unroll
       for (int j = 0; j < RMAX; ++j) {
         const int i = tid + j * BLOCK;
         if (i < n0) {
           const int r = TWO ? rank2((int)Hits<FMT>::pix(hs(j))) : bm_rank(Hbm, pf, (int)Hits<FMT>::pix(hs(j)));
-          const bool d = Hits<FMT>::dup(hs(j));
-          vals[r] = d ? 0.0 : Hits<FMT>::val(hs(j));
-          any_dup |= d;
+          if (Hits<FMT>::dup(hs(j))) atomicAdd(&vals[r], Hits<FMT>::val(hs(j)));
+          else vals[r] = Hits<FMT>::val(hs(j));
           if (nnz <= OL_MAX && ((own >> j) & 1u)) olist[r] = Hits<FMT>::pix(hs(j));
-        }
-      }
-      if (any_dup) ctr[C_PDUP] = 1;
-      __syncthreads();
-      if (ctr[C_PDUP]) {
-#pragma unroll
-        for (int j = 0; j < RMAX; ++j) {
-          const int i = tid + j * BLOCK;
-          if (i < n0 && Hits<FMT>::dup(hs(j)))
-            atomicAdd(&vals[TWO ? rank2((int)Hits<FMT>::pix(hs(j))) : bm_rank(Hbm, pf, (int)Hits<FMT>::pix(hs(j)))],
-                      Hits<FMT>::val(hs(j)));
         }
       }
     }
@@ -768,57 +761,42 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         ld8_async_v(pd[j], hits.h);
       }
     }
-    if constexpr (ASYNC) {
-      // counted waits are per wave: wave 0 waits, lane 0 uses the ticket.  The test is on the laundered tid (an
-      // exec-masked branch, not a scalar one), the form scripts/check_async_regs.py recognises as wave-0 only
-      if ((tid >> 6) == 0) vm_wait1<1 + 2 * RC>(ticket);
+    // wave 0: the ticket and npos's descriptor (issued at the top of this iteration, before chunks 2 and 3 or their
+    // stand-ins): lane 0 resolves the ticket, the lanes store the descriptor for the end of the tail stream.  Counted
+    // waits are per wave; the test is on the laundered tid (an exec-masked branch, not a scalar one), the form
+    // scripts/check_async_regs.py recognises as wave-0 only
+    if ((tid >> 6) == 0) {
+      if constexpr (ASYNC) {
+        vm_wait1<2 * RC>(ticket);
+        vm_wait1<2 * RC>(dword);
+      }
+      if (tid == 0) ctr[C_NEXT] = (int)sched_resolve<SRC>(S, ticket);
+      if (npos >= 0 && lane < DESC_QWORDS) reinterpret_cast<uint64_t*>(DN)[lane] = dword;
     }
-    if (tid == 0) ctr[C_NEXT] = (int)sched_resolve<SRC>(S, ticket);
     __syncthreads();
     const int64_t n2pos = uni(ctr[C_NEXT]);
     STAMP(1);
 
-    // ---- phase 2: fused principal-image statistics, then level index per pixel -------------------
-    double sx = 0.0, sxx = 0.0, s0 = 0.0, npx_pos = 0.0, vmax = 0.0;
-    {
+    // ---- phase 2: fused principal-image statistics: each wave's sums into red, read after the tail stream's
+    // closing barrier (nothing before it needs them), so no barrier of its own
+    if (!skip) {
       double acc[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
-      if (!skip) {
-        for (int r = tid; r < nnz; r += BLOCK) {
-          const double v = vals[r];
-          acc[0] += v;
-          acc[1] += v * v;
-          if (v > 0.0) {
-            acc[2] += v;
-            acc[3] += 1.0;
-          }
-          acc[4] = v > acc[4] ? v : acc[4];
+      for (int r = tid; r < nnz; r += BLOCK) {
+        const double v = vals[r];
+        acc[0] += v;
+        acc[1] += v * v;
+        if (v > 0.0) {
+          acc[2] += v;
+          acc[3] += 1.0;
         }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = wave_sum_dpp(acc[q]);
-        acc[4] = wave_max_dpp(acc[4]);
-        if (lane == 0) {
-#pragma unroll
-          for (int q = 0; q < 5; ++q) red[q * NW + wid] = acc[q];
-        }
+        acc[4] = v > acc[4] ? v : acc[4];
       }
-      if ((tid >> 6) == 0) {  // wave 0 (exec-masked branch, see the ticket's wait)
-        if constexpr (ASYNC) vm_wait1<2 * RC>(dword);  // chunks 2 and 3 (or their stand-ins) were issued after it
-        if (npos >= 0 && lane < DESC_QWORDS) reinterpret_cast<uint64_t*>(DN)[lane] = dword;
-      }
-      __syncthreads();
-      if (!skip) {
-        double t[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
 #pragma unroll
-        for (int w = 0; w < NW; ++w) {
+      for (int q = 0; q < 4; ++q) acc[q] = wave_sum_dpp(acc[q]);
+      acc[4] = wave_max_dpp(acc[4]);
+      if (lane == 0) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) t[q] += red[q * NW + w];
-          t[4] = red[4 * NW + w] > t[4] ? red[4 * NW + w] : t[4];
-        }
-        sx = t[0];
-        sxx = t[1];
-        s0 = t[2];
-        npx_pos = t[3];
-        vmax = t[4];
+        for (int q = 0; q < 5; ++q) red[q * NW + wid] = acc[q];
       }
     }
 #ifndef SMG_ABL
@@ -826,10 +804,6 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
                    // 4 = tail chunk 0 only, 8 = no duplicate deferral, 16 = no principal lookups in the tail,
                    // 32 = no exact eL / Kruskal, 64 = no screen, 128 = no levels
 #endif
-    const bool chaos_ok = !skip && (sx > 0.0) && (npx_pos >= 4.0) && !(SMG_ABL & 1);
-    if (chaos_ok && nnz > OL_MAX && !(SMG_ABL & 128)) {  // else after the screen, if it finds candidates
-      for (int r = tid; r < nnz; r += BLOCK) Lv[r] = (uint8_t)level_fast(vals[r], vmax, P);
-    }
     STAMP(2);
 
     // ---- phase 5: tail windows, one stream of window-aligned 64-point groups -------------------------
@@ -1039,7 +1013,29 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       issue_chunk(DN, 0, pa);
       issue_chunk(DN, 1, pb);
     }
+    if (!skip) clear_table();  // for phase d (its space held the previous ion's chaos candidates)
     __syncthreads();
+    // the principal statistics (phase 2's per-wave sums, in wave order) and the level index per pixel
+    double sx = 0.0, sxx = 0.0, s0 = 0.0, npx_pos = 0.0, vmax = 0.0;
+    if (!skip) {
+      double t[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[q] += red[q * NW + w];
+        t[4] = red[4 * NW + w] > t[4] ? red[4 * NW + w] : t[4];
+      }
+      sx = t[0];
+      sxx = t[1];
+      s0 = t[2];
+      npx_pos = t[3];
+      vmax = t[4];
+    }
+    const bool chaos_ok = !skip && (sx > 0.0) && (npx_pos >= 4.0) && !(SMG_ABL & 1);
+    if (chaos_ok && nnz > OL_MAX && !(SMG_ABL & 128)) {  // else after the screen, if it finds candidates
+      for (int r = tid; r < nnz; r += BLOCK) Lv[r] = (uint8_t)level_fast(vals[r], vmax, P);
+      __syncthreads();  // the values are read here before the pixel list (olist) overwrites them in the chaos phase
+    }
     STAMP(9);
     // ---- deferred duplicate candidates: exact per-(pixel, window) sums, squared into the partials --------
     // Thread t owns list slot t (segment t / DSEG, entry t % DSEG); the entries are summed per key in an LDS
@@ -1057,13 +1053,6 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         skip = true;
       } else if (nd_tot > 0 && !(SMG_ABL & 512)) {
         static_assert(NW * DSEG == BLOCK, "one list slot per thread");
-        if (!SMG_TBL0) {
-          for (int i = tid; i < DTBL; i += BLOCK) {
-            tkey[i] = 0xFFFFFFFFu;
-            tval[i] = 0.0;
-          }
-          __syncthreads();
-        }
         if ((tid % DSEG) < dcnt[tid / DSEG] && !tbl_add<DTBL>(tkey, tval, dkey[tid], dval[tid])) ctr[C_ABORT] = 1;
         __syncthreads();
         if (ctr[C_ABORT]) {
@@ -1489,10 +1478,11 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       }
     }
     if (npos < 0) break;
+    if (began && wid != 0) clear_set_vals(tid - WAVE, BLOCK - WAVE);  // (the chaos phase is done with both)
     pos = npos;
     npos = n2pos;
     cur ^= 1;
-    __syncthreads();  // the next ion re-initialises the LDS structures
+    __syncthreads();  // the next ion starts on cleared LDS structures
     STAMP(7);
   }
   STAMP_FLUSH();
