@@ -17,10 +17,11 @@
 //     digit in LDS so that the stores come out as contiguous runs per digit;
 //   * 78 KB of LDS per workgroup (one 64 KB exchange buffer, which holds the wave histograms while ranking, the
 //     keys, then the values): two tiles per CU, so one tile's loads overlap the other's ranking and stores;
-//   * the first pass reads the keys in dataset order and sets the duplicate-candidate flag (smg_flag_duplicates)
-//     on the way: a bit per position marks the spectrum starts (from sp_off, one small kernel), so a point's
-//     spectrum neighbours are its dataset neighbours across no start (spectra must be m/z-sorted and no pixel
-//     shared: the host takes the separate flag pass otherwise); no pixel is read.
+//   * the duplicate-candidate flags (smg_flag_duplicates) are computed by the histogram pass, which reads the keys
+//     in dataset order anyway: a bit per position marks the spectrum starts (from sp_off, one small kernel), so a
+//     point's spectrum neighbours are its dataset neighbours across no start (spectra must be m/z-sorted and no
+//     pixel shared: the host takes the separate flag pass otherwise); no pixel is read.  The first sort pass sets
+//     bit 31 of each hit from one flag bit per position.
 // Traffic per pass: 12 B read + 12 B written per point plus 2-8 B of look-back status per 1 KB of tile.
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -88,9 +89,24 @@ __device__ __forceinline__ T block_excl_scan(T v, T* red) {
   return off + x - v;
 }
 
-// digit histograms of every pass in one read of the keys: per-workgroup LDS counts, then one global add per bin
+// The duplicate-candidate flag of the point at position i (the flag pass's rule, smg_prep.hip flag_tile_store):
+// its spectrum's previous or next point lies within one window width, compared in f64.  m: its m/z, mp / mn: the
+// m/z at positions i - 1 / i + 1, st0 / st1: spectrum starts at i / i + 1.
+__device__ __forceinline__ bool dup_flag(int64_t i, int64_t n, uint32_t k, uint32_t kp, uint32_t kn, bool st0, bool st1,
+                                         double slack) {
+  const double m = (double)__uint_as_float(k), mp = (double)__uint_as_float(kp), mn = (double)__uint_as_float(kn);
+  const bool fp = i > 0 && !st0 && m - mp <= slack * m;
+  const bool fn = i + 1 < n && !st1 && mn - m <= slack * mn;
+  return fp || fn;
+}
+
+// digit histograms of every pass in one read of the keys: per-workgroup LDS counts, then one global add per bin.
+// With flags != nullptr it also writes the duplicate-candidate flag of every point (one bit per position, dataset
+// order; spectrum starts in starts[]) for the first sort pass, which then only reads them.
 __global__ void __launch_bounds__(HST_T) sort_hist_kernel(const uint32_t* __restrict__ keys, int64_t n, int passes,
-                                                          int dbits, unsigned long long* __restrict__ hist) {
+                                                          int dbits, unsigned long long* __restrict__ hist,
+                                                          const uint32_t* __restrict__ starts,
+                                                          uint32_t* __restrict__ flags, double slack) {
   __shared__ uint32_t h[SRT_MAXP * SRT_BINS];
   for (int i = threadIdx.x; i < SRT_MAXP * SRT_BINS; i += HST_T) h[i] = 0;
   __syncthreads();
@@ -137,6 +153,35 @@ __global__ void __launch_bounds__(HST_T) sort_hist_kernel(const uint32_t* __rest
   const int64_t h0 = head < n ? head : n;
   const int64_t n4 = (n - h0) >> 2;
   const uint4* k4 = reinterpret_cast<const uint4*>(keys + h0);
+  auto start = [&](int64_t i) -> bool { return i < n && ((starts[i >> 5] >> (i & 31)) & 1u); };
+  // flags of one point (positions outside the whole-chunk range: the head, the tail); atomicOr into its word
+  auto flag1 = [&](int64_t i) {
+    const uint32_t k = keys[i], kp = i > 0 ? keys[i - 1] : 0u, kn = i + 1 < n ? keys[i + 1] : 0u;
+    if (dup_flag(i, n, k, kp, kn, start(i), start(i + 1), slack)) atomicOr(&flags[i >> 5], 1u << (i & 31));
+  };
+  // flags of a chunk's quad: the neighbours come from the adjacent lanes, the chunk's two outer ones from memory;
+  // with the chunk 32-point aligned (h0 == 0), eight lanes' nibbles make one flag word, stored by the first of them
+  auto flag4 = [&](int64_t ch, const uint4 q) {  // wave-uniform
+    const int64_t i = h0 + (ch * 64 + lane) * 4;
+    uint32_t kp = __shfl_up(q.w, 1, 64), kn = __shfl_down(q.x, 1, 64);
+    if (lane == 0) kp = i > 0 ? keys[i - 1] : 0u;
+    if (lane == 63) kn = i + 4 < n ? keys[i + 4] : 0u;
+    const uint32_t sw0 = starts[i >> 5], sw1 = starts[(i + 4) >> 5];
+    auto st = [&](int j) { const int64_t p = i + j; return ((((p >> 5) == (i >> 5)) ? sw0 : sw1) >> (p & 31)) & 1u; };
+    uint32_t nib = (uint32_t)dup_flag(i, n, q.x, kp, q.y, st(0), st(1), slack) |
+                   ((uint32_t)dup_flag(i + 1, n, q.y, q.x, q.z, st(1), st(2), slack) << 1) |
+                   ((uint32_t)dup_flag(i + 2, n, q.z, q.y, q.w, st(2), st(3), slack) << 2) |
+                   ((uint32_t)dup_flag(i + 3, n, q.w, q.z, kn, st(3), i + 4 < n ? st(4) : 0u, slack) << 3);
+    if (h0 == 0) {
+      uint32_t word = nib;
+#pragma unroll
+      for (int j = 1; j < 8; ++j) word |= __shfl_down(nib, j, 8) << (4 * j);
+      if ((lane & 7) == 0) flags[i >> 5] = word;
+    } else if (nib) {
+      atomicOr(&flags[i >> 5], nib << (i & 31));
+      if ((i & 31) > 28) atomicOr(&flags[(i >> 5) + 1], nib >> (32 - (i & 31)));
+    }
+  };
   // whole waves over chunks of 64 quads (wave-uniform loop bounds), four chunks' loads in flight per round
   const int64_t nw = stride >> 6, nchunk = n4 >> 6;
   int64_t c = ((int64_t)blockIdx.x * HST_T + threadIdx.x) >> 6;
@@ -145,12 +190,25 @@ __global__ void __launch_bounds__(HST_T) sort_hist_kernel(const uint32_t* __rest
 #pragma unroll
     for (int r = 0; r < 4; ++r) q[r] = k4[(c + r * nw) * 64 + lane];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) add4(q[r]);
+    for (int r = 0; r < 4; ++r) {
+      add4(q[r]);
+      if (flags) flag4(c + r * nw, q[r]);
+    }
   }
-  for (; c < nchunk; c += nw) add4(k4[c * 64 + lane]);
+  for (; c < nchunk; c += nw) {
+    const uint4 q = k4[c * 64 + lane];
+    add4(q);
+    if (flags) flag4(c, q);
+  }
   const int64_t t = (int64_t)blockIdx.x * HST_T + threadIdx.x;
-  if (t < h0) add(keys[t]);
-  for (int64_t i = h0 + nchunk * 256 + t; i < n; i += stride) add(keys[i]);
+  if (t < h0) {
+    add(keys[t]);
+    if (flags) flag1(t);
+  }
+  for (int64_t i = h0 + nchunk * 256 + t; i < n; i += stride) {
+    add(keys[i]);
+    if (flags) flag1(i);
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < passes * SRT_BINS; i += HST_T)
     if (h[i]) atomicAdd(&hist[i], (unsigned long long)h[i]);
@@ -185,8 +243,8 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
                                                                     uint64_t* __restrict__ vout, int64_t n, int shift,
                                                                     int dbits, const int64_t* __restrict__ binbase,
                                                                     S* __restrict__ status,
-                                                                    unsigned* __restrict__ ticket, double slack,
-                                                                    const uint32_t* __restrict__ starts) {
+                                                                    unsigned* __restrict__ ticket,
+                                                                    const uint32_t* __restrict__ flagbits) {
   constexpr bool SPLIT = SRT_TILE * 8 > 65536;
   constexpr int XWORDS = 65536 / 8;
   // exchange buffer: the wave histograms (u16 [SRT_WAVES][SRT_BINS]) while ranking, then the tile's keys in digit
@@ -228,40 +286,13 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
 
   uint32_t fmask = 0;  // FLAG: bit u = the duplicate-candidate flag of the thread's point u
   if constexpr (FLAG) {
+    // the flags were computed by the histogram pass (one bit per dataset position, in flagbits)
     static_assert(SRT_IPT <= 32, "one flag bit per point in a 32-bit mask");
-    static_assert(SRT_TILE * 4 + (SRT_TILE / 32 + 1) * 4 <= 65536, "keys and spectrum-start bits share the buffer");
-    // the tile's keys in dataset order and its spectrum-start bits for positions [0, SRT_TILE] (tiles start on
-    // a word boundary); the points just outside the tile from memory
-    uint32_t* sb = xk + SRT_TILE;
-    const int64_t ia = base - 1, ib = base + SRT_TILE;
-    uint32_t ka = 0, kb = 0;
-    if (ia >= 0) ka = kin[ia];
-    if (ib < n) kb = kin[ib];
-    const int64_t nwords = (n + 31) >> 5;
-    for (int i = tid; i <= SRT_TILE / 32; i += SRT_T) {
-      const int64_t wi = (base >> 5) + i;
-      sb[i] = wi < nwords ? starts[wi] : 0u;
-    }
 #pragma unroll
-    for (int u = 0; u < SRT_IPT; ++u) xk[w * (64 * SRT_IPT) + u * 64 + lane] = k[u];
-    __syncthreads();
-    auto start = [&](int p) { return (sb[p >> 5] >> (p & 31)) & 1u; };
-    // in a rolled loop reading everything from LDS (unrolled, the compiler overlaps all the points and spills)
-#pragma unroll 2
     for (int u = 0; u < SRT_IPT; ++u) {
-      const int p = w * (64 * SRT_IPT) + u * 64 + lane;
-      const int64_t i = base + p;
-      const uint32_t kp = p > 0 ? xk[p - 1] : ka, kn = p + 1 < SRT_TILE ? xk[p + 1] : kb;
-      // the flag pass's test (smg_prep.hip flag_tile_store): the spectrum's previous / next point within one
-      // window width, in f64
-      const double m = (double)__uint_as_float(xk[p]), m2 = (double)__uint_as_float(kn);
-      const bool fp = i > 0 && !start(p) && m - (double)__uint_as_float(kp) <= slack * m;
-      const bool fn = i + 1 < n && !start(p + 1) && m2 - m <= slack * m2;
-      fmask |= (uint32_t)((fp || fn) && i < n) << u;
+      const int64_t i = wbase + u * 64 + lane;
+      if (i < n) fmask |= ((flagbits[i >> 5] >> (i & 31)) & 1u) << u;
     }
-    __syncthreads();
-    reinterpret_cast<uint4*>(xbuf)[tid] = make_uint4(0u, 0u, 0u, 0u);  // the wave histograms again
-    __syncthreads();
   }
 
   // ranking: each wave counts its rows in order (row u, lane) -- the stable order of its points -- into its own
@@ -423,7 +454,7 @@ struct SortPlan {
   int passes, dbits;
   int64_t ntiles;
   bool wide;  // 64-bit look-back words
-  size_t off_hist, off_base, off_status, status_bytes, off_s0, start_bytes, off_tk, off_tv, total;
+  size_t off_hist, off_base, off_status, status_bytes, off_s0, start_bytes, off_fl, off_tk, off_tv, total;
 };
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -445,7 +476,8 @@ static SortPlan sort_plan(int64_t n, int key_bits) {
   p.status_bytes = (size_t)(p.passes < 2 ? p.passes : 2) * (size_t)p.ntiles * SRT_BINS * sw;
   p.off_s0 = align_up(p.off_status + p.status_bytes, 256);  // FLAG pass: spectrum-start bits
   p.start_bytes = (size_t)((n + 31) / 32 + 2) * 4;
-  p.off_tk = align_up(p.off_s0 + p.start_bytes, 256);
+  p.off_fl = align_up(p.off_s0 + p.start_bytes, 256);  // FLAG pass: the flag bits (the same size)
+  p.off_tk = align_up(p.off_fl + p.start_bytes, 256);
   p.off_tv = align_up(p.off_tk + (size_t)n * 4, 256);
   p.total = p.off_tv + (size_t)n * 8;
   return p;
@@ -495,9 +527,9 @@ static int roc_workspace(int64_t n, size_t* bytes) {
 
 template <typename S>
 static int run_passes(const SortPlan& P, const uint32_t* mz, const uint64_t* hits, int64_t n, uint32_t* ko,
-                      uint64_t* vo, unsigned char* ws, bool flag, double slack, hipStream_t st) {
+                      uint64_t* vo, unsigned char* ws, bool flag, hipStream_t st) {
   const size_t region = (size_t)P.ntiles * SRT_BINS;  // look-back words per pass
-  const uint32_t* starts = reinterpret_cast<const uint32_t*>(ws + P.off_s0);
+  const uint32_t* flagbits = reinterpret_cast<const uint32_t*>(ws + P.off_fl);
   unsigned* tickets = reinterpret_cast<unsigned*>(ws);
   const int64_t* binbase = reinterpret_cast<const int64_t*>(ws + P.off_base);
   S* status = reinterpret_cast<S*>(ws + P.off_status);
@@ -514,10 +546,10 @@ static int run_passes(const SortPlan& P, const uint32_t* mz, const uint64_t* hit
     if (p >= 2) SMG_HIP(hipMemsetAsync(sp, 0, region * sizeof(S), st));  // pass p - 2's words
     if (flag && p == 0)
       hipLaunchKernelGGL((sort_pass_kernel<S, true>), dim3((unsigned)P.ntiles), dim3(SRT_T), 0, st, ki, vi, kdst,
-                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, slack, starts);
+                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, flagbits);
     else
       hipLaunchKernelGGL((sort_pass_kernel<S, false>), dim3((unsigned)P.ntiles), dim3(SRT_T), 0, st, ki, vi, kdst,
-                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, slack, nullptr);
+                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, nullptr);
     SMG_LAUNCH_CHECK();
     ki = kdst;
     vi = vdst;
@@ -541,17 +573,8 @@ static int native_sort(const float* mz, const uint64_t* hits, int64_t n, int key
   // tickets, histograms and the first two passes' look-back words start at zero
   SMG_HIP(hipMemsetAsync(ws, 0, P.off_status + P.status_bytes, st));
   const uint32_t* keys = reinterpret_cast<const uint32_t*>(mz);
-  int64_t hb = (n + (int64_t)HST_T * 16 - 1) / ((int64_t)HST_T * 16);
-  if (hb > 2048) hb = 2048;
-  hipLaunchKernelGGL(sort_hist_kernel, dim3((unsigned)hb), dim3(HST_T), 0, st, keys, n, P.passes, P.dbits,
-                     reinterpret_cast<unsigned long long*>(ws + P.off_hist));
-  SMG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(sort_scan_kernel, dim3((unsigned)P.passes), dim3(SRT_BINS), 0, st,
-                     reinterpret_cast<const unsigned long long*>(ws + P.off_hist),
-                     reinterpret_cast<int64_t*>(ws + P.off_base));
-  SMG_LAUNCH_CHECK();
-  if (flag) {
-    SMG_HIP(hipMemsetAsync(ws + P.off_s0, 0, P.start_bytes, st));
+  if (flag) {  // spectrum starts first: the histogram pass computes the flags from them
+    SMG_HIP(hipMemsetAsync(ws + P.off_s0, 0, P.off_fl + P.start_bytes - P.off_s0, st));  // start and flag bits
     int64_t g = (n_spectra + 255) / 256;
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(sort_mark_starts_kernel, dim3((unsigned)g), dim3(256), 0, st, sp_off, n_spectra, n,
@@ -559,9 +582,20 @@ static int native_sort(const float* mz, const uint64_t* hits, int64_t n, int key
     SMG_LAUNCH_CHECK();
   }
   const double slack = 2.0 * ppm * 1e-6 / (1.0 - ppm * 1e-6) * (1.0 + 1e-9);
+  int64_t hb = (n + (int64_t)HST_T * 16 - 1) / ((int64_t)HST_T * 16);
+  if (hb > 2048) hb = 2048;
+  hipLaunchKernelGGL(sort_hist_kernel, dim3((unsigned)hb), dim3(HST_T), 0, st, keys, n, P.passes, P.dbits,
+                     reinterpret_cast<unsigned long long*>(ws + P.off_hist),
+                     flag ? reinterpret_cast<const uint32_t*>(ws + P.off_s0) : nullptr,
+                     flag ? reinterpret_cast<uint32_t*>(ws + P.off_fl) : nullptr, slack);
+  SMG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sort_scan_kernel, dim3((unsigned)P.passes), dim3(SRT_BINS), 0, st,
+                     reinterpret_cast<const unsigned long long*>(ws + P.off_hist),
+                     reinterpret_cast<int64_t*>(ws + P.off_base));
+  SMG_LAUNCH_CHECK();
   uint32_t* ko = reinterpret_cast<uint32_t*>(mz_sorted);
-  return P.wide ? run_passes<unsigned long long>(P, keys, hits, n, ko, hits_sorted, ws, flag, slack, st)
-                : run_passes<uint32_t>(P, keys, hits, n, ko, hits_sorted, ws, flag, slack, st);
+  return P.wide ? run_passes<unsigned long long>(P, keys, hits, n, ko, hits_sorted, ws, flag, st)
+                : run_passes<uint32_t>(P, keys, hits, n, ko, hits_sorted, ws, flag, st);
 }
 
 }  // namespace smg
