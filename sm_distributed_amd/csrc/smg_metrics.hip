@@ -1255,7 +1255,10 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       // level index L: precomputed for every principal pixel when there are many candidates, else computed
       // on demand from the values (intact: olist sits behind them, candidates elsewhere) for the few principal
       // pixels around the candidates
-      const bool lazyL = (nnz <= OL_MAX) && (ncand * 16 < nnz);
+      // few candidates (<= one wave: most noise images): wave 0 alone computes their eL and runs Kruskal, with no
+      // barrier (the eL loop below gives them to wave 0's lanes); the other waves go on to the ion's end
+      const bool few = ncand <= WAVE;
+      const bool lazyL = (nnz <= OL_MAX) && (few || ncand * 16 < nnz);
       if (!skip && ncand > 0 && nnz <= OL_MAX && !lazyL) {
         for (int r = tid; r < nnz; r += BLOCK) Lv[r] = (uint8_t)level_fast(vals[r], vmax, P);
         __syncthreads();
@@ -1329,14 +1332,22 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
           eL8[c] = (uint8_t)mn;
           emax_local = max(emax_local, mn);
         }
-        if (emax_local > 0) atomicMax(&ctr[C_EMAX], emax_local);
-        __syncthreads();
+        int emax_all;
+        if (few) {  // wave 0's lanes hold every candidate: the maximum without LDS or barrier
+          int m = emax_local;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, WAVE));
+          emax_all = m;
+        } else {
+          if (emax_local > 0) atomicMax(&ctr[C_EMAX], emax_local);
+          __syncthreads();
+          emax_all = ctr[C_EMAX];
+        }
         STAMP(5);
 
         // ---- phase 4b: Kruskal over eL (levels descending) with an LDS union-find -------------------
         double sum_c = 0.0;
-        const int emax_all = ctr[C_EMAX];
-        if (emax_all > 0 && ncand <= WAVE) {
+        if (emax_all > 0 && few) {
           // few candidates (most noise images): wave 0 alone, one candidate per lane; forward neighbours
           // found by comparing pixel indices across lanes, union-find over candidate indices in LDS; no
           // bitmap rebuild and no barrier.  Only wave 0 needs the result (finalize).
