@@ -24,8 +24,9 @@ m = E.ion_metrics(peaks, dions, lo, hi, nlevels=30)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 L.smg_debug_stamps(buf, 16)
-names = ["p0 load+zero", "p1 bitmap/prefix/vals", "p2-3 stats+levels", "d duplicate table", "p4a screen",
-         "p4a exact eL", "p4b kruskal", "record+loop", "p5 tail windows", "issue next+barrier"]
+names = ["p0 load+zero", "p1 ticket wait+barrier", "p2-3 stats+levels", "d duplicate table", "p4a screen",
+         "p4a exact eL", "p4b kruskal", "record+loop", "p5 tail windows", "tail barrier+stats", "issue next+clear",
+         "p1 bitmap/prefix/vals"]
 n = dions.n_ions
 tot = sum(buf[i] for i in range(len(names)))
 print(os.path.basename(_lib.LIB_PATH))

@@ -761,6 +761,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         ld8_async_v(pd[j], hits.h);
       }
     }
+    STAMP(11);
     // wave 0: the ticket and npos's descriptor (issued at the top of this iteration, before chunks 2 and 3 or their
     // stand-ins): lane 0 resolves the ticket, the lanes store the descriptor for the end of the tail stream.  Counted
     // waits are per wave; the test is on the laundered tid (an exec-masked branch, not a scalar one), the form
@@ -1014,6 +1015,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       issue_chunk(DN, 1, pb);
     }
     if (!skip) clear_table();  // for phase d (its space held the previous ion's chaos candidates)
+    STAMP(10);
     __syncthreads();
     // the principal statistics (phase 2's per-wave sums, in wave order) and the level index per pixel
     double sx = 0.0, sxx = 0.0, s0 = 0.0, npx_pos = 0.0, vmax = 0.0;
@@ -1255,10 +1257,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       // level index L: precomputed for every principal pixel when there are many candidates, else computed
       // on demand from the values (intact: olist sits behind them, candidates elsewhere) for the few principal
       // pixels around the candidates
-      // few candidates (<= one wave: most noise images): wave 0 alone computes their eL and runs Kruskal, with no
-      // barrier (the eL loop below gives them to wave 0's lanes); the other waves go on to the ion's end
-      const bool few = ncand <= WAVE;
-      const bool lazyL = (nnz <= OL_MAX) && (few || ncand * 16 < nnz);
+      const bool lazyL = (nnz <= OL_MAX) && (ncand * 16 < nnz);
       if (!skip && ncand > 0 && nnz <= OL_MAX && !lazyL) {
         for (int r = tid; r < nnz; r += BLOCK) Lv[r] = (uint8_t)level_fast(vals[r], vmax, P);
         __syncthreads();
@@ -1332,22 +1331,14 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
           eL8[c] = (uint8_t)mn;
           emax_local = max(emax_local, mn);
         }
-        int emax_all;
-        if (few) {  // wave 0's lanes hold every candidate: the maximum without LDS or barrier
-          int m = emax_local;
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, WAVE));
-          emax_all = m;
-        } else {
-          if (emax_local > 0) atomicMax(&ctr[C_EMAX], emax_local);
-          __syncthreads();
-          emax_all = ctr[C_EMAX];
-        }
+        if (emax_local > 0) atomicMax(&ctr[C_EMAX], emax_local);
+        __syncthreads();
         STAMP(5);
 
         // ---- phase 4b: Kruskal over eL (levels descending) with an LDS union-find -------------------
         double sum_c = 0.0;
-        if (emax_all > 0 && few) {
+        const int emax_all = ctr[C_EMAX];
+        if (emax_all > 0 && ncand <= WAVE) {
           // few candidates (most noise images): wave 0 alone, one candidate per lane; forward neighbours
           // found by comparing pixel indices across lanes, union-find over candidate indices in LDS; no
           // bitmap rebuild and no barrier.  Only wave 0 needs the result (finalize).
