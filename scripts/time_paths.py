@@ -1,5 +1,5 @@
 """Diagnostic: ion-stage time of the normal passes, the forced dense path and the hot-spot clip
-(do_preprocessing, dense path) on one synthetic workload; max |difference| normal vs forced dense.
+(do_preprocessing) on one synthetic workload; max |difference| normal vs forced dense.
 
 usage: time_paths.py [nrows ncols peaks n_sf]   (default config 3: 500 500 2000 20000)
 """
@@ -50,5 +50,8 @@ finally:
 err = max(float(np.abs(g_n[c] - g_p[c]).max()) for c in cols)
 print(f"forced pixel-indexed dense {t_p:.2f} ms, max|d| vs normal {err:.1e}, wide ions normal "
       f"{int(((g_n['flags'] & 0x20) != 0).sum())}", flush=True)
-t_c, g_c = timed(reps=2, do_preprocessing=True, q=99.0)
-print(f"do_preprocessing (q99 clip, dense path) {t_c:.2f} ms", flush=True)
+t_c, g_c = timed(reps=3, do_preprocessing=True, q=99.0)
+fc = g_c["flags"]
+print(f"do_preprocessing (q99 clip) {t_c:.2f} ms = {t_c / t_n:.2f}x normal (LDS passes "
+      f"{int((((fc & 2) == 0) & ((fc & 1) != 0)).sum())}, wide pass {int(((fc & 0x20) != 0).sum())}, "
+      f"pixel-indexed {int((((fc & 2) != 0) & ((fc & 0x20) == 0) & ((fc & 1) != 0)).sum())} ions)", flush=True)

@@ -246,6 +246,127 @@ struct Lay2 : Lay<NW, CAPC> {
 constexpr int NPX_TWO_MAX = 1 << 23;  // two-level pass: top-level prefix over <= 2^23/4096 + 2 words
 constexpr int TOPCAP = NPX_TWO_MAX / 4096 + 2;
 
+// The digit of an MSD radix-select pass: over the 256 bin counts (16-B aligned), the bin d whose cumulative count
+// first exceeds k (four bins per lane, one DPP scan, one ballot), computed by every wave for itself (no broadcast):
+// returns d, sets k to k minus the count below d and cnt to the count of d (wave-uniform).
+__device__ __forceinline__ int hist_find(const uint32_t* hist, int& k, int& cnt) {
+  const int lane = threadIdx.x & 63;
+  const uint4 c = reinterpret_cast<const uint4*>(hist)[lane];
+  const int s4 = (int)(c.x + c.y + c.z + c.w);
+  const int incl = wave_incl_scan_dpp(s4);
+  const uint64_t over = __ballot(incl > k);
+  const int L = over ? __ffsll((unsigned long long)over) - 1 : WAVE - 1;
+  const int b0 = incl - s4, b1 = b0 + (int)c.x, b2 = b1 + (int)c.y, b3 = b2 + (int)c.z;
+  const int j = b1 > k ? 0 : b2 > k ? 1 : b3 > k ? 2 : 3;  // (no indexed array: it would live in scratch)
+  const int base = j == 0 ? b0 : j == 1 ? b1 : j == 2 ? b2 : b3;
+  const int cj = (int)(j == 0 ? c.x : j == 1 ? c.y : j == 2 ? c.z : c.w);
+  const int d = __shfl(4 * lane + j, L, WAVE);
+  const int kb = __shfl(k - base, L, WAVE);
+  cnt = __shfl(cj, L, WAVE);
+  k = kb;
+  return d;
+}
+
+// The i0-th smallest (0-based) of a set of positive doubles and, with pair, the (i0 + 1)-th (i0 + 1 < n): an MSD
+// radix select over the f64 bit patterns (positive values: ordered like the values), one 8-bit LDS histogram per
+// byte (two buffers in turn: a pass clears the next one while every wave reads the current one, so a pass takes two
+// barriers), that stops as soon as the selected byte prefix holds a single element (it is then fetched whole),
+// usually after three or four of the eight bytes.  The next order statistic is the same value when more elements
+// than needed equal it, else the smallest value above it (one pass for both).  visit(f) calls f(bits) for each
+// element this thread owns (any partition of the set over the NT threads of the block; called once per pass, so it
+// must enumerate the same set every time).  hist: 2 x 256 u32 (16-B aligned), sh: 1 int, dsh: 1 u64 of LDS.
+// lo, hi: the bit patterns of the set's smallest and largest elements when known (else 0, ~0): the passes start at
+// the first byte where they differ (the bytes above it are common to every element), and none runs when they agree.
+template <int NT, class Visit>
+__device__ void select_pair(Visit&& visit, int i0, bool pair, uint32_t* hist, int* sh, unsigned long long* dsh,
+                            double& a, double& b, uint64_t lo = 0ull, uint64_t hi = ~0ull) {
+  const int tid = threadIdx.x;
+  const uint64_t diff = lo ^ hi;
+  if (diff == 0ull) {  // every element is the same value
+    a = b = __longlong_as_double((long long)lo);
+    return;
+  }
+  const int top = (63 - __clzll((long long)diff)) & ~7;  // shift of the highest differing byte
+  uint64_t mask = top == 56 ? 0ull : ~((1ull << (top + 8)) - 1ull);
+  uint64_t prefix = lo & mask;
+  int k = i0;
+  for (int i = tid; i < 256; i += NT) hist[i] = 0u;
+  if (tid == 0) *dsh = ~0ull;
+  __syncthreads();
+  int cur = 0;
+  for (int shift = top; shift >= 0; shift -= 8) {
+    uint32_t* h = hist + 256 * cur;
+    visit([&](uint64_t bits) {
+      if ((bits & mask) == prefix) atomicAdd(&h[(bits >> shift) & 255u], 1u);
+    });
+    __syncthreads();
+    int cnt;
+    const int d = hist_find(h, k, cnt);
+    for (int i = tid; i < 256; i += NT) hist[256 * (cur ^ 1) + i] = 0u;  // the next pass's buffer
+    cur ^= 1;
+    prefix |= (uint64_t)d << shift;
+    mask |= 255ull << shift;
+    if (cnt == 1 && shift > 0) {  // a single element carries the prefix: it is the one
+      visit([&](uint64_t bits) {
+        if ((bits & mask) == prefix) *dsh = bits;
+      });
+      __syncthreads();
+      prefix = *dsh;
+      break;
+    }
+    __syncthreads();  // the next buffer is clear before the next pass's adds
+  }
+  a = __longlong_as_double((long long)prefix);
+  b = a;
+  if (!pair) {
+    __syncthreads();  // (dsh is read above before any later use of the scratch)
+    return;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    sh[0] = 0;
+    *dsh = ~0ull;
+  }
+  __syncthreads();
+  int le = 0;
+  uint64_t above = ~0ull;
+  visit([&](uint64_t bits) {
+    if (bits <= prefix) ++le;
+    else above = bits < above ? bits : above;
+  });
+  if (le) atomicAdd(&sh[0], le);
+  if (above != ~0ull) atomicMin(dsh, (unsigned long long)above);
+  __syncthreads();
+  if (sh[0] < i0 + 2) b = __longlong_as_double((long long)*dsh);  // fewer than i0 + 2 elements <= a
+  __syncthreads();
+}
+
+// np.percentile(positive values, q) ('linear' method: numpy's _compute_virtual_index with alpha = beta = 1,
+// _get_indexes, _get_gamma, _lerp) of the n > 0 positive values visit enumerates (select_pair's contract)
+template <int NT, class Visit>
+__device__ double percentile_of(Visit&& visit, int n, double q, uint32_t* hist, int* sh, unsigned long long* dsh,
+                                uint64_t lo = 0ull, uint64_t hi = ~0ull) {
+  const double qq = q / 100.0;
+  const double vi = (double)n * qq + (1.0 + qq * (1.0 - 1.0 - 1.0)) - 1.0;
+  int i0, i1;
+  double gamma;
+  if (vi >= (double)(n - 1)) {
+    i0 = i1 = n - 1;
+    gamma = 0.0;
+  } else if (vi < 0.0) {
+    i0 = i1 = 0;
+    gamma = 0.0;
+  } else {
+    i0 = (int)floor(vi);
+    i1 = i0 + 1;
+    gamma = vi - floor(vi);
+  }
+  double a, b;
+  select_pair<NT>(visit, i0, i1 != i0, hist, sh, dsh, a, b, lo, hi);
+  const double d = b - a;
+  return gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
+}
+
 // open-addressing f64 accumulators keyed by u32 (EMPTY = 0xFFFFFFFF); returns false when full
 template <int NSLOT>
 __device__ __forceinline__ bool tbl_add(uint32_t* keys, double* vals, uint32_t key, double v) {
@@ -462,7 +583,7 @@ __global__ void ion_desc8_kernel(Hits<FMT> hits, const int64_t* __restrict__ lo,
 // Ions that do not fit (K > MAXK, principal window > CAPC, list/table overflows) go to `rej_list`: positions
 // (SRC_RANGES pass, read by the big-ion pass) or ion indices (SRC_LIST pass, read by the dense kernel).
 // ---------------------------------------------------------------------------------------------
-template <int FMT, int LB, int LRMAX, int LRC, int WPE, int SRC, bool TWO>
+template <int FMT, int LB, int LRMAX, int LRC, int WPE, int SRC, bool TWO, bool CLIP = false>
 __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     Hits<FMT> hits, IonDesc* __restrict__ desc, Sched S, Params P, double* __restrict__ oc,
     double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags,
@@ -500,6 +621,16 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   uint32_t* epix_r = reinterpret_cast<uint32_t*>(vals);                 // E pixels, rank order
   uint8_t* eLr = Lv;                                                    // rank order
   uint32_t* par = reinterpret_cast<uint32_t*>(vals) + CAPC;             // rank order
+  // CLIP (the hot-spot clip): the radix select's histogram and scalars, each window's threshold, positive count and
+  // smallest / largest value bits, in the level region (free until the levels, which come after the tail)
+  static_assert(CAPC >= 2048 + 16 + 8 + MAXK * 28, "clip scratch fits the level region");
+  uint32_t* c_hist = reinterpret_cast<uint32_t*>(Lv);  // 2 x 256 bins
+  int* c_sh = reinterpret_cast<int*>(Lv + 2048);
+  unsigned long long* c_dsh = reinterpret_cast<unsigned long long*>(Lv + 2064);
+  double* c_thr = reinterpret_cast<double*>(Lv + 2072);
+  unsigned long long* c_lo = reinterpret_cast<unsigned long long*>(Lv + 2072 + MAXK * 8);
+  unsigned long long* c_hi = reinterpret_cast<unsigned long long*>(Lv + 2072 + MAXK * 16);
+  int* c_n = reinterpret_cast<int*>(Lv + 2072 + MAXK * 24);
 
   // two-level pixel set (TWO): compact words W = Hbm as u64, their rank prefix B, top-level bitmap T
   const uint64_t* W64 = reinterpret_cast<const uint64_t*>(Hbm);
@@ -571,7 +702,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   auto hs = [&](int j) -> Reg& { return j < RC ? pc[j] : (j < 2 * RC ? pd[j - RC] : pe[j - 2 * RC]); };
   // Asynchronous (inline-asm, counted-wait) loads in the main pass only; the big-ion pass (~1% of the ions at
   // config 3) uses compiler-tracked loads: its 8-deep principal slots made the compiler copy in-flight registers
-  constexpr bool ASYNC = (FMT == SMG_HITS_PACKED_F32) && LB <= 512;
+  constexpr bool ASYNC = (FMT == SMG_HITS_PACKED_F32) && LB <= 512 && !CLIP;
   // principal window (<= CAPC points, RMAX per thread).  Async form: every slot issues exactly one load
   // (clamped to the window's last point, or to hit 0 for an empty window) so that the counted waits hold.
   auto issue_principal = [&](const IonDesc* D) {
@@ -749,7 +880,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         }
       }
     }
-    if (!skip) {  // the principal registers are consumed: tail chunks 2 and 3 go in flight
+    if (!skip && !CLIP) {  // the principal registers are consumed: tail chunks 2 and 3 go in flight
       issue_chunk(D, 2, pc);
       issue_chunk(D, 3, pd);
     } else if constexpr (ASYNC) {
@@ -777,6 +908,46 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     __syncthreads();
     const int64_t n2pos = uni(ctr[C_NEXT]);
     STAMP(1);
+    if constexpr (CLIP) {
+      // the hot-spot clip of the principal image: its q-th percentile over the positive values, every value above
+      // it lowered to it (each thread its own slots, as phase 2 reads them; the tail's lookups after a barrier)
+      if (!skip) {
+        int cnt = 0;
+        uint64_t plo = ~0ull, phi = 0ull;
+        for (int r = tid; r < nnz; r += BLOCK) {
+          const double v = vals[r];
+          if (v > 0.0) {
+            const uint64_t b = (uint64_t)__double_as_longlong(v);
+            ++cnt;
+            plo = b < plo ? b : plo;
+            phi = b > phi ? b : phi;
+          }
+        }
+        if (tid == 0) {
+          c_n[0] = 0;
+          c_lo[0] = ~0ull;
+          c_hi[0] = 0ull;
+        }
+        __syncthreads();
+        if (cnt) {
+          atomicAdd(&c_n[0], cnt);
+          atomicMin(&c_lo[0], (unsigned long long)plo);
+          atomicMax(&c_hi[0], (unsigned long long)phi);
+        }
+        __syncthreads();
+        const int n0p = c_n[0];
+        if (n0p > 0) {
+          const double thr = percentile_of<BLOCK>(
+              [&](auto&& f) {
+                for (int r = tid; r < nnz; r += BLOCK)
+                  if (vals[r] > 0.0) f((uint64_t)__double_as_longlong(vals[r]));
+              },
+              n0p, P.q, c_hist, c_sh, c_dsh, c_lo[0], c_hi[0]);
+          for (int r = tid; r < nnz; r += BLOCK)
+            if (vals[r] > thr) vals[r] = thr;
+        }
+      }
+    }
 
     // ---- phase 2: fused principal-image statistics: each wave's sums into red, read after the tail stream's
     // closing barrier (nothing before it needs them), so no barrier of its own
@@ -808,7 +979,176 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     STAMP(2);
 
     // ---- phase 5: tail windows, one stream of window-aligned 64-point groups -------------------------
-    if (!skip && !(SMG_ABL & 2)) {
+    if constexpr (CLIP) {
+      // The hot-spot clip: each tail image is clipped at the q-th percentile of its positive pixels before its
+      // sums, so Σy, Σy², Σxy, Σy[x>0] all come from the clipped pixel values (not from the prefix sums).  A
+      // window's pixel values: its unflagged points' values (the only point of their pixel in the window,
+      // smg_flag_duplicates) and the per-pixel sums of its flagged points (the duplicate table, keyed (pixel,
+      // window)).  1. the flagged points into the table, positive unflagged points counted per window; 2. each
+      // window's threshold by a radix select over both (its groups re-read once per pass); 3. the clipped
+      // unflagged points into this wave's partials; 4. each flagged pixel's clipped sum (the same wide-pass scheme,
+      // wide_clip_tail).  Groups are window-aligned: a group's window is uniform.
+      if (!skip) {
+        const int ng = uni(D->ngroups);
+        int gsv[MAXK];
+#pragma unroll
+        for (int kk = 0; kk < MAXK; ++kk) gsv[kk] = D->gs[kk];
+        auto win_of = [&](int G) {
+          int k = 1;
+#pragma unroll
+          for (int kk = 2; kk < MAXK; ++kk) k += (G >= gsv[kk]) ? 1 : 0;
+          return k;
+        };
+        auto xval = [&](uint32_t p) -> double {  // the (clipped) principal value at pixel p, 0 outside the image
+          if constexpr (TWO) {
+            const int r = rank2((int)p);
+            return r >= 0 ? vals[r] : 0.0;
+          } else {
+            return bm_test(Hbm, (int)p) ? vals[bm_rank(Hbm, pf, (int)p)] : 0.0;
+          }
+        };
+        auto bits_of = [](double v) { return (uint64_t)__double_as_longlong(v); };
+        constexpr int GU = 4;  // groups per wave with loads in flight together
+        // groups [g0, g1) in rounds of GU per wave: body(k, valid, hit) per group, uniform (k: the group's window)
+        auto groups = [&](int g0, int g1, auto&& body) {
+          for (int G0 = g0; G0 < g1; G0 += GU * NW) {
+            Reg h[GU];
+            int kg[GU];
+            bool vg[GU];
+#pragma unroll
+            for (int u = 0; u < GU; ++u) {
+              const int G = G0 + u * NW + wid;
+              kg[u] = win_of(G);
+              const int i = G * 64 + lane;
+              vg[u] = G < g1 && i < D->end[kg[u]];
+              h[u] = vg[u] ? hits.load(D->base[kg[u]] + i) : Hits<FMT>::zero();
+            }
+#pragma unroll
+            for (int u = 0; u < GU; ++u)
+              if (G0 + u * NW + wid < g1) body(kg[u], vg[u], h[u]);
+          }
+        };
+        clear_table();  // (its space held the previous ion's chaos candidates)
+        if (tid < MAXK) {
+          c_n[tid] = 0;
+          c_lo[tid] = ~0ull;
+          c_hi[tid] = 0ull;
+        }
+        __syncthreads();  // (also: the clipped principal values before the lookups below)
+        {  // 1.
+          int cpos = 0, kc = -1;
+          uint64_t plo = ~0ull, phi = 0ull;
+          auto flush = [&]() {
+            const int t = __builtin_amdgcn_readlane(wave_incl_scan_dpp(cpos), 63);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+              const uint64_t l2 = (uint64_t)__shfl_xor((unsigned long long)plo, o, WAVE);
+              const uint64_t h2 = (uint64_t)__shfl_xor((unsigned long long)phi, o, WAVE);
+              plo = l2 < plo ? l2 : plo;
+              phi = h2 > phi ? h2 : phi;
+            }
+            if (lane == 0 && t) {
+              atomicAdd(&c_n[kc], t);
+              atomicMin(&c_lo[kc], (unsigned long long)plo);
+              atomicMax(&c_hi[kc], (unsigned long long)phi);
+            }
+            cpos = 0;
+            plo = ~0ull;
+            phi = 0ull;
+          };
+          groups(0, ng, [&](int k, bool valid, const Reg& h) {
+            if (k != kc) {
+              if (kc >= 0) flush();
+              kc = k;
+            }
+            const bool fl = valid && Hits<FMT>::dup(h);
+            if (fl && !tbl_add<DTBL>(tkey, tval, (Hits<FMT>::pix(h) << 3) | (uint32_t)k, Hits<FMT>::val(h)))
+              ctr[C_ABORT] = 1;
+            if (valid && !fl && Hits<FMT>::val(h) > 0.0) {
+              const uint64_t b = bits_of(Hits<FMT>::val(h));
+              ++cpos;
+              plo = b < plo ? b : plo;
+              phi = b > phi ? b : phi;
+            }
+          });
+          if (kc >= 0) flush();
+        }
+        __syncthreads();
+        if (ctr[C_ABORT]) {  // more flagged pixels than the table holds: the next pass scores this ion
+          reject();
+          skip = true;
+        } else {
+          for (int i = tid; i < DTBL; i += BLOCK) {
+            const uint32_t key = tkey[i];
+            if (key != 0xFFFFFFFFu && tval[i] > 0.0) {
+              const int k = (int)(key & 7u);
+              atomicAdd(&c_n[k], 1);
+              atomicMin(&c_lo[k], (unsigned long long)bits_of(tval[i]));
+              atomicMax(&c_hi[k], (unsigned long long)bits_of(tval[i]));
+            }
+          }
+          __syncthreads();
+          // 2.
+          for (int k = 1; k < K; ++k) {
+            const int nk = c_n[k];
+            double thr = INFINITY;
+            if (nk > 0) {
+              const int g0 = gsv[k], g1 = (k + 1 < MAXK && gsv[k + 1] < ng) ? gsv[k + 1] : ng;
+              thr = percentile_of<BLOCK>(
+                  [&](auto&& f) {
+                    groups(g0, g1, [&](int, bool valid, const Reg& h) {
+                      if (valid && !Hits<FMT>::dup(h) && Hits<FMT>::val(h) > 0.0) f(bits_of(Hits<FMT>::val(h)));
+                    });
+                    for (int i = tid; i < DTBL; i += BLOCK) {
+                      const uint32_t key = tkey[i];
+                      if (key != 0xFFFFFFFFu && (int)(key & 7u) == k && tval[i] > 0.0) f(bits_of(tval[i]));
+                    }
+                  },
+                  nk, P.q, c_hist, c_sh, c_dsh, c_lo[k], c_hi[k]);
+            }
+            if (tid == 0) c_thr[k] = thr;
+          }
+          __syncthreads();
+          // 3. (a wave's partials of window k: part[k][wid], written by this wave only)
+          groups(0, ng, [&](int k, bool valid, const Reg& h) {
+            double a4[4] = {0.0, 0.0, 0.0, 0.0};
+            if (valid && !Hits<FMT>::dup(h)) {
+              const double thr = c_thr[k], v = Hits<FMT>::val(h);
+              const double y = v > thr ? thr : v;
+              const double x = xval(Hits<FMT>::pix(h));
+              if (x > 0.0) a4[0] = y;
+              a4[1] = y;
+              a4[2] = y * y;
+              a4[3] = x * y;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) a4[q] = wave_sum_dpp(a4[q]);
+            if (lane == 0) {
+              double* pk = part + ((size_t)k * NW + wid) * 4;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) pk[q] += a4[q];
+            }
+          });
+          __syncthreads();  // pass 3's plain partial updates before pass 4's atomics
+          // 4. (the table is cleared by the same threads before the tail barrier)
+          for (int i = tid; i < DTBL; i += BLOCK) {
+            const uint32_t key = tkey[i];
+            if (key != 0xFFFFFFFFu) {
+              const int k = (int)(key & 7u);
+              const double thr = c_thr[k], Y = tval[i];
+              const double y = Y > thr ? thr : Y;
+              const double x = xval(key >> 3);
+              double* pk = part + (size_t)k * NW * 4;
+              if (x > 0.0) atomicAdd(&pk[0], y);
+              atomicAdd(&pk[1], y);
+              atomicAdd(&pk[2], y * y);
+              atomicAdd(&pk[3], x * y);
+            }
+          }
+        }
+        if (tid < NW) dcnt[tid] = 0;
+      }
+    } else if (!skip && !(SMG_ABL & 2)) {
       const int ng = uni(D->ngroups);
       // Window sums of y and y^2 come from the prefix sums (descriptor); the stream only joins the tail against
       // the principal image (sum xy, sum y[x>0]: nonzero for the few points whose pixel is in the principal
@@ -1011,8 +1351,10 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     // ---- the registers of ion b are dead: ion b+1's principal window and first two chunks go in flight
     if (npos >= 0 && desc_lds_ok(DN, CAPC)) {
       issue_principal(DN);
-      issue_chunk(DN, 0, pa);
-      issue_chunk(DN, 1, pb);
+      if constexpr (!CLIP) {
+        issue_chunk(DN, 0, pa);
+        issue_chunk(DN, 1, pb);
+      }
     }
     if (!skip) clear_table();  // for phase d (its space held the previous ion's chaos candidates)
     STAMP(10);
@@ -1455,7 +1797,8 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
       IonRec* G = reinterpret_cast<IonRec*>(desc + pos);
       const int k = lane;
       if (k < K) {
-        double sk = 0.0, syy = D->syy[k], sxy = 0.0;  // Σy² + the squared per-pixel sums of duplicate candidates
+        // Σy² + the squared per-pixel sums of duplicate candidates (CLIP: the clipped image's sums, Σy too)
+        double sk = 0.0, syy = CLIP ? 0.0 : D->syy[k], sxy = 0.0, sy = 0.0;
         if (k == 0) {
           sk = s0;
         } else {
@@ -1463,6 +1806,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
           for (int w = 0; w < NW; ++w) {
             const double* pk = part + ((size_t)k * NW + w) * 4;
             sk += pk[0];
+            sy += pk[1];
             syy += pk[2];
             sxy += pk[3];
           }
@@ -1470,6 +1814,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         G->s[k] = sk;
         G->sxy[k] = sxy;
         G->syy[k] = syy;
+        if (CLIP && k > 0) G->sy[k] = sy;
       }
       if (lane == 0) {
         G->sx = sx;
@@ -1893,75 +2238,6 @@ __device__ int tail_window(const Hits<FMT>& hits, int64_t a, int64_t b, const do
   return n;
 }
 
-// k-th smallest (0-based) of n positive doubles (list, written by this block): MSB-first radix select over
-// the IEEE bits (monotonic for positive values), 8 passes of an 8-bit LDS histogram.
-// The i0-th smallest value of list[0..n) and, with pair, the (i0 + 1)-th (i0 + 1 < n): an MSD radix select over
-// the f64 bit patterns (the values are positive: their patterns are ordered like the values) that stops as soon as
-// the selected byte prefix holds a single element (it is then fetched whole), usually after three or four of the
-// eight bytes.  The next order statistic is the same value when more elements than needed equal it, else the
-// smallest value above it (one pass for both).  sh: 4 ints, dsh: 1 u64 of LDS.
-__device__ void block_select_pair(const double* list, int n, int i0, bool pair, uint32_t* hist, int* sh,
-                                  unsigned long long* dsh, double& a, double& b) {
-  const int tid = threadIdx.x;
-  uint64_t prefix = 0ull, mask = 0ull;
-  int k = i0;
-  for (int shift = 56; shift >= 0; shift -= 8) {
-    for (int i = tid; i < 256; i += DBLOCK) hist[i] = 0u;
-    __syncthreads();
-    for (int i = tid; i < n; i += DBLOCK) {
-      const uint64_t bits = (uint64_t)__double_as_longlong(ld_agent(&list[i]));
-      if ((bits & mask) == prefix) atomicAdd(&hist[(bits >> shift) & 255u], 1u);
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int c = 0, d = 0;
-      for (; d < 255; ++d) {
-        if (c + (int)hist[d] > k) break;
-        c += (int)hist[d];
-      }
-      sh[0] = d;
-      sh[1] = k - c;
-      sh[2] = (int)hist[d];
-    }
-    __syncthreads();
-    prefix |= (uint64_t)sh[0] << shift;
-    mask |= 255ull << shift;
-    k = sh[1];
-    const int cnt = sh[2];
-    __syncthreads();
-    if (cnt == 1 && shift > 0) {  // a single element carries the prefix: it is the one
-      for (int i = tid; i < n; i += DBLOCK) {
-        const uint64_t bits = (uint64_t)__double_as_longlong(ld_agent(&list[i]));
-        if ((bits & mask) == prefix) *dsh = bits;
-      }
-      __syncthreads();
-      prefix = *dsh;
-      __syncthreads();
-      break;
-    }
-  }
-  a = __longlong_as_double((long long)prefix);
-  b = a;
-  if (!pair) return;
-  if (tid == 0) {
-    sh[3] = 0;
-    *dsh = ~0ull;
-  }
-  __syncthreads();
-  int le = 0;
-  uint64_t above = ~0ull;
-  for (int i = tid; i < n; i += DBLOCK) {
-    const uint64_t bits = (uint64_t)__double_as_longlong(ld_agent(&list[i]));
-    if (bits <= prefix) ++le;
-    else above = bits < above ? bits : above;
-  }
-  atomicAdd(&sh[3], le);
-  if (above != ~0ull) atomicMin(dsh, (unsigned long long)above);
-  __syncthreads();
-  if (sh[3] < i0 + 2) b = __longlong_as_double((long long)*dsh);  // fewer than i0 + 2 elements <= a
-  __syncthreads();
-}
-
 // Gated hot-spot clip (image_generation.do_preprocessing / q; the oracle's quantile_clip): every pixel above
 // np.percentile(positive pixels, q) ('linear' method) is set to that value.  The image is zero outside its n
 // listed pixels; vals is scratch for their values.
@@ -1981,27 +2257,12 @@ __device__ void clip_image(double* img, const uint32_t* list, int n_list, double
   const int n = sh[2];
   __syncthreads();
   if (n == 0) return;
-  // numpy _compute_virtual_index (alpha = beta = 1), _get_indexes, _get_gamma, _lerp
-  const double qq = q / 100.0;
-  const double vi = (double)n * qq + (1.0 + qq * (1.0 - 1.0 - 1.0)) - 1.0;
-  int i0, i1;
-  double gamma;
-  if (vi >= (double)(n - 1)) {
-    i0 = i1 = n - 1;
-    gamma = 0.0;
-  } else if (vi < 0.0) {
-    i0 = i1 = 0;
-    gamma = 0.0;
-  } else {
-    i0 = (int)floor(vi);
-    i1 = i0 + 1;
-    gamma = vi - floor(vi);
-  }
   __shared__ unsigned long long sel_u64;
-  double a, b;
-  block_select_pair(vals, n, i0, i1 != i0, hist, sh, &sel_u64, a, b);
-  const double d = b - a;
-  const double thr = gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
+  const double thr = percentile_of<DBLOCK>(
+      [&](auto&& f) {
+        for (int i = tid; i < n; i += DBLOCK) f((uint64_t)__double_as_longlong(ld_agent(&vals[i])));
+      },
+      n, q, hist, sh, &sel_u64);
   for (int i = tid; i < n_list; i += DBLOCK) {
     const uint32_t p = list[i];
     const double v = ld_agent(&img[p]);
@@ -2022,7 +2283,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_dense_kernel(
   __shared__ double kst[4 * MAXK_DENSE];
   __shared__ int sh_ion;
   __shared__ int sh_ctr[4];
-  __shared__ uint32_t sh_hist[256];
+  __shared__ __attribute__((aligned(16))) uint32_t sh_hist[512];
   __shared__ int sh_sel[4];
   const int tid = threadIdx.x;
   DenseSlot S = dense_slot(scratch + (size_t)blockIdx.x * slot_bytes, P.npx);
@@ -2494,7 +2755,221 @@ struct RankBits {
   }
 };
 
+// The wide pass's tail windows under the hot-spot clip (CLIP, image_generation.do_preprocessing): each tail image is
+// clipped at the q-th percentile of its positive pixels before its sums, so its Σy, Σy², Σxy and Σy[x>0] come from
+// the clipped pixel values, not from the hit prefix sums.  A window's pixel values are its unflagged points' values
+// (the only point of their pixel in the window, smg_flag_duplicates) and the per-pixel sums of its flagged points.
+//  1. one stream over the tail: flagged points summed per (window, pixel) in the tables (LDS, then the slot's global
+//     table; an overflow sends the ion to the pixel-indexed kernel), positive unflagged points counted per window;
+//  2. per window, its threshold by an MSD radix select over those values (select_pair: the window's points and the
+//     tables, re-read once per pass);
+//  3. a second stream: the clipped unflagged points' sums, x gathered by rank;
+//  4. the table entries: each flagged pixel's clipped sum into its window's sums, then the entry released.
+// kst rows as in the kernel: 0 Σy[x>0], 1 Σy, 2 Σy², 3 Σxy (window k at column k).
 template <int FMT>
+__device__ void wide_clip_tail(const Hits<FMT>& hits, int K, double q, int npx, const RankBits& R, const WideSlot& S,
+                               const int64_t* sh_tb, const int64_t* sh_tlo, const int64_t* sh_tn, uint32_t* ltkey,
+                               double* ltval, double* kst, int* sh_nown, int* sh_ctr, uint32_t* c_hist, int* c_sh,
+                               unsigned long long* c_dsh, double* c_thr, int* c_n) {
+  using H = Hits<FMT>;
+  const int tid = threadIdx.x, lane = tid & 63;
+  constexpr int U = FMT == SMG_HITS_PACKED_F32 ? TDU : WDU;
+  constexpr int64_t TSTEP = (int64_t)DBLOCK * U;  // the kernel's batch (sh_tb pads each window to a whole batch)
+  const int64_t T = sh_tb[K - 1];
+  if (tid < MAXK_DENSE) c_n[tid] = 0;
+  __syncthreads();
+  auto insert_global = [&](uint32_t key, double y) {
+    uint32_t h = (key * 0x9E3779B1u) >> (32 - WIDE_HT_LOG2);
+    bool own = false, done = false;
+    for (int t = 0; t < WIDE_PROBES; ++t) {
+      const uint32_t old = atomicCAS(&S.hkey[h], WIDE_EMPTY, key);
+      if (old == WIDE_EMPTY || old == key) {
+        atomicAdd(&S.hval[h], y);
+        own = old == WIDE_EMPTY;
+        done = true;
+        break;
+      }
+      h = (h + 1) & (WIDE_HT - 1);
+    }
+    if (!done) sh_ctr[3] = 1;
+    return own ? (int)h : -1;
+  };
+  auto insert = [&](bool act, uint32_t key, double y) {  // uniform call: act = this lane has an entry
+    bool placed = !act;
+    if (act) {
+      uint32_t h = (key * 0x9E3779B1u) >> (32 - WIDE_LT_LOG2);
+      for (int t = 0; t < WIDE_LT_PROBES; ++t) {
+        const uint32_t old = atomicCAS(&ltkey[h], WIDE_EMPTY, key);
+        if (old == WIDE_EMPTY || old == key) {
+          atomicAdd(&ltval[h], y);
+          placed = true;
+          break;
+        }
+        h = (h + 1) & (WIDE_LT - 1);
+      }
+    }
+    int gh = -1;
+    if (__ballot(!placed)) {
+      if (!placed) gh = insert_global(key, y);
+    }
+    const int idx = wave_append(gh >= 0, sh_nown);
+    if (gh >= 0) S.hown[idx] = (uint32_t)gh;
+  };
+  // batches of U points per lane, each inside one window (uniform kb); body(kb, off, n, r)
+  auto stream = [&](auto&& body) {
+    int kb = 0;
+    for (int64_t v0 = 0; v0 < T; v0 += TSTEP) {
+      while (v0 >= sh_tb[kb + 1]) ++kb;
+      kb = __builtin_amdgcn_readfirstlane(kb);
+      const int64_t off = v0 - sh_tb[kb], n = sh_tn[kb], a = sh_tlo[kb];
+      typename H::Reg r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t lv = off + (int64_t)u * DBLOCK + tid;
+        r[u] = hits.load(a + (lv < n ? lv : n - 1));
+      }
+      body(kb, off, n, r);
+    }
+  };
+  auto bits_of = [](double v) { return (uint64_t)__double_as_longlong(v); };
+
+  // 1. flagged points -> tables; positive unflagged points counted per window
+  {
+    int cpos = 0, kc = 0;
+    auto flush = [&]() {
+      const int t = __builtin_amdgcn_readlane(wave_incl_scan_dpp(cpos), 63);
+      if (lane == 0 && t) atomicAdd(&c_n[kc + 1], t);
+      cpos = 0;
+    };
+    stream([&](int kb, int64_t off, int64_t n, const typename H::Reg (&r)[U]) {
+      if (kb != kc) {
+        flush();
+        kc = kb;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool valid = off + (int64_t)u * DBLOCK + tid < n;
+        const bool fl = valid && H::dup(r[u]);
+        insert(fl, (uint32_t)kb * (uint32_t)npx + H::pix(r[u]), fl ? (double)H::val(r[u]) : 0.0);
+        cpos += (valid && !H::dup(r[u]) && H::val(r[u]) > 0.0) ? 1 : 0;
+      }
+    });
+    flush();
+  }
+  slot_sync();  // the tables' sums are complete (LDS; L2 for the global entries)
+  const int no = *sh_nown;
+  auto count_entry = [&](uint32_t key, double y) {
+    if (y > 0.0) atomicAdd(&c_n[(int)(key / (uint32_t)npx) + 1], 1);
+  };
+  for (int i = tid; i < WIDE_LT; i += DBLOCK) {
+    const uint32_t key = ltkey[i];
+    if (key != WIDE_EMPTY) count_entry(key, ltval[i]);
+  }
+  for (int j = tid; j < no; j += DBLOCK) {
+    const uint32_t sl = S.hown[j];
+    count_entry(ld_agent(&S.hkey[sl]), ld_agent(&S.hval[sl]));
+  }
+  __syncthreads();
+
+  // 2. thresholds
+  for (int k = 1; k < K; ++k) {
+    const int nk = c_n[k];
+    double thr = INFINITY;
+    if (nk > 0 && !sh_ctr[3]) {
+      const int64_t a = sh_tlo[k - 1], n = sh_tn[k - 1];
+      const uint32_t kk = (uint32_t)(k - 1);
+      thr = percentile_of<DBLOCK>(
+          [&](auto&& f) {
+            for (int64_t i = tid; i < n; i += DBLOCK) {
+              const typename H::Reg h = hits.load(a + i);
+              if (!H::dup(h) && H::val(h) > 0.0) f(bits_of((double)H::val(h)));
+            }
+            for (int i = tid; i < WIDE_LT; i += DBLOCK) {
+              const uint32_t key = ltkey[i];
+              if (key != WIDE_EMPTY && key / (uint32_t)npx == kk && ltval[i] > 0.0) f(bits_of(ltval[i]));
+            }
+            for (int j = tid; j < no; j += DBLOCK) {
+              const uint32_t sl = S.hown[j];
+              if (ld_agent(&S.hkey[sl]) / (uint32_t)npx == kk) {
+                const double y = ld_agent(&S.hval[sl]);
+                if (y > 0.0) f(bits_of(y));
+              }
+            }
+          },
+          nk, q, c_hist, c_sh, c_dsh);
+    }
+    if (tid == 0) c_thr[k] = thr;
+  }
+  __syncthreads();
+
+  // 3. the clipped unflagged points
+  {
+    double as = 0.0, axy = 0.0, ay = 0.0, ayy = 0.0;
+    int kacc = 0;
+    auto flush = [&]() {
+      const double t0 = wave_sum_dpp(as), t1 = wave_sum_dpp(ay), t2 = wave_sum_dpp(ayy), t3 = wave_sum_dpp(axy);
+      if (lane == 0) {
+        atomicAdd(&kst[0 * MAXK_DENSE + kacc + 1], t0);
+        atomicAdd(&kst[1 * MAXK_DENSE + kacc + 1], t1);
+        atomicAdd(&kst[2 * MAXK_DENSE + kacc + 1], t2);
+        atomicAdd(&kst[3 * MAXK_DENSE + kacc + 1], t3);
+      }
+      as = axy = ay = ayy = 0.0;
+    };
+    stream([&](int kb, int64_t off, int64_t n, const typename H::Reg (&r)[U]) {
+      if (kb != kacc) {
+        flush();
+        kacc = kb;
+      }
+      const double thr = c_thr[kb + 1];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool valid = off + (int64_t)u * DBLOCK + tid < n;
+        if (valid && !H::dup(r[u])) {
+          const double v = H::val(r[u]);
+          const double y = v > thr ? thr : v;
+          const uint32_t p = H::pix(r[u]);
+          const double x = R.test(p) ? ld_agent(&S.vals[R.rank(p)]) : 0.0;
+          if (x > 0.0) as += y;
+          axy += x * y;
+          ay += y;
+          ayy += y * y;
+        }
+      }
+    });
+    flush();
+  }
+
+  // 4. the flagged pixels' clipped sums; the entries are released for the next ion
+  auto add_pixel = [&](uint32_t key, double Y) {
+    const uint32_t kk = key / (uint32_t)npx, p = key - kk * (uint32_t)npx;
+    const int k = (int)kk + 1;
+    const double thr = c_thr[k];
+    const double y = Y > thr ? thr : Y;
+    const double x = R.test(p) ? ld_agent(&S.vals[R.rank(p)]) : 0.0;
+    if (x > 0.0) atomicAdd(&kst[0 * MAXK_DENSE + k], y);
+    atomicAdd(&kst[1 * MAXK_DENSE + k], y);
+    atomicAdd(&kst[2 * MAXK_DENSE + k], y * y);
+    atomicAdd(&kst[3 * MAXK_DENSE + k], x * y);
+  };
+  for (int i = tid; i < WIDE_LT; i += DBLOCK) {
+    const uint32_t key = ltkey[i];
+    if (key != WIDE_EMPTY) {
+      add_pixel(key, ltval[i]);
+      ltkey[i] = WIDE_EMPTY;
+      ltval[i] = 0.0;
+    }
+  }
+  for (int j = tid; j < no; j += DBLOCK) {
+    const uint32_t sl = S.hown[j];
+    add_pixel(ld_agent(&S.hkey[sl]), ld_agent(&S.hval[sl]));
+    S.hkey[sl] = WIDE_EMPTY;
+    S.hval[sl] = 0.0;
+  }
+  __syncthreads();  // (released entries reach L2 before the next ion's inserts: slot_syncs lie between)
+}
+
+template <int FMT, bool CLIP>
 __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     Hits<FMT> hits, const DD4* __restrict__ cum, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
     const int64_t* __restrict__ ion_off, const double* __restrict__ theor, Params P,
@@ -2515,6 +2990,13 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
   __shared__ int64_t sh_tb[MAXK_DENSE + 1];  // tail stream: offset of window k at k - 1 (+ the total)
   __shared__ int64_t sh_tlo[MAXK_DENSE];     // first point of window k at k - 1
   __shared__ int64_t sh_tn[MAXK_DENSE];      // length of window k at k - 1
+  // CLIP (do_preprocessing): the radix select's histogram and scalars, each window's threshold and positive count
+  __shared__ __attribute__((aligned(16))) uint32_t c_hist[CLIP ? 512 : 4];
+  __shared__ int c_sh[4];
+  __shared__ unsigned long long c_dsh;
+  __shared__ double c_thr[CLIP ? MAXK_DENSE : 1];
+  __shared__ int c_n[CLIP ? MAXK_DENSE : 1];
+  __shared__ unsigned long long c_lo[CLIP ? 1 : 1], c_hi[CLIP ? 1 : 1];  // the principal's value bounds
   const int tid = threadIdx.x;
   const int npx = P.npx, n64 = (npx + 63) / 64, nsb = (n64 + 1023) / 1024;
   const int n64p = (int)wide_n64p(npx);  // n64 words + zero words to a whole 4-word group (row7 reads one past)
@@ -2688,6 +3170,60 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     }
     if (np < npx) mx = mx > 0.0 ? mx : 0.0;  // unlisted pixels are zero
     dblock_sum<4>(acc, red);
+    if constexpr (CLIP) {
+      // the hot-spot clip of the principal image: its q-th percentile over the acc[3] positive values, every value
+      // above it lowered to it, then the statistics again
+      const int n0 = (int)acc[3];
+      if (n0 > 0) {
+        // the smallest and largest positive value's bits bound the select's passes
+        uint64_t plo = ~0ull, phi = 0ull;
+        for (int r = tid; r < np; r += DBLOCK) {
+          const double v = ld_agent(&S.vals[r]);
+          if (v > 0.0) {
+            const uint64_t b = (uint64_t)__double_as_longlong(v);
+            plo = b < plo ? b : plo;
+            phi = b > phi ? b : phi;
+          }
+        }
+        if (tid == 0) {
+          c_lo[0] = ~0ull;
+          c_hi[0] = 0ull;
+        }
+        __syncthreads();
+        if (plo != ~0ull) {
+          atomicMin(&c_lo[0], (unsigned long long)plo);
+          atomicMax(&c_hi[0], (unsigned long long)phi);
+        }
+        __syncthreads();
+        const double thr = percentile_of<DBLOCK>(
+            [&](auto&& f) {
+              for (int r = tid; r < np; r += DBLOCK) {
+                const double v = ld_agent(&S.vals[r]);
+                if (v > 0.0) f((uint64_t)__double_as_longlong(v));
+              }
+            },
+            n0, P.q, c_hist, c_sh, &c_dsh, c_lo[0], c_hi[0]);
+        acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
+        mx = -INFINITY;
+        for (int r = tid; r < np; r += DBLOCK) {
+          double v = ld_agent(&S.vals[r]);
+          if (v > thr) {
+            v = thr;
+            S.vals[r] = thr;
+          }
+          acc[0] += v;
+          acc[1] += v * v;
+          if (v > 0.0) {
+            acc[2] += v;
+            acc[3] += 1.0;
+          }
+          mx = v > mx ? v : mx;
+        }
+        if (np < npx) mx = mx > 0.0 ? mx : 0.0;
+        dblock_sum<4>(acc, red);
+        slot_sync();  // the clipped values are visible to the tail's gathers
+      }
+    }
     {
       const double vmax = block_max<DNW>(mx, red);
       if (tid == 0) {  // kept in the LDS until chaos / finalize (frees registers for the tail stream)
@@ -2723,12 +3259,15 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
       }
     }
     __syncthreads();
-    if (tid < K - 1) {
+    if (!CLIP && tid < K - 1) {  // (CLIP: Σy, Σy² of the clipped images come from the clip stream below)
       const double2 ws = window_sums<FMT>(hits, cum, lo[w0 + 1 + tid], hi[w0 + 1 + tid]);
       kst[1 * MAXK_DENSE + tid + 1] = ws.x;
       kst[2 * MAXK_DENSE + tid + 1] = ws.y;
     }
-    {
+    if constexpr (CLIP) {
+      wide_clip_tail<FMT>(hits, K, P.q, npx, R, S, sh_tb, sh_tlo, sh_tn, ltkey, ltval, kst, &sh_nown, sh_ctr, c_hist, c_sh,
+                          &c_dsh, c_thr, c_n);
+    } else {
       const int64_t T = sh_tb[K - 1];
       double as = 0.0, axy = 0.0;  // the lane's Σy[x > 0], Σxy in window kacc
       int kacc = 0;
@@ -3234,7 +3773,8 @@ __global__ void list_all_kernel(uint32_t* list, uint32_t* count, const int64_t* 
 #endif
 static constexpr int DENSE_SLOTS = SMG_DENSE_SLOTS;  // dense-path workgroups (one scratch slot each)
 static constexpr size_t DENSE_BM_LDS_MAX = 152 * 1024;  // dense kernel: LDS presence bitmap up to this size
-static constexpr size_t WIDE_LDS_MAX = 160 * 1024 - 4096;  // wide pass: dynamic LDS (static arrays ~2.3 KB)
+static constexpr size_t WIDE_LDS_MAX = 160 * 1024 - 4096;  // wide pass: dynamic LDS (static arrays ~2.9 KB)
+static constexpr size_t WIDE_LDS_MAX_CLIP = 160 * 1024 - 6144;  // its CLIP instantiation (static arrays ~4.9 KB)
 // workspace: header (pass counters at word 0.., per-XCD range counters at word 64..), two ion lists,
 // the ion descriptors, dense scratch slots
 static constexpr size_t WS_HEADER = 2048;
@@ -3356,15 +3896,18 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   if (lds_main < (size_t)SMG_MAIN_LDS_MIN) lds_main = SMG_MAIN_LDS_MIN;
 #endif
   const size_t lds_big = two ? Big2Lay::bytes(P.npx) : BigLay::bytes(P.npx);
-  // the hot-spot clip needs whole images: every ion takes the dense path.  Images above NPX_LDS_MAX pixels go to
+  // the hot-spot clip (do_preprocessing) clips every image before its sums: the LDS passes and the wide pass have
+  // CLIP instantiations (ion_pipe_kernel<..., CLIP>, ion_wide_kernel<FMT, true>), the pixel-indexed kernel clips
+  // its images in place.  Images above NPX_LDS_MAX pixels go to
   // the rank-indexed wide pass when its LDS bitmap fits: it outruns the two-level LDS passes on them (config-5
   // rank shard: the big two-level pass scored 3,958 ions in 18.4 ms, the wide pass 586k in 255 ms, and the main
   // two-level pass spent 6.7 ms rejecting every ion, profiles/round3/r3c5_*); smg_debug_force_two_level keeps
   // the two-level passes for the parity suite
-  const bool wide_fits = !P.clip && g_force_dense != 2 && wide_lds_bytes(P.npx) <= WIDE_LDS_MAX;
+  const size_t wide_max = P.clip ? WIDE_LDS_MAX_CLIP : WIDE_LDS_MAX;
+  const bool wide_fits = g_force_dense != 2 && wide_lds_bytes(P.npx) <= wide_max;
   const bool lds_ok = two ? (!wide_fits || g_force_two_level) : P.npx <= NPX_LDS_MAX;
-  const bool main_ok = !P.clip && !g_force_dense && lds_ok && lds_main <= MAIN_LDS;
-  const bool big_ok = !P.clip && !g_force_dense && lds_ok && lds_big <= BIG_LDS;
+  const bool main_ok = !g_force_dense && lds_ok && lds_main <= MAIN_LDS;
+  const bool big_ok = !g_force_dense && lds_ok && lds_big <= BIG_LDS;
   const int cus = device_cus();
   if (main_ok || big_ok) {
 #ifndef SMG_DESC8
@@ -3381,8 +3924,10 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   }
   if (main_ok) {
     Sched SA{n_ions, hdr + HDR_XCD, nullptr, nullptr};
-    auto k1 = two ? &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, true>
-                  : &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, false>;
+    auto k1 = P.clip ? (two ? &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, true, true>
+                            : &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, false, true>)
+                     : (two ? &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, true>
+                            : &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, false>);
     SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k1), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_main));
     // MAIN_WGPCU resident workgroups per CU, a multiple of the XCD count
@@ -3399,8 +3944,10 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   }
   if (big_ok) {
     Sched SB{0, hdr + 1, list_a, hdr + 0};
-    auto k2 = two ? &ion_pipe_kernel<FMT, BIG_BLOCK, BIG2_RMAX, BIG_RC, 1, SRC_LIST, true>
-                  : &ion_pipe_kernel<FMT, BIG_BLOCK, BIG_RMAX, BIG_RC, 1, SRC_LIST, false>;
+    auto k2 = P.clip ? (two ? &ion_pipe_kernel<FMT, BIG_BLOCK, BIG2_RMAX, BIG_RC, 1, SRC_LIST, true, true>
+                            : &ion_pipe_kernel<FMT, BIG_BLOCK, BIG_RMAX, BIG_RC, 1, SRC_LIST, false, true>)
+                     : (two ? &ion_pipe_kernel<FMT, BIG_BLOCK, BIG2_RMAX, BIG_RC, 1, SRC_LIST, true>
+                            : &ion_pipe_kernel<FMT, BIG_BLOCK, BIG_RMAX, BIG_RC, 1, SRC_LIST, false>);
     SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k2), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_big));
     const int nwg2 = (int)(n_ions < cus ? n_ions : cus);
@@ -3423,17 +3970,18 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
     SMG_LAUNCH_CHECK();
   }
   const int nslots = (int)(n_ions < DENSE_SLOTS ? n_ions : DENSE_SLOTS);
-  // dense path: the rank-indexed wide pass where the image's bitmap + rank prefix fit the LDS (no clip); the
-  // pixel-indexed kernel takes its rejects (or everything)
+  // dense path: the rank-indexed wide pass where the image's bitmap + rank prefix fit the LDS (with the clip: its
+  // CLIP instantiation); the pixel-indexed kernel takes its rejects (or everything)
   const uint32_t* dlist = list_b;
   uint32_t* dcount = hdr + 2;
   uint32_t* dnext = hdr + 3;
   const size_t wide_lds = wide_lds_bytes(P.npx);
-  if (!P.clip && g_force_dense != 2 && wide_lds <= WIDE_LDS_MAX) {
-    SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ion_wide_kernel<FMT>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)wide_lds));
+  if (wide_fits) {
+    auto kw = P.clip ? &ion_wide_kernel<FMT, true> : &ion_wide_kernel<FMT, false>;
+    SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kw), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)wide_lds));
     PassTimer tm(SMG_PASS_WIDE, st);
-    hipLaunchKernelGGL(ion_wide_kernel<FMT>, dim3((unsigned)nslots), dim3(DBLOCK), wide_lds, st, hits,
+    hipLaunchKernelGGL(kw, dim3((unsigned)nslots), dim3(DBLOCK), wide_lds, st, hits,
                        reinterpret_cast<const DD4*>(hit_cum), lo, hi, ion_off,
                        theor, P, list_b, hdr + 2, hdr + 3, list_a, hdr + 4, slots, slot_bytes, oc, osp, osc, omsm,
                        oflags);

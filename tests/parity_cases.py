@@ -163,6 +163,12 @@ def make_case(name: str):
     if name == "clip_q50_conn8":
         ds, ions, ppm, _ = make_case("zeros_rect")
         return ds, ions, ppm, {"do_preprocessing": True, "q": 50.0, "connectivity": 8}
+    if name == "clip_dups_heavy":  # the clip with many flagged tail pixels (LDS table overflow -> global table)
+        ds, ions, ppm, _ = make_case("dups_heavy")
+        return ds, ions, ppm, {"do_preprocessing": True, "q": 90.0}
+    if name == "clip_large":   # the clip on a > 2^18-pixel image with planted blobs (wide pass, q 99.5)
+        ds, ions, ppm, _ = make_case("large_image")
+        return ds, ions, ppm, {"do_preprocessing": True, "q": 99.5}
     if name == "wide_range":   # intensities over ~1e-3..1e9 with the bright mass BEFORE the scored windows: the
         # window sums must not depend on the total intensity (or squared intensity) preceding them in m/z order
         ions = syn.make_ion_table(30, seed=151, decoy_seed=152, mass_range=(480.0, 880.0))
@@ -189,7 +195,7 @@ def make_case(name: str):
 
 CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels", "nlevels1", "big_window", "huge_window",
          "large_image", "xl_image", "large_blobs", "boundary", "long_tail", "dups_heavy", "kmix", "clip99", "clip_q50_conn8",
-         "wide_range", "wide_overflow"]
+         "clip_dups_heavy", "clip_large", "wide_range", "wide_overflow"]
 
 
 def oracle_run(ds, ions, ppm, nlevels=30, connectivity=4, erosion_border=0, q=99.0, do_preprocessing=False):

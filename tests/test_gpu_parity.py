@@ -130,7 +130,8 @@ def test_forced_two_level_large_blobs_reaches_big_pass():
 
 # every LDS-path case again with the two-level pixel set forced (smg_debug_force_two_level)
 TWO_LEVEL_CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels",
-                   "big_window", "boundary", "long_tail", "dups_heavy", "kmix"]
+                   "big_window", "boundary", "long_tail", "dups_heavy", "kmix", "clip99", "clip_q50_conn8",
+                   "clip_dups_heavy"]
 
 
 @pytest.mark.parametrize("name", TWO_LEVEL_CASES)
@@ -146,7 +147,7 @@ def test_forced_two_level_matches_oracle(name):
     has = (m["flags"] & 1) != 0
     lds = has & ((m["flags"] & 2) == 0)
     assert ((m["flags"][lds] & 0x10) != 0).all()
-    assert lds.any() or name == "dups_heavy"  # its duplicate lists overflow every LDS pass
+    assert lds.any() or name in ("dups_heavy", "clip_dups_heavy")  # duplicate lists / tables overflow the LDS passes
     idx = {k: i for i, k in enumerate(zip(ions.sf_ids.tolist(), ions.adducts.tolist()))}
     assert set(zip(ions.sf_ids[has].tolist(), ions.adducts[has].tolist())) == set(df.index.tolist())
     rows = np.array([idx[k] for k in df.index.tolist()], dtype=np.int64)
@@ -159,7 +160,7 @@ def test_forced_two_level_matches_oracle(name):
 @pytest.mark.parametrize("mode", [1, 2])
 def test_forced_dense_matches_oracle(name, mode):
     """Every case again with every ion on the dense path (smg_debug_force_dense): mode 1 = the rank-indexed wide
-    pass where the image fits it (its rejects and the clip on the pixel-indexed kernel), mode 2 = the pixel-indexed
+    pass where the image fits it (with the clip too; its rejects on the pixel-indexed kernel), mode 2 = the pixel-indexed
     kernel alone (sparse scatter into the slot's pixel-sized images, owner lists, candidate-only chaos)."""
     from sm_distributed_amd import _lib
     ds, ions, ppm, kw, imgs, df, _, _, _, _ = _run_case(name)
@@ -173,8 +174,10 @@ def test_forced_dense_matches_oracle(name, mode):
     has = (m["flags"] & 1) != 0
     assert ((m["flags"][has] & 2) != 0).all()
     wide = (m["flags"] & 0x20) != 0
-    if mode == 2 or kw.get("do_preprocessing") or name == "xl_image":
+    if mode == 2 or name == "xl_image":
         assert not wide.any()
+    elif kw.get("do_preprocessing"):  # the wide pass clips; a table overflow would send an ion to the pixel kernel
+        assert has.any() and wide[has].sum() >= 0.9 * has.sum()
     elif name == "wide_overflow":  # every ion's tail duplicates overflow the wide pass's table
         assert has.any() and not wide[has].any()
     else:
@@ -225,6 +228,21 @@ def test_wide_pass_reached_without_forcing():
     _, _, _, _, _, _, _, m, _, _ = _run_case("wide_overflow")
     has = (m["flags"] & 1) != 0
     assert has.any() and ((m["flags"][has] & 2) != 0).all() and not ((m["flags"][has] & 0x20) != 0).any()
+
+
+def test_clip_runs_on_the_fast_paths():
+    """The hot-spot clip (do_preprocessing) runs where the unclipped search would: the LDS passes (CLIP
+    instantiations: each image clipped before its sums) on images up to 2^18 pixels, the rank-indexed wide pass on
+    larger ones -- not only on the pixel-indexed kernel.  (clip_dups_heavy's flagged tail pixels overflow the LDS
+    passes' duplicate table: those ions go on to the dense path, which the parity tests check.)"""
+    for name in ("clip99", "clip_q50_conn8"):
+        m = _run_case(name)[7]
+        has = (m["flags"] & 1) != 0
+        lds = has & ((m["flags"] & 2) == 0)
+        assert has.any() and lds.sum() >= 0.5 * has.sum(), name
+    m = _run_case("clip_large")[7]
+    has = (m["flags"] & 1) != 0
+    assert has.any() and ((m["flags"][has] & (0x20 | 2)) == (0x20 | 2)).all()
 
 
 def test_lds_pipeline_paths_exercised():
