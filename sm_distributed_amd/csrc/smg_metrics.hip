@@ -367,6 +367,147 @@ __device__ double percentile_of(Visit&& visit, int n, double q, uint32_t* hist, 
   return gamma >= 0.5 ? b - d * (1.0 - gamma) : a + d * gamma;
 }
 
+// The q-th percentiles of several sets at once (the hot-spot clip's tail images): one MSD radix select per set (the
+// scheme of select_pair, percentile_of's index arithmetic), all sets of a batch of SB advancing together so that
+// each round reads the elements once for every set in it (the tail windows' points come from HBM / L2: one latency
+// per round instead of one per set and pass).  State per set in LDS; wave j finishes the round of the batch's set j
+// (its 256-bin histogram: the digit, then the bins cleared for the next round).  visit(f) calls f(set, bits) for
+// every element this thread owns (the same partition every round); n[set]: the set's size (0: no clip, thr +inf).
+struct SelSet {
+  unsigned long long prefix, mask, dsh;  // selected prefix and its mask; FETCH: the element; PAIR: min above
+  double gamma;
+  int k, i0, shift, phase, le, pair;
+};
+enum { SEL_RADIX = 0, SEL_FETCH = 1, SEL_PAIR = 2, SEL_DONE = 3 };
+__device__ __forceinline__ void sel_init(SelSet& st, int n, double q) {
+  const double qq = q / 100.0;
+  const double vi = (double)n * qq + (1.0 + qq * (1.0 - 1.0 - 1.0)) - 1.0;  // numpy _compute_virtual_index
+  int i0, i1;
+  double gamma;
+  if (vi >= (double)(n - 1)) {
+    i0 = i1 = n - 1;
+    gamma = 0.0;
+  } else if (vi < 0.0) {
+    i0 = i1 = 0;
+    gamma = 0.0;
+  } else {
+    i0 = (int)floor(vi);
+    i1 = i0 + 1;
+    gamma = vi - floor(vi);
+  }
+  st.prefix = st.mask = 0ull;
+  st.dsh = ~0ull;
+  st.gamma = gamma;
+  st.k = st.i0 = i0;
+  st.shift = 56;
+  st.phase = n > 0 ? SEL_RADIX : SEL_DONE;
+  st.le = 0;
+  st.pair = i1 != i0;
+}
+// thr[s] for the sets [0, nsets); st: SB states, hist: SB x 256 u32 (16-B aligned), flag: 2 ints of LDS.  lo, hi
+// (optional): each set's smallest and largest element bits -- its passes start at the first byte where they differ.
+template <int NT, int SB, class Visit>
+__device__ void select_batch(Visit&& visit, int nsets, const int* n, double q, double* thr, SelSet* st, uint32_t* hist,
+                             int* flag, const unsigned long long* lo = nullptr, const unsigned long long* hi = nullptr) {
+  static_assert(NT / WAVE >= SB, "a wave per set of the batch");
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  for (int b0 = 0; b0 < nsets; b0 += SB) {
+    const int nb = nsets - b0 < SB ? nsets - b0 : SB;
+    if (tid < nb) {
+      SelSet& S = st[tid];
+      sel_init(S, n[b0 + tid], q);
+      if (n[b0 + tid] == 0) thr[b0 + tid] = INFINITY;
+      if (lo != nullptr && S.phase == SEL_RADIX) {
+        const uint64_t l = lo[b0 + tid], d = l ^ (uint64_t)hi[b0 + tid];
+        if (d == 0ull) {  // every element is the same value
+          thr[b0 + tid] = __longlong_as_double((long long)l);
+          S.phase = SEL_DONE;
+        } else {
+          const int top = (63 - __clzll((long long)d)) & ~7;
+          S.shift = top;
+          S.mask = top == 56 ? 0ull : ~((1ull << (top + 8)) - 1ull);
+          S.prefix = l & S.mask;
+        }
+      }
+    }
+    for (int i = tid; i < SB * 256; i += NT) hist[i] = 0u;
+    if (tid == 0) flag[0] = flag[1] = 1;
+    __syncthreads();
+    for (int round = 0; flag[round & 1]; ++round) {
+      visit([&](int set, uint64_t bits) {
+        const int j = set - b0;
+        if ((unsigned)j >= (unsigned)nb) return;
+        SelSet& S = st[j];
+        const int ph = S.phase;
+        if (ph == SEL_DONE) return;
+        const uint64_t pre = S.prefix;
+        if (ph == SEL_PAIR) {
+          if (bits <= pre) atomicAdd(&S.le, 1);
+          else atomicMin(&S.dsh, (unsigned long long)bits);
+        } else if ((bits & S.mask) == pre) {
+          if (ph == SEL_RADIX) atomicAdd(&hist[j * 256 + ((bits >> S.shift) & 255u)], 1u);
+          else S.dsh = bits;  // SEL_FETCH: the one element with the prefix
+        }
+      });
+      if (tid == 0) flag[(round + 1) & 1] = 0;
+      __syncthreads();
+      if (wid < nb) {
+        SelSet& S = st[wid];
+        const int ph = S.phase;  // (wave-uniform)
+        bool done_now = false;
+        if (ph == SEL_RADIX) {
+          int k = S.k, cnt;
+          const int d = hist_find(hist + wid * 256, k, cnt);
+          reinterpret_cast<uint4*>(hist + wid * 256)[lane] = make_uint4(0u, 0u, 0u, 0u);
+          if (lane == 0) {
+            const int sh = S.shift;
+            S.prefix |= (unsigned long long)d << sh;
+            S.mask |= 255ull << sh;
+            S.k = k;
+            if (cnt == 1 && sh > 0) {
+              S.phase = SEL_FETCH;
+            } else if (sh == 0) {
+              done_now = true;
+            } else {
+              S.shift = sh - 8;
+            }
+          }
+        } else if (ph == SEL_FETCH) {
+          if (lane == 0) {
+            S.prefix = S.dsh;
+            done_now = true;
+          }
+        } else if (ph == SEL_PAIR) {
+          if (lane == 0) {
+            const double a = __longlong_as_double((long long)S.prefix);
+            const double b = S.le < S.i0 + 2 ? __longlong_as_double((long long)S.dsh) : a;
+            const double dd = b - a, g = S.gamma;
+            thr[b0 + wid] = g >= 0.5 ? b - dd * (1.0 - g) : a + dd * g;
+            S.phase = SEL_DONE;
+          }
+        }
+        if (lane == 0) {
+          if (done_now) {  // the i0-th element is known: the pair pass next, or the threshold now
+            if (S.pair) {
+              S.phase = SEL_PAIR;
+              S.le = 0;
+              S.dsh = ~0ull;
+            } else {
+              thr[b0 + wid] = __longlong_as_double((long long)S.prefix);
+              S.phase = SEL_DONE;
+            }
+          }
+          if (S.phase != SEL_DONE) flag[(round + 1) & 1] = 1;
+        }
+      }
+      __syncthreads();
+    }
+    // every thread has read the final flag (and is done with the batch's states) before the next batch, or the
+    // next call, writes them: without this a thread still testing the loop condition sees the next batch's flag
+    __syncthreads();
+  }
+}
+
 // open-addressing f64 accumulators keyed by u32 (EMPTY = 0xFFFFFFFF); returns false when full
 template <int NSLOT>
 __device__ __forceinline__ bool tbl_add(uint32_t* keys, double* vals, uint32_t key, double v) {
@@ -623,14 +764,19 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   uint32_t* par = reinterpret_cast<uint32_t*>(vals) + CAPC;             // rank order
   // CLIP (the hot-spot clip): the radix select's histogram and scalars, each window's threshold, positive count and
   // smallest / largest value bits, in the level region (free until the levels, which come after the tail)
-  static_assert(CAPC >= 2048 + 16 + 8 + MAXK * 28, "clip scratch fits the level region");
-  uint32_t* c_hist = reinterpret_cast<uint32_t*>(Lv);  // 2 x 256 bins
-  int* c_sh = reinterpret_cast<int*>(Lv + 2048);
-  unsigned long long* c_dsh = reinterpret_cast<unsigned long long*>(Lv + 2064);
-  double* c_thr = reinterpret_cast<double*>(Lv + 2072);
-  unsigned long long* c_lo = reinterpret_cast<unsigned long long*>(Lv + 2072 + MAXK * 8);
-  unsigned long long* c_hi = reinterpret_cast<unsigned long long*>(Lv + 2072 + MAXK * 16);
-  int* c_n = reinterpret_cast<int*>(Lv + 2072 + MAXK * 24);
+  // (the level region and the duplicate lists behind it, which the clip does not use)
+  constexpr int CSB = 4;  // tail windows per select batch
+  static_assert(LY::o_tkey - LY::o_L >= 4336 + 24 + MAXK * 28 && CSB * sizeof(SelSet) <= 224,
+                "clip scratch fits the level and duplicate-list regions");
+  uint32_t* c_hist = reinterpret_cast<uint32_t*>(Lv);  // CSB x 256 bins (the principal's select: 2 x 256)
+  SelSet* c_st = reinterpret_cast<SelSet*>(Lv + 4096);
+  int* c_flag = reinterpret_cast<int*>(Lv + 4320);
+  int* c_sh = reinterpret_cast<int*>(Lv + 4336);
+  unsigned long long* c_dsh = reinterpret_cast<unsigned long long*>(Lv + 4352);
+  double* c_thr = reinterpret_cast<double*>(Lv + 4360);
+  unsigned long long* c_lo = reinterpret_cast<unsigned long long*>(Lv + 4360 + MAXK * 8);
+  unsigned long long* c_hi = reinterpret_cast<unsigned long long*>(Lv + 4360 + MAXK * 16);
+  int* c_n = reinterpret_cast<int*>(Lv + 4360 + MAXK * 24);
 
   // two-level pixel set (TWO): compact words W = Hbm as u64, their rank prefix B, top-level bitmap T
   const uint64_t* W64 = reinterpret_cast<const uint64_t*>(Hbm);
@@ -1088,27 +1234,18 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
             }
           }
           __syncthreads();
-          // 2.
-          for (int k = 1; k < K; ++k) {
-            const int nk = c_n[k];
-            double thr = INFINITY;
-            if (nk > 0) {
-              const int g0 = gsv[k], g1 = (k + 1 < MAXK && gsv[k + 1] < ng) ? gsv[k + 1] : ng;
-              thr = percentile_of<BLOCK>(
-                  [&](auto&& f) {
-                    groups(g0, g1, [&](int, bool valid, const Reg& h) {
-                      if (valid && !Hits<FMT>::dup(h) && Hits<FMT>::val(h) > 0.0) f(bits_of(Hits<FMT>::val(h)));
-                    });
-                    for (int i = tid; i < DTBL; i += BLOCK) {
-                      const uint32_t key = tkey[i];
-                      if (key != 0xFFFFFFFFu && (int)(key & 7u) == k && tval[i] > 0.0) f(bits_of(tval[i]));
-                    }
-                  },
-                  nk, P.q, c_hist, c_sh, c_dsh, c_lo[k], c_hi[k]);
-            }
-            if (tid == 0) c_thr[k] = thr;
-          }
-          __syncthreads();
+          // 2. (set s = window s + 1; every round reads the whole tail once for the batch's windows)
+          select_batch<BLOCK, CSB>(
+              [&](auto&& f) {
+                groups(0, ng, [&](int k, bool valid, const Reg& h) {
+                  if (valid && !Hits<FMT>::dup(h) && Hits<FMT>::val(h) > 0.0) f(k - 1, bits_of(Hits<FMT>::val(h)));
+                });
+                for (int i = tid; i < DTBL; i += BLOCK) {
+                  const uint32_t key = tkey[i];
+                  if (key != 0xFFFFFFFFu && tval[i] > 0.0) f((int)(key & 7u) - 1, bits_of(tval[i]));
+                }
+              },
+              K - 1, c_n + 1, P.q, c_thr + 1, c_st, c_hist, c_flag, c_lo + 1, c_hi + 1);
           // 3. (a wave's partials of window k: part[k][wid], written by this wave only)
           groups(0, ng, [&](int k, bool valid, const Reg& h) {
             double a4[4] = {0.0, 0.0, 0.0, 0.0};
@@ -2770,7 +2907,7 @@ template <int FMT>
 __device__ void wide_clip_tail(const Hits<FMT>& hits, int K, double q, int npx, const RankBits& R, const WideSlot& S,
                                const int64_t* sh_tb, const int64_t* sh_tlo, const int64_t* sh_tn, uint32_t* ltkey,
                                double* ltval, double* kst, int* sh_nown, int* sh_ctr, uint32_t* c_hist, int* c_sh,
-                               unsigned long long* c_dsh, double* c_thr, int* c_n) {
+                               unsigned long long* c_dsh, double* c_thr, int* c_n, SelSet* c_st, int* c_flag) {
   using H = Hits<FMT>;
   const int tid = threadIdx.x, lane = tid & 63;
   constexpr int U = FMT == SMG_HITS_PACKED_F32 ? TDU : WDU;
@@ -2871,36 +3008,29 @@ __device__ void wide_clip_tail(const Hits<FMT>& hits, int K, double q, int npx, 
   }
   __syncthreads();
 
-  // 2. thresholds
-  for (int k = 1; k < K; ++k) {
-    const int nk = c_n[k];
-    double thr = INFINITY;
-    if (nk > 0 && !sh_ctr[3]) {
-      const int64_t a = sh_tlo[k - 1], n = sh_tn[k - 1];
-      const uint32_t kk = (uint32_t)(k - 1);
-      thr = percentile_of<DBLOCK>(
-          [&](auto&& f) {
-            for (int64_t i = tid; i < n; i += DBLOCK) {
-              const typename H::Reg h = hits.load(a + i);
-              if (!H::dup(h) && H::val(h) > 0.0) f(bits_of((double)H::val(h)));
-            }
-            for (int i = tid; i < WIDE_LT; i += DBLOCK) {
-              const uint32_t key = ltkey[i];
-              if (key != WIDE_EMPTY && key / (uint32_t)npx == kk && ltval[i] > 0.0) f(bits_of(ltval[i]));
-            }
-            for (int j = tid; j < no; j += DBLOCK) {
-              const uint32_t sl = S.hown[j];
-              if (ld_agent(&S.hkey[sl]) / (uint32_t)npx == kk) {
-                const double y = ld_agent(&S.hval[sl]);
-                if (y > 0.0) f(bits_of(y));
-              }
-            }
-          },
-          nk, q, c_hist, c_sh, c_dsh);
-    }
-    if (tid == 0) c_thr[k] = thr;
+  // 2. thresholds: every window's radix select, four windows per batch advancing together (each round reads the
+  // whole tail once); set s = window s + 1
+  if (!sh_ctr[3]) {
+    select_batch<DBLOCK, 4>(
+        [&](auto&& f) {
+          stream([&](int kb, int64_t off, int64_t n, const typename H::Reg (&r)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+              if (off + (int64_t)u * DBLOCK + tid < n && !H::dup(r[u]) && H::val(r[u]) > 0.0)
+                f(kb, bits_of((double)H::val(r[u])));
+          });
+          for (int i = tid; i < WIDE_LT; i += DBLOCK) {
+            const uint32_t key = ltkey[i];
+            if (key != WIDE_EMPTY && ltval[i] > 0.0) f((int)(key / (uint32_t)npx), bits_of(ltval[i]));
+          }
+          for (int j = tid; j < no; j += DBLOCK) {
+            const uint32_t sl = S.hown[j];
+            const double y = ld_agent(&S.hval[sl]);
+            if (y > 0.0) f((int)(ld_agent(&S.hkey[sl]) / (uint32_t)npx), bits_of(y));
+          }
+        },
+        K - 1, c_n + 1, q, c_thr + 1, c_st, c_hist, c_flag);
   }
-  __syncthreads();
 
   // 3. the clipped unflagged points
   {
@@ -2991,7 +3121,9 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
   __shared__ int64_t sh_tlo[MAXK_DENSE];     // first point of window k at k - 1
   __shared__ int64_t sh_tn[MAXK_DENSE];      // length of window k at k - 1
   // CLIP (do_preprocessing): the radix select's histogram and scalars, each window's threshold and positive count
-  __shared__ __attribute__((aligned(16))) uint32_t c_hist[CLIP ? 512 : 4];
+  __shared__ __attribute__((aligned(16))) uint32_t c_hist[CLIP ? 1024 : 4];
+  __shared__ SelSet c_st[CLIP ? 4 : 1];
+  __shared__ int c_flag[2];
   __shared__ int c_sh[4];
   __shared__ unsigned long long c_dsh;
   __shared__ double c_thr[CLIP ? MAXK_DENSE : 1];
@@ -3176,8 +3308,11 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
       const int n0 = (int)acc[3];
       if (n0 > 0) {
         // the smallest and largest positive value's bits bound the select's passes
+#ifndef SMG_CLIP_PLOHI  // 1: bound the principal's select by its value range (an extra pass; slower, r4clipab)
+#define SMG_CLIP_PLOHI 0
+#endif
         uint64_t plo = ~0ull, phi = 0ull;
-        for (int r = tid; r < np; r += DBLOCK) {
+        for (int r = SMG_CLIP_PLOHI ? tid : np; r < np; r += DBLOCK) {
           const double v = ld_agent(&S.vals[r]);
           if (v > 0.0) {
             const uint64_t b = (uint64_t)__double_as_longlong(v);
@@ -3202,7 +3337,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
                 if (v > 0.0) f((uint64_t)__double_as_longlong(v));
               }
             },
-            n0, P.q, c_hist, c_sh, &c_dsh, c_lo[0], c_hi[0]);
+            n0, P.q, c_hist, c_sh, &c_dsh, SMG_CLIP_PLOHI ? c_lo[0] : 0ull, SMG_CLIP_PLOHI ? c_hi[0] : ~0ull);
         acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
         mx = -INFINITY;
         for (int r = tid; r < np; r += DBLOCK) {
@@ -3266,7 +3401,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     }
     if constexpr (CLIP) {
       wide_clip_tail<FMT>(hits, K, P.q, npx, R, S, sh_tb, sh_tlo, sh_tn, ltkey, ltval, kst, &sh_nown, sh_ctr, c_hist, c_sh,
-                          &c_dsh, c_thr, c_n);
+                          &c_dsh, c_thr, c_n, c_st, c_flag);
     } else {
       const int64_t T = sh_tb[K - 1];
       double as = 0.0, axy = 0.0;  // the lane's Σy[x > 0], Σxy in window kacc
@@ -3774,7 +3909,7 @@ __global__ void list_all_kernel(uint32_t* list, uint32_t* count, const int64_t* 
 static constexpr int DENSE_SLOTS = SMG_DENSE_SLOTS;  // dense-path workgroups (one scratch slot each)
 static constexpr size_t DENSE_BM_LDS_MAX = 152 * 1024;  // dense kernel: LDS presence bitmap up to this size
 static constexpr size_t WIDE_LDS_MAX = 160 * 1024 - 4096;  // wide pass: dynamic LDS (static arrays ~2.9 KB)
-static constexpr size_t WIDE_LDS_MAX_CLIP = 160 * 1024 - 6144;  // its CLIP instantiation (static arrays ~4.9 KB)
+static constexpr size_t WIDE_LDS_MAX_CLIP = 160 * 1024 - 8192;  // its CLIP instantiation (static arrays ~7.7 KB)
 // workspace: header (pass counters at word 0.., per-XCD range counters at word 64..), two ion lists,
 // the ion descriptors, dense scratch slots
 static constexpr size_t WS_HEADER = 2048;

@@ -332,7 +332,10 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
   const uint32_t lstart = (uint32_t)block_excl_scan<int64_t>((int64_t)cnt, s_red);
   if (d < nb) {
     int64_t excl = 0;
-    if (t > 0) {
+#ifndef SMG_SRT_NOLB
+#define SMG_SRT_NOLB 0  // diagnostic (timing only, wrong order): no look-back; every tile writes from its bin's start
+#endif
+    if (t > 0 && !SMG_SRT_NOLB) {
       // SMG_SRT_LB earlier tiles' words loaded together per round trip, consumed newest first until an inclusive
       // prefix; a word not yet published ends the round (the ones before it are kept, the walk resumes there)
       for (int64_t j = t - 1;;) {
