@@ -39,7 +39,9 @@ def two_calls():
 out = {}
 for name, impl, fn in [("flag pass + rocPRIM sort", 0, two_calls), ("flag pass + hand-written sort", 1, two_calls),
                        ("rocPRIM sort alone", 0, peaks.sort), ("hand-written sort alone", 1, peaks.sort),
-                       ("fused flag_and_sort", 1, lambda: peaks.flag_and_sort(2.0))]:
+                       ("fused flag_and_sort", 1, lambda: peaks.flag_and_sort(2.0)),
+                       ("hand-written look-back sort alone", 2, peaks.sort),
+                       ("fused flag_and_sort, look-back", 2, lambda: peaks.flag_and_sort(2.0))]:
     lib().smg_debug_sort_impl(impl)
     lo, med = timed(fn)
     if "alone" not in name:

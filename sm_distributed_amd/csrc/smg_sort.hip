@@ -232,6 +232,93 @@ __global__ void __launch_bounds__(256) sort_mark_starts_kernel(const int64_t* __
   }
 }
 
+// Reduce-then-scan offsets of one pass (no look-back chain: each tile's global offsets are known before its
+// scatter).  sort_count_kernel: every tile's digit counts, tile-major (counts[t][d], coalesced); sort_chunk_sum_kernel:
+// per chunk of SRT_CT tiles, each digit's total; sort_chunk_scan_kernel: per digit, the exclusive prefix over the chunks
+// from the digit's base; sort_tile_offsets_kernel: per chunk, each tile's offsets (in place of its counts).  The
+// scan reads ~2 x 4 B per tile and digit; the count pass re-reads the keys (4 B per point).
+constexpr int SRT_CT = 64;  // tiles per chunk of the offsets scan
+template <typename S>
+__global__ void __launch_bounds__(SRT_T) sort_count_kernel(const uint32_t* __restrict__ kin, int64_t n, int shift,
+                                                           int dbits, S* __restrict__ counts) {
+  static_assert(SRT_T == SRT_BINS && SRT_IPT % 4 == 0, "a thread per digit; keys in 16-byte loads");
+  __shared__ uint32_t h[SRT_BINS];
+  const int tid = threadIdx.x;
+  h[tid] = 0u;
+  __syncthreads();
+  const int64_t t = blockIdx.x, base = t * SRT_TILE;
+  const uint32_t mask = (1u << dbits) - 1u;
+  if (base + SRT_TILE <= n && (reinterpret_cast<uintptr_t>(kin) & 15) == 0) {
+    const uint4* k4 = reinterpret_cast<const uint4*>(kin + base);
+    uint4 q[SRT_IPT / 4];
+#pragma unroll
+    for (int u = 0; u < SRT_IPT / 4; ++u) q[u] = k4[u * SRT_T + tid];
+#pragma unroll
+    for (int u = 0; u < SRT_IPT / 4; ++u) {
+      atomicAdd(&h[(q[u].x >> shift) & mask], 1u);
+      atomicAdd(&h[(q[u].y >> shift) & mask], 1u);
+      atomicAdd(&h[(q[u].z >> shift) & mask], 1u);
+      atomicAdd(&h[(q[u].w >> shift) & mask], 1u);
+    }
+  } else {
+    for (int64_t i = base + tid; i < n && i < base + SRT_TILE; i += SRT_T) atomicAdd(&h[(kin[i] >> shift) & mask], 1u);
+  }
+  __syncthreads();
+  counts[t * SRT_BINS + tid] = (S)h[tid];
+}
+template <typename S>
+__global__ void __launch_bounds__(SRT_BINS) sort_chunk_sum_kernel(const S* __restrict__ counts, int64_t ntiles,
+                                                                  S* __restrict__ ctot) {
+  const int d = threadIdx.x;
+  const int64_t c = blockIdx.x, t0 = c * SRT_CT, t1 = t0 + SRT_CT < ntiles ? t0 + SRT_CT : ntiles;
+  S s = 0;
+  for (int64_t t = t0; t < t1; ++t) s += counts[t * SRT_BINS + d];
+  ctot[c * SRT_BINS + d] = s;
+}
+// one workgroup per digit: the exclusive prefix of its chunk totals (1024 chunks per round, a carried base)
+constexpr int SRT_SCAN_T = 1024;
+template <typename S>
+__global__ void __launch_bounds__(SRT_SCAN_T) sort_chunk_scan_kernel(S* __restrict__ ctot, int64_t nchunks,
+                                                                     const int64_t* __restrict__ binbase) {
+  __shared__ S wsum[SRT_SCAN_T / 64];
+  const int d = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  S run = (S)binbase[d];
+  for (int64_t c0 = 0; c0 < nchunks; c0 += SRT_SCAN_T) {
+    const int64_t c = c0 + tid;
+    const S x = c < nchunks ? ctot[c * SRT_BINS + d] : (S)0;
+    S inc = x;  // inclusive prefix within the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const S y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    S before = run, total = 0;
+#pragma unroll
+    for (int i = 0; i < SRT_SCAN_T / 64; ++i) {
+      const S t = wsum[i];
+      before += i < w ? t : (S)0;
+      total += t;
+    }
+    if (c < nchunks) ctot[c * SRT_BINS + d] = before + inc - x;
+    run += total;
+    __syncthreads();
+  }
+}
+template <typename S>
+__global__ void __launch_bounds__(SRT_BINS) sort_tile_offsets_kernel(S* __restrict__ counts, int64_t ntiles,
+                                                                     const S* __restrict__ ctot) {
+  const int d = threadIdx.x;
+  const int64_t c = blockIdx.x, t0 = c * SRT_CT, t1 = t0 + SRT_CT < ntiles ? t0 + SRT_CT : ntiles;
+  S run = ctot[c * SRT_BINS + d];
+  for (int64_t t = t0; t < t1; ++t) {
+    const S x = counts[t * SRT_BINS + d];
+    counts[t * SRT_BINS + d] = run;
+    run += x;
+  }
+}
+
 // One LSD pass over digit bits [shift, shift + dbits).  FLAG: the first pass, which also sets the duplicate-
 // candidate flag (bit 31 of the hit) from the dataset-order neighbours.
 // Values go through LDS whole (8-byte words) when a tile's values fit the 64 KB exchange buffer, else as two
@@ -244,7 +331,8 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
                                                                     int dbits, const int64_t* __restrict__ binbase,
                                                                     S* __restrict__ status,
                                                                     unsigned* __restrict__ ticket,
-                                                                    const uint32_t* __restrict__ flagbits) {
+                                                                    const uint32_t* __restrict__ flagbits,
+                                                                    const S* __restrict__ offsets) {
   constexpr bool SPLIT = SRT_TILE * 8 > 65536;
   constexpr int XWORDS = 65536 / 8;
   // exchange buffer: the wave histograms (u16 [SRT_WAVES][SRT_BINS]) while ranking, then the tile's keys in digit
@@ -261,9 +349,19 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
   uint16_t* wh = reinterpret_cast<uint16_t*>(xbuf);
   uint32_t* xk = reinterpret_cast<uint32_t*>(xbuf);
   reinterpret_cast<uint4*>(xbuf)[tid] = make_uint4(0u, 0u, 0u, 0u);  // 512 x 16 B: the 8 KB of wave histograms
-  if (tid == 0) s_tile = atomicAdd(ticket, 1u);
+  // with the tiles' offsets given (reduce-then-scan) a tile is its block; else tiles go in ticket order (look-back)
+  if (tid == 0 && offsets == nullptr) s_tile = atomicAdd(ticket, 1u);
   __syncthreads();
-  const int64_t t = s_tile;
+  // reduce-then-scan: blocks go to the XCDs in turn (block b on XCD b % 8), so XCD x takes a contiguous run of tiles;
+  // its scattered runs into each digit's range then abut in its own L2 (consecutive tiles' pieces of one line merge
+  // there instead of reaching HBM as partial lines from two XCDs)
+  int64_t t;
+  if (offsets != nullptr) {
+    const int64_t nt = gridDim.x, b = blockIdx.x, x = b % 8, q = nt / 8, r = nt % 8;
+    t = x * q + (x < r ? x : r) + b / 8;
+  } else {
+    t = s_tile;
+  }
   const int64_t base = t * SRT_TILE;
   const int64_t wbase = base + (int64_t)w * (64 * SRT_IPT);  // a wave's points: SRT_IPT rows of 64 consecutive
   const uint32_t mask = (1u << dbits) - 1u;
@@ -327,7 +425,7 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
       wh[ww * SRT_BINS + d] = (uint16_t)cnt;
       cnt += c;
     }
-    status_store(status + t * SRT_BINS + d, (S)((t == 0 ? (S)2 : (S)1) << SH) | (S)cnt);
+    if (offsets == nullptr) status_store(status + t * SRT_BINS + d, (S)((t == 0 ? (S)2 : (S)1) << SH) | (S)cnt);
   }
   const uint32_t lstart = (uint32_t)block_excl_scan<int64_t>((int64_t)cnt, s_red);
   if (d < nb) {
@@ -335,7 +433,9 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
 #ifndef SMG_SRT_NOLB
 #define SMG_SRT_NOLB 0  // diagnostic (timing only, wrong order): no look-back; every tile writes from its bin's start
 #endif
-    if (t > 0 && !SMG_SRT_NOLB) {
+    if (offsets != nullptr) {
+      excl = (int64_t)offsets[t * SRT_BINS + d] - binbase[d];  // (the offsets include the bin base)
+    } else if (t > 0 && !SMG_SRT_NOLB) {
       // SMG_SRT_LB earlier tiles' words loaded together per round trip, consumed newest first until an inclusive
       // prefix; a word not yet published ends the round (the ones before it are kept, the walk resumes there)
       for (int64_t j = t - 1;;) {
@@ -455,7 +555,7 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
 // ---- host side ---------------------------------------------------------------------------------------------
 struct SortPlan {
   int passes, dbits;
-  int64_t ntiles;
+  int64_t ntiles, nchunks;
   bool wide;  // 64-bit look-back words
   size_t off_hist, off_base, off_status, status_bytes, off_s0, start_bytes, off_fl, off_tk, off_tv, total;
 };
@@ -477,6 +577,10 @@ static SortPlan sort_plan(int64_t n, int key_bits) {
   // two look-back regions, used by alternate passes: the region of pass p >= 2 is zeroed again after pass p - 2
   // (the workspace does not grow with the number of passes: ~2 B per point at 64-bit words)
   p.status_bytes = (size_t)(p.passes < 2 ? p.passes : 2) * (size_t)p.ntiles * SRT_BINS * sw;
+  // reduce-then-scan (the default): the tiles' counts / offsets and the chunk totals in the same space
+  p.nchunks = (p.ntiles + SRT_CT - 1) / SRT_CT;
+  const size_t rts = (size_t)(p.ntiles + p.nchunks) * SRT_BINS * sw;
+  if (p.status_bytes < rts) p.status_bytes = rts;
   p.off_s0 = align_up(p.off_status + p.status_bytes, 256);  // FLAG pass: spectrum-start bits
   p.start_bytes = (size_t)((n + 31) / 32 + 2) * 4;
   p.off_fl = align_up(p.off_s0 + p.start_bytes, 256);  // FLAG pass: the flag bits (the same size)
@@ -486,7 +590,9 @@ static SortPlan sort_plan(int64_t n, int key_bits) {
   return p;
 }
 
-// 0 = rocPRIM onesweep (A/B reference), 1 = the hand-written sort (default)
+// 0 = rocPRIM onesweep (A/B reference), 1 = the hand-written sort with reduce-then-scan tile offsets and XCD-contiguous
+// tiles (default; 9.85 ms at config 3), 2 = the same with decoupled look-back in ticket order (round 3; 11.15 ms,
+// profiles/round4/r4sort3_*)
 static int g_sort_impl = 1;
 
 #ifndef SMG_SORT_RADIX_BITS
@@ -540,19 +646,37 @@ static int run_passes(const SortPlan& P, const uint32_t* mz, const uint64_t* hit
   uint64_t* tv = reinterpret_cast<uint64_t*>(ws + P.off_tv);
   const uint32_t* ki = mz;
   const uint64_t* vi = hits;
+  const bool rts = g_sort_impl != 2;
+  S* counts = status;                                   // reduce-then-scan: [ntiles][bins] counts, then offsets
+  S* ctot = status + (size_t)P.ntiles * SRT_BINS;       // [nchunks][bins] chunk totals, then chunk offsets
   for (int p = 0; p < P.passes; ++p) {
     // the last pass writes the caller's arrays, the ones before alternate with the workspace copy
     const bool to_out = ((P.passes - 1 - p) & 1) == 0;
     uint32_t* kdst = to_out ? ko : tk;
     uint64_t* vdst = to_out ? vo : tv;
     S* sp = status + (size_t)(p & 1) * region;
-    if (p >= 2) SMG_HIP(hipMemsetAsync(sp, 0, region * sizeof(S), st));  // pass p - 2's words
+    const S* offs = nullptr;
+    if (rts) {
+      const int64_t* bb = binbase + p * SRT_BINS;
+      hipLaunchKernelGGL(sort_count_kernel<S>, dim3((unsigned)P.ntiles), dim3(SRT_T), 0, st, ki, n, p * P.dbits,
+                         P.dbits, counts);
+      hipLaunchKernelGGL(sort_chunk_sum_kernel<S>, dim3((unsigned)P.nchunks), dim3(SRT_BINS), 0, st, counts,
+                         P.ntiles, ctot);
+      hipLaunchKernelGGL(sort_chunk_scan_kernel<S>, dim3((unsigned)(1 << P.dbits)), dim3(SRT_SCAN_T), 0, st, ctot,
+                         P.nchunks, bb);
+      hipLaunchKernelGGL(sort_tile_offsets_kernel<S>, dim3((unsigned)P.nchunks), dim3(SRT_BINS), 0, st, counts,
+                         P.ntiles, ctot);
+      SMG_LAUNCH_CHECK();
+      offs = counts;
+    } else if (p >= 2) {
+      SMG_HIP(hipMemsetAsync(sp, 0, region * sizeof(S), st));  // pass p - 2's look-back words
+    }
     if (flag && p == 0)
       hipLaunchKernelGGL((sort_pass_kernel<S, true>), dim3((unsigned)P.ntiles), dim3(SRT_T), 0, st, ki, vi, kdst,
-                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, flagbits);
+                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, flagbits, offs);
     else
       hipLaunchKernelGGL((sort_pass_kernel<S, false>), dim3((unsigned)P.ntiles), dim3(SRT_T), 0, st, ki, vi, kdst,
-                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, nullptr);
+                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, nullptr, offs);
     SMG_LAUNCH_CHECK();
     ki = kdst;
     vi = vdst;
@@ -667,7 +791,7 @@ int smg_sort_points_flag(const int64_t* sp_off, int64_t n_spectra, const float* 
 }
 
 int smg_debug_sort_impl(int32_t which) {
-  SMG_CHECK_ARG(which == 0 || which == 1, "which: 0 = rocPRIM, 1 = hand-written");
+  SMG_CHECK_ARG(which >= 0 && which <= 2, "which: 0 = rocPRIM, 1 = hand-written (reduce-then-scan), 2 = hand-written (look-back)");
   g_sort_impl = which;
   return SMG_OK;
 }

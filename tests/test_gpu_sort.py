@@ -3,9 +3,11 @@
 The reference sorts each segment's peaks by m/z (formula_imager_segm.py:73-74); only the set of points per
 window matters downstream, but the sort here is stable, so its output is one exact array:
 * smg_sort_points == the points permuted by a stable argsort of the m/z values (torch.sort(stable=True)), at
-  sizes around the 8192-point tile, with heavy ties, over 1 to 4 radix passes and with the 64-bit look-back words
+  sizes around the 8192-point tile, with heavy ties, over 1 to 4 radix passes and with 64-bit tile offsets
   (more than 2^30 points);
-* the same arrays as rocPRIM's onesweep sort (smg_debug_sort_impl(0)) on a synthetic dataset;
+* the same arrays as rocPRIM's onesweep sort (smg_debug_sort_impl(0)) on a synthetic dataset, and as the
+  hand-written sort's round-3 form, whose tiles find their offsets by decoupled look-back in ticket order
+  (smg_debug_sort_impl(2)) instead of the reduce-then-scan offsets;
 * smg_sort_points_flag == smg_flag_duplicates followed by smg_sort_points, bit for bit, on synthetic datasets and
   on the parity cases; datasets it does not cover (a spectrum not m/z-sorted, a shared pixel) take the two calls.
 """
@@ -64,7 +66,7 @@ def test_sort_any_number_of_passes(lo, hi, bits):
 
 
 def test_sort_more_than_2p30_points_wide_lookback():
-    """n >= 2^30 takes the 64-bit look-back words."""
+    """n >= 2^30 takes 64-bit tile offsets (reduce-then-scan counts and chunk totals)."""
     import torch
     n = (1 << 30) + 12345
     mz, hits = _random_points(n, seed=11, ties=True)
@@ -99,6 +101,23 @@ def test_native_sort_identical_to_rocprim():
     a = (p.mz_sorted.clone(), p.hits_sorted.clone())
     try:
         assert lib().smg_debug_sort_impl(0) == 0
+        p.sort()
+        torch.cuda.synchronize()
+    finally:
+        lib().smg_debug_sort_impl(1)
+    assert torch.equal(a[0], p.mz_sorted) and torch.equal(a[1], p.hits_sorted)
+
+
+@pytest.mark.parametrize("n", [8193, 1_000_003])
+def test_reduce_then_scan_identical_to_lookback(n):
+    import torch
+    from sm_distributed_amd._lib import lib
+    mz, hits = _random_points(n, seed=n, ties=True)
+    p = _peaks(mz, hits).sort()
+    torch.cuda.synchronize()
+    a = (p.mz_sorted.clone(), p.hits_sorted.clone())
+    try:
+        assert lib().smg_debug_sort_impl(2) == 0
         p.sort()
         torch.cuda.synchronize()
     finally:
