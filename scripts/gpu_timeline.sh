@@ -11,7 +11,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --hip-runtime-trace --output-format c
   python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --chain-steps 0 > gpurun_out/$TAG/api.log 2>&1 \
   || { tail -20 gpurun_out/$TAG/api.log; exit 1; }
 K=$(find /tmp/tl_api -name "*kernel_trace.csv" | head -1); H=$(find /tmp/tl_api -name "*hip_api_trace.csv" | head -1)
-python3 scripts/timeline_gaps.py $K $H > gpurun_out/$TAG/api_timeline.txt || exit 1
+python3 scripts/timeline_gaps.py $K $H --start ${START:-sort_mark_starts_kernel} > gpurun_out/$TAG/api_timeline.txt || exit 1
 if [ "${SHARD:-1}" = "1" ]; then
   ONLY_RANK=3 timeout -k 10 400 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d /tmp/tl_shard -o run -- \
     python3 scripts/time_shards.py 8 > gpurun_out/$TAG/shard.log 2>&1 || { tail -20 gpurun_out/$TAG/shard.log; exit 1; }

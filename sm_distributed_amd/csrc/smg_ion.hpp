@@ -261,15 +261,29 @@ struct Sched {
   const uint32_t* count;  // SRC_LIST
 };
 
+// The XCD this workgroup runs on (HW_REG_XCC_ID, 0-7).  Blocks are observed to be dealt round-robin over the XCDs,
+// but which XCD a block lands on is not fixed, and with other work resident (a copy kernel on another stream) the
+// deal can skip an XCD, so blockIdx % 8 no longer groups the blocks of one XCD; the register is exact.  Speed only:
+// any range may be scored by any workgroup.
+__device__ __forceinline__ int home_xcd() {
+  if constexpr (XCDS == 1) {
+    return 0;
+  } else {
+    int x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    return x % XCDS;
+  }
+}
+
 template <int SRC>
 __device__ __forceinline__ uint32_t sched_issue(const Sched& S) {
-  if constexpr (SRC == SRC_RANGES) return atomicAdd(&S.ctr[(blockIdx.x % XCDS) * CTR_STRIDE], 1u);
+  if constexpr (SRC == SRC_RANGES) return atomicAdd(&S.ctr[home_xcd() * CTR_STRIDE], 1u);
   else return atomicAdd(S.ctr, 1u);
 }
 // the same ticket, asynchronously (see atomic_add_rtn_async); valid after the counted wait
 template <int SRC>
 __device__ __forceinline__ void sched_issue_async(const Sched& S, uint32_t& t) {
-  if constexpr (SRC == SRC_RANGES) atomic_add_rtn_async(t, &S.ctr[(blockIdx.x % XCDS) * CTR_STRIDE], 1u);
+  if constexpr (SRC == SRC_RANGES) atomic_add_rtn_async(t, &S.ctr[home_xcd() * CTR_STRIDE], 1u);
   else atomic_add_rtn_async(t, S.ctr, 1u);
 }
 
@@ -277,7 +291,7 @@ __device__ __forceinline__ void sched_issue_async(const Sched& S, uint32_t& t) {
 template <int SRC>
 __device__ __forceinline__ int64_t sched_resolve(const Sched& S, uint32_t t) {
   if constexpr (SRC == SRC_RANGES) {
-    const int home = blockIdx.x % XCDS;
+    const int home = home_xcd();
     for (int i = 0; i < XCDS; ++i) {
       const int x = (home + i) % XCDS;
       const int64_t a = S.n * x / XCDS, b = S.n * (x + 1) / XCDS;

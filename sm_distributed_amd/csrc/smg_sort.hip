@@ -222,6 +222,14 @@ __global__ void __launch_bounds__(SRT_BINS) sort_scan_kernel(const unsigned long
   binbase[p * SRT_BINS + d] = block_excl_scan<int64_t>((int64_t)hist[p * SRT_BINS + d], red);
 }
 
+// the digits' bases of one pass from their totals (reduce-then-scan: no histogram pass)
+__global__ void __launch_bounds__(SRT_BINS) sort_digit_base_kernel(const int64_t* __restrict__ total,
+                                                                   int64_t* __restrict__ binbase) {
+  __shared__ int64_t red[SRT_WAVES];
+  const int d = threadIdx.x;
+  binbase[d] = block_excl_scan<int64_t>(total[d], red);
+}
+
 // FLAG pass: one bit per point position marking the first point of a spectrum (sp_off; an empty spectrum marks
 // its successor's start, which that one marks anyway)
 __global__ void __launch_bounds__(256) sort_mark_starts_kernel(const int64_t* __restrict__ sp_off, int64_t n_spectra,
@@ -238,16 +246,22 @@ __global__ void __launch_bounds__(256) sort_mark_starts_kernel(const int64_t* __
 // from the digit's base; sort_tile_offsets_kernel: per chunk, each tile's offsets (in place of its counts).  The
 // scan reads ~2 x 4 B per tile and digit; the count pass re-reads the keys (4 B per point).
 constexpr int SRT_CT = 64;  // tiles per chunk of the offsets scan
+// With flags != nullptr (the first pass of flag_and_sort) it also writes the duplicate-candidate flag of every point
+// of the tile (one bit per dataset position; spectrum starts in starts[]), the rule of dup_flag: the keys are read
+// in dataset order here, a quad per lane, the neighbours of a quad's ends from the adjacent lanes (or memory).
 template <typename S>
 __global__ void __launch_bounds__(SRT_T) sort_count_kernel(const uint32_t* __restrict__ kin, int64_t n, int shift,
-                                                           int dbits, S* __restrict__ counts) {
+                                                           int dbits, S* __restrict__ counts,
+                                                           const uint32_t* __restrict__ starts,
+                                                           uint32_t* __restrict__ flags, double slack) {
   static_assert(SRT_T == SRT_BINS && SRT_IPT % 4 == 0, "a thread per digit; keys in 16-byte loads");
   __shared__ uint32_t h[SRT_BINS];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
   h[tid] = 0u;
   __syncthreads();
   const int64_t t = blockIdx.x, base = t * SRT_TILE;
   const uint32_t mask = (1u << dbits) - 1u;
+  auto start = [&](int64_t i) -> uint32_t { return i < n ? (starts[i >> 5] >> (i & 31)) & 1u : 0u; };
   if (base + SRT_TILE <= n && (reinterpret_cast<uintptr_t>(kin) & 15) == 0) {
     const uint4* k4 = reinterpret_cast<const uint4*>(kin + base);
     uint4 q[SRT_IPT / 4];
@@ -260,8 +274,35 @@ __global__ void __launch_bounds__(SRT_T) sort_count_kernel(const uint32_t* __res
       atomicAdd(&h[(q[u].z >> shift) & mask], 1u);
       atomicAdd(&h[(q[u].w >> shift) & mask], 1u);
     }
+    if (flags != nullptr) {
+#pragma unroll
+      for (int u = 0; u < SRT_IPT / 4; ++u) {
+        const int64_t i = base + (int64_t)(u * SRT_T + tid) * 4;  // 32-point aligned per 8 lanes (base % 32 == 0)
+        uint32_t kp = __shfl_up(q[u].w, 1, 64), kn = __shfl_down(q[u].x, 1, 64);
+        if (lane == 0) kp = i > 0 ? kin[i - 1] : 0u;
+        if (lane == 63) kn = i + 4 < n ? kin[i + 4] : 0u;
+        const uint32_t sw = starts[i >> 5];
+        auto st = [&](int j) { return (sw >> ((i + j) & 31)) & 1u; };  // j < 4: the quad's word
+        const uint32_t st4 = ((i + 4) & 31) ? st(4) : start(i + 4);
+        const uint32_t nib = (uint32_t)dup_flag(i, n, q[u].x, kp, q[u].y, st(0), st(1), slack) |
+                             ((uint32_t)dup_flag(i + 1, n, q[u].y, q[u].x, q[u].z, st(1), st(2), slack) << 1) |
+                             ((uint32_t)dup_flag(i + 2, n, q[u].z, q[u].y, q[u].w, st(2), st(3), slack) << 2) |
+                             ((uint32_t)dup_flag(i + 3, n, q[u].w, q[u].z, kn, st(3), st4, slack) << 3);
+        uint32_t word = nib;
+#pragma unroll
+        for (int j = 1; j < 8; ++j) word |= __shfl_down(nib, j, 8) << (4 * j);
+        if ((lane & 7) == 0) flags[i >> 5] = word;
+      }
+    }
   } else {
-    for (int64_t i = base + tid; i < n && i < base + SRT_TILE; i += SRT_T) atomicAdd(&h[(kin[i] >> shift) & mask], 1u);
+    for (int64_t i = base + tid; i < n && i < base + SRT_TILE; i += SRT_T) {
+      const uint32_t k = kin[i];
+      atomicAdd(&h[(k >> shift) & mask], 1u);
+      if (flags != nullptr) {
+        const uint32_t kp = i > 0 ? kin[i - 1] : 0u, kn = i + 1 < n ? kin[i + 1] : 0u;
+        if (dup_flag(i, n, k, kp, kn, start(i), start(i + 1), slack)) atomicOr(&flags[i >> 5], 1u << (i & 31));
+      }
+    }
   }
   __syncthreads();
   counts[t * SRT_BINS + tid] = (S)h[tid];
@@ -277,12 +318,15 @@ __global__ void __launch_bounds__(SRT_BINS) sort_chunk_sum_kernel(const S* __res
 }
 // one workgroup per digit: the exclusive prefix of its chunk totals (1024 chunks per round, a carried base)
 constexpr int SRT_SCAN_T = 1024;
+// (binbase == nullptr: the prefixes start at 0 and the digit's total goes to total[d]; the bases are added when the
+// tiles' offsets are formed, sort_tile_offsets_kernel)
 template <typename S>
 __global__ void __launch_bounds__(SRT_SCAN_T) sort_chunk_scan_kernel(S* __restrict__ ctot, int64_t nchunks,
-                                                                     const int64_t* __restrict__ binbase) {
+                                                                     const int64_t* __restrict__ binbase,
+                                                                     int64_t* __restrict__ total) {
   __shared__ S wsum[SRT_SCAN_T / 64];
   const int d = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  S run = (S)binbase[d];
+  S run = binbase != nullptr ? (S)binbase[d] : (S)0;
   for (int64_t c0 = 0; c0 < nchunks; c0 += SRT_SCAN_T) {
     const int64_t c = c0 + tid;
     const S x = c < nchunks ? ctot[c * SRT_BINS + d] : (S)0;
@@ -294,24 +338,26 @@ __global__ void __launch_bounds__(SRT_SCAN_T) sort_chunk_scan_kernel(S* __restri
     }
     if (lane == 63) wsum[w] = inc;
     __syncthreads();
-    S before = run, total = 0;
+    S before = run, all = 0;
 #pragma unroll
     for (int i = 0; i < SRT_SCAN_T / 64; ++i) {
       const S t = wsum[i];
       before += i < w ? t : (S)0;
-      total += t;
+      all += t;
     }
     if (c < nchunks) ctot[c * SRT_BINS + d] = before + inc - x;
-    run += total;
+    run += all;
     __syncthreads();
   }
+  if (total != nullptr && tid == 0) total[d] = (int64_t)run;
 }
 template <typename S>
 __global__ void __launch_bounds__(SRT_BINS) sort_tile_offsets_kernel(S* __restrict__ counts, int64_t ntiles,
-                                                                     const S* __restrict__ ctot) {
+                                                                     const S* __restrict__ ctot,
+                                                                     const int64_t* __restrict__ binbase) {
   const int d = threadIdx.x;
   const int64_t c = blockIdx.x, t0 = c * SRT_CT, t1 = t0 + SRT_CT < ntiles ? t0 + SRT_CT : ntiles;
-  S run = ctot[c * SRT_BINS + d];
+  S run = ctot[c * SRT_BINS + d] + (binbase != nullptr ? (S)binbase[d] : (S)0);
   for (int64_t t = t0; t < t1; ++t) {
     const S x = counts[t * SRT_BINS + d];
     counts[t * SRT_BINS + d] = run;
@@ -349,19 +395,30 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
   uint16_t* wh = reinterpret_cast<uint16_t*>(xbuf);
   uint32_t* xk = reinterpret_cast<uint32_t*>(xbuf);
   reinterpret_cast<uint4*>(xbuf)[tid] = make_uint4(0u, 0u, 0u, 0u);  // 512 x 16 B: the 8 KB of wave histograms
-  // with the tiles' offsets given (reduce-then-scan) a tile is its block; else tiles go in ticket order (look-back)
-  if (tid == 0 && offsets == nullptr) s_tile = atomicAdd(ticket, 1u);
-  __syncthreads();
-  // reduce-then-scan: blocks go to the XCDs in turn (block b on XCD b % 8), so XCD x takes a contiguous run of tiles;
-  // its scattered runs into each digit's range then abut in its own L2 (consecutive tiles' pieces of one line merge
-  // there instead of reaching HBM as partial lines from two XCDs)
-  int64_t t;
-  if (offsets != nullptr) {
-    const int64_t nt = gridDim.x, b = blockIdx.x, x = b % 8, q = nt / 8, r = nt % 8;
-    t = x * q + (x < r ? x : r) + b / 8;
-  } else {
-    t = s_tile;
+  // Look-back: tiles in ticket order.  Reduce-then-scan (offsets given): XCD x takes tiles from its own contiguous
+  // eighth of the input (ticket[x]; HW_REG_XCC_ID says which XCD this is), then steals from the next ones when its
+  // eighth is done; its scattered runs into each digit's range then abut in its own L2 (consecutive tiles' pieces of
+  // one line merge there instead of reaching HBM as partial lines from two XCDs).  Each block takes one tile, so
+  // every tile is taken exactly once.
+  if (tid == 0) {
+    if (offsets == nullptr) {
+      s_tile = atomicAdd(ticket, 1u);
+    } else {
+      int home;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(home));
+      const int64_t nt = gridDim.x, q = nt / 8, r = nt % 8;
+      for (int i = 0; i < 8; ++i) {
+        const int64_t x = (home + i) % 8, a = x * q + (x < r ? x : r), len = q + (x < r ? 1 : 0);
+        const unsigned k = atomicAdd(ticket + x, 1u);
+        if ((int64_t)k < len) {
+          s_tile = (unsigned)(a + k);
+          break;
+        }
+      }
+    }
   }
+  __syncthreads();
+  const int64_t t = s_tile;
   const int64_t base = t * SRT_TILE;
   const int64_t wbase = base + (int64_t)w * (64 * SRT_IPT);  // a wave's points: SRT_IPT rows of 64 consecutive
   const uint32_t mask = (1u << dbits) - 1u;
@@ -636,7 +693,7 @@ static int roc_workspace(int64_t n, size_t* bytes) {
 
 template <typename S>
 static int run_passes(const SortPlan& P, const uint32_t* mz, const uint64_t* hits, int64_t n, uint32_t* ko,
-                      uint64_t* vo, unsigned char* ws, bool flag, hipStream_t st) {
+                      uint64_t* vo, unsigned char* ws, bool flag, double slack, hipStream_t st) {
   const size_t region = (size_t)P.ntiles * SRT_BINS;  // look-back words per pass
   const uint32_t* flagbits = reinterpret_cast<const uint32_t*>(ws + P.off_fl);
   unsigned* tickets = reinterpret_cast<unsigned*>(ws);
@@ -657,26 +714,33 @@ static int run_passes(const SortPlan& P, const uint32_t* mz, const uint64_t* hit
     S* sp = status + (size_t)(p & 1) * region;
     const S* offs = nullptr;
     if (rts) {
-      const int64_t* bb = binbase + p * SRT_BINS;
+      // counts (with the duplicate flags in the first pass of flag_and_sort), chunk totals, the digits' totals and
+      // bases (no histogram pass), the tiles' offsets
+      int64_t* bb = const_cast<int64_t*>(binbase) + p * SRT_BINS;
+      int64_t* totals = reinterpret_cast<int64_t*>(ws + P.off_hist);
+      const bool fl0 = flag && p == 0;
       hipLaunchKernelGGL(sort_count_kernel<S>, dim3((unsigned)P.ntiles), dim3(SRT_T), 0, st, ki, n, p * P.dbits,
-                         P.dbits, counts);
+                         P.dbits, counts, fl0 ? reinterpret_cast<const uint32_t*>(ws + P.off_s0) : nullptr,
+                         fl0 ? const_cast<uint32_t*>(flagbits) : nullptr, slack);
       hipLaunchKernelGGL(sort_chunk_sum_kernel<S>, dim3((unsigned)P.nchunks), dim3(SRT_BINS), 0, st, counts,
                          P.ntiles, ctot);
-      hipLaunchKernelGGL(sort_chunk_scan_kernel<S>, dim3((unsigned)(1 << P.dbits)), dim3(SRT_SCAN_T), 0, st, ctot,
-                         P.nchunks, bb);
+      hipLaunchKernelGGL(sort_chunk_scan_kernel<S>, dim3(SRT_BINS), dim3(SRT_SCAN_T), 0, st, ctot, P.nchunks,
+                         (const int64_t*)nullptr, totals);
+      hipLaunchKernelGGL(sort_digit_base_kernel, dim3(1), dim3(SRT_BINS), 0, st, totals, bb);
       hipLaunchKernelGGL(sort_tile_offsets_kernel<S>, dim3((unsigned)P.nchunks), dim3(SRT_BINS), 0, st, counts,
-                         P.ntiles, ctot);
+                         P.ntiles, ctot, bb);
       SMG_LAUNCH_CHECK();
       offs = counts;
     } else if (p >= 2) {
       SMG_HIP(hipMemsetAsync(sp, 0, region * sizeof(S), st));  // pass p - 2's look-back words
     }
+    unsigned* tk_p = rts ? tickets + 8 * p : tickets + p;  // (reduce-then-scan: one counter per XCD and pass)
     if (flag && p == 0)
       hipLaunchKernelGGL((sort_pass_kernel<S, true>), dim3((unsigned)P.ntiles), dim3(SRT_T), 0, st, ki, vi, kdst,
-                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, flagbits, offs);
+                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tk_p, flagbits, offs);
     else
       hipLaunchKernelGGL((sort_pass_kernel<S, false>), dim3((unsigned)P.ntiles), dim3(SRT_T), 0, st, ki, vi, kdst,
-                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tickets + p, nullptr, offs);
+                         vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tk_p, nullptr, offs);
     SMG_LAUNCH_CHECK();
     ki = kdst;
     vi = vdst;
@@ -697,8 +761,9 @@ static int native_sort(const float* mz, const uint64_t* hits, int64_t n, int key
     return SMG_ERR_UNSUPPORTED;
   }
   unsigned char* ws = reinterpret_cast<unsigned char*>(workspace);
+  const bool rts = g_sort_impl != 2;  // reduce-then-scan: no histogram pass, no look-back words
   // tickets, histograms and the first two passes' look-back words start at zero
-  SMG_HIP(hipMemsetAsync(ws, 0, P.off_status + P.status_bytes, st));
+  SMG_HIP(hipMemsetAsync(ws, 0, rts ? P.off_status : P.off_status + P.status_bytes, st));
   const uint32_t* keys = reinterpret_cast<const uint32_t*>(mz);
   if (flag) {  // spectrum starts first: the histogram pass computes the flags from them
     SMG_HIP(hipMemsetAsync(ws + P.off_s0, 0, P.off_fl + P.start_bytes - P.off_s0, st));  // start and flag bits
@@ -709,20 +774,22 @@ static int native_sort(const float* mz, const uint64_t* hits, int64_t n, int key
     SMG_LAUNCH_CHECK();
   }
   const double slack = 2.0 * ppm * 1e-6 / (1.0 - ppm * 1e-6) * (1.0 + 1e-9);
-  int64_t hb = (n + (int64_t)HST_T * 16 - 1) / ((int64_t)HST_T * 16);
-  if (hb > 2048) hb = 2048;
-  hipLaunchKernelGGL(sort_hist_kernel, dim3((unsigned)hb), dim3(HST_T), 0, st, keys, n, P.passes, P.dbits,
-                     reinterpret_cast<unsigned long long*>(ws + P.off_hist),
-                     flag ? reinterpret_cast<const uint32_t*>(ws + P.off_s0) : nullptr,
-                     flag ? reinterpret_cast<uint32_t*>(ws + P.off_fl) : nullptr, slack);
-  SMG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(sort_scan_kernel, dim3((unsigned)P.passes), dim3(SRT_BINS), 0, st,
-                     reinterpret_cast<const unsigned long long*>(ws + P.off_hist),
-                     reinterpret_cast<int64_t*>(ws + P.off_base));
-  SMG_LAUNCH_CHECK();
+  if (!rts) {  // look-back form: every pass's digit bases (and the flags) from one read of the keys first
+    int64_t hb = (n + (int64_t)HST_T * 16 - 1) / ((int64_t)HST_T * 16);
+    if (hb > 2048) hb = 2048;
+    hipLaunchKernelGGL(sort_hist_kernel, dim3((unsigned)hb), dim3(HST_T), 0, st, keys, n, P.passes, P.dbits,
+                       reinterpret_cast<unsigned long long*>(ws + P.off_hist),
+                       flag ? reinterpret_cast<const uint32_t*>(ws + P.off_s0) : nullptr,
+                       flag ? reinterpret_cast<uint32_t*>(ws + P.off_fl) : nullptr, slack);
+    SMG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sort_scan_kernel, dim3((unsigned)P.passes), dim3(SRT_BINS), 0, st,
+                       reinterpret_cast<const unsigned long long*>(ws + P.off_hist),
+                       reinterpret_cast<int64_t*>(ws + P.off_base));
+    SMG_LAUNCH_CHECK();
+  }
   uint32_t* ko = reinterpret_cast<uint32_t*>(mz_sorted);
-  return P.wide ? run_passes<unsigned long long>(P, keys, hits, n, ko, hits_sorted, ws, flag, st)
-                : run_passes<uint32_t>(P, keys, hits, n, ko, hits_sorted, ws, flag, st);
+  return P.wide ? run_passes<unsigned long long>(P, keys, hits, n, ko, hits_sorted, ws, flag, slack, st)
+                : run_passes<uint32_t>(P, keys, hits, n, ko, hits_sorted, ws, flag, slack, st);
 }
 
 }  // namespace smg

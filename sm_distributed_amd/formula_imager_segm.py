@@ -19,6 +19,7 @@ ion, window m/z in ion-major order, processing orders) is built on the device fr
 from __future__ import annotations
 
 import ctypes
+import os
 import warnings
 
 import numpy as np
@@ -318,8 +319,8 @@ def _stage_buffers(device, n):
 
 class FrameIndex:
     """device_frame in two halves around a kernel launch.  ``stage(keep)`` (device bool[n_ion], queued before the
-    launch) copies the row mask to a persistent pinned buffer on a copy stream of its own -- nothing is queued on
-    the compute stream in front of the kernel and nothing synchronises -- and takes the pinned block the
+    launch) copies the row mask to a persistent pinned buffer on a copy stream of its own, which the compute stream
+    waits for before the kernel (no copy runs beside it; the host does not synchronise) -- and takes the pinned block the
     DataFrame's columns will live in.  ``frame(cols)`` (after the launch) builds the MultiIndex on the host from
     the mask while the kernel still runs, then compacts the metric columns on the device (a scatter, no host
     synchronisation) and copies them to that block."""
@@ -341,6 +342,10 @@ class FrameIndex:
                 self.ev = torch.cuda.Event()
                 self.ev.record(cs)
             keep.record_stream(cs)
+            # the compute stream waits for the copy: the copy may run as a blit kernel, and one queued beside the
+            # persistent ion kernel (every CU's LDS held) was seen to time-slice it (35 -> 53-73 ms per launch, in
+            # ~10 ms steps, after the first ~8 steps of a bench)
+            main.wait_event(self.ev)
             self.keep_host = buf[:n]
             # the DataFrame's own pinned block (caching host allocator: reused once an earlier frame is freed),
             # taken before the kernel: a pinned allocation while a kernel runs remaps host memory and was seen to
@@ -630,7 +635,9 @@ def compute_sf_images(sc, ds, sf_peak_df, ppm):
         off, mz, it = spectra_from_duck(ds)
         peaks = DevicePeaks.from_arrays(off, mz, it, np.asarray(ds.norm_img_pixel_inds), ds.get_dims())
     main = torch.cuda.current_stream(peaks.device)
-    side = _side_stream(peaks.device)
+    # SMG_LAYOUT_SIDE=0 (diagnostic): the ion layout's kernels queue behind the sort on the main stream (its host
+    # work still overlaps the sort) instead of running beside it on the side stream
+    side = _side_stream(peaks.device) if os.environ.get("SMG_LAYOUT_SIDE", "1") != "0" else main
     side.wait_stream(main)  # the side stream may reuse memory the main stream released
     peaks.flag_and_sort(ppm)
     peaks.prefix_sums()
