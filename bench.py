@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rebalance", action="store_true",
                     help="N > 1: keep the cost model's cut (default: re-cut once from every rank's measured time)")
+    ap.add_argument("--no-head-cut", action="store_true",
+                    help="N > 1: re-cut without rank 0's assembly time (default: rank 0's shard is cut smaller by "
+                         "it, since the other ranks start the next search while rank 0 assembles the table)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target wall of the CPU baseline sample")
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="cap on CPU-baseline workers (a GPU box's CPU share is 16 cores per GPU)")
@@ -203,13 +206,16 @@ def main():
         if not args.no_rebalance:
             # the cut re-made from every rank's measured shard time (one all_gather of N floats): the cost model's
             # per-rank residuals would otherwise set the slowest rank's time
-            t_rank = torch.tensor([_rank_seconds(D, plan, peaks, ds_config)], dtype=torch.float64, device=device)
-            ts = [torch.zeros_like(t_rank) for _ in range(world)]
-            dist.all_gather(ts, t_rank)
-            times = [float(x.item()) for x in ts]
-            plan = D.rebalance(plan, formulas, peaks, times)
-            log(f"[rank {rank}] rebalanced from measured shard times (ms) {[round(x * 1e3, 2) for x in times]}: "
-                f"counts {plan.counts}")
+            t_rank = _rank_seconds(D, plan, peaks, ds_config)
+            t_head = 0.0 if args.no_head_cut else _assembly_seconds(D, plan, peaks, ds_config)
+            tt = torch.tensor([t_rank, t_head], dtype=torch.float64, device=device)
+            ts = [torch.zeros_like(tt) for _ in range(world)]
+            dist.all_gather(ts, tt)
+            times = [float(x[0].item()) for x in ts]
+            head = float(ts[0][1].item())  # rank 0's
+            plan = D.rebalance(plan, formulas, peaks, times, head_seconds=head)
+            log(f"[rank {rank}] rebalanced from measured shard times (ms) {[round(x * 1e3, 2) for x in times]}, "
+                f"rank-0 assembly {head * 1e3:.2f} ms: counts {plan.counts}")
         step_fn = lambda: D.score_sharded(plan, peaks, ds_config)[0]
         my_formulas = plan.formulas
     elif shard_only:
@@ -366,6 +372,25 @@ def _rank_seconds(D, plan, peaks, ds_config, reps=3):
         t = time.perf_counter()
         D._device_rows(plan, peaks, ds_config)
         torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t)
+    return best
+
+
+def _assembly_seconds(D, plan, peaks, ds_config, reps=3):
+    """Rank 0's assembly of the gathered table (rows_to_frame, its steady-state form: the row placement kept from
+    the previous search), best of ``reps``; 0 on the other ranks.  Every rank scores and gathers once (a
+    collective)."""
+    import torch
+    rows, _ = D._device_rows(plan, peaks, ds_config)
+    table = D.gather_rows(rows, plan)
+    if table is None:
+        return 0.0
+    D.rows_to_frame(table, plan.global_keys)
+    best = float("inf")
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        D.rows_to_frame(table, plan.global_keys)
         best = min(best, time.perf_counter() - t)
     return best
 

@@ -1,7 +1,9 @@
 """Per-rank critical path of the sharded (multi-GPU) step, measured on ONE GPU: every rank's shard of a
 W-way plan (config 3 by default) is scored in turn with the product code (distributed._device_rows), broken into
 slice copy, compute_sf_images and sf_image_metrics rows, plus the rank-0 assembly (rows_to_frame) of all ranks'
-rows.  The N-GPU step is then ~ max over ranks + all-gather + assembly.
+rows.  One search alone takes ~ max over ranks + gather + assembly; back to back (bench.py) the other ranks start
+the next search while rank 0 assembles, so the re-cut gives rank 0 that much less (rebalance's head_seconds) and
+a step takes ~ max(rank 0 + assembly, the other ranks) + gather.
 
 usage: time_shards.py [W=8] [nrows ncols peaks n_sf]
 CONFIG=5: BASELINE config 5 (1000x1000 px, Poisson(5000), 40k formulas x 6 adducts in both polarities); every rank
@@ -124,20 +126,31 @@ def run_ranks(plans, tag):
   return rows_all, worst, times
 
 
+def table_of(rows_all):
+    n_max = max(x.shape[0] for x in rows_all)
+    table = torch.full((W * n_max, 5), -1.0, dtype=torch.float64, device="cuda")
+    for r, x in enumerate(rows_all):
+        table[r * n_max:r * n_max + x.shape[0]] = x
+    return table, n_max
+
+
 plans = [D.plan_shards(formulas, peaks, ppm, W, r) for r in range(W)]
 rows_all, worst, times = run_ranks(plans, "cost model")
 if ONLY >= 0:
     sys.exit(0)
 worst0 = worst
-# the plan re-cut from the measured per-rank times (what bench.py does after its warm-up: one all_gather of W floats)
-plans = [D.rebalance(p, formulas, peaks, times) for p in plans]
+# rank 0's assembly (the steady-state form, placement cached), then the plan re-cut from the measured per-rank
+# times with it as rank 0's head (what bench.py does after its warm-up: one all_gather of W + 1 floats)
+table, _ = table_of(rows_all)
+D.rows_to_frame(table, plans[0].global_keys)
+t_head, _ = timed(lambda: D.rows_to_frame(table, plans[0].global_keys))
+NO_HEAD = bool(os.environ.get("NO_HEAD"))
+print(f"rank-0 assembly of the cost-model table {t_head:.2f} ms (head cut {'off' if NO_HEAD else 'on'})", flush=True)
+plans = [D.rebalance(p, formulas, peaks, times, head_seconds=0.0 if NO_HEAD else t_head * 1e-3) for p in plans]
 print("rebalanced counts", plans[0].counts, flush=True)
 rows_all, worst, times = run_ranks(plans, "rebalanced")
 print(f"max rank: cost model {worst0:.2f} ms, rebalanced {worst:.2f} ms", flush=True)
-n_max = max(x.shape[0] for x in rows_all)
-table = torch.full((W * n_max, 5), -1.0, dtype=torch.float64, device="cuda")
-for r, x in enumerate(rows_all):
-    table[r * n_max:r * n_max + x.shape[0]] = x
+table, n_max = table_of(rows_all)
 plan0 = plans[0]
 t_asm, df = timed(lambda: D.rows_to_frame(table, plan0.global_keys))
 # assembly breakdown
@@ -174,6 +187,10 @@ same = df1 is not None and df.index.equals(df1.index) and np.allclose(df.to_nump
                                                                        atol=1e-12)
 print(f"assembly (rank 0) {t_asm:.2f} ms; table identical to 1 GPU: {same}")
 gather_est = n_max * 40 / 50e9 * 1e3 + 0.05  # W-1 blocks over W-1 xGMI links into rank 0 at once, ~50 GB/s each
-est = worst + gather_est + t_asm
-print(f"estimated {W}-GPU step {est:.2f} ms = max rank {worst:.2f} + gather ~{gather_est:.2f} + assembly "
-      f"{t_asm:.2f}; strong-scaling efficiency {t1 / (W * est):.2f}")
+est1 = worst + gather_est + t_asm
+others = max(times[1:]) * 1e3
+est = max(times[0] * 1e3 + t_asm, others) + gather_est
+print(f"one search alone {est1:.2f} ms = max rank {worst:.2f} + gather ~{gather_est:.2f} + assembly {t_asm:.2f}")
+print(f"estimated {W}-GPU step (back to back) {est:.2f} ms = max(rank 0 {times[0] * 1e3:.2f} + assembly "
+      f"{t_asm:.2f}, other ranks {others:.2f}) + gather ~{gather_est:.2f}; strong-scaling efficiency "
+      f"{t1 / (W * est):.2f}")

@@ -34,9 +34,10 @@ import pandas as pd
 C_WINDOW_POINT = 6.2e-12
 C_ION = 2.0e-9
 C_SLICE_POINT = 54e-12
-# Rank 0 alone assembles the gathered rows into the DataFrame (rows_to_frame, ~1.3 ms at config 3).  Its shard is
-# NOT cut smaller for it: the assembly needs every rank's rows, so it starts only after the gather, i.e. after the
-# slowest rank -- a smaller rank-0 shard would only make the other shards (and the step) longer.
+# Rank 0 alone assembles the gathered rows into the DataFrame (rows_to_frame, ~0.8 ms at config 3).  One search
+# alone ends with it after the gather, but back to back (the bench, a search per dataset) the other ranks return
+# after the gather and start the next search while rank 0 assembles: rank 0's shard is then cut smaller by the
+# assembly (rebalance's head_seconds), so that every rank reaches the next gather together.
 
 ROW_FIELDS = ("ion", "chaos", "spatial", "spectral", "msm")
 
@@ -133,10 +134,13 @@ def plan_shards(formulas, peaks_or_mz, ppm, world, rank, bins=8192):
     return _plan_from_costs(formulas, order, cost, ppm, world, rank)
 
 
-def rebalance(plan, formulas, peaks_or_mz, rank_seconds, bins=8192):
+def rebalance(plan, formulas, peaks_or_mz, rank_seconds, bins=8192, head_seconds=0.0):
     """The plan re-cut from measured per-rank step times (one value per rank, e.g. all_gathered after a first
     search): every rank's ions get its measured/estimated ratio as a cost factor, and the shards are cut again on
     the corrected costs (the linear model of ion_costs leaves +-5 % per-rank residuals that no refit removes).
+    ``head_seconds``: rank 0's assembly of the gathered table (rows_to_frame), which the other ranks do not wait
+    for -- they return after the gather and start the next search -- so rank 0's shard is cut that much smaller
+    (shard_bounds' head) and every rank reaches the next gather together.
     Deterministic: every rank computes the same cut from the same times.  Returns this rank's new ShardPlan."""
     order, cost = _principal_costs(formulas, peaks_or_mz, plan.ppm, bins)
     t = np.asarray(rank_seconds, dtype=np.float64)
@@ -147,12 +151,14 @@ def rebalance(plan, formulas, peaks_or_mz, rank_seconds, bins=8192):
         est = float(cost[a:b].sum())
         if b > a and est > 0:
             scaled[a:b] *= t[r] / est
-    return _plan_from_costs(formulas, order, scaled, plan.ppm, plan.world, plan.rank)
+    if not np.isfinite(head_seconds) or head_seconds < 0.0:
+        raise ValueError("head_seconds: a time >= 0")
+    return _plan_from_costs(formulas, order, scaled, plan.ppm, plan.world, plan.rank, head=float(head_seconds))
 
 
-def _plan_from_costs(formulas, order, cost, ppm, world, rank):
+def _plan_from_costs(formulas, order, cost, ppm, world, rank, head=0.0):
     from .formula_imager_segm import IonKeys
-    bounds = shard_bounds(cost, world)
+    bounds = shard_bounds(cost, world, head)
     a, b = bounds[rank]
     mine = np.sort(order[a:b])                        # back to (sf_id, adduct) order
     shard = formulas.subset(mine)
@@ -262,14 +268,18 @@ def rows_to_frame(table, global_keys):
     gi = t[:, 0].long()
     gi = torch.where(gi >= 0, gi, torch.full_like(gi, n))
     cache = global_keys.__dict__.get("_frame_cache")
-    if (cache is not None and t.device.type == "cuda" and cache[0].device == t.device and cache[0].shape == gi.shape
-            and bool(torch.equal(cache[0], gi))):
+    if cache is not None and t.device.type == "cuda" and cache[0].device == t.device and cache[0].shape == gi.shape:
+        # the cached placement, checked on the device and copied back with the columns: one synchronisation
         rows_sel, mi = cache[1], cache[2]
+        differs = torch.ne(cache[0], gi).any().reshape(1)
         cols = t[rows_sel, 1:5].T.contiguous()  # [4, rows] in table order
         host = torch.empty(cols.shape, dtype=torch.float64, pin_memory=True)
+        flag = torch.empty(1, dtype=torch.bool, pin_memory=True)
+        flag.copy_(differs, non_blocking=True)
         host.copy_(cols, non_blocking=True)
         torch.cuda.current_stream(t.device).synchronize()
-        return pd.DataFrame(host.numpy().T, index=mi, columns=METRIC_COLUMNS, copy=False)
+        if not bool(flag[0]):
+            return pd.DataFrame(host.numpy().T, index=mi, columns=METRIC_COLUMNS, copy=False)
     # the gathered row of every ion (-1: none), then the ions with a row in table order and their rows
     row = torch.full((n + 1,), -1, dtype=torch.int64, device=t.device)
     row[gi] = torch.arange(t.shape[0], device=t.device)

@@ -172,3 +172,26 @@ def test_rebalance_recuts_from_measured_times():
     np.testing.assert_array_equal(got, np.arange(f.n_ions))
     with pytest.raises(ValueError):
         D.rebalance(plans[0], f, mz, [1.0, 0.0, 1.0])
+
+
+def test_rebalance_head_cuts_rank0_smaller():
+    """rebalance(head_seconds=...): rank 0's assembly of the gathered table is work the other ranks do not wait for
+    in back-to-back searches, so its shard is cut smaller by it (shard_bounds' head); every ion stays in exactly
+    one shard, the cut is the same on every rank, a negative head is refused."""
+    from sm_distributed_amd import distributed as D
+    ds, ions, ppm, f = _case()
+    mz = torch.from_numpy(ds.mz.astype(np.float32))
+    world = 3
+    plans = [D.plan_shards(f, mz, ppm, world, r) for r in range(world)]
+    est = plans[0].est_cost
+    head = 0.3 * est[0]
+    new = [D.rebalance(p, f, mz, est, head_seconds=head) for p in plans]
+    assert all(p.counts == new[0].counts for p in new) and sum(new[0].counts) == f.n_ions
+    assert new[0].counts[0] < plans[0].counts[0]
+    got = np.sort(np.concatenate([p.ion_idx for p in new]))
+    np.testing.assert_array_equal(got, np.arange(f.n_ions))
+    # rank 0's estimated cost plus the head is about every other rank's
+    e = new[0].est_cost
+    assert abs((e[0] + head) - e[1]) < 0.1 * e[1] and abs(e[1] - e[2]) < 0.1 * e[1]
+    with pytest.raises(ValueError):
+        D.rebalance(plans[0], f, mz, est, head_seconds=-1.0)

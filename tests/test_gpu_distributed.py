@@ -76,6 +76,33 @@ def test_every_rank_shard_on_one_gpu_equals_single_gpu_table(world):
         assert np.abs(df[c].values - exp[c].values).max() <= 1e-5
 
 
+def test_assembly_cache_follows_the_gathered_rows():
+    """rows_to_frame's steady-state path (distributed.py: the row placement of the previous table, checked on the
+    device and copied back with the columns) gives the single-GPU table for a repeated table, for the same rows
+    in another block order (same shape, other placement: the check must reject the cached one) and back."""
+    import torch
+    from sm_distributed_amd import distributed as D
+    from sm_distributed_amd import engine as E
+    from sm_distributed_amd.formulas import FormulasSegm
+    ds, ions, ppm, kw = make_case("dups")
+    pm, dims = ds.pixel_map_dims()
+    peaks = E.DevicePeaks.from_arrays(ds.sp_off, ds.mz, ds.ints, pm, dims)
+    formulas = FormulasSegm.from_ion_table(ions, ppm)
+    conf = {"image_generation": {"ppm": ppm, "nlevels": 30, "q": 99, "do_preprocessing": False}}
+    world = 3
+    rows = [D._device_rows(D.plan_shards(formulas, peaks, ppm, world, r), peaks, conf)[0] for r in range(world)]
+    gk = D.plan_shards(formulas, peaks, ppm, world, 0).global_keys
+    ref = _api_table(peaks, formulas, ppm)
+    a = torch.cat(rows)
+    b = torch.cat(rows[::-1])
+    assert a.is_cuda and not torch.equal(a[:, 0], b[:, 0])
+    for t in (a, a, b, b, a):
+        df = D.rows_to_frame(t, gk)
+        assert list(df.index) == list(ref.index)
+        for c in ("chaos", "spatial", "spectral", "msm"):
+            np.testing.assert_allclose(df[c].values, ref[c].values, rtol=0, atol=1e-12)
+
+
 def test_score_sharded_world1_rccl():
     import torch.distributed as dist
     from sm_distributed_amd import distributed as D
