@@ -271,10 +271,12 @@ __device__ __forceinline__ int hist_find(const uint32_t* hist, int& k, int& cnt)
 // radix select over the f64 bit patterns (positive values: ordered like the values), one 8-bit LDS histogram per
 // byte (two buffers in turn: a pass clears the next one while every wave reads the current one, so a pass takes two
 // barriers), that stops as soon as the selected byte prefix holds a single element (it is then fetched whole),
-// usually after three or four of the eight bytes.  The next order statistic is the same value when more elements
-// than needed equal it, else the smallest value above it (one pass for both).  visit(f) calls f(bits) for each
-// element this thread owns (any partition of the set over the NT threads of the block; called once per pass, so it
-// must enumerate the same set every time).  hist: 2 x 256 u32 (16-B aligned), sh: 1 int, dsh: 1 u64 of LDS.
+// usually after three or four of the eight bytes.  The next order statistic is then the smallest element above the
+// prefix, found in the same fetch pass; after a select down to the last byte (the element repeats) it is the same
+// value when more elements than needed equal it, else the smallest value above it (one more pass).  visit(f) calls
+// f(bits) for each element this thread owns (any partition of the set over the NT threads of the block; called once
+// per pass, so it must enumerate the same set every time).  hist: 2 x 256 u32 (16-B aligned), sh: 1 int, dsh: 2 u64
+// of LDS.
 // lo, hi: the bit patterns of the set's smallest and largest elements when known (else 0, ~0): the passes start at
 // the first byte where they differ (the bytes above it are common to every element), and none runs when they agree.
 template <int NT, class Visit>
@@ -291,9 +293,10 @@ __device__ void select_pair(Visit&& visit, int i0, bool pair, uint32_t* hist, in
   uint64_t prefix = lo & mask;
   int k = i0;
   for (int i = tid; i < 256; i += NT) hist[i] = 0u;
-  if (tid == 0) *dsh = ~0ull;
+  if (tid == 0) dsh[0] = dsh[1] = ~0ull;
   __syncthreads();
   int cur = 0;
+  bool fetched = false;
   for (int shift = top; shift >= 0; shift -= 8) {
     uint32_t* h = hist + 256 * cur;
     visit([&](uint64_t bits) {
@@ -306,19 +309,25 @@ __device__ void select_pair(Visit&& visit, int i0, bool pair, uint32_t* hist, in
     cur ^= 1;
     prefix |= (uint64_t)d << shift;
     mask |= 255ull << shift;
-    if (cnt == 1 && shift > 0) {  // a single element carries the prefix: it is the one
+    if (cnt == 1 && shift > 0) {  // a single element carries the prefix: it is the one, the next is above the prefix
+      uint64_t abv = ~0ull;
       visit([&](uint64_t bits) {
-        if ((bits & mask) == prefix) *dsh = bits;
+        const uint64_t mb = bits & mask;
+        if (mb == prefix) dsh[0] = bits;
+        else if (mb > prefix) abv = bits < abv ? bits : abv;
       });
+      if (pair && abv != ~0ull) atomicMin(&dsh[1], (unsigned long long)abv);
       __syncthreads();
-      prefix = *dsh;
+      prefix = dsh[0];
+      fetched = true;
       break;
     }
     __syncthreads();  // the next buffer is clear before the next pass's adds
   }
   a = __longlong_as_double((long long)prefix);
   b = a;
-  if (!pair) {
+  if (!pair || fetched) {
+    if (pair) b = __longlong_as_double((long long)dsh[1]);  // i0 + 1 < n: an element lies above
     __syncthreads();  // (dsh is read above before any later use of the scratch)
     return;
   }
@@ -374,11 +383,19 @@ __device__ double percentile_of(Visit&& visit, int n, double q, uint32_t* hist, 
 // (its 256-bin histogram: the digit, then the bins cleared for the next round).  visit(f) calls f(set, bits) for
 // every element this thread owns (the same partition every round); n[set]: the set's size (0: no clip, thr +inf).
 struct SelSet {
-  unsigned long long prefix, mask, dsh;  // selected prefix and its mask; FETCH: the element; PAIR: min above
+  unsigned long long prefix, mask, dsh;  // selected prefix and its mask; FETCH, FPAIR: the element; PAIR: min above
   double gamma;
-  int k, i0, shift, phase, le, pair;
+  union {
+    struct {
+      int k, le;  // RADIX: the rank left to select; PAIR: the count <= the element
+    };
+    unsigned long long above;  // FPAIR: the smallest element above the prefix
+  };
+  int i0, shift, phase, pair;
 };
-enum { SEL_RADIX = 0, SEL_FETCH = 1, SEL_PAIR = 2, SEL_DONE = 3 };
+// FPAIR: the prefix holds one element; one pass fetches it and the smallest element above it (the next order
+// statistic).  PAIR: after a select down to the last byte.
+enum { SEL_RADIX = 0, SEL_FETCH = 1, SEL_PAIR = 2, SEL_DONE = 3, SEL_FPAIR = 4 };
 __device__ __forceinline__ void sel_init(SelSet& st, int n, double q) {
   const double qq = q / 100.0;
   const double vi = (double)n * qq + (1.0 + qq * (1.0 - 1.0 - 1.0)) - 1.0;  // numpy _compute_virtual_index
@@ -404,11 +421,24 @@ __device__ __forceinline__ void sel_init(SelSet& st, int n, double q) {
   st.le = 0;
   st.pair = i1 != i0;
 }
+// A set's top-16-bit summary, OR-accumulated over its elements: high half the OR of each element's top 16 bits, low
+// half the OR of their complements (so the AND of the top 16 bits is its complement).  Bits where the two agree are
+// common to every element: oa_lo / oa_hi are bounds with those bits whose first differing byte (select_pair's start)
+// is at or below the first byte where the elements' top 16 bits differ.
+__device__ __forceinline__ uint32_t top16_oa(uint64_t bits) {
+  const uint32_t t = (uint32_t)(bits >> 48);
+  return (t << 16) | (~t & 0xFFFFu);
+}
+__device__ __forceinline__ uint64_t oa_lo(uint32_t oa) { return (uint64_t)(~oa & 0xFFFFu) << 48; }
+__device__ __forceinline__ uint64_t oa_hi(uint32_t oa) { return ((uint64_t)(oa >> 16) << 48) | 0xFFFFFFFFFFFFull; }
+
 // thr[s] for the sets [0, nsets); st: SB states, hist: SB x 256 u32 (16-B aligned), flag: 2 ints of LDS.  lo, hi
-// (optional): each set's smallest and largest element bits -- its passes start at the first byte where they differ.
+// (optional): each set's smallest and largest element bits -- its passes start at the first byte where they differ;
+// or oa (optional): each set's top16_oa summary, the same from the bounds it gives.
 template <int NT, int SB, class Visit>
 __device__ void select_batch(Visit&& visit, int nsets, const int* n, double q, double* thr, SelSet* st, uint32_t* hist,
-                             int* flag, const unsigned long long* lo = nullptr, const unsigned long long* hi = nullptr) {
+                             int* flag, const unsigned long long* lo = nullptr, const unsigned long long* hi = nullptr,
+                             const uint32_t* oa = nullptr) {
   static_assert(NT / WAVE >= SB, "a wave per set of the batch");
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
   for (int b0 = 0; b0 < nsets; b0 += SB) {
@@ -417,8 +447,9 @@ __device__ void select_batch(Visit&& visit, int nsets, const int* n, double q, d
       SelSet& S = st[tid];
       sel_init(S, n[b0 + tid], q);
       if (n[b0 + tid] == 0) thr[b0 + tid] = INFINITY;
-      if (lo != nullptr && S.phase == SEL_RADIX) {
-        const uint64_t l = lo[b0 + tid], d = l ^ (uint64_t)hi[b0 + tid];
+      if ((lo != nullptr || oa != nullptr) && S.phase == SEL_RADIX) {
+        const uint64_t l = lo != nullptr ? (uint64_t)lo[b0 + tid] : oa_lo(oa[b0 + tid]);
+        const uint64_t d = l ^ (lo != nullptr ? (uint64_t)hi[b0 + tid] : oa_hi(oa[b0 + tid]));
         if (d == 0ull) {  // every element is the same value
           thr[b0 + tid] = __longlong_as_double((long long)l);
           S.phase = SEL_DONE;
@@ -444,9 +475,14 @@ __device__ void select_batch(Visit&& visit, int nsets, const int* n, double q, d
         if (ph == SEL_PAIR) {
           if (bits <= pre) atomicAdd(&S.le, 1);
           else atomicMin(&S.dsh, (unsigned long long)bits);
-        } else if ((bits & S.mask) == pre) {
-          if (ph == SEL_RADIX) atomicAdd(&hist[j * 256 + ((bits >> S.shift) & 255u)], 1u);
-          else S.dsh = bits;  // SEL_FETCH: the one element with the prefix
+        } else {
+          const uint64_t mb = bits & S.mask;
+          if (mb == pre) {
+            if (ph == SEL_RADIX) atomicAdd(&hist[j * 256 + ((bits >> S.shift) & 255u)], 1u);
+            else S.dsh = bits;  // SEL_FETCH, SEL_FPAIR: the one element with the prefix
+          } else if (ph == SEL_FPAIR && mb > pre) {
+            atomicMin(&S.above, (unsigned long long)bits);
+          }
         }
       });
       if (tid == 0) flag[(round + 1) & 1] = 0;
@@ -465,7 +501,8 @@ __device__ void select_batch(Visit&& visit, int nsets, const int* n, double q, d
             S.mask |= 255ull << sh;
             S.k = k;
             if (cnt == 1 && sh > 0) {
-              S.phase = SEL_FETCH;
+              S.phase = S.pair ? SEL_FPAIR : SEL_FETCH;
+              if (S.pair) S.above = ~0ull;  // (k is spent)
             } else if (sh == 0) {
               done_now = true;
             } else {
@@ -476,6 +513,14 @@ __device__ void select_batch(Visit&& visit, int nsets, const int* n, double q, d
           if (lane == 0) {
             S.prefix = S.dsh;
             done_now = true;
+          }
+        } else if (ph == SEL_FPAIR) {
+          if (lane == 0) {
+            const double a = __longlong_as_double((long long)S.dsh);
+            const double b = __longlong_as_double((long long)S.above);  // i0 + 1 < n: an element lies above
+            const double dd = b - a, g = S.gamma;
+            thr[b0 + wid] = g >= 0.5 ? b - dd * (1.0 - g) : a + dd * g;
+            S.phase = SEL_DONE;
           }
         } else if (ph == SEL_PAIR) {
           if (lane == 0) {
@@ -771,8 +816,8 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
   uint32_t* c_hist = reinterpret_cast<uint32_t*>(Lv);  // CSB x 256 bins (the principal's select: 2 x 256)
   SelSet* c_st = reinterpret_cast<SelSet*>(Lv + 4096);
   int* c_flag = reinterpret_cast<int*>(Lv + 4320);
-  int* c_sh = reinterpret_cast<int*>(Lv + 4336);
-  unsigned long long* c_dsh = reinterpret_cast<unsigned long long*>(Lv + 4352);
+  unsigned long long* c_dsh = reinterpret_cast<unsigned long long*>(Lv + 4328);  // 2
+  int* c_sh = reinterpret_cast<int*>(Lv + 4344);
   double* c_thr = reinterpret_cast<double*>(Lv + 4360);
   unsigned long long* c_lo = reinterpret_cast<unsigned long long*>(Lv + 4360 + MAXK * 8);
   unsigned long long* c_hi = reinterpret_cast<unsigned long long*>(Lv + 4360 + MAXK * 16);
@@ -2394,12 +2439,12 @@ __device__ void clip_image(double* img, const uint32_t* list, int n_list, double
   const int n = sh[2];
   __syncthreads();
   if (n == 0) return;
-  __shared__ unsigned long long sel_u64;
+  __shared__ unsigned long long sel_u64[2];
   const double thr = percentile_of<DBLOCK>(
       [&](auto&& f) {
         for (int i = tid; i < n; i += DBLOCK) f((uint64_t)__double_as_longlong(ld_agent(&vals[i])));
       },
-      n, q, hist, sh, &sel_u64);
+      n, q, hist, sh, sel_u64);
   for (int i = tid; i < n_list; i += DBLOCK) {
     const uint32_t p = list[i];
     const double v = ld_agent(&img[p]);
@@ -2907,13 +2952,17 @@ template <int FMT>
 __device__ void wide_clip_tail(const Hits<FMT>& hits, int K, double q, int npx, const RankBits& R, const WideSlot& S,
                                const int64_t* sh_tb, const int64_t* sh_tlo, const int64_t* sh_tn, uint32_t* ltkey,
                                double* ltval, double* kst, int* sh_nown, int* sh_ctr, uint32_t* c_hist, int* c_sh,
-                               unsigned long long* c_dsh, double* c_thr, int* c_n, SelSet* c_st, int* c_flag) {
+                               unsigned long long* c_dsh, double* c_thr, int* c_n, SelSet* c_st, int* c_flag,
+                               uint32_t* c_oa) {
   using H = Hits<FMT>;
   const int tid = threadIdx.x, lane = tid & 63;
   constexpr int U = FMT == SMG_HITS_PACKED_F32 ? TDU : WDU;
   constexpr int64_t TSTEP = (int64_t)DBLOCK * U;  // the kernel's batch (sh_tb pads each window to a whole batch)
   const int64_t T = sh_tb[K - 1];
-  if (tid < MAXK_DENSE) c_n[tid] = 0;
+  if (tid < MAXK_DENSE) {
+    c_n[tid] = 0;
+    c_oa[tid] = 0u;
+  }
   __syncthreads();
   auto insert_global = [&](uint32_t key, double y) {
     uint32_t h = (key * 0x9E3779B1u) >> (32 - WIDE_HT_LOG2);
@@ -2970,13 +3019,16 @@ __device__ void wide_clip_tail(const Hits<FMT>& hits, int K, double q, int npx, 
   };
   auto bits_of = [](double v) { return (uint64_t)__double_as_longlong(v); };
 
-  // 1. flagged points -> tables; positive unflagged points counted per window
+  // 1. flagged points -> tables; positive unflagged points counted per window (and their top16_oa summary)
   {
     int cpos = 0, kc = 0;
+    uint32_t oa = 0u;
     auto flush = [&]() {
       const int t = __builtin_amdgcn_readlane(wave_incl_scan_dpp(cpos), 63);
       if (lane == 0 && t) atomicAdd(&c_n[kc + 1], t);
+      if (oa) atomicOr(&c_oa[kc + 1], oa);
       cpos = 0;
+      oa = 0u;
     };
     stream([&](int kb, int64_t off, int64_t n, const typename H::Reg (&r)[U]) {
       if (kb != kc) {
@@ -2988,7 +3040,9 @@ __device__ void wide_clip_tail(const Hits<FMT>& hits, int K, double q, int npx, 
         const bool valid = off + (int64_t)u * DBLOCK + tid < n;
         const bool fl = valid && H::dup(r[u]);
         insert(fl, (uint32_t)kb * (uint32_t)npx + H::pix(r[u]), fl ? (double)H::val(r[u]) : 0.0);
-        cpos += (valid && !H::dup(r[u]) && H::val(r[u]) > 0.0) ? 1 : 0;
+        const bool pos = valid && !H::dup(r[u]) && H::val(r[u]) > 0.0;
+        cpos += pos ? 1 : 0;
+        oa |= pos ? top16_oa(bits_of((double)H::val(r[u]))) : 0u;
       }
     });
     flush();
@@ -2996,7 +3050,11 @@ __device__ void wide_clip_tail(const Hits<FMT>& hits, int K, double q, int npx, 
   slot_sync();  // the tables' sums are complete (LDS; L2 for the global entries)
   const int no = *sh_nown;
   auto count_entry = [&](uint32_t key, double y) {
-    if (y > 0.0) atomicAdd(&c_n[(int)(key / (uint32_t)npx) + 1], 1);
+    if (y > 0.0) {
+      const int k = (int)(key / (uint32_t)npx) + 1;
+      atomicAdd(&c_n[k], 1);
+      atomicOr(&c_oa[k], top16_oa(bits_of(y)));
+    }
   };
   for (int i = tid; i < WIDE_LT; i += DBLOCK) {
     const uint32_t key = ltkey[i];
@@ -3029,7 +3087,7 @@ __device__ void wide_clip_tail(const Hits<FMT>& hits, int K, double q, int npx, 
             if (y > 0.0) f((int)(ld_agent(&S.hkey[sl]) / (uint32_t)npx), bits_of(y));
           }
         },
-        K - 1, c_n + 1, q, c_thr + 1, c_st, c_hist, c_flag);
+        K - 1, c_n + 1, q, c_thr + 1, c_st, c_hist, c_flag, nullptr, nullptr, c_oa + 1);
   }
 
   // 3. the clipped unflagged points
@@ -3099,6 +3157,7 @@ __device__ void wide_clip_tail(const Hits<FMT>& hits, int K, double q, int npx, 
   __syncthreads();  // (released entries reach L2 before the next ion's inserts: slot_syncs lie between)
 }
 
+constexpr int PRV = 4;  // wide pass clip: principal values per lane held in registers (np <= PRV * DBLOCK)
 template <int FMT, bool CLIP>
 __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     Hits<FMT> hits, const DD4* __restrict__ cum, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
@@ -3125,10 +3184,10 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
   __shared__ SelSet c_st[CLIP ? 4 : 1];
   __shared__ int c_flag[2];
   __shared__ int c_sh[4];
-  __shared__ unsigned long long c_dsh;
+  __shared__ unsigned long long c_dsh[2];
   __shared__ double c_thr[CLIP ? MAXK_DENSE : 1];
   __shared__ int c_n[CLIP ? MAXK_DENSE : 1];
-  __shared__ unsigned long long c_lo[CLIP ? 1 : 1], c_hi[CLIP ? 1 : 1];  // the principal's value bounds
+  __shared__ uint32_t c_oa[CLIP ? MAXK_DENSE : 1];  // top16_oa of the positive values: the principal at 0, window k at k
   const int tid = threadIdx.x;
   const int npx = P.npx, n64 = (npx + 63) / 64, nsb = (n64 + 1023) / 1024;
   const int n64p = (int)wide_n64p(npx);  // n64 words + zero words to a whole 4-word group (row7 reads one past)
@@ -3226,6 +3285,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     // the statistics re-read all values.)
     const int ndp = sh_ctr[2];
     const bool fused = ndp <= WIDE_DL;
+    if (CLIP && tid == 0) c_oa[0] = 0u;  // (read after the statistics' block reduction)
     if (fused) {
       for (int j = tid; j < ndp; j += DBLOCK) S.vals[R.rank(ld_agent(&S.dkey[j]))] = 0.0;
     } else {
@@ -3234,6 +3294,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     slot_sync();
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     double mx = -INFINITY;
+    uint32_t poa = 0u;  // CLIP: top16_oa of the positive values
     for (int64_t i0 = a0; i0 < b0; i0 += (int64_t)DBLOCK * WDU) {
       typename H::Reg r[WDU];
 #pragma unroll
@@ -3259,6 +3320,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
               if (v > 0.0) {
                 acc[2] += v;
                 acc[3] += 1.0;
+                if constexpr (CLIP) poa |= top16_oa((uint64_t)__double_as_longlong(v));
               }
               mx = v > mx ? v : mx;
             }
@@ -3275,6 +3337,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
         if (v > 0.0) {
           acc[2] += v;
           acc[3] += 1.0;
+          if constexpr (CLIP) poa |= top16_oa((uint64_t)__double_as_longlong(v));
         }
         mx = v > mx ? v : mx;
       }
@@ -3295,53 +3358,26 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
           if (v > 0.0) {
             acc[2] += v;
             acc[3] += 1.0;
+            if constexpr (CLIP) poa |= top16_oa(vb[j]);
           }
           mx = v > mx ? v : mx;
         }
       }
     }
     if (np < npx) mx = mx > 0.0 ? mx : 0.0;  // unlisted pixels are zero
+    if (CLIP && poa) atomicOr(&c_oa[0], poa);
     dblock_sum<4>(acc, red);
     if constexpr (CLIP) {
       // the hot-spot clip of the principal image: its q-th percentile over the acc[3] positive values, every value
       // above it lowered to it, then the statistics again
       const int n0 = (int)acc[3];
       if (n0 > 0) {
-        // the smallest and largest positive value's bits bound the select's passes
-#ifndef SMG_CLIP_PLOHI  // 1: bound the principal's select by its value range (an extra pass; slower, r4clipab)
-#define SMG_CLIP_PLOHI 0
-#endif
-        uint64_t plo = ~0ull, phi = 0ull;
-        for (int r = SMG_CLIP_PLOHI ? tid : np; r < np; r += DBLOCK) {
-          const double v = ld_agent(&S.vals[r]);
-          if (v > 0.0) {
-            const uint64_t b = (uint64_t)__double_as_longlong(v);
-            plo = b < plo ? b : plo;
-            phi = b > phi ? b : phi;
-          }
-        }
-        if (tid == 0) {
-          c_lo[0] = ~0ull;
-          c_hi[0] = 0ull;
-        }
-        __syncthreads();
-        if (plo != ~0ull) {
-          atomicMin(&c_lo[0], (unsigned long long)plo);
-          atomicMax(&c_hi[0], (unsigned long long)phi);
-        }
-        __syncthreads();
-        const double thr = percentile_of<DBLOCK>(
-            [&](auto&& f) {
-              for (int r = tid; r < np; r += DBLOCK) {
-                const double v = ld_agent(&S.vals[r]);
-                if (v > 0.0) f((uint64_t)__double_as_longlong(v));
-              }
-            },
-            n0, P.q, c_hist, c_sh, &c_dsh, SMG_CLIP_PLOHI ? c_lo[0] : 0ull, SMG_CLIP_PLOHI ? c_hi[0] : ~0ull);
+        // the bits common to the positive values' top 16 (gathered with the statistics) skip the select's first
+        // pass or two
+        const uint32_t oa = c_oa[0];
         acc[0] = acc[1] = acc[2] = acc[3] = 0.0;
         mx = -INFINITY;
-        for (int r = tid; r < np; r += DBLOCK) {
-          double v = ld_agent(&S.vals[r]);
+        auto clip_one = [&](int r, double v, double thr) {
           if (v > thr) {
             v = thr;
             S.vals[r] = thr;
@@ -3353,6 +3389,35 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
             acc[3] += 1.0;
           }
           mx = v > mx ? v : mx;
+        };
+        if (np <= PRV * DBLOCK) {
+          // up to PRV values per lane: held in registers for the select's passes and the clip (one read)
+          uint64_t pv[PRV];
+#pragma unroll
+          for (int j = 0; j < PRV; ++j) {
+            const int r = tid + j * DBLOCK;
+            pv[j] = r < np ? (uint64_t)__double_as_longlong(ld_agent(&S.vals[r])) : 0ull;
+          }
+          const double thr = percentile_of<DBLOCK>(
+              [&](auto&& f) {
+#pragma unroll
+                for (int j = 0; j < PRV; ++j)
+                  if ((int64_t)pv[j] > 0) f(pv[j]);  // v > 0 (sign clear, not +0)
+              },
+              n0, P.q, c_hist, c_sh, c_dsh, oa_lo(oa), oa_hi(oa));
+#pragma unroll
+          for (int j = 0; j < PRV; ++j)
+            if (tid + j * DBLOCK < np) clip_one(tid + j * DBLOCK, __longlong_as_double((long long)pv[j]), thr);
+        } else {
+          const double thr = percentile_of<DBLOCK>(
+              [&](auto&& f) {
+                for (int r = tid; r < np; r += DBLOCK) {
+                  const double v = ld_agent(&S.vals[r]);
+                  if (v > 0.0) f((uint64_t)__double_as_longlong(v));
+                }
+              },
+              n0, P.q, c_hist, c_sh, c_dsh, oa_lo(oa), oa_hi(oa));
+          for (int r = tid; r < np; r += DBLOCK) clip_one(r, ld_agent(&S.vals[r]), thr);
         }
         if (np < npx) mx = mx > 0.0 ? mx : 0.0;
         dblock_sum<4>(acc, red);
@@ -3401,7 +3466,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
     }
     if constexpr (CLIP) {
       wide_clip_tail<FMT>(hits, K, P.q, npx, R, S, sh_tb, sh_tlo, sh_tn, ltkey, ltval, kst, &sh_nown, sh_ctr, c_hist, c_sh,
-                          &c_dsh, c_thr, c_n, c_st, c_flag);
+                          c_dsh, c_thr, c_n, c_st, c_flag, c_oa);
     } else {
       const int64_t T = sh_tb[K - 1];
       double as = 0.0, axy = 0.0;  // the lane's Σy[x > 0], Σxy in window kacc
@@ -3959,6 +4024,26 @@ struct PassEvents {
   hipEvent_t ev0, ev1;
 };
 static std::vector<PassEvents> g_pass_events;
+// drained events are kept for reuse: after the first timed searches no event is created (a creation can reach the
+// device while a persistent pass runs)
+static std::vector<hipEvent_t> g_ev_pool;
+static hipEvent_t ev_take() {
+  {
+    std::lock_guard<std::mutex> g(g_ev_mu);
+    if (!g_ev_pool.empty()) {
+      hipEvent_t e = g_ev_pool.back();
+      g_ev_pool.pop_back();
+      return e;
+    }
+  }
+  hipEvent_t e = nullptr;
+  return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
+static void ev_give(hipEvent_t e) {  // caller holds g_ev_mu
+  if (!e) return;
+  if (g_ev_pool.size() < 4096) g_ev_pool.push_back(e);
+  else (void)hipEventDestroy(e);
+}
 
 // opens a timed region for one pass launch on `st` (no-op unless smg_debug_time_main_pass is on)
 struct PassTimer {
@@ -3967,11 +4052,9 @@ struct PassTimer {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   PassTimer(int p, hipStream_t s) : pass(p), st(s) {
     if (!g_time_main) return;
-    if (hipEventCreate(&ev0) != hipSuccess) {
-      ev0 = nullptr;
-      return;
-    }
-    if (hipEventCreate(&ev1) != hipSuccess) ev1 = nullptr;
+    ev0 = ev_take();
+    if (!ev0) return;
+    ev1 = ev_take();
     if (!ev1 || hipEventRecord(ev0, st) != hipSuccess) release();
   }
   ~PassTimer() {
@@ -3988,9 +4071,10 @@ struct PassTimer {
     }
     g_pass_events.push_back({pass, ev0, ev1});
   }
-  void release() {  // destroys whatever was created; no record is kept
-    if (ev0) (void)hipEventDestroy(ev0);
-    if (ev1) (void)hipEventDestroy(ev1);
+  void release() {  // returns whatever was taken; no record is kept
+    std::lock_guard<std::mutex> g(g_ev_mu);
+    ev_give(ev0);
+    ev_give(ev1);
     ev0 = ev1 = nullptr;
   }
   static constexpr size_t kMaxPassEvents = 16384;
@@ -4181,6 +4265,14 @@ int smg_debug_force_two_level(int32_t on) {
 
 int smg_debug_time_main_pass(int32_t on) {
   g_time_main = on ? 1 : 0;
+  if (on) {  // events for ~170 searches made now, not while a pass runs
+    std::lock_guard<std::mutex> g(g_ev_mu);
+    while (g_ev_pool.size() < 2048) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreate(&e) != hipSuccess) break;
+      g_ev_pool.push_back(e);
+    }
+  }
   return SMG_OK;
 }
 
@@ -4203,8 +4295,8 @@ static int drain_pass_times(int only, int32_t* pass, double* ms, int32_t cap, in
       }
       ++k;
     }
-    (void)hipEventDestroy(e.ev0);
-    (void)hipEventDestroy(e.ev1);
+    ev_give(e.ev0);
+    ev_give(e.ev1);
   }
   g_pass_events.clear();
   *n = k;

@@ -343,6 +343,82 @@ __device__ __forceinline__ DD4 dd4_shfl_up(const DD4& v, int o) {
   return DD4{__shfl_up(v.xh, o, 64), __shfl_up(v.xl, o, 64), __shfl_up(v.yh, o, 64), __shfl_up(v.yl, o, 64)};
 }
 
+// packed hits: 16-byte loads, two points per lane, so one row-sum pass of the wave gives two blocks' sums (lanes 0-31
+// one block, 32-63 the next); each iteration's 16 blocks land in lanes 0-15, which store them with one instruction
+// and add them into per-lane double-double accumulators (one dd4_add for all sixteen), summed in lane order at the
+// end.  The order of every sum is fixed (the blocks' pair-then-row order; the chunk total by lane, then by wave).
+constexpr int BS_PAIRS = 8;  // block pairs per wave and iteration
+static_assert(PS_CHUNK % (4 * 2 * BS_PAIRS) == 0, "waves take whole iterations of blocks");
+__device__ __forceinline__ double rows16_sum(double v) {  // every lane: the sum of its 16-lane row
+  v += dpp_d<DPP_QP_1032>(v);
+  v += dpp_d<DPP_QP_2301>(v);
+  v += dpp_d<DPP_ROR4>(v);
+  v += dpp_d<DPP_ROR8>(v);
+  return v;
+}
+__global__ void __launch_bounds__(PS_T) chunk_sums_packed_kernel(const uint64_t* __restrict__ hits, int64_t n,
+                                                                 DD4* __restrict__ bs, DD4* __restrict__ ctot) {
+  __shared__ DD4 wt[PS_T / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t nblk = (n + 63) >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * PS_CHUNK;
+  const bool al16 = (reinterpret_cast<uintptr_t>(hits) & 15) == 0;
+  DD4 acc{0.0, 0.0, 0.0, 0.0};  // lane j < 16: blocks j, j + 16, ... of this wave
+  constexpr int PER_WAVE = PS_CHUNK / (PS_T / 64);
+  constexpr int BPI = 2 * BS_PAIRS;  // blocks per iteration
+  const int half = lane >> 5, hl = lane & 31;
+  for (int g = 0; g < PER_WAVE; g += BPI) {
+    const int64_t blk0 = c0 + (int64_t)w * PER_WAVE + g;
+    if (blk0 >= nblk) break;  // wave-uniform
+    uint64_t h0[BS_PAIRS], h1[BS_PAIRS];
+#pragma unroll
+    for (int j = 0; j < BS_PAIRS; ++j) {
+      const int64_t i = (blk0 + 2 * j + half) * 64 + 2 * hl;  // this lane's two points
+      h0[j] = h1[j] = 0ull;
+      if (i + 1 < n && al16) {
+        const ulonglong2 q = reinterpret_cast<const ulonglong2*>(hits + i)[0];
+        h0[j] = q.x;
+        h1[j] = q.y;
+      } else {
+        if (i < n) h0[j] = hits[i];
+        if (i + 1 < n) h1[j] = hits[i + 1];
+      }
+    }
+    double ma = 0.0, mb = 0.0;  // lane k < 16: block k of the iteration
+#pragma unroll
+    for (int j = 0; j < BS_PAIRS; ++j) {
+      const double v0 = (double)__uint_as_float((uint32_t)(h0[j] >> 32));
+      const double v1 = (double)__uint_as_float((uint32_t)(h1[j] >> 32));
+      const bool d0 = ((uint32_t)h0[j] >> 31) != 0u, d1 = ((uint32_t)h1[j] >> 31) != 0u;
+      const double s = rows16_sum(v0 + v1);
+      const double q = rows16_sum((d0 ? 0.0 : v0 * v0) + (d1 ? 0.0 : v1 * v1));
+      const double a0 = readlane_d(s, 0) + readlane_d(s, 16), a1 = readlane_d(s, 32) + readlane_d(s, 48);
+      const double b0 = readlane_d(q, 0) + readlane_d(q, 16), b1 = readlane_d(q, 32) + readlane_d(q, 48);
+      ma = lane == 2 * j ? a0 : (lane == 2 * j + 1 ? a1 : ma);
+      mb = lane == 2 * j ? b0 : (lane == 2 * j + 1 ? b1 : mb);
+    }
+    if (lane < BPI && blk0 + lane < nblk) {
+      const DD4 d{ma, 0.0, mb, 0.0};
+      bs[blk0 + lane] = d;
+      acc = dd4_add(acc, d);
+    }
+  }
+  DD4 t = acc;  // lane 0 gathers lanes 1..15 in order
+#pragma unroll
+  for (int j = 1; j < BPI; ++j) {
+    const DD4 o{__shfl(acc.xh, j, 64), __shfl(acc.xl, j, 64), __shfl(acc.yh, j, 64), __shfl(acc.yl, j, 64)};
+    t = dd4_add(t, o);
+  }
+  if (lane == 0) wt[w] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    DD4 c = wt[0];
+#pragma unroll
+    for (int i = 1; i < PS_T / 64; ++i) c = dd4_add(c, wt[i]);
+    ctot[blockIdx.x] = c;
+  }
+}
+
 template <int FMT>
 __global__ void __launch_bounds__(PS_T) chunk_sums_kernel(const void* __restrict__ hits,
                                                           const double* __restrict__ hit_vals, int64_t n,
@@ -664,8 +740,8 @@ int smg_hit_prefix_sums(int32_t hit_format, const void* hits, const double* hit_
   p += ((size_t)nch * sizeof(DD4) + 255) / 256 * 256;
   DD4* cbase = reinterpret_cast<DD4*>(p);
   if (hit_format == SMG_HITS_PACKED_F32)
-    hipLaunchKernelGGL(chunk_sums_kernel<SMG_HITS_PACKED_F32>, dim3((unsigned)nch), dim3(PS_T), 0, st, hits,
-                       hit_vals, n_points, bs, ctot);
+    hipLaunchKernelGGL(chunk_sums_packed_kernel, dim3((unsigned)nch), dim3(PS_T), 0, st,
+                       static_cast<const uint64_t*>(hits), n_points, bs, ctot);
   else
     hipLaunchKernelGGL(chunk_sums_kernel<SMG_HITS_SPLIT_F64>, dim3((unsigned)nch), dim3(PS_T), 0, st, hits,
                        hit_vals, n_points, bs, ctot);
