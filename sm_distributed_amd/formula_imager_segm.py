@@ -332,7 +332,16 @@ class FrameIndex:
     def stage(self, keep):
         import torch
         self.keep = keep
-        if keep.device.type == "cuda":
+        if keep.device.type == "cuda" and _one_stream():
+            n = keep.numel()
+            main = torch.cuda.current_stream(keep.device)
+            _, buf = _stage_buffers(keep.device, n)
+            buf[:n].copy_(keep.view(torch.uint8), non_blocking=True)
+            self.ev = torch.cuda.Event()
+            self.ev.record(main)
+            self.keep_host = buf[:n]
+            self.cols_host = torch.empty(4 * n, dtype=torch.float64, pin_memory=True)
+        elif keep.device.type == "cuda":
             n = keep.numel()
             main = torch.cuda.current_stream(keep.device)
             cs, buf = _stage_buffers(keep.device, n)
@@ -612,8 +621,15 @@ class IonImageSet:
 _SIDE = {}
 
 
+def _one_stream():
+    """SMG_ONE_STREAM=1: every queued operation of a search on the caller's stream (no side or copy stream)."""
+    return os.environ.get("SMG_ONE_STREAM", "0") == "1"
+
+
 def _side_stream(device):
     import torch
+    if _one_stream():
+        return torch.cuda.current_stream(device)
     key = str(device)
     if key not in _SIDE:
         _SIDE[key] = torch.cuda.Stream(device=device)
