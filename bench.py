@@ -261,6 +261,8 @@ def main():
         import gc
         gc.collect()
         gc.freeze()
+    clock = ClockSampler(torch.cuda.get_device_properties(device))
+    clock.start()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     marks = []
@@ -275,6 +277,7 @@ def main():
     if sharded:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    sclk = clock.stop()
     L.smg_debug_time_main_pass(0)
     pass_ms = _pass_times(L)
     n_rows = df if isinstance(df, int) else (len(df) if df is not None else 0)
@@ -286,7 +289,7 @@ def main():
     per_step = np.diff([t0] + marks) * 1e3
     if len(per_step):
         log(f"[rank {rank}] step ms: min {per_step.min():.2f} median {np.median(per_step):.2f} "
-            f"max {per_step.max():.2f}")
+            f"max {per_step.max():.2f}; shader clock MHz {sclk}")
         if os.environ.get("SMG_BENCH_VERBOSE"):
             log(f"[rank {rank}] steps: " + " ".join(f"{x:.1f}" for x in per_step))
             log(f"[rank {rank}] pass launches (pass:ms): " + " ".join(f"{p}:{t:.2f}" for p, t in pass_ms))
@@ -350,6 +353,7 @@ def main():
                 "rccl_world_size": rccl_world,
                 "shard_est_cost_s": plan.est_cost if plan is not None else None,
             },
+            "sclk_mhz": sclk,
             "first_step_ms": first_step_ms,
             "cold_cache_step_ms": cold_ms,
             "step_ms_min_median_max": ([float(per_step.min()), float(np.median(per_step)), float(per_step.max())]
@@ -377,6 +381,72 @@ def _rank_seconds(D, plan, peaks, ds_config, reps=3):
         torch.cuda.synchronize()
         best = min(best, time.perf_counter() - t)
     return best
+
+
+class ClockSampler:
+    """The GPU's shader clock over the timed region (diagnostic: some boxes of the pool cap it, and the
+    latency-bound ion kernel's time follows it): the current DPM level of the device's pp_dpm_sclk (sysfs, the
+    card whose PCI bus matches; the only readable one otherwise) read every 20 ms by a host thread.  stop() returns
+    {"min", "median", "max", "samples"} in MHz, or None where sysfs does not expose it."""
+
+    def __init__(self, props):
+        import glob
+        self.path = None
+        cands = []
+        for dev in sorted(glob.glob("/sys/class/drm/card*/device")):
+            f = os.path.join(dev, "pp_dpm_sclk")
+            try:
+                with open(f) as fh:
+                    fh.read()
+                slot = ""
+                with open(os.path.join(dev, "uevent")) as fh:
+                    for ln in fh:
+                        if ln.startswith("PCI_SLOT_NAME="):
+                            slot = ln.strip().split("=", 1)[1]
+                cands.append((f, slot))
+            except OSError:
+                continue
+        bus = getattr(props, "pci_bus_id", None)
+        match = [f for f, slot in cands if bus is not None and slot.split(":")[1:2] == [f"{bus:02x}"]]
+        if len(match) == 1:
+            self.path = match[0]
+        elif len(cands) == 1:
+            self.path = cands[0][0]
+        self.samples = []
+        self._stop = threading.Event()
+        self._thr = None
+
+    def _read(self):
+        with open(self.path) as fh:
+            for ln in fh:
+                if ln.rstrip().endswith("*"):
+                    return float(ln.split(":")[1].strip().split("M")[0])
+        return None
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                v = self._read()
+            except (OSError, ValueError, IndexError):
+                v = None
+            if v is not None:
+                self.samples.append(v)
+            self._stop.wait(0.02)
+
+    def start(self):
+        if self.path:
+            self._thr = threading.Thread(target=self._run, daemon=True)
+            self._thr.start()
+
+    def stop(self):
+        if self._thr is None:
+            return None
+        self._stop.set()
+        self._thr.join()
+        if not self.samples:
+            return None
+        v = np.asarray(self.samples)
+        return {"min": float(v.min()), "median": float(np.median(v)), "max": float(v.max()), "samples": int(v.size)}
 
 
 def _assembly_seconds(D, plan, peaks, ds_config, reps=3):

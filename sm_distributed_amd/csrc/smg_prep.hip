@@ -343,12 +343,13 @@ __device__ __forceinline__ DD4 dd4_shfl_up(const DD4& v, int o) {
   return DD4{__shfl_up(v.xh, o, 64), __shfl_up(v.xl, o, 64), __shfl_up(v.yh, o, 64), __shfl_up(v.yl, o, 64)};
 }
 
-// packed hits: 16-byte loads, two points per lane, so one row-sum pass of the wave gives two blocks' sums (lanes 0-31
-// one block, 32-63 the next); each iteration's 16 blocks land in lanes 0-15, which store them with one instruction
-// and add them into per-lane double-double accumulators (one dd4_add for all sixteen), summed in lane order at the
-// end.  The order of every sum is fixed (the blocks' pair-then-row order; the chunk total by lane, then by wave).
-constexpr int BS_PAIRS = 8;  // block pairs per wave and iteration
-static_assert(PS_CHUNK % (4 * 2 * BS_PAIRS) == 0, "waves take whole iterations of blocks");
+// packed hits: each lane loads four consecutive points (two 16-byte loads), so a 64-point block is one 16-lane row
+// and one row-sum pass of the wave gives four blocks' sums; each iteration's 16 blocks land in lanes 0-15, which
+// store them with one instruction and add them into per-lane double-double accumulators (one dd4_add for all
+// sixteen), summed in lane order at the end.  The order of every sum is fixed (a block: the lane's four points
+// pairwise, then the row; the chunk total by lane, then by wave).
+constexpr int BS_QUADS = 4;  // four-block groups per wave and iteration
+static_assert(PS_CHUNK % (4 * 4 * BS_QUADS) == 0, "waves take whole iterations of blocks");
 __device__ __forceinline__ double rows16_sum(double v) {  // every lane: the sum of its 16-lane row
   v += dpp_d<DPP_QP_1032>(v);
   v += dpp_d<DPP_QP_2301>(v);
@@ -365,37 +366,48 @@ __global__ void __launch_bounds__(PS_T) chunk_sums_packed_kernel(const uint64_t*
   const bool al16 = (reinterpret_cast<uintptr_t>(hits) & 15) == 0;
   DD4 acc{0.0, 0.0, 0.0, 0.0};  // lane j < 16: blocks j, j + 16, ... of this wave
   constexpr int PER_WAVE = PS_CHUNK / (PS_T / 64);
-  constexpr int BPI = 2 * BS_PAIRS;  // blocks per iteration
-  const int half = lane >> 5, hl = lane & 31;
+  constexpr int BPI = 4 * BS_QUADS;  // blocks per iteration
+  const int row = lane >> 4, rl = lane & 15;
   for (int g = 0; g < PER_WAVE; g += BPI) {
     const int64_t blk0 = c0 + (int64_t)w * PER_WAVE + g;
     if (blk0 >= nblk) break;  // wave-uniform
-    uint64_t h0[BS_PAIRS], h1[BS_PAIRS];
+    uint64_t h[BS_QUADS][4];
 #pragma unroll
-    for (int j = 0; j < BS_PAIRS; ++j) {
-      const int64_t i = (blk0 + 2 * j + half) * 64 + 2 * hl;  // this lane's two points
-      h0[j] = h1[j] = 0ull;
-      if (i + 1 < n && al16) {
-        const ulonglong2 q = reinterpret_cast<const ulonglong2*>(hits + i)[0];
-        h0[j] = q.x;
-        h1[j] = q.y;
+    for (int j = 0; j < BS_QUADS; ++j) {
+      const int64_t i = (blk0 + 4 * j + row) * 64 + 4 * rl;  // this lane's four points
+#pragma unroll
+      for (int u = 0; u < 4; ++u) h[j][u] = 0ull;
+      if (i + 3 < n && al16) {
+        const ulonglong2 q0 = reinterpret_cast<const ulonglong2*>(hits + i)[0];
+        const ulonglong2 q1 = reinterpret_cast<const ulonglong2*>(hits + i)[1];
+        h[j][0] = q0.x;
+        h[j][1] = q0.y;
+        h[j][2] = q1.x;
+        h[j][3] = q1.y;
       } else {
-        if (i < n) h0[j] = hits[i];
-        if (i + 1 < n) h1[j] = hits[i + 1];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (i + u < n) h[j][u] = hits[i + u];
       }
     }
     double ma = 0.0, mb = 0.0;  // lane k < 16: block k of the iteration
 #pragma unroll
-    for (int j = 0; j < BS_PAIRS; ++j) {
-      const double v0 = (double)__uint_as_float((uint32_t)(h0[j] >> 32));
-      const double v1 = (double)__uint_as_float((uint32_t)(h1[j] >> 32));
-      const bool d0 = ((uint32_t)h0[j] >> 31) != 0u, d1 = ((uint32_t)h1[j] >> 31) != 0u;
-      const double s = rows16_sum(v0 + v1);
-      const double q = rows16_sum((d0 ? 0.0 : v0 * v0) + (d1 ? 0.0 : v1 * v1));
-      const double a0 = readlane_d(s, 0) + readlane_d(s, 16), a1 = readlane_d(s, 32) + readlane_d(s, 48);
-      const double b0 = readlane_d(q, 0) + readlane_d(q, 16), b1 = readlane_d(q, 32) + readlane_d(q, 48);
-      ma = lane == 2 * j ? a0 : (lane == 2 * j + 1 ? a1 : ma);
-      mb = lane == 2 * j ? b0 : (lane == 2 * j + 1 ? b1 : mb);
+    for (int j = 0; j < BS_QUADS; ++j) {
+      double v[4], q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u] = (double)__uint_as_float((uint32_t)(h[j][u] >> 32));
+        q[u] = ((uint32_t)h[j][u] >> 31) != 0u ? 0.0 : v[u] * v[u];
+      }
+      const double s = rows16_sum((v[0] + v[1]) + (v[2] + v[3]));
+      const double t = rows16_sum((q[0] + q[1]) + (q[2] + q[3]));
+      const double a0 = readlane_d(s, 0), a1 = readlane_d(s, 16), a2 = readlane_d(s, 32), a3 = readlane_d(s, 48);
+      const double b0 = readlane_d(t, 0), b1 = readlane_d(t, 16), b2 = readlane_d(t, 32), b3 = readlane_d(t, 48);
+      if ((lane >> 2) == j) {
+        const int r = lane & 3;
+        ma = r == 0 ? a0 : r == 1 ? a1 : r == 2 ? a2 : a3;
+        mb = r == 0 ? b0 : r == 1 ? b1 : r == 2 ? b2 : b3;
+      }
     }
     if (lane < BPI && blk0 + lane < nblk) {
       const DD4 d{ma, 0.0, mb, 0.0};
