@@ -11,6 +11,10 @@
   (``_device_rows``: m/z slice, sort, images, scores) and reassembled by ``rows_to_frame`` gives the single-GPU
   table: the same index in the same order, and metrics equal to 1e-12 (the slice's block prefix sums start at
   other points, so tail-window sums may differ in the last bit; the count of bit-identical values is printed).
+* The whole table again with every ion forced onto each dense kernel (smg_debug_force_dense: 1 = the rank-indexed
+  wide pass, 2 = the pixel-indexed kernel), independent implementations of the same metrics: the same rows and
+  every metric of all ~0.95M rows within 1e-9 of the LDS passes' table (and, with the hot-spot clip, of each
+  other), a whole-table cross-check beyond the oracle sample.
 * ``estimate_fdr`` (fdr.py:70-88) of the full msm table (sf_image_metrics_est_fdr's join, its exact-zero ties)
   vs the oracle's pandas restatement: identical digitised FDR for every target ion, identical annotations at
   FDR 0.1.
@@ -51,7 +55,7 @@ def c3():
     cnt = (ims.hi - ims.lo).cpu().numpy()
     win_off = ims.ions_dev.win_off.cpu().numpy()
     return dict(ions=ions, peaks=peaks, formulas=formulas, conf=conf, dims=dims, df=df, df2=df2, cnt=cnt,
-                win_off=win_off, keys=ims.ion_keys)
+                win_off=win_off, keys=ims.ion_keys, dds=dds, sf_peak_df=sf_peak_df)
 
 
 def test_api_table_rows_are_ions_with_hits(c3):
@@ -118,6 +122,41 @@ def test_eight_way_shards_reassemble_single_gpu_table(c3):
     assert np.abs(a - b).max(initial=0.0) <= 1e-12
     print(f"8-way reassembly: {len(df):,} rows, {int((a == b).sum()):,} of {a.size:,} values bit-identical, "
           f"max |diff| {np.abs(a - b).max(initial=0.0):.3e}")
+
+
+def _forced_table(c3, mode, conf):
+    from sm_distributed_amd import _lib
+    from sm_distributed_amd.formula_imager_segm import compute_sf_images
+    from sm_distributed_amd.formula_img_validator import sf_image_metrics
+    L = _lib.lib()
+    L.smg_debug_force_dense(mode)
+    try:
+        ims = compute_sf_images(None, c3["dds"], c3["sf_peak_df"], PPM)
+        return sf_image_metrics(ims, None, c3["formulas"], c3["dds"], conf)
+    finally:
+        L.smg_debug_force_dense(0)
+
+
+@pytest.mark.timeout(900)
+def test_full_table_on_every_kernel(c3):
+    ref = c3["df"]
+    for mode in (1, 2):
+        df = _forced_table(c3, mode, c3["conf"])
+        assert df.index.equals(ref.index), f"forced mode {mode}: rows differ"
+        d = np.abs(df.to_numpy() - ref.to_numpy())
+        assert d.max(initial=0.0) <= 1e-9, (mode, float(d.max()))
+        print(f"forced dense mode {mode}: {len(df):,} rows, max |diff| vs the LDS passes {d.max(initial=0.0):.2e}")
+    # with the hot-spot clip (q99): the LDS passes, the wide pass and the pixel-indexed kernel agree on every row
+    clip = {"image_generation": dict(c3["conf"]["image_generation"], do_preprocessing=True)}
+    t0 = _forced_table(c3, 0, clip)
+    assert t0.index.equals(ref.index)
+    assert not np.allclose(t0.to_numpy(), ref.to_numpy()), "the clip must change some metric"
+    for mode in (1, 2):
+        df = _forced_table(c3, mode, clip)
+        assert df.index.equals(t0.index), f"clip, forced mode {mode}: rows differ"
+        d = np.abs(df.to_numpy() - t0.to_numpy())
+        assert d.max(initial=0.0) <= 1e-9, (mode, float(d.max()))
+        print(f"clip q99, forced dense mode {mode}: max |diff| vs the LDS passes {d.max(initial=0.0):.2e}")
 
 
 @pytest.mark.timeout(900)
