@@ -4,7 +4,7 @@
 * ``compute_sf_images(None, ResidentDataset(peaks), formulas.get_sf_peak_df(), 2.0)`` + ``sf_image_metrics(...)``
   with ``FormulasSegm.from_ion_table`` (bench.py's step; formula_imager_segm.py:142-161,
   formula_img_validator.py:93-122): the table's rows are exactly the ions with >= 1 non-empty window, and a seeded
-  576-ion sample across the whole m/z range (512 uniform + 64 planted) matches the oracle within 1e-5 in the
+  ~4600-ion sample across the whole m/z range (4096 uniform + 512 planted) matches the oracle within 1e-5 in the
   DataFrame.  This covers the device layout's fast paths (dense key table, stable compaction of ion_order),
   smg_align_windows, the PeakInts alignment and FrameIndex at 0.98M ions.
 * An 8-way plan (distributed.plan_shards): every rank's shard scored on this GPU by the product per-rank scorer
@@ -82,8 +82,8 @@ def test_api_table_rows_are_ions_with_hits(c3):
 def test_api_table_sample_matches_oracle(c3):
     ions, df = c3["ions"], c3["df"]
     rng = np.random.default_rng(2024)
-    pick = rng.choice(ions.n_ions, size=512, replace=False)
-    pick = np.unique(np.concatenate([pick, planted_ions(ions)[:64]]))
+    pick = rng.choice(ions.n_ions, size=4096, replace=False)
+    pick = np.unique(np.concatenate([pick, planted_ions(ions)[:512]]))
     first = ions.peak_mz[ions.win_off[:-1]][pick]
     assert first.min() < 250 and first.max() > 850, "sample must span the m/z range"
     rows, wins, sizes, npts, wall = oracle_rows(ions, pick, c3["peaks"], c3["dims"], PPM, NLEVELS)
