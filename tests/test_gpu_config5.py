@@ -12,8 +12,8 @@ pass with the pixel-indexed pass taking its rejects, scores), as rank r of the 8
   over the slice's sorted m/z: window membership bit-exact;
 * the shard's rows are exactly its ions with >= 1 non-empty window (formula_img_validator.py:115-118);
 * the rows of all 8 shards, reassembled by rows_to_frame (the rank-0 assembly), cover every ion with a hit once;
-* a seeded sample of every shard (8 uniform ions, planted targets, and ions of every pass that scored some: wide
-  pass and pixel-indexed pass, both polarities) is imaged and scored by the oracle from every point of its
+* a seeded sample of every shard (32 uniform ions, up to 8 planted targets, and ions of every pass that scored some: wide
+  pass and pixel-indexed pass, up to 4 each; both polarities) is imaged and scored by the oracle from every point of its
   windows (formula_imager_segm.py:66-92 + formula_img_validator.py:72-84): metrics within 1e-5.
 H1 (formula_imager_segm.py:68-69 chunking) does not arise: windows are complete on the device by construction.
 """
@@ -104,10 +104,10 @@ def test_config5_all_eight_shards(c5):
         wide = g[(glob >= 0) & ((fl & SMG_ION_WIDE) != 0)]
         pix = g[(glob >= 0) & ((fl & SMG_ION_DENSE) != 0) & ((fl & SMG_ION_WIDE) == 0)]
         lds = g[(glob >= 0) & ((fl & SMG_ION_DENSE) == 0)]
-        pick = [rng.choice(plan.ion_idx, size=8, replace=False), np.intersect1d(planted, plan.ion_idx)[:4]]
+        pick = [rng.choice(plan.ion_idx, size=32, replace=False), np.intersect1d(planted, plan.ion_idx)[:8]]
         for cat in (wide, pix, lds):
             if len(cat):
-                pick.append(rng.choice(cat, size=min(2, len(cat)), replace=False))
+                pick.append(rng.choice(cat, size=min(4, len(cat)), replace=False))
         picks.append(np.unique(np.concatenate(pick)))
         stats.append((r, n_shard, int(has.sum()), len(wide), len(pix), len(lds), sl.n_points, plan.mz_lo, plan.mz_hi))
         rows_all.append(rows)
