@@ -80,6 +80,8 @@ def parse():
                          "--shard-rank): one rank of a multi-GPU run measured alone")
     ap.add_argument("--shard-rank", type=int, default=0)
     ap.add_argument("--dry-run", action="store_true", help="stop every rank before GPU initialisation")
+    ap.add_argument("--legacy-main", action="store_true",
+                    help="A/B: the main pass on ion_pipe_kernel<512> instead of ion_sparse_kernel (smg_debug_main_kernel(0))")
     args = ap.parse_args()
     if args.config == "5":
         for k, v in CONFIG5.items():
@@ -244,6 +246,8 @@ def main():
 
     # ---- the metric: timed API steps --------------------------------------------------------------------
     L = _lib.lib()
+    if args.legacy_main:
+        _lib_check(L.smg_debug_main_kernel(0))
     # the pass timers (HIP events around every pass launch) are on from the warm-up: their first event creations,
     # which may reach the device while a persistent pass runs, fall in the warm-up
     timers = not os.environ.get("SMG_BENCH_NO_TIMERS")  # (A/B: the timed steps without pass timers)
@@ -529,13 +533,17 @@ def pass_roofline(args, pass_ms, chain, is_single):
         return None, passes
     dom = max(scoring, key=lambda d: d["ms_avg"])
     name = _lib.PASS_NAMES[dom["pass"]]
+    legacy_main = not chain.get("main_pass_sparse", True)  # smg_debug_main_kernel(0): ion_pipe_kernel<512> ran
+    if legacy_main and dom["pass"] == _lib.SMG_PASS_MAIN:
+        name = "ion_pipe_kernel<512> (main LDS pass)"
     # the LDS passes leave their scores' arithmetic to ion_finalize_kernel (a few per cent of their work): its
     # whole time is charged to the dominant LDS pass, so the roofline does not gain from moving work out of it
     fin = passes.get(_lib.PASS_NAMES[_lib.SMG_PASS_FINALIZE])
     fin_ms = fin["ms_avg"] if fin and dom["pass"] in (_lib.SMG_PASS_MAIN, _lib.SMG_PASS_BIG) else 0.0
     ms_charged = dom["ms_avg"] + fin_ms
     ach = ALG_BYTES_PER_POINT * dom["window_points"] / (ms_charged * 1e-3) / 1e9
-    key = {1: "ion_pipe_kernel[512]", 2: "ion_pipe_kernel[1024]", 3: "ion_wide_kernel", 4: "ion_dense_kernel"}
+    key = {1: "ion_pipe_kernel[512]" if legacy_main else "ion_sparse_kernel", 2: "ion_pipe_kernel[1024]",
+           3: "ion_wide_kernel", 4: "ion_dense_kernel"}
     traffic, src = measured_traffic(key[dom["pass"]], "config5" if args.config == "5" else "config3") \
         if is_single else (None, None)
     roofline = {"bound": "hbm", "kernel": name, "achieved": ach, "peak": HBM_PEAK_GBS,
@@ -611,7 +619,7 @@ def device_chain(args, peaks, formulas, plan):
     stages = {nm: float(np.mean([e[j].elapsed_time(e[j + 1]) for e in events])) for j, nm in enumerate(names)}
     return {"ms_per_step": ms, "ions_per_s": n_scored / (ms * 1e-3), "n_scored": n_scored, "stages_ms": stages,
             "sum_window_points": sum_hits, "n_points": pk.n_points, "pass_window_points": pass_pts,
-            "pass_ions": pass_ions}
+            "pass_ions": pass_ions, "main_pass_sparse": bool(((fl & _lib.SMG_ION_SPARSE) != 0).any())}
 
 
 def measured_traffic(kernel, workload):

@@ -40,6 +40,7 @@ extern "C" {
 #define SMG_ION_BIG 0x8u         /* scored by the big-ion LDS pass (1024-thread workgroup, whole LDS) */
 #define SMG_ION_TWO_LEVEL 0x10u  /* LDS pass with the two-level pixel set (images > 2^18 pixels) */
 #define SMG_ION_WIDE 0x20u       /* dense path, rank-indexed wide pass (LDS presence bitmap + rank prefix) */
+#define SMG_ION_SPARSE 0x40u     /* main pass with the sparse principal set (ion_sparse_kernel, 256-thread workgroups) */
 
 /* hit formats accepted by smg_ion_metrics */
 #define SMG_HITS_PACKED_F32 0    /* uint64: low 32 bits pixel index, high 32 bits float32 intensity */
@@ -203,10 +204,20 @@ int smg_debug_force_dense(int32_t on);
 /* smg_sort_points' implementation: 1 = the hand-written sort (default), 0 = rocPRIM's onesweep radix sort (kept for
  * A/B timing; smg_sort_points_flag always uses the hand-written one).  Process-wide; returns 0. */
 int smg_debug_sort_impl(int32_t which);
+/* The main LDS pass: 1 = ion_sparse_kernel where it applies (default: packed f32 hits, no hot-spot clip, images up
+ * to 2^18 pixels whose rows fit its chaos bands), 0 = ion_pipe_kernel<512> for every image (kept for A/B timing and
+ * so that the parity suite covers both).  Process-wide; returns 0. */
+int smg_debug_main_kernel(int32_t which);
+/* Diagnostic builds only (-DSMG_STAMPS, libsmg_stamps.so): per-phase cycles of the main passes summed over their
+ * workgroups since the last call (ion_pipe_kernel: smg_debug_stamps; ion_sparse_kernel: smg_debug_sparse_stamps),
+ * reset on read; SMG_ERR_UNSUPPORTED in the shipped build. */
+int smg_debug_stamps(unsigned long long* host_out, int n);
+int smg_debug_sparse_stamps(unsigned long long* host_out, int n);
 
 /* passes of smg_ion_metrics, as reported by smg_debug_pass_times */
 #define SMG_PASS_DESC 0   /* ion descriptors (ion_desc8_kernel) */
-#define SMG_PASS_MAIN 1   /* main LDS pass (ion_pipe_kernel<512>, two workgroups per CU) */
+#define SMG_PASS_MAIN 1   /* main LDS pass: ion_sparse_kernel (four 256-thread workgroups per CU, SMG_ION_SPARSE)
+                             or, where it does not apply / smg_debug_main_kernel(0), ion_pipe_kernel<512> */
 #define SMG_PASS_BIG 2    /* big-ion LDS pass over the main pass's rejects (ion_pipe_kernel<1024>): SMG_ION_BIG */
 #define SMG_PASS_WIDE 3   /* rank-indexed wide pass (ion_wide_kernel): SMG_ION_WIDE */
 #define SMG_PASS_DENSE 4  /* pixel-indexed pass (ion_dense_kernel): SMG_ION_DENSE without SMG_ION_WIDE */

@@ -18,12 +18,13 @@ SMG_ION_CHAOS_NAN = 0x4
 SMG_ION_BIG = 0x8
 SMG_ION_TWO_LEVEL = 0x10
 SMG_ION_WIDE = 0x20
+SMG_ION_SPARSE = 0x40
 SMG_HITS_PACKED_F32 = 0
 PIXEL_MASK = 0x7FFFFFFF   # bit 31 of the pixel field = duplicate-candidate flag
 SMG_HITS_SPLIT_F64 = 1
 # pass ids of smg_debug_pass_times
 SMG_PASS_DESC, SMG_PASS_MAIN, SMG_PASS_BIG, SMG_PASS_WIDE, SMG_PASS_DENSE, SMG_PASS_FINALIZE = range(6)
-PASS_NAMES = {0: "ion_desc8_kernel", 1: "ion_pipe_kernel<512> (main LDS pass)",
+PASS_NAMES = {0: "ion_desc8_kernel", 1: "ion_sparse_kernel (main LDS pass)",
               2: "ion_pipe_kernel<1024> (big-ion LDS pass)", 3: "ion_wide_kernel (wide pass)",
               4: "ion_dense_kernel (pixel-indexed pass)", 5: "ion_finalize_kernel (LDS passes' scores)"}
 
@@ -58,6 +59,9 @@ PROTOTYPES = {
     "smg_debug_force_two_level": (ctypes.c_int, [_I32]),
     "smg_debug_force_dense": (ctypes.c_int, [_I32]),
     "smg_debug_sort_impl": (ctypes.c_int, [_I32]),
+    "smg_debug_main_kernel": (ctypes.c_int, [_I32]),
+    "smg_debug_stamps": (ctypes.c_int, [_P, ctypes.c_int]),
+    "smg_debug_sparse_stamps": (ctypes.c_int, [_P, ctypes.c_int]),
     "smg_debug_time_main_pass": (ctypes.c_int, [_I32]),
     "smg_debug_main_pass_times": (ctypes.c_int, [_P, _I32, ctypes.POINTER(_I32)]),
     "smg_debug_pass_times": (ctypes.c_int, [_P, _P, _I32, ctypes.POINTER(_I32)]),

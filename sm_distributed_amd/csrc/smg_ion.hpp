@@ -316,4 +316,29 @@ __device__ __forceinline__ bool desc_lds_ok(const IonDesc* D, int capc) {
   return K >= 1 && K <= MAXK && D->end[0] <= capc && D->ngroups >= 0;
 }
 
+// (key, f64 sum) open-addressing table in LDS (empty key 0xFFFFFFFF): adds v to key's sum; false when full
+template <int NSLOT>
+__device__ __forceinline__ bool tbl_add(uint32_t* keys, double* vals, uint32_t key, double v) {
+  uint32_t h = (key * 2654435761u) >> (32 - __builtin_ctz(NSLOT));
+  for (int probe = 0; probe < NSLOT; ++probe) {
+    const uint32_t old = atomicCAS(&keys[h], 0xFFFFFFFFu, key);
+    if (old == 0xFFFFFFFFu || old == key) {
+      atomicAdd(&vals[h], v);
+      return true;
+    }
+    h = (h + 1) & (NSLOT - 1);
+  }
+  return false;
+}
+
+// ---- the sparse main pass (smg_sparse.hip) ----------------------------------------------------------------
+// true when the 256-thread sparse-set main pass takes this image geometry (packed hits, no clip, <= 2^18 pixels,
+// chaos bands of >= 8 rows); launch_sparse_main launches it with the main pass's interface (positions it cannot
+// score go to rej_list / rej_count for the big-ion pass)
+bool sparse_main_fits(const Params& P);
+int launch_sparse_main(Hits<SMG_HITS_PACKED_F32> hits, IonDesc* desc, Sched S, const Params& P, double* oc,
+                       double* osp, double* osc, double* omsm, uint32_t* oflags, uint32_t* rej_list,
+                       uint32_t* rej_count, int cus, hipStream_t st);
+int sparse_read_stamps(unsigned long long* host_out, int n);
+
 }  // namespace smg

@@ -554,20 +554,6 @@ __device__ void select_batch(Visit&& visit, int nsets, const int* n, double q, d
 }
 
 // open-addressing f64 accumulators keyed by u32 (EMPTY = 0xFFFFFFFF); returns false when full
-template <int NSLOT>
-__device__ __forceinline__ bool tbl_add(uint32_t* keys, double* vals, uint32_t key, double v) {
-  uint32_t h = (key * 2654435761u) >> (32 - __builtin_ctz(NSLOT));
-  for (int probe = 0; probe < NSLOT; ++probe) {
-    const uint32_t old = atomicCAS(&keys[h], 0xFFFFFFFFu, key);
-    if (old == 0xFFFFFFFFu || old == key) {
-      atomicAdd(&vals[h], v);
-      return true;
-    }
-    h = (h + 1) & (NSLOT - 1);
-  }
-  return false;
-}
-
 
 // (sum v, sum v^2 of unflagged points) over the points [i & ~63, i) of hit i's 64-point block
 template <int FMT>
@@ -1798,7 +1784,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
           rowcol(p, P, rp, cp);
           const int clo = 2 - cp > 0 ? 2 - cp : 0, chi = P.ncols - cp + 2 < 5 ? P.ncols - cp + 2 : 5;
           const uint32_t cv5 = ((1u << chi) - 1u) & ~((1u << clo) - 1u);  // columns cp-2..cp+2 in the image
-          uint32_t Lrow[5];
+          uint64_t Lrow[5];  // 8 bits per column: level indices go up to nlevels <= 254
 #pragma unroll
           for (int d = 0; d < 5; ++d) {
             const int row = rp - 2 + d;
@@ -1817,18 +1803,18 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
               r1 = pf[w + 1];
             }
             const uint32_t bits = rv ? (uint32_t)((b ? ((w0 >> b) | (w1 << (64 - b))) : w0) & 31u) & cv5 : 0u;
-            uint32_t packed = 0;
+            uint64_t packed = 0;
             for (uint32_t rest = bits; rest; rest &= rest - 1u) {
               const int j = __builtin_ctz(rest);
               const int bj = b + j;  // bit of column cp-2+j in w0 (bj < 64) or w1
               const int r = bj < 64 ? r0 + __popcll(w0 & ((1ull << bj) - 1ull))
                                     : r1 + __popcll(w1 & ((1ull << (bj - 64)) - 1ull));
               const uint32_t L = lazyL ? (uint32_t)level_fast(vals[r], vmax, P) : (uint32_t)Lv[r];
-              packed |= L << (6 * j);
+              packed |= (uint64_t)L << (8 * j);
             }
             Lrow[d] = packed;
           }
-#define SMG_L(r, cc) ((Lrow[r] >> (6 * (cc))) & 63u)
+#define SMG_L(r, cc) ((uint32_t)((Lrow[r] >> (8 * (cc))) & 0xFFull))
           int mn = 1 << 20;
           bool outside = false;
 #pragma unroll
@@ -4012,6 +3998,7 @@ using BigLay = Lay<BIG_BLOCK / WAVE, BIG_BLOCK * BIG_RMAX>;
 static constexpr int BIG2_RMAX = 4;
 using Main2Lay = Lay2<MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX>;
 using Big2Lay = Lay2<BIG_BLOCK / WAVE, BIG_BLOCK * BIG2_RMAX>;
+static int g_main_kernel = 1;      // smg_debug_main_kernel: 1 the sparse main pass where it applies, 0 ion_pipe_kernel
 static int g_force_two_level = 0;  // smg_debug_force_two_level: two-level passes for every image size
 static int g_force_dense = 0;      // smg_debug_force_dense: 1 every ion on the dense path, 2 pixel-indexed only
 // smg_debug_time_main_pass: HIP events recorded on the launch stream around every pass launch of
@@ -4125,7 +4112,11 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   const size_t wide_max = P.clip ? WIDE_LDS_MAX_CLIP : WIDE_LDS_MAX;
   const bool wide_fits = g_force_dense != 2 && wide_lds_bytes(P.npx) <= wide_max;
   const bool lds_ok = two ? (!wide_fits || g_force_two_level) : P.npx <= NPX_LDS_MAX;
-  const bool main_ok = !g_force_dense && lds_ok && lds_main <= MAIN_LDS;
+  // the main pass: ion_sparse_kernel (four 256-thread workgroups per CU, a sparse principal set) where it applies,
+  // else ion_pipe_kernel<512>; either hands its rejects (positions) to the big-ion pass
+  const bool sparse = FMT == SMG_HITS_PACKED_F32 && g_main_kernel == 1 && !g_force_dense && !two &&
+                      sparse_main_fits(P);
+  const bool main_ok = !g_force_dense && lds_ok && (sparse || lds_main <= MAIN_LDS);
   const bool big_ok = !g_force_dense && lds_ok && lds_big <= BIG_LDS;
   const int cus = device_cus();
   if (main_ok || big_ok) {
@@ -4141,9 +4132,16 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
                          hi, ion_off, theor, reinterpret_cast<const DD4*>(hit_cum), ion_order, n_ions, desc);
     SMG_LAUNCH_CHECK();
   }
-  if (main_ok) {
+  if (main_ok && sparse) {
     Sched SA{n_ions, hdr + HDR_XCD, nullptr, nullptr};
-    auto k1 = P.clip ? (two ? &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, true, true>
+    PassTimer tm(SMG_PASS_MAIN, st);
+    if constexpr (FMT == SMG_HITS_PACKED_F32) {
+      const int rc = launch_sparse_main(hits, desc, SA, P, oc, osp, osc, omsm, oflags, list_a, hdr + 0, cus, st);
+      if (rc != SMG_OK) return rc;
+    }
+  } else if (main_ok) {
+    Sched SA{n_ions, hdr + HDR_XCD, nullptr, nullptr};
+    auto k1 =P.clip ? (two ? &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, true, true>
                             : &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, false, true>)
                      : (two ? &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, true>
                             : &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, false>);
@@ -4257,6 +4255,14 @@ int smg_debug_wide_check(unsigned long long* host_out) {
   return SMG_OK;
 }
 #endif
+
+int smg_debug_main_kernel(int32_t which) {
+  SMG_CHECK_ARG(which == 0 || which == 1, "main kernel must be 0 (ion_pipe_kernel) or 1 (ion_sparse_kernel)");
+  g_main_kernel = which;
+  return SMG_OK;
+}
+
+int smg_debug_sparse_stamps(unsigned long long* host_out, int n) { return sparse_read_stamps(host_out, n); }
 
 int smg_debug_force_two_level(int32_t on) {
   g_force_two_level = on ? 1 : 0;

@@ -1,0 +1,1080 @@
+// Sparse-set main pass (ion_sparse_kernel): the fused imaging + MSM scoring of ion_pipe_kernel (smg_metrics.hip)
+// with a per-ion LDS footprint that does not grow with the image.
+//
+// Replaces, in frulo/SM_distributed (the same rows as ion_pipe_kernel):
+//   formula_imager_segm.py:84-92   per-window COO construction   (_gen_iso_images)
+//   formula_img_validator.py:72-84 compute(): spectral / spatial / chaos (pyImagingMSpec / cpyImagingMSpec restated)
+//
+// Why: ion_pipe_kernel keeps the principal image as an image-sized presence bitmap + rank prefix (39 KB at 500x500
+// px) plus f64 values: 78 KB per 512-thread workgroup, two per CU.  The same code at 256 threads and four
+// workgroups per CU ran 1.47x faster where its LDS fits (profiles/round5/r5_occupancy_ab.txt).  This kernel gets
+// there at 500x500 px: 40,448 B per 256-thread workgroup, four per CU.
+//
+// Per-ion structures (LDS):
+//  * entries: the principal window's points sorted by (pixel, window position), one u32 per point -- the pixel,
+//    with bit 31 set on every point after the first of its pixel (a "hole": coo.toarray() sums it into the first);
+//  * dir: a bucket directory over 2^bs-pixel buckets (<= 1024 of them): entries [dir[b], dir[b+1]) hold bucket b's
+//    pixels.  A pixel's rank (entry index) is found by a short scan of its bucket;
+//  * values: f32 per entry (the packed hits carry f32 intensities, so a single point's value is exact); a pixel
+//    with several points keeps its f64 sum -- summed in window order, as coo.toarray() adds them -- in a side table
+//    its entry points to;
+//  * a blocked Bloom filter (2^15 bits, two bits per pixel in one word) answers the tail stream's membership test
+//    with one LDS read; its positives (~1% false) are resolved exactly after the stream, as ion_pipe_kernel resolves
+//    its parked principal hits;
+//  * chaos: the level index per entry (u8); the 7x7 screen reads presence rows from band bitmaps rebuilt, band by
+//    band, in the LDS the values and the filter leave behind (two bands at 500x500); candidates' exact eL and the
+//    Kruskal pass look pixels up in the directory / a candidate hash, never in an image-sized array.
+// Everything else (software pipeline with counted waits, the tail stream of window-aligned 64-point groups with
+// parked events, the flagged-point lists and table, the threshold-decomposition chaos, the record for
+// ion_finalize_kernel) is ion_pipe_kernel's.
+#include "smg_common.hpp"
+#include "smg_ion.hpp"
+
+namespace smg {
+
+#ifdef SMG_STAMPS
+__device__ unsigned long long g_sp_stamps[16];
+#define SP_STAMP_DECL()                                            \
+  __shared__ unsigned long long _sacc[16];                         \
+  unsigned long long _st0 = 0, _st1 = 0;                           \
+  if (threadIdx.x == 0) {                                          \
+    for (int _i = 0; _i < 16; ++_i) _sacc[_i] = 0;                 \
+    _st0 = __builtin_amdgcn_s_memtime();                           \
+  }
+#define SP_STAMP(i)                                                \
+  do {                                                             \
+    if (threadIdx.x == 0) {                                        \
+      _st1 = __builtin_amdgcn_s_memtime();                         \
+      _sacc[i] += _st1 - _st0;                                     \
+      _st0 = _st1;                                                 \
+    }                                                              \
+  } while (0)
+#define SP_STAMP_FLUSH()                                           \
+  do {                                                             \
+    if (threadIdx.x == 0)                                          \
+      for (int _i = 0; _i < 16; ++_i) atomicAdd(&g_sp_stamps[_i], _sacc[_i]); \
+  } while (0)
+#else
+#define SP_STAMP_DECL()
+#define SP_STAMP(i)
+#define SP_STAMP_FLUSH()
+#endif
+
+namespace {
+
+constexpr int SP_BLOCK = 256, SP_RMAX = 10, SP_RC = 2, SP_WPE = 4, SP_WGPCU = 4;
+constexpr int SP_NW = SP_BLOCK / WAVE;
+constexpr int SP_CAPC = SP_BLOCK * SP_RMAX;  // principal points per ion (more: the big-ion pass)
+constexpr int SP_NBMAX = 1024;               // bucket directory entries
+constexpr int SP_FWORDS = 1024;              // Bloom filter: 2^15 bits
+constexpr int SP_DSEG = 64;                  // deferred flagged tail points per wave
+constexpr int SP_DTBL = 256;                 // their (pixel, window)-keyed sums
+constexpr int SP_SIDE = 336;                 // f64 sums of pixels with >= 2 principal points
+constexpr int SP_CCAP = 768;                 // chaos survivors + candidates
+constexpr int SP_HSZ = 2048;                 // Kruskal: candidate hash
+constexpr int SP_BMAX = 128;                 // points per bucket (more: the big-ion pass)
+constexpr uint32_t SP_HOLE = 0x80000000u;
+constexpr uint32_t SP_SIDEREF = 0xFFF00000u;  // an f32 NaN pattern: the entry's value is side[w & 0xFFFFF]
+constexpr uint32_t SP_EMPTY = 0xFFFFFFFFu;
+constexpr uint32_t SP_LDS_BYTES = 40448;      // 4 x 40,448 B <= 160 KiB: four workgroups per CU
+enum { S_NE = 0, S_EMAX, S_ABORT, S_SIDE, S_NEXT, S_NS, S_MAXB, S_NCTR = 8 };
+
+constexpr uint32_t c16(uint32_t x) { return (x + 15u) & ~15u; }
+
+// LDS carve (bytes).  A persistent part, then a region U with two views: the principal / tail view (Bloom filter,
+// values, bucket counters inside the values' space, flagged-point lists and table, side sums) and the chaos view (band bitmap
+// or candidate hash + union-find at its start, the survivor / candidate list at its end).  The end-of-ion clear
+// zeroes the filter and the counters only, both inside the band space: the chaos list at U's end stays intact for
+// wave 0's few-candidate Kruskal while the other waves clear.
+struct SpLay {
+  static constexpr uint32_t o_ekey = 0;
+  static constexpr uint32_t o_L = o_ekey + SP_CAPC * 4;
+  static constexpr uint32_t o_dir = c16(o_L + SP_CAPC);
+  static constexpr uint32_t o_part = c16(o_dir + (SP_NBMAX + 2) * 2);
+  static constexpr uint32_t o_red = c16(o_part + MAXK * SP_NW * 4 * 8);
+  static constexpr uint32_t o_ctr = c16(o_red + 8 * SP_NW * 8);
+  static constexpr uint32_t o_wsc = c16(o_ctr + S_NCTR * 4);
+  static constexpr uint32_t o_desc = c16(o_wsc + SP_NW * 4);
+  static constexpr uint32_t o_U = c16(o_desc + 2 * 384);
+  // principal / tail view
+  static constexpr uint32_t o_F = o_U;
+  static constexpr uint32_t o_evals = o_F + SP_FWORDS * 4;
+  static constexpr uint32_t o_cnt = o_evals;  // bucket counters: build only (the values are written after)
+  static constexpr uint32_t o_dkey = c16(o_evals + SP_CAPC * 4);
+  static constexpr uint32_t o_dval = c16(o_dkey + SP_NW * SP_DSEG * 4);
+  static constexpr uint32_t o_dcnt = c16(o_dval + SP_NW * SP_DSEG * 8);
+  static constexpr uint32_t o_tkey = c16(o_dcnt + SP_NW * 4);
+  static constexpr uint32_t o_tval = c16(o_tkey + SP_DTBL * 4);
+  static constexpr uint32_t o_side = c16(o_tval + SP_DTBL * 8);  // read until the levels are computed
+  static constexpr uint32_t o_tend = c16(o_side + SP_SIDE * 8);
+  // chaos view
+  static constexpr uint32_t o_cel = SP_LDS_BYTES - SP_CCAP;
+  static constexpr uint32_t o_clist = o_cel - SP_CCAP * 4;
+  static constexpr uint32_t o_band = o_U;  // guard word, then the band's bits
+  static constexpr uint32_t o_hash = o_U;
+  static constexpr uint32_t o_par = o_hash + SP_HSZ * 4;
+  // data words of a band: a guard word in front, two zero words behind, and the uint4 rounding of the zeroing
+  static constexpr int band_words = (int)((o_clist - o_band) / 4) - 6;
+  static_assert(o_tend <= SP_LDS_BYTES, "principal / tail view fits");
+  static_assert(o_cnt + SP_NBMAX * 4 <= o_dkey, "bucket counters inside the values' space");
+  static_assert(o_par + SP_CCAP * 4 <= o_clist, "Kruskal hash + union-find below the chaos list");
+  static_assert(o_F + SP_FWORDS * 4 <= o_clist && o_cnt + SP_NBMAX * 4 <= o_clist, "cleared words below the list");
+  static_assert(SP_LDS_BYTES % 512 == 0 && 4 * SP_LDS_BYTES <= 160 * 1024, "four workgroups per CU");
+};
+
+struct SpGeo {
+  int32_t bs;         // bucket = pixel >> bs
+  int32_t band_rows;  // image rows screened per chaos band
+};
+
+__device__ __forceinline__ uint32_t sp_hash(uint32_t p) { return __umul24(p, 0x9E37B1u) ^ (p >> 14); }
+__device__ __forceinline__ uint32_t sp_fword(uint32_t h) { return (h >> 6) & (uint32_t)(SP_FWORDS - 1); }
+__device__ __forceinline__ uint32_t sp_fmask(uint32_t h) { return (1u << (h & 31u)) | (1u << ((h >> 16) & 31u)); }
+
+__device__ __forceinline__ double sp_val(uint32_t w, const double* side) {
+  return (w & 0xFFF00000u) == SP_SIDEREF ? side[w & 0xFFFFFu] : (double)__uint_as_float(w);
+}
+
+// entry index of principal pixel p (-1: not in the principal image); holes never match
+__device__ __forceinline__ int sp_lookup(const uint32_t* ekey, const uint16_t* dir, uint32_t p, int bs) {
+  const uint32_t b = p >> bs;
+  int i = dir[b];
+  const int e = dir[b + 1];
+  for (; i < e; ++i) {
+    const uint32_t w = ekey[i];
+    if (w == p) return i;
+    if ((w & ~SP_HOLE) > p) break;
+  }
+  return -1;
+}
+
+// level_fast with the division v / vmax replaced by v * (1 / vmax) where that cannot change the answer: the two
+// level comparisons that decide it must hold with a margin above the product's error (<= 2 ulp), else the exact
+// division decides.  Returns exactly level_fast(v, vmax, P) (= #{i : linspace(0,1,n)[i] < v / vmax}, v <= vmax).
+__device__ __forceinline__ int sp_level(double v, double vmax, double rcp, const Params& P) {
+  const int n = P.nlevels;
+  if (n == 1 || !(v > 0.0)) return level_fast(v, vmax, P);
+  const double na = v * rcp;
+  if (!(na < 1.0 - 1e-12)) return level_fast(v, vmax, P);
+  const double tol = na * 1e-15;
+  int j = (int)(na * (double)(n - 1));
+  j = j < 0 ? 0 : (j > n - 1 ? n - 1 : j);
+  while (j > 0 && !((double)(j - 1) * P.step < na)) --j;
+  while (j < n - 1 && (double)j * P.step < na) ++j;
+  const bool lo_ok = j == 0 || (double)(j - 1) * P.step < na - tol;
+  const bool hi_ok = j == n - 1 || (double)j * P.step >= na + tol;
+  return (lo_ok && hi_ok) ? j : level_fast(v, vmax, P);
+}
+
+template <int LB, int RMAX, int RC, int WPE>
+__global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
+    Hits<SMG_HITS_PACKED_F32> hits, IonDesc* __restrict__ desc, Sched S, Params P, SpGeo G, double* __restrict__ oc,
+    double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags,
+    uint32_t* __restrict__ rej_list, uint32_t* __restrict__ rej_count) {
+  using H = Hits<SMG_HITS_PACKED_F32>;
+  using Reg = uint64_t;
+  constexpr int BLOCK = LB;
+  constexpr int NW = LB / WAVE;
+  constexpr int GPC = BLOCK * RC / 64;  // 64-point groups per chunk
+  constexpr int CAPC = BLOCK * RMAX;
+  static_assert(CAPC == SP_CAPC && NW == SP_NW, "layout geometry");
+  static_assert(RMAX >= 2 * RC, "principal slots double as two tail buffers");
+  static_assert(NW * SP_DSEG == BLOCK, "one deferred-list slot per thread");
+  static_assert(SP_NBMAX == 4 * BLOCK, "four bucket counters per thread");
+  static_assert(CAPC <= 4096, "window positions in 12 bits of the sort key");
+  using LY = SpLay;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* ekey = reinterpret_cast<uint32_t*>(smem + LY::o_ekey);
+  uint8_t* L8 = smem + LY::o_L;
+  uint16_t* dir = reinterpret_cast<uint16_t*>(smem + LY::o_dir);
+  double* part = reinterpret_cast<double*>(smem + LY::o_part);  // [MAXK][NW][4]: s_k, sy, syy, sxy
+  double* red = reinterpret_cast<double*>(smem + LY::o_red);
+  double* side = reinterpret_cast<double*>(smem + LY::o_side);
+  int* ctr = reinterpret_cast<int*>(smem + LY::o_ctr);
+  int* wsc = reinterpret_cast<int*>(smem + LY::o_wsc);
+  IonDesc* dsl = reinterpret_cast<IonDesc*>(smem + LY::o_desc);
+  uint32_t* F = reinterpret_cast<uint32_t*>(smem + LY::o_F);
+  uint32_t* evals = reinterpret_cast<uint32_t*>(smem + LY::o_evals);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + LY::o_cnt);
+  uint32_t* dkey = reinterpret_cast<uint32_t*>(smem + LY::o_dkey);
+  double* dval = reinterpret_cast<double*>(smem + LY::o_dval);
+  int* dcnt = reinterpret_cast<int*>(smem + LY::o_dcnt);
+  uint32_t* tkey = reinterpret_cast<uint32_t*>(smem + LY::o_tkey);
+  double* tval = reinterpret_cast<double*>(smem + LY::o_tval);
+  uint32_t* clist = reinterpret_cast<uint32_t*>(smem + LY::o_clist);
+  uint8_t* cel = smem + LY::o_cel;
+  uint32_t* band = reinterpret_cast<uint32_t*>(smem + LY::o_band) + 1;  // band[-1]: zero guard word
+  uint32_t* htab = reinterpret_cast<uint32_t*>(smem + LY::o_hash);
+  uint32_t* par = reinterpret_cast<uint32_t*>(smem + LY::o_par);
+
+  // tid and lane are laundered at the top of every ion iteration (as in ion_pipe_kernel)
+  int tid = threadIdx.x;
+  int lane = tid & 63;
+  const int wid = uni(tid >> 6);
+  const int bs = G.bs;
+  const int nr = P.nrows, ncl = P.ncols;
+
+  // register buffers: tail chunks through a ring of four (pa, pb, pc, pd); the next ion's principal window arrives
+  // in pc, pd, pe (RMAX slots), which become tail buffers once the principal build has consumed them
+  constexpr int RE = RMAX - 2 * RC > 0 ? RMAX - 2 * RC : 1;
+  Reg pa[RC], pb[RC], pc[RC], pd[RC], pe[RE];
+#pragma unroll
+  for (int j = 0; j < RC; ++j) pa[j] = pb[j] = pc[j] = pd[j] = 0ull;
+#pragma unroll
+  for (int j = 0; j < RE; ++j) pe[j] = 0ull;
+  auto hs = [&](int j) -> Reg& { return j < RC ? pc[j] : (j < 2 * RC ? pd[j - RC] : pe[j - 2 * RC]); };
+  // every slot issues exactly one load (clamped to the window's last point, or hit 0 for an empty window), so that
+  // the counted waits hold on every path
+  auto issue_principal = [&](const IonDesc* D) {
+    const int n0 = D->end[0];
+    const int64_t a = D->base[0];
+#pragma unroll
+    for (int j = 0; j < RMAX; ++j) {
+      const int i = tid + j * BLOCK;
+      ld8_async_v(hs(j), hits.h + (n0 > 0 ? a + min(i, n0 - 1) : 0));
+    }
+  };
+  // tail chunk c: groups [c*GPC, (c+1)*GPC); slot j of wave w holds group c*GPC + j*NW + w; exactly RC loads
+  auto issue_chunk = [&](const IonDesc* D, int c, Reg (&buf)[RC]) {
+    const int ng = D->ngroups;
+    int gsv[MAXK];
+#pragma unroll
+    for (int kk = 2; kk < MAXK; ++kk) gsv[kk] = D->gs[kk];
+#pragma unroll
+    for (int j = 0; j < RC; ++j) {
+      const int Gi = c * GPC + j * NW + wid;
+      int k = 1;
+#pragma unroll
+      for (int kk = 2; kk < MAXK; ++kk) k += (Gi >= gsv[kk]) ? 1 : 0;
+      const int64_t bk = D->base[k];
+      const int ek = D->end[k];
+      const int64_t idx = Gi < ng ? bk + (int64_t)Gi * 64 + min(lane, ek - Gi * 64 - 1) : 0;
+      ld8_async_v(buf[j], hits.h + idx);
+    }
+  };
+
+  SP_STAMP_DECL();
+  // the Bloom filter and the bucket counters start zeroed (here, then at the end of every ion that used them, by the
+  // waves other than wave 0 while it writes the record); the counters too
+  auto clear_fc = [&](int t0, int nt) {
+    uint4* zf = reinterpret_cast<uint4*>(F);
+    uint4* zc = reinterpret_cast<uint4*>(cnt);
+    for (int i = t0; i < SP_FWORDS / 4; i += nt) zf[i] = make_uint4(0, 0, 0, 0);
+    for (int i = t0; i < SP_NBMAX / 4; i += nt) zc[i] = make_uint4(0, 0, 0, 0);
+    if (t0 < S_NCTR && t0 != S_NEXT) ctr[t0] = 0;
+  };
+  auto clear_table = [&]() {
+    for (int i = tid; i < SP_DTBL; i += BLOCK) {
+      tkey[i] = 0xFFFFFFFFu;
+      tval[i] = 0.0;
+    }
+  };
+  clear_fc(tid, BLOCK);
+  if (tid == 0) ctr[S_NEXT] = (int)sched_resolve<SRC_RANGES>(S, sched_issue<SRC_RANGES>(S));
+  __syncthreads();
+  int64_t pos = -1;  // ion scored in this iteration (-1: none; the first iteration only issues loads)
+  int64_t npos = uni(ctr[S_NEXT]);
+  int cur = 0;
+  while (true) {
+    asm volatile("" : "+v"(tid));
+    asm volatile("" : "+v"(lane));
+    const IonDesc* D = &dsl[cur];
+    IonDesc* DN = &dsl[cur ^ 1];
+    // the ticket of the ion after npos, consumed after the principal build (wave 0 issues after it exactly one
+    // descriptor load, then the 2*RC loads of tail chunks 2 and 3 or their stand-ins)
+    uint32_t ticket = 0;
+    if (tid == 0) sched_issue_async<SRC_RANGES>(S, ticket);
+    uint64_t dword = 0;
+    if ((tid >> 6) == 0)
+      ld8_async_wave0(dword, reinterpret_cast<const uint64_t*>(desc + (npos >= 0 ? npos : 0)) +
+                                 (lane < DESC_QWORDS ? lane : 0));
+    bool skip = pos < 0;
+    int K = 0, ion = 0, n0 = 0;
+    auto reject = [&]() {
+      if (tid == 0) rej_list[atomicAdd(rej_count, 1u)] = (uint32_t)pos;
+    };
+    if (!skip) {
+      K = uni(D->K);
+      ion = uni(D->ion);
+      n0 = uni(D->end[0]);
+      if (K == 0) {
+        if (tid == 0) {
+          oc[ion] = osp[ion] = osc[ion] = omsm[ion] = 0.0;
+          oflags[ion] = 0;
+        }
+        skip = true;
+      } else if (!desc_lds_ok(D, CAPC)) {
+        reject();
+        skip = true;
+      }
+    }
+    const bool began = !skip;  // this ion uses the filter and the counters (cleared again at its end)
+    SP_STAMP(0);
+
+    // ---- principal image -> sorted entries, bucket directory, Bloom filter, values -------------------------------
+    // the principal statistics (sum x, sum x^2, sum x[x>0], #(x>0), max) over the image's pixels, per thread in a fixed
+    // order: single-point pixels from the registers, summed pixels by their first entry
+    double acc[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
+    auto stat = [&](double v) {
+      acc[0] += v;
+      acc[1] += v * v;
+      if (v > 0.0) {
+        acc[2] += v;
+        acc[3] += 1.0;
+      }
+      acc[4] = v > acc[4] ? v : acc[4];
+    };
+    uint32_t aw[(RMAX + 1) / 2];  // u16 pairs: a point's arrival index in its bucket, later its sorted entry index
+    uint32_t stbits = 0;          // 2 bits per slot: 0 single point, 1 first of several, 2 later point (hole)
+#pragma unroll
+    for (int j = 0; j < (RMAX + 1) / 2; ++j) aw[j] = 0u;
+    auto aw_get = [&](int j) -> uint32_t { return (aw[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; };
+    auto aw_set = [&](int j, uint32_t v) {
+      aw[j >> 1] = (aw[j >> 1] & ~(0xFFFFu << ((j & 1) * 16))) | (v << ((j & 1) * 16));
+    };
+    // the principal window was issued before this ion's tail chunks 0 and 1.  Waited on every path (a skipped
+    // position has nothing older in flight; the wait only gets stricter), so that the wait dominates every use of
+    // the principal registers in the separate blocks below
+    vm_wait<2 * RC>(pc);
+    vm_wait<2 * RC>(pd);
+    vm_wait<2 * RC>(pe);
+    if (!skip) {
+      for (int i = tid; i < MAXK * NW * 4; i += BLOCK) part[i] = 0.0;
+      bool bad = false;
+#pragma unroll
+      for (int j = 0; j < RMAX; ++j) {
+        const int i = tid + j * BLOCK;
+        if (i < n0) {
+          const uint32_t p = H::pix(hs(j));
+          const float v = __uint_as_float((uint32_t)(hs(j) >> 32));
+          if ((v != v) || p >= (uint32_t)P.npx) {  // NaN intensities / foreign pixels: the big-ion pass (f64 values)
+            bad = true;
+          } else {
+            const uint32_t h = sp_hash(p);
+            atomicOr(&F[sp_fword(h)], sp_fmask(h));
+            aw_set(j, atomicAdd(&cnt[p >> bs], 1u) & 0xFFFFu);
+          }
+        }
+      }
+      if (bad) ctr[S_ABORT] = 1;
+      __syncthreads();
+      if (ctr[S_ABORT]) {
+        reject();
+        skip = true;
+      }
+    }
+    if (!skip) {
+      // exclusive scan of the bucket counts -> dir (four counters per thread), and the largest bucket
+      const uint4 c4 = reinterpret_cast<const uint4*>(cnt)[tid];
+      const int tot = (int)(c4.x + c4.y + c4.z + c4.w);
+      const int mx = (int)max(max(c4.x, c4.y), max(c4.z, c4.w));
+      const int inc = wave_incl_scan_dpp(tot);
+      int wmx = mx;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) wmx = max(wmx, __shfl_xor(wmx, o, 64));
+      if (lane == 63) wsc[wid] = inc;
+      if (lane == 0 && wmx > SP_BMAX) ctr[S_MAXB] = 1;
+      __syncthreads();
+      int off = inc - tot;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) off += (w < wid) ? wsc[w] : 0;
+      const uint32_t d0 = (uint32_t)off, d1 = d0 + c4.x, d2 = d1 + c4.y, d3 = d2 + c4.z;
+      reinterpret_cast<uint2*>(dir)[tid] = make_uint2(d0 | (d1 << 16), d2 | (d3 << 16));
+      if (tid == BLOCK - 1) dir[SP_NBMAX] = (uint16_t)(d3 + c4.w);
+      __syncthreads();
+      if (ctr[S_MAXB]) {  // a crowded bucket (the sort below is quadratic in it): the big-ion pass
+        reject();
+        skip = true;
+      }
+    }
+    SP_STAMP(1);
+    if (!skip) {
+      // unsorted keys (pixel << 12 | window position) at the bucket's arrival slots ...
+#pragma unroll
+      for (int j = 0; j < RMAX; ++j) {
+        const int i = tid + j * BLOCK;
+        if (i < n0) {
+          const uint32_t p = H::pix(hs(j));
+          ekey[dir[p >> bs] + aw_get(j)] = (p << 12) | (uint32_t)i;
+        }
+      }
+      __syncthreads();
+      // ... each point's rank among its bucket's keys, and whether its pixel has other points before / after it
+#pragma unroll
+      for (int j = 0; j < RMAX; ++j) {
+        const int i = tid + j * BLOCK;
+        if (i < n0) {
+          const uint32_t p = H::pix(hs(j)), key = (p << 12) | (uint32_t)i;
+          const int s0 = dir[p >> bs], s1 = dir[(p >> bs) + 1];
+          int rank = 0;
+          bool before = false, after = false;
+          for (int k = s0; k < s1; ++k) {
+            const uint32_t w = ekey[k];
+            rank += w < key ? 1 : 0;
+            const bool same = (w >> 12) == p;
+            before |= same && w < key;
+            after |= same && w > key;
+          }
+          aw_set(j, (uint32_t)(s0 + rank));
+          stbits |= (before ? 2u : (after ? 1u : 0u)) << (2 * j);
+        }
+      }
+      __syncthreads();
+      // ... then the sorted entries and the values at them (a pixel's points are consecutive, first one first)
+#pragma unroll
+      for (int j = 0; j < RMAX; ++j) {
+        const int i = tid + j * BLOCK;
+        if (i < n0) {
+          const uint32_t p = H::pix(hs(j));
+          const uint32_t st = (stbits >> (2 * j)) & 3u;
+          const int f = (int)aw_get(j);
+          ekey[f] = p | (st == 2u ? SP_HOLE : 0u);
+          const uint32_t vb = (uint32_t)(hs(j) >> 32);
+          evals[f] = vb;
+          if (st == 0u) stat((double)__uint_as_float(vb));
+        }
+      }
+    }
+    // the principal registers are consumed: tail chunks 2 and 3 go in flight (or the same number of stand-in loads, so
+    // that the waits below count 2*RC younger loads on every path)
+    if (!skip) {
+      issue_chunk(D, 2, pc);
+      issue_chunk(D, 3, pd);
+    } else {
+#pragma unroll
+      for (int j = 0; j < RC; ++j) {
+        ld8_async_v(pc[j], hits.h);
+        ld8_async_v(pd[j], hits.h);
+      }
+    }
+    if (!skip) {
+      __syncthreads();
+      // pixels with several points: the f64 sum in window order (coo.toarray()), kept in the side table
+      for (int i = tid; i < n0; i += BLOCK) {
+        const uint32_t w = ekey[i];
+        if ((w & SP_HOLE) || i + 1 >= n0 || ekey[i + 1] != (w | SP_HOLE)) continue;
+        double s = (double)__uint_as_float(evals[i]);
+        for (int k = i + 1; k < n0 && ekey[k] == (w | SP_HOLE); ++k) s += (double)__uint_as_float(evals[k]);
+        const int slot = atomicAdd(&ctr[S_SIDE], 1);
+        if (slot < SP_SIDE) {
+          side[slot] = s;
+          evals[i] = SP_SIDEREF | (uint32_t)slot;
+        } else {
+          ctr[S_ABORT] = 1;
+        }
+        stat(s);
+      }
+    }
+    SP_STAMP(2);
+    // wave 0: the ticket and npos's descriptor (issued at the top of this iteration, before chunks 2 and 3 or their
+    // stand-ins); the test is on the laundered tid (an exec-masked branch: scripts/check_async_regs.py's wave-0 form)
+    if ((tid >> 6) == 0) {
+      vm_wait1<2 * RC>(ticket);
+      vm_wait1<2 * RC>(dword);
+      if (tid == 0) ctr[S_NEXT] = (int)sched_resolve<SRC_RANGES>(S, ticket);
+      if (npos >= 0 && lane < DESC_QWORDS) reinterpret_cast<uint64_t*>(DN)[lane] = dword;
+    }
+    __syncthreads();
+    const int64_t n2pos = uni(ctr[S_NEXT]);
+    if (!skip && ctr[S_ABORT]) {  // more summed pixels than the side table holds
+      reject();
+      skip = true;
+    }
+    // the statistics' per-wave sums into red, read after the tail stream's closing barrier
+    if (!skip) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = wave_sum_dpp(acc[q]);
+      acc[4] = wave_max_dpp(acc[4]);
+      if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < 5; ++q) red[q * NW + wid] = acc[q];
+      }
+    }
+    SP_STAMP(3);
+
+    // ---- tail windows, one stream of window-aligned 64-point groups ------------------------------------------------
+    if (!skip) {
+      const int ng = uni(D->ngroups);
+      int curk = 1;
+      int nd = 0;  // this wave's deferred flagged points (uniform)
+      uint32_t* wdkey = dkey + wid * SP_DSEG;
+      double* wdval = dval + wid * SP_DSEG;
+      int gnext = uni(D->gs[2]);
+      int wend = uni(D->end[1]);
+      // Events: a filter positive (the point's pixel may be principal: Σxy, Σy[x>0]) or a flagged point (summed per
+      // (pixel, window) before squaring).  Two per lane are parked in registers (the raw hit and its window, bit 4: a
+      // filter positive) and resolved after the stream for all lanes at once; a lane's third and later events are
+      // handled in place.  Partials: part[k][wid], written only by this wave, lanes of one instruction in hardware
+      // order -- deterministic.
+      Reg ev0 = 0ull, ev1 = 0ull;
+      int evk0 = 0, evk1 = 0, nev = 0;
+      auto add_x = [&](bool hit, int r, const Reg& h, int k) {
+        if (__ballot(hit)) {
+          if (hit) {
+            const double x = sp_val(evals[r], side);
+            const double v = H::val(h);
+            double* pk = part + ((size_t)k * NW + wid) * 4;
+            atomicAdd(&pk[3], x * v);
+            if (x > 0.0) atomicAdd(&pk[0], v);
+          }
+        }
+      };
+      auto handle = [&](bool pred, const Reg& h, int k, bool inb) {
+        const uint32_t p = H::pix(h);
+        const int r = (pred && inb) ? sp_lookup(ekey, dir, p, bs) : -1;
+        add_x(r >= 0, r, h, k);
+        const bool dup = pred && H::dup(h);
+        const uint64_t dm = __ballot(dup);
+        if (dm) {
+          const int e = nd + (int)__popcll(dm & ((1ull << lane) - 1ull));
+          if (dup && e < SP_DSEG) {
+            wdkey[e] = (p << 3) | (uint32_t)k;
+            wdval[e] = H::val(h);
+          }
+          nd += (int)__popcll(dm);
+        }
+      };
+      auto process = [&](int c, Reg (&buf)[RC]) {
+        uint32_t fw[RC], fm[RC];
+#pragma unroll
+        for (int j = 0; j < RC; ++j) {
+          const uint32_t h = sp_hash(H::pix(buf[j]));
+          fw[j] = F[sp_fword(h)];
+          fm[j] = sp_fmask(h);
+        }
+#pragma unroll
+        for (int j = 0; j < RC; ++j) {
+          const int Gi = c * GPC + j * NW + wid;
+          if (Gi < ng) {
+            while (Gi >= gnext) {  // this wave moves on to a later window (uniform)
+              ++curk;
+              gnext = curk + 1 < MAXK ? uni(D->gs[curk + 1]) : 0x7FFFFFFF;
+              wend = uni(D->end[curk]);
+            }
+            const bool valid = lane < wend - Gi * 64;
+            const Reg h = buf[j];
+            const bool in = valid && (fw[j] & fm[j]) == fm[j];
+            const bool ev = in || (valid && H::dup(h));
+            const bool s0 = ev && nev == 0, s1 = ev && nev == 1;
+            ev0 = s0 ? h : ev0;
+            evk0 = s0 ? (curk | (in ? 16 : 0)) : evk0;
+            ev1 = s1 ? h : ev1;
+            evk1 = s1 ? (curk | (in ? 16 : 0)) : evk1;
+            const bool ovf = ev && nev >= 2;
+            nev += ev ? 1 : 0;
+            if (__ballot(ovf)) handle(ovf, h, curk, in);
+          }
+        }
+      };
+      // chunks 0 and 1 are in flight (issued during the previous iteration); later chunks one ahead (refills are
+      // issued unconditionally so that exactly 3*RC loads follow each buffer's)
+      for (int c = 0; c * GPC < ng; c += 4) {
+        vm_wait<3 * RC>(pa);
+        process(c, pa);
+        issue_chunk(D, c + 4, pa);
+        if ((c + 1) * GPC >= ng) break;
+        vm_wait<3 * RC>(pb);
+        process(c + 1, pb);
+        issue_chunk(D, c + 5, pb);
+        if ((c + 2) * GPC >= ng) break;
+        vm_wait<3 * RC>(pc);
+        process(c + 2, pc);
+        issue_chunk(D, c + 6, pc);
+        if ((c + 3) * GPC >= ng) break;
+        vm_wait<3 * RC>(pd);
+        process(c + 3, pd);
+        issue_chunk(D, c + 7, pd);
+      }
+      // the parked events, both at once
+      if (__ballot(nev > 0)) {
+        const uint32_t p0 = H::pix(ev0), p1 = H::pix(ev1);
+        const int r0 = (nev > 0 && (evk0 & 16)) ? sp_lookup(ekey, dir, p0, bs) : -1;
+        const int r1 = (nev > 1 && (evk1 & 16)) ? sp_lookup(ekey, dir, p1, bs) : -1;
+        add_x(r0 >= 0, r0, ev0, evk0 & 15);
+        add_x(r1 >= 0, r1, ev1, evk1 & 15);
+        const bool d0 = nev > 0 && H::dup(ev0);
+        const bool d1 = nev > 1 && H::dup(ev1);
+        const uint64_t m0 = __ballot(d0), m1 = __ballot(d1);
+        if (m0 | m1) {
+          const uint64_t below = (1ull << lane) - 1ull;
+          const int e0 = nd + (int)__popcll(m0 & below);
+          const int e1 = nd + (int)__popcll(m0) + (int)__popcll(m1 & below);
+          if (d0 && e0 < SP_DSEG) {
+            wdkey[e0] = (p0 << 3) | (uint32_t)(evk0 & 15);
+            wdval[e0] = H::val(ev0);
+          }
+          if (d1 && e1 < SP_DSEG) {
+            wdkey[e1] = (p1 << 3) | (uint32_t)(evk1 & 15);
+            wdval[e1] = H::val(ev1);
+          }
+          nd += (int)(__popcll(m0) + __popcll(m1));
+        }
+      }
+      if (lane == 0) dcnt[wid] = nd;
+    }
+    SP_STAMP(4);
+    // ---- the registers of ion b are dead: ion b+1's principal window and first two chunks go in flight
+    if (npos >= 0 && desc_lds_ok(DN, CAPC)) {
+      issue_principal(DN);
+      issue_chunk(DN, 0, pa);
+      issue_chunk(DN, 1, pb);
+    }
+    if (!skip) clear_table();
+    __syncthreads();
+    SP_STAMP(5);
+    // the principal statistics (per-wave sums, in wave order)
+    double sx = 0.0, sxx = 0.0, s0 = 0.0, npx_pos = 0.0, vmax = 0.0;
+    if (!skip) {
+      double t[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[q] += red[q * NW + w];
+        t[4] = red[4 * NW + w] > t[4] ? red[4 * NW + w] : t[4];
+      }
+      sx = t[0];
+      sxx = t[1];
+      s0 = t[2];
+      npx_pos = t[3];
+      vmax = t[4];
+    }
+    const bool chaos_ok = !skip && (sx > 0.0) && (npx_pos >= 4.0);
+    // ---- deferred flagged points: exact per-(pixel, window) sums, squared into the partials -----------------------
+    if (!skip) {
+      int nd_tot = 0, nd_max = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        nd_tot += dcnt[w];
+        nd_max = max(nd_max, dcnt[w]);
+      }
+      if (nd_max > SP_DSEG) {
+        reject();
+        skip = true;
+      } else if (nd_tot > 0) {
+        if ((tid % SP_DSEG) < dcnt[tid / SP_DSEG] && !tbl_add<SP_DTBL>(tkey, tval, dkey[tid], dval[tid]))
+          ctr[S_ABORT] = 1;
+        __syncthreads();
+        if (ctr[S_ABORT]) {
+          reject();
+          skip = true;
+        } else {
+          for (int i = tid; i < SP_DTBL; i += BLOCK) {
+            const uint32_t key = tkey[i];
+            if (key != 0xFFFFFFFFu) {
+              const double y = tval[i];
+              atomicAdd(&part[(size_t)(key & 7u) * NW * 4 + 2], y * y);
+            }
+          }
+          __syncthreads();  // (the table's space becomes the chaos list / band bitmaps)
+        }
+      }
+    }
+    SP_STAMP(6);
+
+    // ---- measure_of_chaos by threshold decomposition (ion_pipe_kernel's scheme) ----------------------------------
+    double chaos_raw = NAN;
+    uint32_t flags = 0;
+    if (!skip && chaos_ok) {
+      // level index per entry (the values die here: their space becomes the band bitmaps)
+      const double rcp = 1.0 / vmax;
+      for (int i = tid; i < n0; i += BLOCK) {
+        const uint32_t w = ekey[i];
+        if (!(w & SP_HOLE)) L8[i] = (uint8_t)sp_level(sp_val(evals[i], side), vmax, rcp, P);
+      }
+      __syncthreads();
+      SP_STAMP(7);
+      // (i) the 7x7 screen, band by band: a band bitmap holds presence rows [rb, re) = the band's rows [r0, r1) and
+      //     three rows either side.  Pass A lists the band's principal pixels with >= 3 principal pixels in their 7x7
+      //     (sparsity pre-filter, erosion border 0) at the top of the chaos list; pass B runs the full screen over
+      //     them and appends candidates (owned pixels of the dilated-covered boxes) at the bottom.
+      const int B = G.band_rows;
+      for (int r0 = 0; r0 < nr; r0 += B) {  // uniform
+        const int r1 = min(r0 + B, nr), rb = max(r0 - 3, 0), re = min(r1 + 3, nr);
+        const int nwords = ((re - rb) * ncl + 31) / 32 + 2;  // data + two zero words behind
+        {
+          uint4* z = reinterpret_cast<uint4*>(band - 1);
+          for (int i = tid; i < (nwords + 1 + 3) / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
+        }
+        if (tid == 0) ctr[S_NS] = 0;
+        const int ncand0 = ctr[S_NE];  // (settled by the previous band's closing barrier)
+        __syncthreads();
+        const int pa0 = rb * ncl, pa1 = re * ncl;
+        {
+          const int i0 = dir[pa0 >> bs], i1 = dir[((pa1 - 1) >> bs) + 1];
+          for (int i = i0 + tid; i < i1; i += BLOCK) {
+            const uint32_t w = ekey[i];
+            if (!(w & SP_HOLE) && w >= (uint32_t)pa0 && w < (uint32_t)pa1) {
+              const uint32_t q = w - (uint32_t)pa0;
+              atomicOr(&band[q >> 5], 1u << (q & 31));
+            }
+          }
+        }
+        __syncthreads();
+        // presence of row `row` (absolute), columns c0 .. c0+6 masked by cv; 0 outside the image
+        auto brow7 = [&](int row, int c0, uint32_t cv) -> uint32_t {
+          const bool rv = (unsigned)row < (unsigned)nr;
+          const int st = (rv ? row - rb : 0) * ncl + c0;  // >= -3: the guard word in front reads as zero
+          const int w = st >> 5;
+          const uint32_t v = __builtin_amdgcn_alignbit(band[w + 1], band[w], (uint32_t)(st & 31)) & cv;
+          return rv ? v : 0u;
+        };
+        auto rows7 = [&](int s, int& rs, int& cs, uint32_t& cv, uint32_t (&Hh)[7]) {
+          rowcol(s, P, rs, cs);
+          const int clo = 3 - cs > 0 ? 3 - cs : 0, chi = ncl - cs + 3 < 7 ? ncl - cs + 3 : 7;
+          cv = ((1u << chi) - 1u) & ~((1u << clo) - 1u);
+#pragma unroll
+          for (int d = 0; d < 7; ++d) Hh[d] = brow7(rs - 3 + d, cs - 3, cv);
+        };
+        auto sparse = [&](const uint32_t (&Hh)[7]) {
+          return !P.erosion_border && (__popc(Hh[0]) + __popc(Hh[1]) + __popc(Hh[2]) + __popc(Hh[3]) +
+                                       __popc(Hh[4]) + __popc(Hh[5]) + __popc(Hh[6])) < 3;
+        };
+        const uint32_t q0 = (uint32_t)(r0 * ncl), q1 = (uint32_t)(r1 * ncl);
+        const int s0e = dir[q0 >> bs], s1e = dir[((q1 - 1) >> bs) + 1];
+        const int room = SP_CCAP - ncand0;  // list slots above the candidates so far
+        bool two_pass = !P.erosion_border;
+        int nsurv = 0;
+        if (two_pass) {
+          for (int ob = s0e; ob < s1e; ob += BLOCK) {  // uniform trip count
+            const int i = ob + tid;
+            const uint32_t w = i < s1e ? ekey[i] : SP_HOLE;
+            const bool ok = !(w & SP_HOLE) && w >= q0 && w < q1;
+            int rs, cs;
+            uint32_t cv, Hh[7];
+            rows7(ok ? (int)w : (int)q0, rs, cs, cv, Hh);
+            const bool surv = ok && !sparse(Hh);
+            const uint64_t m = __ballot(surv);
+            if (m) {
+              int wbase = 0;
+              if (lane == 0) wbase = atomicAdd(&ctr[S_NS], (int)__popcll(m));
+              const int idx = __builtin_amdgcn_readfirstlane(wbase) + (int)__popcll(m & ((1ull << lane) - 1ull));
+              if (surv && idx < room) clist[SP_CCAP - 1 - idx] = w;
+            }
+          }
+          __syncthreads();
+          nsurv = ctr[S_NS];
+          if (nsurv > room / 2) two_pass = false;  // crowded: screen every pixel of the band (no list)
+        }
+        const int cap = two_pass ? SP_CCAP - nsurv : SP_CCAP;  // candidates stay below the unread survivors
+        const int nscr = two_pass ? nsurv : s1e - s0e;
+        for (int ob = 0; ob < nscr; ob += BLOCK) {  // uniform trip count: wave-compacted appends
+          const int oi = ob + tid;
+          int s = (int)q0;
+          bool ok = false;
+          if (oi < nscr) {
+            if (two_pass) {
+              s = (int)clist[SP_CCAP - 1 - oi];
+              ok = true;
+            } else {
+              const uint32_t w = ekey[s0e + oi];
+              ok = !(w & SP_HOLE) && w >= q0 && w < q1;
+              s = ok ? (int)w : (int)q0;
+            }
+          }
+          int rs, cs;
+          uint32_t cv, Hh[7];
+          rows7(s, rs, cs, cv, Hh);
+          uint32_t pass = 0;
+          if (ok && !sparse(Hh)) {
+            uint32_t Dl[7];
+            Dl[0] = Dl[6] = 0;
+#pragma unroll
+            for (int d = 1; d <= 5; ++d) {
+              const int row = rs - 3 + d;
+              const bool rv = row >= 0 && row < nr;
+              uint32_t x = (Hh[d] | (Hh[d] << 1) | (Hh[d] >> 1) | Hh[d - 1] | Hh[d + 1]) & cv;
+              if (!rv) x = 0;
+              if (P.erosion_border) x |= rv ? (~cv & 0x7Fu) : 0x7Fu;
+              Dl[d] = x & 0x7Fu;
+            }
+#define SP_HB(dr, dc) ((Hh[3 + (dr)] >> (3 + (dc))) & 1u)
+#define SP_BOX(dr, dc) ((((Dl[2 + (dr)] >> (2 + (dc))) & 7u) == 7u) && (((Dl[3 + (dr)] >> (2 + (dc))) & 7u) == 7u) && \
+                        (((Dl[4 + (dr)] >> (2 + (dc))) & 7u) == 7u))
+            const bool in_l = cs > 0, in_r = cs + 1 < ncl, in_u = rs > 0, in_d = rs + 1 < nr;
+            if (SP_BOX(0, 0) && !SP_HB(-1, 0) && !SP_HB(0, -1)) pass |= 1u;
+            if (in_r && SP_BOX(0, 1) && !SP_HB(-1, 1)) pass |= 2u;
+            if (in_l && SP_BOX(0, -1) && !SP_HB(-1, -1) && !SP_HB(0, -2) && !SP_HB(0, -1)) pass |= 4u;
+            if (in_u && SP_BOX(-1, 0) && !SP_HB(-2, 0) && !SP_HB(-1, -1) && !SP_HB(-1, 0) && !SP_HB(-1, 1))
+              pass |= 8u;
+            if (in_d && SP_BOX(1, 0)) pass |= 16u;
+#undef SP_BOX
+#undef SP_HB
+          }
+          const int cnt1 = __popc(pass);
+          const int inc = wave_incl_scan_dpp(cnt1);
+          const int wtot = __builtin_amdgcn_readlane(inc, 63);
+          if (wtot > 0) {
+            int wbase = 0;
+            if (lane == 63) wbase = atomicAdd(&ctr[S_NE], wtot);
+            int idx = __builtin_amdgcn_readlane(wbase, 63) + inc - cnt1;
+            while (pass) {
+              const int ci = __ffs(pass) - 1;
+              pass &= pass - 1;
+              const int p = s + (ci == 1 ? 1 : ci == 2 ? -1 : ci == 3 ? -ncl : ci == 4 ? ncl : 0);
+              if (idx < cap) clist[idx] = (uint32_t)p;
+              else ctr[S_ABORT] = 1;
+              ++idx;
+            }
+          }
+        }
+        __syncthreads();
+      }
+      SP_STAMP(8);
+      const int ncand = ctr[S_NE];
+      if (ctr[S_ABORT] || ncand > SP_CCAP) {  // more candidates than the list holds: the big-ion pass
+        reject();
+        skip = true;
+      }
+      if (!skip) {
+        // (ii) exact eL(p) = min_{q in box(p)} max_{q' in cross[q], in image} L(q') for every candidate, the levels of
+        //      its 5x5 neighbourhood's principal pixels found in the directory (entries are in pixel order), packed 8
+        //      bits per column
+        int emax_local = 0;
+        for (int c = tid; c < ncand; c += BLOCK) {
+          const int p = (int)clist[c];
+          int rp, cp;
+          rowcol(p, P, rp, cp);
+          uint64_t Lrow[5];
+#pragma unroll
+          for (int d = 0; d < 5; ++d) {
+            const int row = rp - 2 + d;
+            uint64_t packed = 0;
+            if ((unsigned)row < (unsigned)nr) {
+              const int base = row * ncl + cp - 2;  // pixel of window column 0
+              const uint32_t lo = (uint32_t)(row * ncl + max(cp - 2, 0)), hi = (uint32_t)(row * ncl + min(cp + 2, ncl - 1));
+              const int e1 = dir[(hi >> bs) + 1];
+              for (int i = dir[lo >> bs]; i < e1; ++i) {
+                const uint32_t w = ekey[i];
+                if (w & SP_HOLE) continue;
+                if (w > hi) break;
+                if (w >= lo) packed |= (uint64_t)L8[i] << (8 * (int)(w - (uint32_t)base));
+              }
+            }
+            Lrow[d] = packed;
+          }
+#define SP_L(r, cc) ((int)((Lrow[r] >> (8 * (cc))) & 0xFFull))
+          int mn = 1 << 20;
+          bool outside = false;
+#pragma unroll
+          for (int a2 = -1; a2 <= 1; ++a2) {
+#pragma unroll
+            for (int b2 = -1; b2 <= 1; ++b2) {
+              const int rq = rp + a2, cq = cp + b2;
+              if (rq < 0 || rq >= nr || cq < 0 || cq >= ncl) {
+                outside = true;
+                continue;
+              }
+              const int R = 2 + a2, C = 2 + b2;
+              int dl = SP_L(R, C);
+              dl = max(dl, SP_L(R - 1, C));
+              dl = max(dl, SP_L(R + 1, C));
+              dl = max(dl, SP_L(R, C - 1));
+              dl = max(dl, SP_L(R, C + 1));
+              mn = min(mn, dl);
+            }
+          }
+#undef SP_L
+          if (outside && !P.erosion_border) mn = 0;
+          if (mn >= (1 << 20)) mn = 0;
+          cel[c] = (uint8_t)mn;
+          emax_local = max(emax_local, mn);
+        }
+        if (emax_local > 0) atomicMax(&ctr[S_EMAX], emax_local);
+        __syncthreads();
+        SP_STAMP(9);
+        // (iii) Kruskal over eL (levels descending), union-find over candidate indices
+        double sum_c = 0.0;
+        const int emax_all = ctr[S_EMAX];
+        if (emax_all > 0 && ncand <= WAVE) {
+          // few candidates (most noise images): wave 0 alone, one candidate per lane, forward neighbours found by
+          // comparing pixel indices across lanes; no barrier (only wave 0 needs the result)
+          if (wid == 0) {
+            uint32_t* upar = reinterpret_cast<uint32_t*>(red);  // 64 entries (red is free until the record)
+            const bool act = lane < ncand;
+            const int p = act ? (int)clist[lane] : -1;
+            const int e = act ? (int)cel[lane] : 0;
+            int rp = 0, cp = 0;
+            rowcol(p < 0 ? 0 : p, P, rp, cp);
+            int nb[4] = {-1, -1, -1, -1};
+            for (int j = 0; j < ncand; ++j) {
+              const int pj = __shfl(p, j, WAVE), ej = __shfl(e, j, WAVE);
+              if (e >= 1 && ej >= 1) {
+                if (cp + 1 < ncl && pj == p + 1) nb[0] = j;
+                if (rp + 1 < nr) {
+                  if (pj == p + ncl) nb[1] = j;
+                  if (P.connectivity == 8 && cp > 0 && pj == p + ncl - 1) nb[2] = j;
+                  if (P.connectivity == 8 && cp + 1 < ncl && pj == p + ncl + 1) nb[3] = j;
+                }
+              }
+            }
+            int eq[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int v = __shfl(e, nb[q] < 0 ? 0 : nb[q], WAVE);
+              eq[q] = nb[q] < 0 ? 0 : (e < v ? e : v);  // edge weight min(eL)
+            }
+            upar[lane] = (uint32_t)lane;
+            double wsum = 0.0;
+            for (int t = emax_all; t >= 1; --t) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q)
+                if (eq[q] == t && uf_unite(upar, (uint32_t)lane, (uint32_t)nb[q])) wsum += (double)t;
+            }
+            sum_c = wave_sum_dpp(e >= 1 ? (double)e : 0.0) - wave_sum_dpp(wsum);
+          }
+        } else if (emax_all > 0) {
+          // the band space is free: a candidate hash (pixel -> index) and the union-find
+          for (int i = tid; i < SP_HSZ; i += BLOCK) htab[i] = SP_EMPTY;
+          __syncthreads();
+          double esum = 0.0;
+          auto hslot = [](uint32_t p) { return (p * 2654435761u) >> (32 - 11); };
+          static_assert(SP_HSZ == 2048 && SP_CCAP <= 1024, "hash geometry");
+          for (int c = tid; c < ncand; c += BLOCK) {
+            par[c] = (uint32_t)c;
+            const int e = cel[c];
+            if (e == 0) continue;
+            esum += (double)e;
+            const uint32_t p = clist[c];
+            uint32_t h = hslot(p);
+            while (atomicCAS(&htab[h], SP_EMPTY, (p << 10) | (uint32_t)c) != SP_EMPTY) h = (h + 1) & (SP_HSZ - 1);
+          }
+          __syncthreads();
+          auto find_c = [&](uint32_t q) -> int {
+            uint32_t h = hslot(q);
+            while (true) {
+              const uint32_t k = htab[h];
+              if (k == SP_EMPTY) return -1;
+              if ((k >> 10) == q) return (int)(k & 1023u);
+              h = (h + 1) & (SP_HSZ - 1);
+            }
+          };
+          double wsum = 0.0;
+          for (int t = emax_all; t >= 1; --t) {
+            for (int c = tid; c < ncand; c += BLOCK) {
+              const int e = cel[c];
+              if (e < t) continue;
+              const int p = (int)clist[c];
+              int rp, cp;
+              rowcol(p, P, rp, cp);
+              auto edge = [&](int q) {
+                const int j = find_c((uint32_t)q);
+                if (j < 0) return;
+                const int eq2 = cel[j];
+                if ((e < eq2 ? e : eq2) == t && uf_unite(par, (uint32_t)c, (uint32_t)j)) wsum += (double)t;
+              };
+              if (cp + 1 < ncl) edge(p + 1);
+              if (rp + 1 < nr) {
+                edge(p + ncl);
+                if (P.connectivity == 8) {
+                  if (cp > 0) edge(p + ncl - 1);
+                  if (cp + 1 < ncl) edge(p + ncl + 1);
+                }
+              }
+            }
+            __syncthreads();
+          }
+          double a2[2] = {esum, wsum};
+          block_sum<BLOCK, 2, true>(a2, red);
+          sum_c = a2[0] - a2[1];
+        }
+        chaos_raw = 1.0 - sum_c / (double)P.nlevels / npx_pos;
+        SP_STAMP(10);
+      }
+    } else if (!skip) {
+      flags |= SMG_ION_CHAOS_NAN;
+    }
+
+    // ---- the ion's sums -> its record (ion_finalize_kernel computes the scores); wave 0, lane k = window k
+    if (!skip && wid == 0) {
+      IonRec* R = reinterpret_cast<IonRec*>(desc + pos);
+      const int k = lane;
+      if (k < K) {
+        double sk = 0.0, syy = D->syy[k], sxy = 0.0;
+        if (k == 0) {
+          sk = s0;
+        } else {
+#pragma unroll
+          for (int w = 0; w < NW; ++w) {
+            const double* pk = part + ((size_t)k * NW + w) * 4;
+            sk += pk[0];
+            syy += pk[2];
+            sxy += pk[3];
+          }
+        }
+        R->s[k] = sk;
+        R->sxy[k] = sxy;
+        R->syy[k] = syy;
+      }
+      if (lane == 0) {
+        R->sx = sx;
+        R->sxx = sxx;
+        R->chaos = chaos_raw;
+        R->flags = flags | SMG_ION_SPARSE | (uint32_t)D->hits;
+        R->state = 1u;
+      }
+    }
+    if (npos < 0) break;
+    if (began && wid != 0) clear_fc(tid - WAVE, BLOCK - WAVE);  // (the chaos phase is done with both)
+    pos = npos;
+    npos = n2pos;
+    cur ^= 1;
+    __syncthreads();  // the next ion starts on cleared structures
+    SP_STAMP(11);
+  }
+  SP_STAMP_FLUSH();
+  // no load of this wave outlives it
+  vm_wait<0>(pa);
+  vm_wait<0>(pb);
+  vm_wait<0>(pc);
+  vm_wait<0>(pd);
+  vm_wait<0>(pe);
+}
+
+SpGeo sparse_geo(const Params& P) {
+  SpGeo G;
+  int lg = 0;
+  while ((1ll << lg) < (long long)P.npx) ++lg;
+  G.bs = lg > 10 ? lg - 10 : 0;  // <= 1024 buckets
+  const long long rows = (long long)SpLay::band_words * 32 / P.ncols;
+  G.band_rows = (int)(rows - 6 > 0x7FFFFFFF ? 0x7FFFFFFF : rows - 6);
+  return G;
+}
+
+}  // namespace
+
+bool sparse_main_fits(const Params& P) {
+  if (P.clip || P.npx <= 0 || P.npx > NPX_LDS_MAX) return false;
+  return sparse_geo(P).band_rows >= 8;
+}
+
+int launch_sparse_main(Hits<SMG_HITS_PACKED_F32> hits, IonDesc* desc, Sched S, const Params& P, double* oc,
+                       double* osp, double* osc, double* omsm, uint32_t* oflags, uint32_t* rej_list,
+                       uint32_t* rej_count, int cus, hipStream_t st) {
+  const SpGeo G = sparse_geo(P);
+  auto k = &ion_sparse_kernel<SP_BLOCK, SP_RMAX, SP_RC, SP_WPE>;
+  SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)SP_LDS_BYTES));
+  // SP_WGPCU resident workgroups per CU, a multiple of the XCD count
+  int64_t nwg = (int64_t)cus * SP_WGPCU;
+  if (nwg > S.n) nwg = ((S.n + XCDS - 1) / XCDS) * XCDS;
+  hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(SP_BLOCK), SP_LDS_BYTES, st, hits, desc, S, P, G, oc, osp, osc, omsm,
+                     oflags, rej_list, rej_count);
+  SMG_LAUNCH_CHECK();
+  return SMG_OK;
+}
+
+int sparse_read_stamps(unsigned long long* host_out, int n) {
+#ifdef SMG_STAMPS
+  SMG_HIP(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_sp_stamps), sizeof(unsigned long long) * (n < 16 ? n : 16)));
+  unsigned long long z[16] = {0};
+  SMG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sp_stamps), z, sizeof(z)));
+  return SMG_OK;
+#else
+  (void)host_out;
+  (void)n;
+  set_error("library built without -DSMG_STAMPS");
+  return SMG_ERR_UNSUPPORTED;
+#endif
+}
+
+}  // namespace smg

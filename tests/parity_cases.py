@@ -187,6 +187,18 @@ def make_case(name: str):
         ds = syn.make_dataset_np(150, 150, 4, seed=163, ions=ions, plant_fraction=1.0, plant_seed=164,
                                  blob_sigma=(400.0, 500.0))
         return add_duplicates(ds, 0.7, 165), ions, 20.0, {}
+    if name == "nlevels100":   # level indices above 63 (the exact eL packs them 8 bits per column)
+        ds, ions, ppm, _ = make_case("basic")
+        return ds, ions, ppm, {"nlevels": 100}
+    if name == "bands":        # 250 x 1000 px: the sparse main pass screens chaos in two row bands; planted blobs give
+        # ions with > 64 chaos candidates (the hash-indexed Kruskal) and blobs across the band boundary
+        full = syn.make_ion_table(16, seed=171, decoy_seed=172)
+        tgt = np.nonzero(np.isin(full.adducts, list(full.target_adducts)))[0][:24]
+        dec = np.nonzero(~np.isin(full.adducts, list(full.target_adducts)))[0][:8]
+        ions = subset_ions(full, np.concatenate([tgt, dec]))
+        ds = syn.make_dataset_np(250, 1000, 3, seed=173, ions=ions, plant_fraction=1.0, plant_seed=174,
+                                 blob_sigma=(4.0, 10.0))
+        return add_duplicates(ds, 0.02, 175), ions, 20.0, {}
     if name == "boundary":
         ds = syn.make_dataset_np(16, 16, 300, seed=71)
         return ds, boundary_ions(ds, 5.0, 40, 72), 5.0, {}
@@ -195,7 +207,7 @@ def make_case(name: str):
 
 CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels", "nlevels1", "big_window", "huge_window",
          "large_image", "xl_image", "large_blobs", "boundary", "long_tail", "dups_heavy", "kmix", "clip99", "clip_q50_conn8",
-         "clip_dups_heavy", "clip_large", "wide_range", "wide_overflow"]
+         "clip_dups_heavy", "clip_large", "wide_range", "wide_overflow", "nlevels100", "bands"]
 
 
 def oracle_run(ds, ions, ppm, nlevels=30, connectivity=4, erosion_border=0, q=99.0, do_preprocessing=False):

@@ -47,6 +47,22 @@ def test_async_load_registers_are_never_touched_in_flight(tmp_path):
     assert n_guarded <= 4, out
 
 
+@pytest.mark.timeout(600)
+def test_sparse_main_pass_async_loads(tmp_path):
+    """ion_sparse_kernel (smg_sparse.hip) keeps ion_pipe_kernel's asynchronous loads: zero violations, and no path
+    that skips a wait (the principal waits dominate every use of those registers; the wave-0 loads are waited where
+    every path from them passes)."""
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    src = os.path.join(ROOT, "sm_distributed_amd", "csrc", "smg_sparse.hip")
+    asm = str(tmp_path / "smg_sparse.s")
+    subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "--cuda-device-only",
+                    "-S", src, "-o", asm], check=True, capture_output=True)
+    n_loads, n_bad, n_guarded, out = _check(asm, "_ZN3smg12_GLOBAL__N_117ion_sparse_kernel")
+    assert n_loads > 0 and n_bad == 0 and n_guarded == 0, out
+
+
 def _kernel(tmp_path, lines):
     s = tmp_path / "k.s"
     s.write_text("\n".join(["_ZN3smg4testE:"] + lines + ["s_endpgm", ".size _ZN3smg4testE"]))

@@ -128,6 +128,52 @@ def test_forced_two_level_large_blobs_reaches_big_pass():
         assert np.abs(df[col].to_numpy() - m[col][rows]).max(initial=0.0) <= METRIC_ATOL, col
 
 
+# cases the sparse main pass (ion_sparse_kernel) scores: packed f32 hits, no hot-spot clip, <= 2^18 pixels
+SPARSE_CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels", "nlevels1",
+                "boundary", "long_tail", "kmix", "wide_range", "nlevels100", "bands"]
+
+
+@pytest.mark.parametrize("name", SPARSE_CASES)
+def test_sparse_main_pass_scores_the_lds_ions(name):
+    """The default main pass is the sparse one: every ion the main pass scored carries SMG_ION_SPARSE (and ion_pipe
+    flags never appear together with it)."""
+    m = _run_case(name)[7]
+    has = (m["flags"] & 1) != 0
+    main = has & ((m["flags"] & (2 | 8)) == 0)
+    assert main.any() or name == "boundary"
+    assert ((m["flags"][main] & 0x40) != 0).all(), name
+    assert not (((m["flags"] & 0x40) != 0) & ((m["flags"] & (2 | 8 | 0x10)) != 0)).any()
+
+
+def test_bands_case_reaches_the_hash_kruskal_and_two_bands():
+    """bands: 1000-column image (two chaos bands) whose planted ions have > 64 chaos candidates on the sparse pass."""
+    ds, ions, ppm, kw, imgs, df, peaks, m, lo, hi = _run_case("bands")
+    sparse = ((m["flags"] & 0x41) == 0x41)
+    assert sparse.sum() >= 8
+    assert (df.chaos > 0).sum() >= 4  # real structure, not only isolated noise
+
+
+@pytest.mark.parametrize("name", SPARSE_CASES)
+def test_legacy_main_pass_matches_oracle(name):
+    """ion_pipe_kernel<512> (smg_debug_main_kernel(0)) stays correct: every sparse-pass case again through it."""
+    from sm_distributed_amd import _lib
+    ds, ions, ppm, kw, imgs, df, _, _, _, _ = _run_case(name)
+    L = _lib.lib()
+    L.smg_debug_main_kernel(0)
+    try:
+        _, m, _, _ = _device_run(ds, ions, ppm, **kw)
+    finally:
+        L.smg_debug_main_kernel(1)
+    has = (m["flags"] & 1) != 0
+    assert not ((m["flags"] & 0x40) != 0).any()
+    idx = {k: i for i, k in enumerate(zip(ions.sf_ids.tolist(), ions.adducts.tolist()))}
+    assert set(zip(ions.sf_ids[has].tolist(), ions.adducts[has].tolist())) == set(df.index.tolist())
+    rows = np.array([idx[k] for k in df.index.tolist()], dtype=np.int64)
+    for col in ("chaos", "spatial", "spectral", "msm"):
+        err = np.abs(df[col].to_numpy() - m[col][rows])
+        assert err.max(initial=0.0) <= METRIC_ATOL, (col, float(err.max()), int(np.argmax(err)))
+
+
 # every LDS-path case again with the two-level pixel set forced (smg_debug_force_two_level)
 TWO_LEVEL_CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels",
                    "big_window", "boundary", "long_tail", "dups_heavy", "kmix", "clip99", "clip_q50_conn8",
@@ -253,7 +299,9 @@ def test_lds_pipeline_paths_exercised():
     main = has & ((m["flags"] & (2 | 8)) == 0)
     tail = np.array([hi[ions.win_off[i] + 1:ions.win_off[i + 1]].sum() - lo[ions.win_off[i] + 1:ions.win_off[i + 1]].sum()
                      for i in range(ions.n_ions)])
-    assert (main & (tail > 4 * 1024)).sum() >= 10  # > 4 register chunks of 1024 points
+    # > 4 register chunks (ion_sparse_kernel: 256 threads x 2 points; ion_pipe_kernel<512>: 512 x 2)
+    sparse = (m["flags"] & 0x40) != 0
+    assert (main & np.where(sparse, tail > 4 * 512, tail > 4 * 1024)).sum() >= 10
     _, _, _, _, _, _, _, m, _, _ = _run_case("dups_heavy")
     assert ((m["flags"] & (2 | 8)) != 0).any()
     ds, ions, ppm, kw, imgs, df, peaks, m, lo, hi = _run_case("kmix")
