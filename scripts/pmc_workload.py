@@ -46,6 +46,8 @@ else:
     mz, hits, dims, info = syn.make_dataset_torch(1000, 1000, 2100, seed=42, device="cuda", ions=ions)
 peaks = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
 dions = E.DeviceIons.from_arrays(ions.win_off, ions.peak_mz, ions.peak_int)
+if os.environ.get("SMG_MAIN_KERNEL"):  # 0 = ion_pipe_kernel<512>, 1 = ion_sparse_kernel (default)
+    _lib.lib().smg_debug_main_kernel(int(os.environ["SMG_MAIN_KERNEL"]))
 m, lo, hi = E.run_hot_path(peaks, dions, 2.0, 30)
 for _ in range(2):
     m = E.ion_metrics(peaks, dions, lo, hi, nlevels=30)

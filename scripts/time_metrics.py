@@ -17,6 +17,8 @@ peaks = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
 dions = E.DeviceIons.from_arrays(ions.win_off, ions.peak_mz, ions.peak_int)
 if os.environ.get("SMG_FORCE_TWO"):  # diagnostic: the two-level LDS passes for every image size
     _lib.lib().smg_debug_force_two_level(1)
+if os.environ.get("SMG_MAIN_KERNEL"):  # A/B: 0 = ion_pipe_kernel<512>, 1 = ion_sparse_kernel
+    _lib.lib().smg_debug_main_kernel(int(os.environ["SMG_MAIN_KERNEL"]))
 m, lo, hi = E.run_hot_path(peaks, dions, 2.0, 30)
 torch.cuda.synchronize()
 ts = []
@@ -38,5 +40,6 @@ else:
     np.savez(ref_path, **{c: got[c] for c in cols + ("flags",)})
     note = "reference variant"
 fl = got["flags"]
-print(f"{os.path.basename(_lib.LIB_PATH)}: ion_metrics min {min(ts)*1e3:.2f} ms median {sorted(ts)[2]*1e3:.2f} ms "
+tag = os.path.basename(_lib.LIB_PATH) + (f" main_kernel={os.environ['SMG_MAIN_KERNEL']}" if os.environ.get("SMG_MAIN_KERNEL") else "")
+print(f"{tag}: ion_metrics min {min(ts)*1e3:.2f} ms median {sorted(ts)[2]*1e3:.2f} ms "
       f"({note}; big {int(((fl & 8) != 0).sum())} dense {int(((fl & 2) != 0).sum())})", flush=True)

@@ -62,7 +62,10 @@ __device__ unsigned long long g_sp_stamps[16];
 
 namespace {
 
-constexpr int SP_BLOCK = 256, SP_RMAX = 10, SP_RC = 2, SP_WPE = 4, SP_WGPCU = 4;
+#ifndef SMG_SP_RC
+#define SMG_SP_RC 2  // tail points per thread per chunk (four chunks in flight)
+#endif
+constexpr int SP_BLOCK = 256, SP_RMAX = 10, SP_RC = SMG_SP_RC, SP_WPE = 4, SP_WGPCU = 4;
 constexpr int SP_NW = SP_BLOCK / WAVE;
 constexpr int SP_CAPC = SP_BLOCK * SP_RMAX;  // principal points per ion (more: the big-ion pass)
 constexpr int SP_NBMAX = 1024;               // bucket directory entries
@@ -77,7 +80,7 @@ constexpr uint32_t SP_HOLE = 0x80000000u;
 constexpr uint32_t SP_SIDEREF = 0xFFF00000u;  // an f32 NaN pattern: the entry's value is side[w & 0xFFFFF]
 constexpr uint32_t SP_EMPTY = 0xFFFFFFFFu;
 constexpr uint32_t SP_LDS_BYTES = 40448;      // 4 x 40,448 B <= 160 KiB: four workgroups per CU
-enum { S_NE = 0, S_EMAX, S_ABORT, S_SIDE, S_NEXT, S_NS, S_MAXB, S_NCTR = 8 };
+enum { S_NE = 0, S_EMAX, S_ABORT, S_SIDE, S_NEXT, S_MAXB, S_NCTR = 8 };
 
 constexpr uint32_t c16(uint32_t x) { return (x + 15u) & ~15u; }
 
@@ -110,15 +113,16 @@ struct SpLay {
   // chaos view
   static constexpr uint32_t o_cel = SP_LDS_BYTES - SP_CCAP;
   static constexpr uint32_t o_clist = o_cel - SP_CCAP * 4;
+  static constexpr uint32_t o_wsurv = o_clist - SP_NW * WAVE * 4;  // per-wave survivor lists (chaos screen)
   static constexpr uint32_t o_band = o_U;  // guard word, then the band's bits
   static constexpr uint32_t o_hash = o_U;
   static constexpr uint32_t o_par = o_hash + SP_HSZ * 4;
   // data words of a band: a guard word in front, two zero words behind, and the uint4 rounding of the zeroing
-  static constexpr int band_words = (int)((o_clist - o_band) / 4) - 6;
+  static constexpr int band_words = (int)((o_wsurv - o_band) / 4) - 6;
   static_assert(o_tend <= SP_LDS_BYTES, "principal / tail view fits");
   static_assert(o_cnt + SP_NBMAX * 4 <= o_dkey, "bucket counters inside the values' space");
-  static_assert(o_par + SP_CCAP * 4 <= o_clist, "Kruskal hash + union-find below the chaos list");
-  static_assert(o_F + SP_FWORDS * 4 <= o_clist && o_cnt + SP_NBMAX * 4 <= o_clist, "cleared words below the list");
+  static_assert(o_par + SP_CCAP * 4 <= o_wsurv, "Kruskal hash + union-find below the chaos lists");
+  static_assert(o_F + SP_FWORDS * 4 <= o_wsurv && o_cnt + SP_NBMAX * 4 <= o_wsurv, "cleared words below the lists");
   static_assert(SP_LDS_BYTES % 512 == 0 && 4 * SP_LDS_BYTES <= 160 * 1024, "four workgroups per CU");
 };
 
@@ -148,22 +152,24 @@ __device__ __forceinline__ int sp_lookup(const uint32_t* ekey, const uint16_t* d
   return -1;
 }
 
-// level_fast with the division v / vmax replaced by v * (1 / vmax) where that cannot change the answer: the two
-// level comparisons that decide it must hold with a margin above the product's error (<= 2 ulp), else the exact
-// division decides.  Returns exactly level_fast(v, vmax, P) (= #{i : linspace(0,1,n)[i] < v / vmax}, v <= vmax).
+// the exact level index (divisions, loops), kept out of line so that the loops calling sp_level stay small
+__device__ __noinline__ int sp_level_exact(double v, double vmax, const Params& P) { return level_fast(v, vmax, P); }
+
+// level_fast(v, vmax, P) = #{i <= n-2 : i*step < v/vmax} (+ [1 < v/vmax], 0 here: v <= vmax) with the division
+// replaced by v * (1/vmax) where that cannot change the answer.  With x = (v/vmax)(n-1) non-integer, the count is
+// floor(x) + 1 (capped at n-1); the two comparisons that decide it are checked against na = v*rcp with a margin above
+// na's error (<= 2 ulp), and anything closer (or v ~ vmax) takes the exact path.  Straight-line: no loops.
 __device__ __forceinline__ int sp_level(double v, double vmax, double rcp, const Params& P) {
   const int n = P.nlevels;
-  if (n == 1 || !(v > 0.0)) return level_fast(v, vmax, P);
+  if (!(v > 0.0)) return 0;  // (vmax > 0 whenever levels are needed)
+  if (n == 1) return 1;
   const double na = v * rcp;
-  if (!(na < 1.0 - 1e-12)) return level_fast(v, vmax, P);
   const double tol = na * 1e-15;
-  int j = (int)(na * (double)(n - 1));
-  j = j < 0 ? 0 : (j > n - 1 ? n - 1 : j);
-  while (j > 0 && !((double)(j - 1) * P.step < na)) --j;
-  while (j < n - 1 && (double)j * P.step < na) ++j;
-  const bool lo_ok = j == 0 || (double)(j - 1) * P.step < na - tol;
+  int j = (int)(na * (double)(n - 1)) + 1;
+  j = j > n - 1 ? n - 1 : j;
+  const bool lo_ok = (double)(j - 1) * P.step < na - tol;
   const bool hi_ok = j == n - 1 || (double)j * P.step >= na + tol;
-  return (lo_ok && hi_ok) ? j : level_fast(v, vmax, P);
+  return (na < 1.0 - 1e-12 && lo_ok && hi_ok) ? j : sp_level_exact(v, vmax, P);
 }
 
 template <int LB, int RMAX, int RC, int WPE>
@@ -203,6 +209,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
   double* tval = reinterpret_cast<double*>(smem + LY::o_tval);
   uint32_t* clist = reinterpret_cast<uint32_t*>(smem + LY::o_clist);
   uint8_t* cel = smem + LY::o_cel;
+  uint32_t* wsurv = reinterpret_cast<uint32_t*>(smem + LY::o_wsurv) + (threadIdx.x >> 6) * WAVE;
   uint32_t* band = reinterpret_cast<uint32_t*>(smem + LY::o_band) + 1;  // band[-1]: zero guard word
   uint32_t* htab = reinterpret_cast<uint32_t*>(smem + LY::o_hash);
   uint32_t* par = reinterpret_cast<uint32_t*>(smem + LY::o_par);
@@ -399,24 +406,46 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         }
       }
       __syncthreads();
-      // ... each point's rank among its bucket's keys, and whether its pixel has other points before / after it
+      // ... each point's rank among its bucket's keys, and whether its pixel has other points before / after it.
+      // The scans of five slots run together (their LDS reads in flight at once), each lane for as many steps as
+      // its longest bucket among them.
 #pragma unroll
-      for (int j = 0; j < RMAX; ++j) {
-        const int i = tid + j * BLOCK;
-        if (i < n0) {
-          const uint32_t p = H::pix(hs(j)), key = (p << 12) | (uint32_t)i;
-          const int s0 = dir[p >> bs], s1 = dir[(p >> bs) + 1];
-          int rank = 0;
-          bool before = false, after = false;
-          for (int k = s0; k < s1; ++k) {
-            const uint32_t w = ekey[k];
-            rank += w < key ? 1 : 0;
-            const bool same = (w >> 12) == p;
-            before |= same && w < key;
-            after |= same && w > key;
+      for (int g = 0; g < RMAX; g += 5) {
+        constexpr int GS = 5;
+        uint32_t sl[GS], rk[GS];
+        int mlen = 0;
+#pragma unroll
+        for (int jj = 0; jj < GS; ++jj) {
+          const int j = g + jj;
+          sl[jj] = 0u;
+          rk[jj] = 0u;
+          if (j < RMAX && tid + j * BLOCK < n0) {
+            const uint32_t b = H::pix(hs(j)) >> bs;
+            const uint32_t s0 = dir[b], s1 = dir[b + 1];
+            sl[jj] = s0 | ((s1 - s0) << 16);
+            mlen = max(mlen, (int)(s1 - s0));
           }
-          aw_set(j, (uint32_t)(s0 + rank));
-          stbits |= (before ? 2u : (after ? 1u : 0u)) << (2 * j);
+        }
+        for (int k = 0; k < mlen; ++k) {
+#pragma unroll
+          for (int jj = 0; jj < GS; ++jj) {
+            const int j = g + jj;
+            if (j < RMAX && k < (int)(sl[jj] >> 16)) {
+              const uint32_t p = H::pix(hs(j)), key = (p << 12) | (uint32_t)(tid + j * BLOCK);
+              const uint32_t w = ekey[(sl[jj] & 0xFFFFu) + k];
+              const bool same = (w >> 12) == p;
+              rk[jj] += (w < key ? 1u : 0u) | ((same && w < key) ? 0x10000u : 0u) | ((same && w > key) ? 0x1000000u : 0u);
+            }
+          }
+        }
+#pragma unroll
+        for (int jj = 0; jj < GS; ++jj) {
+          const int j = g + jj;
+          if (j < RMAX && tid + j * BLOCK < n0) {
+            aw_set(j, (sl[jj] & 0xFFFFu) + (rk[jj] & 0xFFFFu));
+            const bool before = (rk[jj] & 0xFF0000u) != 0u, after = (rk[jj] >> 24) != 0u;
+            stbits |= (before ? 2u : (after ? 1u : 0u)) << (2 * j);
+          }
         }
       }
       __syncthreads();
@@ -449,16 +478,19 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
     }
     if (!skip) {
       __syncthreads();
-      // pixels with several points: the f64 sum in window order (coo.toarray()), kept in the side table
-      for (int i = tid; i < n0; i += BLOCK) {
-        const uint32_t w = ekey[i];
-        if ((w & SP_HOLE) || i + 1 >= n0 || ekey[i + 1] != (w | SP_HOLE)) continue;
-        double s = (double)__uint_as_float(evals[i]);
-        for (int k = i + 1; k < n0 && ekey[k] == (w | SP_HOLE); ++k) s += (double)__uint_as_float(evals[k]);
+      // pixels with several points: the f64 sum in window order (coo.toarray()), kept in the side table; each such
+      // pixel's first point (state 1) sums the entries behind its own
+#pragma unroll
+      for (int j = 0; j < RMAX; ++j) {
+        if (((stbits >> (2 * j)) & 3u) != 1u) continue;
+        const int f = (int)aw_get(j);
+        const uint32_t w = ekey[f];
+        double s = (double)__uint_as_float(evals[f]);
+        for (int k = f + 1; k < n0 && ekey[k] == (w | SP_HOLE); ++k) s += (double)__uint_as_float(evals[k]);
         const int slot = atomicAdd(&ctr[S_SIDE], 1);
         if (slot < SP_SIDE) {
           side[slot] = s;
-          evals[i] = SP_SIDEREF | (uint32_t)slot;
+          evals[f] = SP_SIDEREF | (uint32_t)slot;
         } else {
           ctr[S_ABORT] = 1;
         }
@@ -685,8 +717,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       SP_STAMP(7);
       // (i) the 7x7 screen, band by band: a band bitmap holds presence rows [rb, re) = the band's rows [r0, r1) and
       //     three rows either side.  Pass A lists the band's principal pixels with >= 3 principal pixels in their 7x7
-      //     (sparsity pre-filter, erosion border 0) at the top of the chaos list; pass B runs the full screen over
-      //     them and appends candidates (owned pixels of the dilated-covered boxes) at the bottom.
+      //     (sparsity pre-filter, erosion border 0) in the wave's own survivor list; pass B runs the full screen over
+      //     full lists (a wave's own: no barrier between the passes) and appends candidates (owned pixels of the
+      //     dilated-covered boxes) to the chaos list.
       const int B = G.band_rows;
       for (int r0 = 0; r0 < nr; r0 += B) {  // uniform
         const int r1 = min(r0 + B, nr), rb = max(r0 - 3, 0), re = min(r1 + 3, nr);
@@ -695,8 +728,6 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
           uint4* z = reinterpret_cast<uint4*>(band - 1);
           for (int i = tid; i < (nwords + 1 + 3) / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
         }
-        if (tid == 0) ctr[S_NS] = 0;
-        const int ncand0 = ctr[S_NE];  // (settled by the previous band's closing barrier)
         __syncthreads();
         const int pa0 = rb * ncl, pa1 = re * ncl;
         {
@@ -731,51 +762,17 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         };
         const uint32_t q0 = (uint32_t)(r0 * ncl), q1 = (uint32_t)(r1 * ncl);
         const int s0e = dir[q0 >> bs], s1e = dir[((q1 - 1) >> bs) + 1];
-        const int room = SP_CCAP - ncand0;  // list slots above the candidates so far
-        bool two_pass = !P.erosion_border;
-        int nsurv = 0;
-        if (two_pass) {
-          for (int ob = s0e; ob < s1e; ob += BLOCK) {  // uniform trip count
-            const int i = ob + tid;
-            const uint32_t w = i < s1e ? ekey[i] : SP_HOLE;
-            const bool ok = !(w & SP_HOLE) && w >= q0 && w < q1;
-            int rs, cs;
-            uint32_t cv, Hh[7];
-            rows7(ok ? (int)w : (int)q0, rs, cs, cv, Hh);
-            const bool surv = ok && !sparse(Hh);
-            const uint64_t m = __ballot(surv);
-            if (m) {
-              int wbase = 0;
-              if (lane == 0) wbase = atomicAdd(&ctr[S_NS], (int)__popcll(m));
-              const int idx = __builtin_amdgcn_readfirstlane(wbase) + (int)__popcll(m & ((1ull << lane) - 1ull));
-              if (surv && idx < room) clist[SP_CCAP - 1 - idx] = w;
-            }
-          }
-          __syncthreads();
-          nsurv = ctr[S_NS];
-          if (nsurv > room / 2) two_pass = false;  // crowded: screen every pixel of the band (no list)
-        }
-        const int cap = two_pass ? SP_CCAP - nsurv : SP_CCAP;  // candidates stay below the unread survivors
-        const int nscr = two_pass ? nsurv : s1e - s0e;
-        for (int ob = 0; ob < nscr; ob += BLOCK) {  // uniform trip count: wave-compacted appends
-          const int oi = ob + tid;
-          int s = (int)q0;
-          bool ok = false;
-          if (oi < nscr) {
-            if (two_pass) {
-              s = (int)clist[SP_CCAP - 1 - oi];
-              ok = true;
-            } else {
-              const uint32_t w = ekey[s0e + oi];
-              ok = !(w & SP_HOLE) && w >= q0 && w < q1;
-              s = ok ? (int)w : (int)q0;
-            }
-          }
+        // pass B on this wave's survivors wsurv[0, wcnt) (lane i takes survivor i): the full screen, candidates
+        // appended to the chaos list (one LDS atomic per wave)
+        auto screen = [&](int wcnt) {
+          __builtin_amdgcn_wave_barrier();  // (the survivor list was written by this wave's lanes)
+          const bool ok = lane < wcnt;
+          const int s = ok ? (int)wsurv[lane] : (int)q0;
           int rs, cs;
           uint32_t cv, Hh[7];
           rows7(s, rs, cs, cv, Hh);
           uint32_t pass = 0;
-          if (ok && !sparse(Hh)) {
+          if (ok) {
             uint32_t Dl[7];
             Dl[0] = Dl[6] = 0;
 #pragma unroll
@@ -811,12 +808,34 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
               const int ci = __ffs(pass) - 1;
               pass &= pass - 1;
               const int p = s + (ci == 1 ? 1 : ci == 2 ? -1 : ci == 3 ? -ncl : ci == 4 ? ncl : 0);
-              if (idx < cap) clist[idx] = (uint32_t)p;
+              if (idx < SP_CCAP) clist[idx] = (uint32_t)p;
               else ctr[S_ABORT] = 1;
               ++idx;
             }
           }
+          __builtin_amdgcn_wave_barrier();  // (the list is refilled after this)
+        };
+        // pass A: the band's principal pixels with >= 3 principal pixels in their 7x7 (every one with erosion border
+        // 1) go to the wave's survivor list; a full list is screened at once, the rest after the band's last round
+        int wcnt = 0;  // (wave-uniform)
+        for (int ob = s0e; ob < s1e; ob += BLOCK) {  // uniform trip count
+          const int i = ob + tid;
+          const uint32_t w = i < s1e ? ekey[i] : SP_HOLE;
+          const bool ok = !(w & SP_HOLE) && w >= q0 && w < q1;
+          int rs, cs;
+          uint32_t cv, Hh[7];
+          rows7(ok ? (int)w : (int)q0, rs, cs, cv, Hh);
+          const bool surv = ok && !sparse(Hh);
+          const uint64_t m = __ballot(surv);
+          const int c = (int)__popcll(m);
+          if (wcnt + c > WAVE) {
+            screen(wcnt);
+            wcnt = 0;
+          }
+          if (surv) wsurv[wcnt + (int)__popcll(m & ((1ull << lane) - 1ull))] = w;
+          wcnt += c;
         }
+        if (wcnt > 0) screen(wcnt);
         __syncthreads();
       }
       SP_STAMP(8);
