@@ -205,7 +205,7 @@ int smg_debug_force_dense(int32_t on);
  * A/B timing; smg_sort_points_flag always uses the hand-written one).  Process-wide; returns 0. */
 int smg_debug_sort_impl(int32_t which);
 /* The main LDS pass: 1 = ion_sparse_kernel where it applies (default: packed f32 hits, no hot-spot clip, images up
- * to 2^18 pixels whose rows fit its chaos bands), 0 = ion_pipe_kernel<512> for every image (kept for A/B timing and
+ * to 2^18 pixels), 0 = ion_pipe_kernel<512> for every image (kept for A/B timing and
  * so that the parity suite covers both).  Process-wide; returns 0. */
 int smg_debug_main_kernel(int32_t which);
 /* Diagnostic builds only (-DSMG_STAMPS, libsmg_stamps.so): per-phase cycles of the main passes summed over their

@@ -25,9 +25,10 @@ m = E.ion_metrics(peaks, dions, lo, hi, nlevels=30)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 L.smg_debug_sparse_stamps(buf, 16)
-names = ["top: ticket, descriptor checks", "build: filter, bucket counts, directory", "sort, values, side sums",
-         "ticket barrier, stats", "tail stream", "issue next ion, tail barrier", "duplicate table",
-         "levels", "chaos screen (bands)", "exact eL", "kruskal", "record, clear, loop barrier"]
+names = ["top: ticket, descriptor checks", "build: filter, bucket counts, directory", "entries, values, side sums",
+         "ticket barrier, stats, levels", "tail stream", "issue next ion, tail barrier", "duplicate table",
+         "(unused)", "chaos screen (bands)", "exact eL", "kruskal", "record, clear, loop barrier"]
+extra = {12: "(tail stream: in counted waits)"}
 f = m.flags.cpu().numpy()
 n = int(((f & 0x41) == 0x41).sum())
 tot = sum(buf[i] for i in range(len(names)))
@@ -35,5 +36,7 @@ print(os.path.basename(_lib.LIB_PATH), f"{nrows}x{ncols} px, Poisson({pk:g}), {n
 print(f"ion_metrics {dt*1e3:.1f} ms; sparse-pass ions {n} of {dions.n_ions}; sum cycles/ion/workgroup {tot/max(n,1):.0f}")
 for i, nm in enumerate(names):
     print(f"  {nm:40s} {buf[i]/max(n,1):10.0f} cycles/ion  {100*buf[i]/max(tot,1):5.1f}%")
+for i, nm in extra.items():
+    print(f"  {nm:40s} {buf[i]/max(n,1):10.0f} cycles/ion")
 print("big-pass ions", int(((f & 8) != 0).sum()), "dense ions", int(((f & 2) != 0).sum()),
       "chaos-NaN ions", int(((f & 4) != 0).sum()))

@@ -7,12 +7,15 @@ if not os.environ.get("SMG_LIB"):
 import torch
 from sm_distributed_amd import engine as E, synthetic as syn
 
-n_sf = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
+a = sys.argv[1:]  # n_sf, or nrows ncols peaks n_sf
+nrows, ncols, pk, n_sf = (int(a[0]), int(a[1]), float(a[2]), int(a[3])) if len(a) >= 4 else \
+    (500, 500, 2000.0, int(a[0]) if a else 20000)
 ions = syn.make_ion_table(n_sf, seed=43, decoy_seed=44)
-mz, hits, dims, info = syn.make_dataset_torch(500, 500, 2000, seed=42, device="cuda", ions=ions)
+mz, hits, dims, info = syn.make_dataset_torch(nrows, ncols, pk, seed=42, device="cuda", ions=ions)
 peaks = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
 dions = E.DeviceIons.from_arrays(ions.win_off, ions.peak_mz, ions.peak_int)
 L = _lib.lib()
+L.smg_debug_main_kernel(0)  # ion_pipe_kernel (the sparse pass has its own stamps: diag_sparse_stamps.py)
 L.smg_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 buf = (ctypes.c_ulonglong * 16)()
 m, lo, hi = E.run_hot_path(peaks, dions, 2.0, 30)

@@ -5,7 +5,8 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 acc = defaultdict(list)
 for r in rows:
     name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
-    short = re.sub(r"\(.*", "", name)
+    short = re.sub(r"\(anonymous namespace\)::", "", name)
+    short = re.sub(r"\(.*", "", short)
     short = re.sub(r"<.*>", "<..>", short)
     m = re.search(r"ion_pipe_kernel<[^,]*, (\d+)", name)
     if m:

@@ -332,8 +332,8 @@ __device__ __forceinline__ bool tbl_add(uint32_t* keys, double* vals, uint32_t k
 }
 
 // ---- the sparse main pass (smg_sparse.hip) ----------------------------------------------------------------
-// true when the 256-thread sparse-set main pass takes this image geometry (packed hits, no clip, <= 2^18 pixels,
-// chaos bands of >= 8 rows); launch_sparse_main launches it with the main pass's interface (positions it cannot
+// true when the 256-thread sparse-set main pass takes this image (packed hits, no clip, <= 2^18 pixels);
+// launch_sparse_main launches it with the main pass's interface (positions it cannot
 // score go to rej_list / rej_count for the big-ion pass)
 bool sparse_main_fits(const Params& P);
 int launch_sparse_main(Hits<SMG_HITS_PACKED_F32> hits, IonDesc* desc, Sched S, const Params& P, double* oc,

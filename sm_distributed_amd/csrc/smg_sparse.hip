@@ -11,19 +11,21 @@
 // there at 500x500 px: 40,448 B per 256-thread workgroup, four per CU.
 //
 // Per-ion structures (LDS):
-//  * entries: the principal window's points sorted by (pixel, window position), one u32 per point -- the pixel,
-//    with bit 31 set on every point after the first of its pixel (a "hole": coo.toarray() sums it into the first);
+//  * entries: the principal window's points grouped by bucket (a counting sort: bucket counts, their scan, each point
+//    at its bucket's arrival slot), one u32 key per point, pixel << 12 | window position; bit 31 marks every point
+//    after the first of its pixel (a "hole": coo.toarray() sums it into the first);
 //  * dir: a bucket directory over 2^bs-pixel buckets (<= 1024 of them): entries [dir[b], dir[b+1]) hold bucket b's
-//    pixels.  A pixel's rank (entry index) is found by a short scan of its bucket;
+//    points.  A pixel's entry (its first point: lowest window position) is found by a short scan of its bucket;
 //  * values: f32 per entry (the packed hits carry f32 intensities, so a single point's value is exact); a pixel
 //    with several points keeps its f64 sum -- summed in window order, as coo.toarray() adds them -- in a side table
 //    its entry points to;
-//  * a blocked Bloom filter (2^15 bits, two bits per pixel in one word) answers the tail stream's membership test
-//    with one LDS read; its positives (~1% false) are resolved exactly after the stream, as ion_pipe_kernel resolves
-//    its parked principal hits;
-//  * chaos: the level index per entry (u8); the 7x7 screen reads presence rows from band bitmaps rebuilt, band by
-//    band, in the LDS the values and the filter leave behind (two bands at 500x500); candidates' exact eL and the
-//    Kruskal pass look pixels up in the directory / a candidate hash, never in an image-sized array.
+//  * a direct-mapped filter F (bit p mod 2^15 for principal pixel p, 4 KB) answers the tail stream's membership test
+//    with one LDS read; its positives (~4% false at 500x500 px) are resolved exactly after the stream, as
+//    ion_pipe_kernel resolves its parked principal hits;
+//  * chaos: the level index per entry (u8); the 7x7 screen's sparsity pre-filter reads its rows from F (a superset
+//    of the principal image whose row segments are runs of bits), the few survivors' rows come exactly from the
+//    directory; candidates' exact eL and the Kruskal pass look pixels up in the directory / a candidate hash, never
+//    in an image-sized array.
 // Everything else (software pipeline with counted waits, the tail stream of window-aligned 64-point groups with
 // parked events, the flagged-point lists and table, the threshold-decomposition chaos, the record for
 // ion_finalize_kernel) is ion_pipe_kernel's.
@@ -54,10 +56,18 @@ __device__ unsigned long long g_sp_stamps[16];
     if (threadIdx.x == 0)                                          \
       for (int _i = 0; _i < 16; ++_i) atomicAdd(&g_sp_stamps[_i], _sacc[_i]); \
   } while (0)
+// wave 0's cycles inside the tail stream's counted waits (part of the tail-stream phase), in slot 12
+#define SP_WAIT_BEGIN() const unsigned long long _tw0 = __builtin_amdgcn_s_memtime()
+#define SP_WAIT_END()                                              \
+  do {                                                             \
+    if (threadIdx.x == 0) _sacc[12] += __builtin_amdgcn_s_memtime() - _tw0; \
+  } while (0)
 #else
 #define SP_STAMP_DECL()
 #define SP_STAMP(i)
 #define SP_STAMP_FLUSH()
+#define SP_WAIT_BEGIN()
+#define SP_WAIT_END()
 #endif
 
 namespace {
@@ -65,6 +75,10 @@ namespace {
 #ifndef SMG_SP_RC
 #define SMG_SP_RC 2  // tail points per thread per chunk (four chunks in flight)
 #endif
+#ifndef SMG_SP_NPARK
+#define SMG_SP_NPARK 4  // tail events parked in registers per thread (later ones are handled in place)
+#endif
+constexpr int SP_NPARK = SMG_SP_NPARK;
 constexpr int SP_BLOCK = 256, SP_RMAX = 10, SP_RC = SMG_SP_RC, SP_WPE = 4, SP_WGPCU = 4;
 constexpr int SP_NW = SP_BLOCK / WAVE;
 constexpr int SP_CAPC = SP_BLOCK * SP_RMAX;  // principal points per ion (more: the big-ion pass)
@@ -85,10 +99,10 @@ enum { S_NE = 0, S_EMAX, S_ABORT, S_SIDE, S_NEXT, S_MAXB, S_NCTR = 8 };
 constexpr uint32_t c16(uint32_t x) { return (x + 15u) & ~15u; }
 
 // LDS carve (bytes).  A persistent part, then a region U with two views: the principal / tail view (Bloom filter,
-// values, bucket counters inside the values' space, flagged-point lists and table, side sums) and the chaos view (band bitmap
-// or candidate hash + union-find at its start, the survivor / candidate list at its end).  The end-of-ion clear
-// zeroes the filter and the counters only, both inside the band space: the chaos list at U's end stays intact for
-// wave 0's few-candidate Kruskal while the other waves clear.
+// values, bucket counters inside the values' space, flagged-point lists and table, side sums) and the chaos view (the
+// filter, still read; the candidate hash + union-find in the values' space; the survivor / candidate lists at U's
+// end).  The end-of-ion clear zeroes the filter and the counters only: the chaos list stays intact for wave 0's
+// few-candidate Kruskal while the other waves clear.
 struct SpLay {
   static constexpr uint32_t o_ekey = 0;
   static constexpr uint32_t o_L = o_ekey + SP_CAPC * 4;
@@ -104,6 +118,7 @@ struct SpLay {
   static constexpr uint32_t o_evals = o_F + SP_FWORDS * 4;
   static constexpr uint32_t o_cnt = o_evals;  // bucket counters: build only (the values are written after)
   static constexpr uint32_t o_dkey = c16(o_evals + SP_CAPC * 4);
+  static constexpr uint32_t o_coll = o_dkey;  // filter collisions: build only (the tail's lists are written after)
   static constexpr uint32_t o_dval = c16(o_dkey + SP_NW * SP_DSEG * 4);
   static constexpr uint32_t o_dcnt = c16(o_dval + SP_NW * SP_DSEG * 8);
   static constexpr uint32_t o_tkey = c16(o_dcnt + SP_NW * 4);
@@ -114,42 +129,50 @@ struct SpLay {
   static constexpr uint32_t o_cel = SP_LDS_BYTES - SP_CCAP;
   static constexpr uint32_t o_clist = o_cel - SP_CCAP * 4;
   static constexpr uint32_t o_wsurv = o_clist - SP_NW * WAVE * 4;  // per-wave survivor lists (chaos screen)
-  static constexpr uint32_t o_band = o_U;  // guard word, then the band's bits
-  static constexpr uint32_t o_hash = o_U;
+  static constexpr uint32_t o_band = o_U;                          // band bitmaps (images above 2^15 pixels)
+  static constexpr int band_bits = (int)(o_wsurv - o_band) * 8;
+  static_assert(o_band % 16 == 0, "band bitmaps are zeroed as uint4");
+  static constexpr uint32_t o_hash = o_evals;  // (the filter F stays intact for the chaos pre-filter)
   static constexpr uint32_t o_par = o_hash + SP_HSZ * 4;
-  // data words of a band: a guard word in front, two zero words behind, and the uint4 rounding of the zeroing
-  static constexpr int band_words = (int)((o_wsurv - o_band) / 4) - 6;
   static_assert(o_tend <= SP_LDS_BYTES, "principal / tail view fits");
   static_assert(o_cnt + SP_NBMAX * 4 <= o_dkey, "bucket counters inside the values' space");
-  static_assert(o_par + SP_CCAP * 4 <= o_wsurv, "Kruskal hash + union-find below the chaos lists");
+  static_assert(o_coll + SP_FWORDS * 4 <= o_tval + 8 * 8 && o_coll + SP_FWORDS * 4 <= SP_LDS_BYTES - SP_CCAP * 5 - SP_NW * WAVE * 4,
+                "collision bits below the chaos lists");
+  static_assert(o_hash >= o_F + SP_FWORDS * 4 && o_par + SP_CCAP * 4 <= o_wsurv, "hash + union-find between F and the lists");
   static_assert(o_F + SP_FWORDS * 4 <= o_wsurv && o_cnt + SP_NBMAX * 4 <= o_wsurv, "cleared words below the lists");
   static_assert(SP_LDS_BYTES % 512 == 0 && 4 * SP_LDS_BYTES <= 160 * 1024, "four workgroups per CU");
 };
 
 struct SpGeo {
   int32_t bs;         // bucket = pixel >> bs
-  int32_t band_rows;  // image rows screened per chaos band
+  int32_t band_rows;  // image rows screened per chaos band (images above 2^15 pixels)
 };
 
-__device__ __forceinline__ uint32_t sp_hash(uint32_t p) { return __umul24(p, 0x9E37B1u) ^ (p >> 14); }
-__device__ __forceinline__ uint32_t sp_fword(uint32_t h) { return (h >> 6) & (uint32_t)(SP_FWORDS - 1); }
-__device__ __forceinline__ uint32_t sp_fmask(uint32_t h) { return (1u << (h & 31u)) | (1u << ((h >> 16) & 31u)); }
+// the filter F: bit p mod 2^15 for every principal pixel p (direct-mapped: a row segment of pixels is a run of bits, so
+// the chaos pre-filter reads it too)
+__device__ __forceinline__ uint32_t sp_fword(uint32_t p) { return (p >> 5) & (uint32_t)(SP_FWORDS - 1); }
+__device__ __forceinline__ uint32_t sp_fmask(uint32_t p) { return 1u << (p & 31u); }
 
 __device__ __forceinline__ double sp_val(uint32_t w, const double* side) {
   return (w & 0xFFF00000u) == SP_SIDEREF ? side[w & 0xFFFFFu] : (double)__uint_as_float(w);
 }
 
-// entry index of principal pixel p (-1: not in the principal image); holes never match
+// entry index of principal pixel p (-1: not in the principal image): among its bucket's entries of pixel p (keys
+// pixel << 12 | window position, in arrival order) the one with the lowest window position, the pixel's first point,
+// which holds the pixel's value (a marked hole has bit 31 set and never matches)
 __device__ __forceinline__ int sp_lookup(const uint32_t* ekey, const uint16_t* dir, uint32_t p, int bs) {
   const uint32_t b = p >> bs;
-  int i = dir[b];
-  const int e = dir[b + 1];
-  for (; i < e; ++i) {
+  const int s0 = dir[b], e = dir[b + 1];
+  int r = -1;
+  uint32_t best = 0xFFFFFFFFu;
+  for (int i = s0; i < e; ++i) {
     const uint32_t w = ekey[i];
-    if (w == p) return i;
-    if ((w & ~SP_HOLE) > p) break;
+    if ((w >> 12) == p && w < best) {
+      best = w;
+      r = i;
+    }
   }
-  return -1;
+  return r;
 }
 
 // the exact level index (divisions, loops), kept out of line so that the loops calling sp_level stay small
@@ -186,7 +209,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
   static_assert(CAPC == SP_CAPC && NW == SP_NW, "layout geometry");
   static_assert(RMAX >= 2 * RC, "principal slots double as two tail buffers");
   static_assert(NW * SP_DSEG == BLOCK, "one deferred-list slot per thread");
-  static_assert(SP_NBMAX == 4 * BLOCK, "four bucket counters per thread");
+  static_assert(SP_NBMAX == 16 * WAVE, "sixteen bucket counters per lane of wave 0");
   static_assert(CAPC <= 4096, "window positions in 12 bits of the sort key");
   using LY = SpLay;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -197,11 +220,11 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
   double* red = reinterpret_cast<double*>(smem + LY::o_red);
   double* side = reinterpret_cast<double*>(smem + LY::o_side);
   int* ctr = reinterpret_cast<int*>(smem + LY::o_ctr);
-  int* wsc = reinterpret_cast<int*>(smem + LY::o_wsc);
   IonDesc* dsl = reinterpret_cast<IonDesc*>(smem + LY::o_desc);
   uint32_t* F = reinterpret_cast<uint32_t*>(smem + LY::o_F);
   uint32_t* evals = reinterpret_cast<uint32_t*>(smem + LY::o_evals);
   uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + LY::o_cnt);
+  uint32_t* coll = reinterpret_cast<uint32_t*>(smem + LY::o_coll);
   uint32_t* dkey = reinterpret_cast<uint32_t*>(smem + LY::o_dkey);
   double* dval = reinterpret_cast<double*>(smem + LY::o_dval);
   int* dcnt = reinterpret_cast<int*>(smem + LY::o_dcnt);
@@ -210,7 +233,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
   uint32_t* clist = reinterpret_cast<uint32_t*>(smem + LY::o_clist);
   uint8_t* cel = smem + LY::o_cel;
   uint32_t* wsurv = reinterpret_cast<uint32_t*>(smem + LY::o_wsurv) + (threadIdx.x >> 6) * WAVE;
-  uint32_t* band = reinterpret_cast<uint32_t*>(smem + LY::o_band) + 1;  // band[-1]: zero guard word
+  uint32_t* band = reinterpret_cast<uint32_t*>(smem + LY::o_band);
   uint32_t* htab = reinterpret_cast<uint32_t*>(smem + LY::o_hash);
   uint32_t* par = reinterpret_cast<uint32_t*>(smem + LY::o_par);
 
@@ -266,8 +289,10 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
   auto clear_fc = [&](int t0, int nt) {
     uint4* zf = reinterpret_cast<uint4*>(F);
     uint4* zc = reinterpret_cast<uint4*>(cnt);
+    uint4* zl = reinterpret_cast<uint4*>(coll);
     for (int i = t0; i < SP_FWORDS / 4; i += nt) zf[i] = make_uint4(0, 0, 0, 0);
     for (int i = t0; i < SP_NBMAX / 4; i += nt) zc[i] = make_uint4(0, 0, 0, 0);
+    for (int i = t0; i < SP_FWORDS / 4; i += nt) zl[i] = make_uint4(0, 0, 0, 0);
     if (t0 < S_NCTR && t0 != S_NEXT) ctr[t0] = 0;
   };
   auto clear_table = [&]() {
@@ -332,7 +357,6 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       acc[4] = v > acc[4] ? v : acc[4];
     };
     uint32_t aw[(RMAX + 1) / 2];  // u16 pairs: a point's arrival index in its bucket, later its sorted entry index
-    uint32_t stbits = 0;          // 2 bits per slot: 0 single point, 1 first of several, 2 later point (hole)
 #pragma unroll
     for (int j = 0; j < (RMAX + 1) / 2; ++j) aw[j] = 0u;
     auto aw_get = [&](int j) -> uint32_t { return (aw[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; };
@@ -357,8 +381,8 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
           if ((v != v) || p >= (uint32_t)P.npx) {  // NaN intensities / foreign pixels: the big-ion pass (f64 values)
             bad = true;
           } else {
-            const uint32_t h = sp_hash(p);
-            atomicOr(&F[sp_fword(h)], sp_fmask(h));
+            // a filter bit set twice: the two points may share a pixel (only those scan their bucket below)
+            if (atomicOr(&F[sp_fword(p)], sp_fmask(p)) & sp_fmask(p)) atomicOr(&coll[sp_fword(p)], sp_fmask(p));
             aw_set(j, atomicAdd(&cnt[p >> bs], 1u) & 0xFFFFu);
           }
         }
@@ -371,23 +395,40 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       }
     }
     if (!skip) {
-      // exclusive scan of the bucket counts -> dir (four counters per thread), and the largest bucket
-      const uint4 c4 = reinterpret_cast<const uint4*>(cnt)[tid];
-      const int tot = (int)(c4.x + c4.y + c4.z + c4.w);
-      const int mx = (int)max(max(c4.x, c4.y), max(c4.z, c4.w));
-      const int inc = wave_incl_scan_dpp(tot);
-      int wmx = mx;
+      // exclusive scan of the bucket counts -> dir, and the largest bucket: wave 0 alone (16 counters per lane), one
+      // barrier
+      if (wid == 0) {
+        const uint4* c4 = reinterpret_cast<const uint4*>(cnt) + lane * 4;
+        uint32_t c[16];
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) wmx = max(wmx, __shfl_xor(wmx, o, 64));
-      if (lane == 63) wsc[wid] = inc;
-      if (lane == 0 && wmx > SP_BMAX) ctr[S_MAXB] = 1;
-      __syncthreads();
-      int off = inc - tot;
+        for (int q = 0; q < 4; ++q) {
+          const uint4 v = c4[q];
+          c[4 * q] = v.x;
+          c[4 * q + 1] = v.y;
+          c[4 * q + 2] = v.z;
+          c[4 * q + 3] = v.w;
+        }
+        uint32_t tot = 0, mx = 0;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) off += (w < wid) ? wsc[w] : 0;
-      const uint32_t d0 = (uint32_t)off, d1 = d0 + c4.x, d2 = d1 + c4.y, d3 = d2 + c4.z;
-      reinterpret_cast<uint2*>(dir)[tid] = make_uint2(d0 | (d1 << 16), d2 | (d3 << 16));
-      if (tid == BLOCK - 1) dir[SP_NBMAX] = (uint16_t)(d3 + c4.w);
+        for (int q = 0; q < 16; ++q) {
+          tot += c[q];
+          mx = max(mx, c[q]);
+        }
+        const int inc = wave_incl_scan_dpp((int)tot);
+        uint32_t run = (uint32_t)inc - tot, d[8];
+#pragma unroll
+        for (int q = 0; q < 16; q += 2) {
+          const uint32_t a = run;
+          run += c[q];
+          d[q / 2] = a | (run << 16);
+          run += c[q + 1];
+        }
+        uint4* dd = reinterpret_cast<uint4*>(dir) + lane * 2;
+        dd[0] = make_uint4(d[0], d[1], d[2], d[3]);
+        dd[1] = make_uint4(d[4], d[5], d[6], d[7]);
+        if (lane == 63) dir[SP_NBMAX] = (uint16_t)inc;
+        if (__ballot(mx > (uint32_t)SP_BMAX)) ctr[S_MAXB] = 1;
+      }
       __syncthreads();
       if (ctr[S_MAXB]) {  // a crowded bucket (the sort below is quadratic in it): the big-ion pass
         reject();
@@ -395,35 +436,43 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       }
     }
     SP_STAMP(1);
+    uint32_t hole_slots = 0;  // bit j: point j is a later point of its pixel (marked in ekey after the ticket barrier)
     if (!skip) {
-      // unsorted keys (pixel << 12 | window position) at the bucket's arrival slots ...
+      // every point's key (pixel << 12 | window position) and value at its bucket's arrival slot (entry index) ...
 #pragma unroll
       for (int j = 0; j < RMAX; ++j) {
         const int i = tid + j * BLOCK;
         if (i < n0) {
           const uint32_t p = H::pix(hs(j));
-          ekey[dir[p >> bs] + aw_get(j)] = (p << 12) | (uint32_t)i;
+          const int f = (int)dir[p >> bs] + (int)aw_get(j);
+          ekey[f] = (p << 12) | (uint32_t)i;
+          evals[f] = (uint32_t)(hs(j) >> 32);
+          aw_set(j, (uint32_t)f);
         }
       }
       __syncthreads();
-      // ... each point's rank among its bucket's keys, and whether its pixel has other points before / after it.
-      // The scans of five slots run together (their LDS reads in flight at once), each lane for as many steps as
-      // its longest bucket among them.
+      // ... then each point whose filter bit was set twice scans its bucket for points of its pixel: none (a single
+      // point, like every point with a filter bit of its own: its value enters the
+      // statistics), only later ones (the pixel's first point: it sums them all, in window order as coo.toarray()
+      // does, into the side table), or an earlier one (a hole).  The scans of five slots run together.
 #pragma unroll
       for (int g = 0; g < RMAX; g += 5) {
         constexpr int GS = 5;
-        uint32_t sl[GS], rk[GS];
+        uint32_t sl[GS], st[GS];
         int mlen = 0;
 #pragma unroll
         for (int jj = 0; jj < GS; ++jj) {
           const int j = g + jj;
           sl[jj] = 0u;
-          rk[jj] = 0u;
+          st[jj] = 0u;
           if (j < RMAX && tid + j * BLOCK < n0) {
-            const uint32_t b = H::pix(hs(j)) >> bs;
-            const uint32_t s0 = dir[b], s1 = dir[b + 1];
-            sl[jj] = s0 | ((s1 - s0) << 16);
-            mlen = max(mlen, (int)(s1 - s0));
+            const uint32_t p = H::pix(hs(j));
+            if (coll[sp_fword(p)] & sp_fmask(p)) {  // (else no other point has its pixel: a single point)
+              const uint32_t b = p >> bs;
+              const uint32_t s0 = dir[b], s1 = dir[b + 1];
+              sl[jj] = s0 | ((s1 - s0) << 16);
+              mlen = max(mlen, (int)(s1 - s0));
+            }
           }
         }
         for (int k = 0; k < mlen; ++k) {
@@ -434,33 +483,46 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
               const uint32_t p = H::pix(hs(j)), key = (p << 12) | (uint32_t)(tid + j * BLOCK);
               const uint32_t w = ekey[(sl[jj] & 0xFFFFu) + k];
               const bool same = (w >> 12) == p;
-              rk[jj] += (w < key ? 1u : 0u) | ((same && w < key) ? 0x10000u : 0u) | ((same && w > key) ? 0x1000000u : 0u);
+              st[jj] |= (same && w < key ? 2u : 0u) | (same && w > key ? 1u : 0u);
             }
           }
         }
 #pragma unroll
         for (int jj = 0; jj < GS; ++jj) {
           const int j = g + jj;
-          if (j < RMAX && tid + j * BLOCK < n0) {
-            aw_set(j, (sl[jj] & 0xFFFFu) + (rk[jj] & 0xFFFFu));
-            const bool before = (rk[jj] & 0xFF0000u) != 0u, after = (rk[jj] >> 24) != 0u;
-            stbits |= (before ? 2u : (after ? 1u : 0u)) << (2 * j);
+          if (j >= RMAX || tid + j * BLOCK >= n0) continue;
+          if (st[jj] & 2u) {
+            hole_slots |= 1u << j;
+          } else if (st[jj] == 0u) {
+            stat((double)__uint_as_float((uint32_t)(hs(j) >> 32)));
+          } else {  // the first point of a pixel with several: their sum in window order
+            const uint32_t p = H::pix(hs(j));
+            const int b0 = (int)(sl[jj] & 0xFFFFu), b1 = b0 + (int)(sl[jj] >> 16);
+            double sum = (double)__uint_as_float((uint32_t)(hs(j) >> 32));
+            uint32_t last = (p << 12) | (uint32_t)(tid + j * BLOCK);
+            while (true) {  // the next point of the pixel by window position
+              uint32_t nk = 0xFFFFFFFFu;
+              int ni = -1;
+              for (int k = b0; k < b1; ++k) {
+                const uint32_t w = ekey[k];
+                if ((w >> 12) == p && w > last && w < nk) {
+                  nk = w;
+                  ni = k;
+                }
+              }
+              if (ni < 0) break;
+              sum += (double)__uint_as_float(evals[ni]);
+              last = nk;
+            }
+            const int slot = atomicAdd(&ctr[S_SIDE], 1);
+            if (slot < SP_SIDE) {
+              side[slot] = sum;
+              evals[aw_get(j)] = SP_SIDEREF | (uint32_t)slot;
+            } else {
+              ctr[S_ABORT] = 1;
+            }
+            stat(sum);
           }
-        }
-      }
-      __syncthreads();
-      // ... then the sorted entries and the values at them (a pixel's points are consecutive, first one first)
-#pragma unroll
-      for (int j = 0; j < RMAX; ++j) {
-        const int i = tid + j * BLOCK;
-        if (i < n0) {
-          const uint32_t p = H::pix(hs(j));
-          const uint32_t st = (stbits >> (2 * j)) & 3u;
-          const int f = (int)aw_get(j);
-          ekey[f] = p | (st == 2u ? SP_HOLE : 0u);
-          const uint32_t vb = (uint32_t)(hs(j) >> 32);
-          evals[f] = vb;
-          if (st == 0u) stat((double)__uint_as_float(vb));
         }
       }
     }
@@ -476,25 +538,14 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         ld8_async_v(pd[j], hits.h);
       }
     }
+    // the statistics' per-wave sums into red (every thread reads them after the ticket barrier)
     if (!skip) {
-      __syncthreads();
-      // pixels with several points: the f64 sum in window order (coo.toarray()), kept in the side table; each such
-      // pixel's first point (state 1) sums the entries behind its own
 #pragma unroll
-      for (int j = 0; j < RMAX; ++j) {
-        if (((stbits >> (2 * j)) & 3u) != 1u) continue;
-        const int f = (int)aw_get(j);
-        const uint32_t w = ekey[f];
-        double s = (double)__uint_as_float(evals[f]);
-        for (int k = f + 1; k < n0 && ekey[k] == (w | SP_HOLE); ++k) s += (double)__uint_as_float(evals[k]);
-        const int slot = atomicAdd(&ctr[S_SIDE], 1);
-        if (slot < SP_SIDE) {
-          side[slot] = s;
-          evals[f] = SP_SIDEREF | (uint32_t)slot;
-        } else {
-          ctr[S_ABORT] = 1;
-        }
-        stat(s);
+      for (int q = 0; q < 4; ++q) acc[q] = wave_sum_dpp(acc[q]);
+      acc[4] = wave_max_dpp(acc[4]);
+      if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < 5; ++q) red[q * NW + wid] = acc[q];
       }
     }
     SP_STAMP(2);
@@ -512,14 +563,37 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       reject();
       skip = true;
     }
-    // the statistics' per-wave sums into red, read after the tail stream's closing barrier
+    // the holes mark their entries (no scan reads the keys any more; a lookup before the mark sees the pixel's first
+    // point anyway: it takes the lowest window position)
+    if (!skip && hole_slots) {
+#pragma unroll
+      for (int j = 0; j < RMAX; ++j)
+        if ((hole_slots >> j) & 1u) ekey[aw_get(j)] |= SP_HOLE;
+    }
+    // the principal statistics (per-wave sums, in wave order)
+    double sx = 0.0, sxx = 0.0, s0 = 0.0, npx_pos = 0.0, vmax = 0.0;
     if (!skip) {
+      double t[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] = wave_sum_dpp(acc[q]);
-      acc[4] = wave_max_dpp(acc[4]);
-      if (lane == 0) {
+      for (int w = 0; w < NW; ++w) {
 #pragma unroll
-        for (int q = 0; q < 5; ++q) red[q * NW + wid] = acc[q];
+        for (int q = 0; q < 4; ++q) t[q] += red[q * NW + w];
+        t[4] = red[4 * NW + w] > t[4] ? red[4 * NW + w] : t[4];
+      }
+      sx = t[0];
+      sxx = t[1];
+      s0 = t[2];
+      npx_pos = t[3];
+      vmax = t[4];
+    }
+    const bool chaos_ok = !skip && (sx > 0.0) && (npx_pos >= 4.0);
+    // the level index per entry, for the chaos phase (the values' space later holds its candidate hash): computed here,
+    // while tail chunks 2 and 3 are in flight (a hole not yet marked gets a level nobody reads)
+    if (chaos_ok) {
+      const double rcp = 1.0 / vmax;
+      for (int i = tid; i < n0; i += BLOCK) {
+        const uint32_t w = ekey[i];
+        if (!(w & SP_HOLE)) L8[i] = (uint8_t)sp_level(sp_val(evals[i], side), vmax, rcp, P);
       }
     }
     SP_STAMP(3);
@@ -534,12 +608,17 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       int gnext = uni(D->gs[2]);
       int wend = uni(D->end[1]);
       // Events: a filter positive (the point's pixel may be principal: Σxy, Σy[x>0]) or a flagged point (summed per
-      // (pixel, window) before squaring).  Two per lane are parked in registers (the raw hit and its window, bit 4: a
-      // filter positive) and resolved after the stream for all lanes at once; a lane's third and later events are
+      // (pixel, window) before squaring).  SP_NPARK per lane are parked in registers (the raw hit and its window, bit 4:
+      // a filter positive) and resolved after the stream for all lanes at once; a lane's third and later events are
       // handled in place.  Partials: part[k][wid], written only by this wave, lanes of one instruction in hardware
       // order -- deterministic.
-      Reg ev0 = 0ull, ev1 = 0ull;
-      int evk0 = 0, evk1 = 0, nev = 0;
+      Reg ev[SP_NPARK];
+      int evk[SP_NPARK], nev = 0;
+#pragma unroll
+      for (int q = 0; q < SP_NPARK; ++q) {
+        ev[q] = 0ull;
+        evk[q] = 0;
+      }
       auto add_x = [&](bool hit, int r, const Reg& h, int k) {
         if (__ballot(hit)) {
           if (hit) {
@@ -570,9 +649,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         uint32_t fw[RC], fm[RC];
 #pragma unroll
         for (int j = 0; j < RC; ++j) {
-          const uint32_t h = sp_hash(H::pix(buf[j]));
-          fw[j] = F[sp_fword(h)];
-          fm[j] = sp_fmask(h);
+          const uint32_t pj = H::pix(buf[j]);
+          fw[j] = F[sp_fword(pj)];
+          fm[j] = sp_fmask(pj);
         }
 #pragma unroll
         for (int j = 0; j < RC; ++j) {
@@ -586,60 +665,92 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
             const bool valid = lane < wend - Gi * 64;
             const Reg h = buf[j];
             const bool in = valid && (fw[j] & fm[j]) == fm[j];
-            const bool ev = in || (valid && H::dup(h));
-            const bool s0 = ev && nev == 0, s1 = ev && nev == 1;
-            ev0 = s0 ? h : ev0;
-            evk0 = s0 ? (curk | (in ? 16 : 0)) : evk0;
-            ev1 = s1 ? h : ev1;
-            evk1 = s1 ? (curk | (in ? 16 : 0)) : evk1;
-            const bool ovf = ev && nev >= 2;
-            nev += ev ? 1 : 0;
+            const bool evt = in || (valid && H::dup(h));
+#pragma unroll
+            for (int q = 0; q < SP_NPARK; ++q) {
+              const bool sq = evt && nev == q;
+              ev[q] = sq ? h : ev[q];
+              evk[q] = sq ? (curk | (in ? 16 : 0)) : evk[q];
+            }
+            const bool ovf = evt && nev >= SP_NPARK;
+            nev += evt ? 1 : 0;
             if (__ballot(ovf)) handle(ovf, h, curk, in);
           }
         }
       };
       // chunks 0 and 1 are in flight (issued during the previous iteration); later chunks one ahead (refills are
       // issued unconditionally so that exactly 3*RC loads follow each buffer's)
+      // refills of this ion's later chunks: the window of the next group to load is tracked like the stream's (groups
+      // only grow along a wave's issues), so that a refill reads the descriptor only when the window changes
+      int ik = 1, ign = uni(D->gs[2]), iend = uni(D->end[1]);
+      int64_t ibase = uni64(D->base[1]);
+      auto refill = [&](int c, Reg (&buf)[RC]) {
+#pragma unroll
+        for (int j = 0; j < RC; ++j) {
+          const int Gi = c * GPC + j * NW + wid;
+          while (Gi >= ign) {  // (uniform)
+            ++ik;
+            ign = ik + 1 < MAXK ? uni(D->gs[ik + 1]) : 0x7FFFFFFF;
+            iend = uni(D->end[ik]);
+            ibase = uni64(D->base[ik]);
+          }
+          const int64_t idx = Gi < ng ? ibase + (int64_t)Gi * 64 + min(lane, iend - Gi * 64 - 1) : 0;
+          ld8_async_v(buf[j], hits.h + idx);
+        }
+      };
       for (int c = 0; c * GPC < ng; c += 4) {
-        vm_wait<3 * RC>(pa);
+        {
+          SP_WAIT_BEGIN();
+          vm_wait<3 * RC>(pa);
+          SP_WAIT_END();
+        }
         process(c, pa);
-        issue_chunk(D, c + 4, pa);
+        refill(c + 4, pa);
         if ((c + 1) * GPC >= ng) break;
-        vm_wait<3 * RC>(pb);
+        {
+          SP_WAIT_BEGIN();
+          vm_wait<3 * RC>(pb);
+          SP_WAIT_END();
+        }
         process(c + 1, pb);
-        issue_chunk(D, c + 5, pb);
+        refill(c + 5, pb);
         if ((c + 2) * GPC >= ng) break;
-        vm_wait<3 * RC>(pc);
+        {
+          SP_WAIT_BEGIN();
+          vm_wait<3 * RC>(pc);
+          SP_WAIT_END();
+        }
         process(c + 2, pc);
-        issue_chunk(D, c + 6, pc);
+        refill(c + 6, pc);
         if ((c + 3) * GPC >= ng) break;
-        vm_wait<3 * RC>(pd);
+        {
+          SP_WAIT_BEGIN();
+          vm_wait<3 * RC>(pd);
+          SP_WAIT_END();
+        }
         process(c + 3, pd);
-        issue_chunk(D, c + 7, pd);
+        refill(c + 7, pd);
       }
-      // the parked events, both at once
+      // the parked events, all at once
       if (__ballot(nev > 0)) {
-        const uint32_t p0 = H::pix(ev0), p1 = H::pix(ev1);
-        const int r0 = (nev > 0 && (evk0 & 16)) ? sp_lookup(ekey, dir, p0, bs) : -1;
-        const int r1 = (nev > 1 && (evk1 & 16)) ? sp_lookup(ekey, dir, p1, bs) : -1;
-        add_x(r0 >= 0, r0, ev0, evk0 & 15);
-        add_x(r1 >= 0, r1, ev1, evk1 & 15);
-        const bool d0 = nev > 0 && H::dup(ev0);
-        const bool d1 = nev > 1 && H::dup(ev1);
-        const uint64_t m0 = __ballot(d0), m1 = __ballot(d1);
-        if (m0 | m1) {
-          const uint64_t below = (1ull << lane) - 1ull;
-          const int e0 = nd + (int)__popcll(m0 & below);
-          const int e1 = nd + (int)__popcll(m0) + (int)__popcll(m1 & below);
-          if (d0 && e0 < SP_DSEG) {
-            wdkey[e0] = (p0 << 3) | (uint32_t)(evk0 & 15);
-            wdval[e0] = H::val(ev0);
+        int r[SP_NPARK];
+#pragma unroll
+        for (int q = 0; q < SP_NPARK; ++q) r[q] = (nev > q && (evk[q] & 16)) ? sp_lookup(ekey, dir, H::pix(ev[q]), bs) : -1;
+#pragma unroll
+        for (int q = 0; q < SP_NPARK; ++q) add_x(r[q] >= 0, r[q], ev[q], evk[q] & 15);
+        const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+        for (int q = 0; q < SP_NPARK; ++q) {
+          const bool dq = nev > q && H::dup(ev[q]);
+          const uint64_t mq = __ballot(dq);
+          if (mq) {
+            const int e = nd + (int)__popcll(mq & below);
+            if (dq && e < SP_DSEG) {
+              wdkey[e] = (H::pix(ev[q]) << 3) | (uint32_t)(evk[q] & 15);
+              wdval[e] = H::val(ev[q]);
+            }
+            nd += (int)__popcll(mq);
           }
-          if (d1 && e1 < SP_DSEG) {
-            wdkey[e1] = (p1 << 3) | (uint32_t)(evk1 & 15);
-            wdval[e1] = H::val(ev1);
-          }
-          nd += (int)(__popcll(m0) + __popcll(m1));
         }
       }
       if (lane == 0) dcnt[wid] = nd;
@@ -654,23 +765,6 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
     if (!skip) clear_table();
     __syncthreads();
     SP_STAMP(5);
-    // the principal statistics (per-wave sums, in wave order)
-    double sx = 0.0, sxx = 0.0, s0 = 0.0, npx_pos = 0.0, vmax = 0.0;
-    if (!skip) {
-      double t[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) t[q] += red[q * NW + w];
-        t[4] = red[4 * NW + w] > t[4] ? red[4 * NW + w] : t[4];
-      }
-      sx = t[0];
-      sxx = t[1];
-      s0 = t[2];
-      npx_pos = t[3];
-      vmax = t[4];
-    }
-    const bool chaos_ok = !skip && (sx > 0.0) && (npx_pos >= 4.0);
     // ---- deferred flagged points: exact per-(pixel, window) sums, squared into the partials -----------------------
     if (!skip) {
       int nd_tot = 0, nd_max = 0;
@@ -697,7 +791,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
               atomicAdd(&part[(size_t)(key & 7u) * NW * 4 + 2], y * y);
             }
           }
-          __syncthreads();  // (the table's space becomes the chaos list / band bitmaps)
+          __syncthreads();  // (the table's space becomes the chaos lists)
         }
       }
     }
@@ -707,63 +801,42 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
     double chaos_raw = NAN;
     uint32_t flags = 0;
     if (!skip && chaos_ok) {
-      // level index per entry (the values die here: their space becomes the band bitmaps)
-      const double rcp = 1.0 / vmax;
-      for (int i = tid; i < n0; i += BLOCK) {
-        const uint32_t w = ekey[i];
-        if (!(w & SP_HOLE)) L8[i] = (uint8_t)sp_level(sp_val(evals[i], side), vmax, rcp, P);
-      }
-      __syncthreads();
       SP_STAMP(7);
-      // (i) the 7x7 screen, band by band: a band bitmap holds presence rows [rb, re) = the band's rows [r0, r1) and
-      //     three rows either side.  Pass A lists the band's principal pixels with >= 3 principal pixels in their 7x7
-      //     (sparsity pre-filter, erosion border 0) in the wave's own survivor list; pass B runs the full screen over
-      //     full lists (a wave's own: no barrier between the passes) and appends candidates (owned pixels of the
-      //     dilated-covered boxes) to the chaos list.
-      const int B = G.band_rows;
-      for (int r0 = 0; r0 < nr; r0 += B) {  // uniform
-        const int r1 = min(r0 + B, nr), rb = max(r0 - 3, 0), re = min(r1 + 3, nr);
-        const int nwords = ((re - rb) * ncl + 31) / 32 + 2;  // data + two zero words behind
-        {
-          uint4* z = reinterpret_cast<uint4*>(band - 1);
-          for (int i = tid; i < (nwords + 1 + 3) / 4; i += BLOCK) z[i] = make_uint4(0, 0, 0, 0);
-        }
-        __syncthreads();
-        const int pa0 = rb * ncl, pa1 = re * ncl;
-        {
-          const int i0 = dir[pa0 >> bs], i1 = dir[((pa1 - 1) >> bs) + 1];
-          for (int i = i0 + tid; i < i1; i += BLOCK) {
-            const uint32_t w = ekey[i];
-            if (!(w & SP_HOLE) && w >= (uint32_t)pa0 && w < (uint32_t)pa1) {
-              const uint32_t q = w - (uint32_t)pa0;
-              atomicOr(&band[q >> 5], 1u << (q & 31));
-            }
-          }
-        }
-        __syncthreads();
-        // presence of row `row` (absolute), columns c0 .. c0+6 masked by cv; 0 outside the image
-        auto brow7 = [&](int row, int c0, uint32_t cv) -> uint32_t {
-          const bool rv = (unsigned)row < (unsigned)nr;
-          const int st = (rv ? row - rb : 0) * ncl + c0;  // >= -3: the guard word in front reads as zero
-          const int w = st >> 5;
-          const uint32_t v = __builtin_amdgcn_alignbit(band[w + 1], band[w], (uint32_t)(st & 31)) & cv;
-          return rv ? v : 0u;
-        };
+      // (i) the 7x7 screen over presence bitmaps: the filter F itself where it is exact (images up to 2^15 pixels: bit
+      //     p for pixel p), else band bitmaps of image rows rebuilt in the LDS the values and the flagged-point lists
+      //     leave behind (two bands at 500x500 px): the band's words zeroed, then a bit set per entry.  Pass A: a
+      //     principal pixel with fewer than three principal pixels in its 7x7 (itself included) cannot own a
+      //     candidate (erosion border 0); the others go to the wave's own survivor list, and pass B (the wave's own
+      //     list: no barrier between the passes) runs the full screen over them, appending candidates (owned pixels
+      //     of the dilated-covered boxes) to the chaos list.
+      // presence of row `row`, columns c0 .. c0+6 (c0 >= -3) masked by cv, from bitmap bm whose bit 0 is pixel org;
+      // 0 outside the image.  Bits outside the image's columns are masked, so the words around the bitmap may hold
+      // anything.
+      auto bmrow7 = [&](const uint32_t* bm, int org, int rdef, int row, int c0, uint32_t cv) -> uint32_t {
+        const bool rv = (unsigned)row < (unsigned)nr;
+        const int st = (rv ? row : rdef) * ncl + c0 - org;  // >= -3
+        const int w = st >> 5;
+        const uint32_t v = __builtin_amdgcn_alignbit(bm[w + 1], bm[w], (uint32_t)(st & 31)) & cv;
+        return rv ? v : 0u;
+      };
+      auto rowcv = [&](int s, int& rs, int& cs, uint32_t& cv) {
+        rowcol(s, P, rs, cs);
+        const int clo = 3 - cs > 0 ? 3 - cs : 0, chi = ncl - cs + 3 < 7 ? ncl - cs + 3 : 7;
+        cv = ((1u << chi) - 1u) & ~((1u << clo) - 1u);
+      };
+      auto sparse = [&](const uint32_t (&Hh)[7]) {
+        return !P.erosion_border && (__popc(Hh[0]) + __popc(Hh[1]) + __popc(Hh[2]) + __popc(Hh[3]) +
+                                     __popc(Hh[4]) + __popc(Hh[5]) + __popc(Hh[6])) < 3;
+      };
+      // passes A and B over the entries [i0, i1) whose pixels lie in [q0, q1), rows read from bm (origin org, rows
+      // rdef.. present)
+      auto screen_range = [&](const uint32_t* bm, int org, int rdef, int i0, int i1, uint32_t q0, uint32_t q1) {
         auto rows7 = [&](int s, int& rs, int& cs, uint32_t& cv, uint32_t (&Hh)[7]) {
-          rowcol(s, P, rs, cs);
-          const int clo = 3 - cs > 0 ? 3 - cs : 0, chi = ncl - cs + 3 < 7 ? ncl - cs + 3 : 7;
-          cv = ((1u << chi) - 1u) & ~((1u << clo) - 1u);
+          rowcv(s, rs, cs, cv);
 #pragma unroll
-          for (int d = 0; d < 7; ++d) Hh[d] = brow7(rs - 3 + d, cs - 3, cv);
+          for (int d = 0; d < 7; ++d) Hh[d] = bmrow7(bm, org, rdef, rs - 3 + d, cs - 3, cv);
         };
-        auto sparse = [&](const uint32_t (&Hh)[7]) {
-          return !P.erosion_border && (__popc(Hh[0]) + __popc(Hh[1]) + __popc(Hh[2]) + __popc(Hh[3]) +
-                                       __popc(Hh[4]) + __popc(Hh[5]) + __popc(Hh[6])) < 3;
-        };
-        const uint32_t q0 = (uint32_t)(r0 * ncl), q1 = (uint32_t)(r1 * ncl);
-        const int s0e = dir[q0 >> bs], s1e = dir[((q1 - 1) >> bs) + 1];
-        // pass B on this wave's survivors wsurv[0, wcnt) (lane i takes survivor i): the full screen, candidates
-        // appended to the chaos list (one LDS atomic per wave)
+        // pass B on this wave's survivors wsurv[0, wcnt) (lane i takes survivor i)
         auto screen = [&](int wcnt) {
           __builtin_amdgcn_wave_barrier();  // (the survivor list was written by this wave's lanes)
           const bool ok = lane < wcnt;
@@ -815,13 +888,11 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
           }
           __builtin_amdgcn_wave_barrier();  // (the list is refilled after this)
         };
-        // pass A: the band's principal pixels with >= 3 principal pixels in their 7x7 (every one with erosion border
-        // 1) go to the wave's survivor list; a full list is screened at once, the rest after the band's last round
         int wcnt = 0;  // (wave-uniform)
-        for (int ob = s0e; ob < s1e; ob += BLOCK) {  // uniform trip count
+        for (int ob = i0; ob < i1; ob += BLOCK) {  // uniform trip count
           const int i = ob + tid;
-          const uint32_t w = i < s1e ? ekey[i] : SP_HOLE;
-          const bool ok = !(w & SP_HOLE) && w >= q0 && w < q1;
+          const uint32_t w = i < i1 ? ekey[i] >> 12 : 0xFFFFFFFFu;  // the pixel (a hole's: >= 2^19)
+          const bool ok = w >= q0 && w < q1;
           int rs, cs;
           uint32_t cv, Hh[7];
           rows7(ok ? (int)w : (int)q0, rs, cs, cv, Hh);
@@ -836,7 +907,31 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
           wcnt += c;
         }
         if (wcnt > 0) screen(wcnt);
+      };
+      if (P.npx <= SP_FWORDS * 32) {  // F is the principal image's presence bitmap
+        screen_range(F, 0, 0, 0, n0, 0u, (uint32_t)P.npx);
         __syncthreads();
+      } else {
+        const int B = G.band_rows;
+        for (int r0 = 0; r0 < nr; r0 += B) {  // uniform
+          const int r1 = min(r0 + B, nr), rb = max(r0 - 3, 0), re = min(r1 + 3, nr);
+          const int b0 = (rb * ncl) >> bs, b1 = (re * ncl - 1) >> bs, org = b0 << bs;
+          // rows [rb, re) of the band bitmap: zeroed, then a bit per entry (holes and the partial buckets' foreign
+          // rows fall outside)
+          const uint32_t span = (uint32_t)(re * ncl - org);
+          const int nw4 = (int)((span + 127u) >> 7);
+          for (int k = tid; k < nw4; k += BLOCK) reinterpret_cast<uint4*>(band)[k] = make_uint4(0u, 0u, 0u, 0u);
+          __syncthreads();
+          const int e1 = dir[b1 + 1];
+          for (int i = dir[b0] + tid; i < e1; i += BLOCK) {
+            const uint32_t q = (ekey[i] >> 12) - (uint32_t)org;
+            if (q < span) atomicOr(&band[q >> 5], 1u << (q & 31u));
+          }
+          __syncthreads();
+          const uint32_t q0 = (uint32_t)(r0 * ncl), q1 = (uint32_t)(r1 * ncl);
+          screen_range(band, org, rb, dir[q0 >> bs], dir[((q1 - 1) >> bs) + 1], q0, q1);
+          __syncthreads();
+        }
       }
       SP_STAMP(8);
       const int ncand = ctr[S_NE];
@@ -863,10 +958,8 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
               const uint32_t lo = (uint32_t)(row * ncl + max(cp - 2, 0)), hi = (uint32_t)(row * ncl + min(cp + 2, ncl - 1));
               const int e1 = dir[(hi >> bs) + 1];
               for (int i = dir[lo >> bs]; i < e1; ++i) {
-                const uint32_t w = ekey[i];
-                if (w & SP_HOLE) continue;
-                if (w > hi) break;
-                if (w >= lo) packed |= (uint64_t)L8[i] << (8 * (int)(w - (uint32_t)base));
+                const uint32_t w = ekey[i] >> 12;  // (a hole's: >= 2^19, outside the range)
+                if (w >= lo && w <= hi) packed |= (uint64_t)L8[i] << (8 * (int)(w - (uint32_t)base));
               }
             }
             Lrow[d] = packed;
@@ -942,7 +1035,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
             sum_c = wave_sum_dpp(e >= 1 ? (double)e : 0.0) - wave_sum_dpp(wsum);
           }
         } else if (emax_all > 0) {
-          // the band space is free: a candidate hash (pixel -> index) and the union-find
+          // a candidate hash (pixel -> index) and the union-find in the values' space
           for (int i = tid; i < SP_HSZ; i += BLOCK) htab[i] = SP_EMPTY;
           __syncthreads();
           double esum = 0.0;
@@ -1054,7 +1147,9 @@ SpGeo sparse_geo(const Params& P) {
   int lg = 0;
   while ((1ll << lg) < (long long)P.npx) ++lg;
   G.bs = lg > 10 ? lg - 10 : 0;  // <= 1024 buckets
-  const long long rows = (long long)SpLay::band_words * 32 / P.ncols;
+  // a band's bitmap holds its rows [rb, re): rows * ncols bits plus a partial bucket in front (and the uint4 rounding
+  // of its zeroing)
+  const long long rows = ((long long)SpLay::band_bits - 2ll * (1ll << G.bs) - 128) / P.ncols;
   G.band_rows = (int)(rows - 6 > 0x7FFFFFFF ? 0x7FFFFFFF : rows - 6);
   return G;
 }
@@ -1063,7 +1158,7 @@ SpGeo sparse_geo(const Params& P) {
 
 bool sparse_main_fits(const Params& P) {
   if (P.clip || P.npx <= 0 || P.npx > NPX_LDS_MAX) return false;
-  return sparse_geo(P).band_rows >= 8;
+  return P.npx <= SP_FWORDS * 32 || sparse_geo(P).band_rows >= 8;
 }
 
 int launch_sparse_main(Hits<SMG_HITS_PACKED_F32> hits, IonDesc* desc, Sched S, const Params& P, double* oc,

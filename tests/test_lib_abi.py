@@ -32,9 +32,12 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_argument_errors_without_gpu():
+    import sm_distributed_amd
     from sm_distributed_amd import _lib
     L = _lib.lib()
     assert b"gfx950" in L.smg_version()
+    assert L.smg_version().decode().startswith(f"smg {sm_distributed_amd.__version__} ")  # one version
+    assert L.smg_debug_main_kernel(2) == -1 and L.smg_debug_main_kernel(1) == 0
     sz = ctypes.c_size_t(0)
     assert L.smg_ion_metrics_workspace_size(10, 0, 5, ctypes.byref(sz)) == -1  # bad shape -> SMG_ERR_INVALID
     assert b"bad arguments" in L.smg_last_error()
