@@ -42,6 +42,12 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# KFD queue evictions of this process (each stops every running kernel for >= one 10-ms tick) are counted per step
+# (sm_distributed_amd/hostmem.py); SMG_NUMA_OPTOUT=1 takes the process out of NUMA-balancing scans, one trigger of
+# them, before torch starts its threads (the pool's boxes run with numa_balancing = 0)
+from sm_distributed_amd import hostmem  # noqa: E402
+
+NUMA_OPTOUT = hostmem.numa_balancing_optout() if os.environ.get("SMG_NUMA_OPTOUT") == "1" else False
 
 METRIC = "MSM-scored ions/sec (HMDB×3 adducts, 250k-px synth) + imaging-kernel HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -203,6 +209,7 @@ def main():
     formulas = FormulasSegm.from_ion_table(ions, args.ppm)
     ds_config = {"image_generation": {"ppm": args.ppm, "nlevels": args.nlevels, "q": 99, "do_preprocessing": False}}
     shard_only = args.shard_of > 1 and not sharded
+    phases = None
     if sharded:
         plan = D.plan_shards(formulas, peaks, args.ppm, world, rank)
         if not args.no_rebalance:
@@ -218,7 +225,21 @@ def main():
             plan = D.rebalance(plan, formulas, peaks, times, head_seconds=head)
             log(f"[rank {rank}] rebalanced from measured shard times (ms) {[round(x * 1e3, 2) for x in times]}, "
                 f"rank-0 assembly {head * 1e3:.2f} ms: counts {plan.counts}")
-        step_fn = lambda: D.score_sharded(plan, peaks, ds_config)[0]
+        phases = []  # per step: this rank's rows, gather (its wait for the slowest rank included), assembly (ms)
+
+        def step_fn():
+            # D.score_sharded's body with a clock between its three parts (a device synchronisation after the
+            # rows: the gather needs them anyway), so that each rank's line says where its step went
+            t_a = time.perf_counter()
+            rows, _ = D._device_rows(plan, peaks, ds_config)
+            torch.cuda.synchronize()
+            t_b = time.perf_counter()
+            table = D.gather_rows(rows, plan)
+            torch.cuda.synchronize()
+            t_c = time.perf_counter()
+            df = D.rows_to_frame(table, plan.global_keys) if table is not None else None
+            phases.append(((t_b - t_a) * 1e3, (t_c - t_b) * 1e3, (time.perf_counter() - t_c) * 1e3))
+            return df
         my_formulas = plan.formulas
     elif shard_only:
         # one rank of an N-way plan measured alone on this GPU: its slice, images, scores and row block (the
@@ -266,6 +287,8 @@ def main():
         gc.collect()
         gc.freeze()
     clock = ClockSampler(torch.cuda.get_device_properties(device))
+    evict = hostmem.EvictionCounter(hostmem.kfd_gpu_id(torch.cuda.get_device_properties(device).pci_bus_id))
+    ev_marks = [evict.read()]
     clock.start()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -275,6 +298,7 @@ def main():
     for _ in range(args.steps):
         df = step_fn()  # ends with the table on the host (a synchronisation)
         marks.append(time.perf_counter())
+        ev_marks.append(evict.read())
         if verbose:  # pinned host allocations so far (diagnostic: step-time outliers)
             host_allocs.append(torch.cuda.host_memory_stats().get("num_host_alloc", -1))
     torch.cuda.synchronize()
@@ -291,14 +315,32 @@ def main():
         elapsed = float(tt.item())
     ms_per_step = elapsed / max(args.steps, 1) * 1e3
     per_step = np.diff([t0] + marks) * 1e3
+    # each step's shader clock: the lowest sample the 20-ms sampler took inside the step (so that an outlier step
+    # carries its own clock)
+    step_clk = [clock.over(a, b) for a, b in zip([t0] + marks[:-1], marks)]
     if len(per_step):
         log(f"[rank {rank}] step ms: min {per_step.min():.2f} median {np.median(per_step):.2f} "
             f"max {per_step.max():.2f}; shader clock MHz {sclk}")
-        if os.environ.get("SMG_BENCH_VERBOSE"):
-            log(f"[rank {rank}] steps: " + " ".join(f"{x:.1f}" for x in per_step))
-            log(f"[rank {rank}] pass launches (pass:ms): " + " ".join(f"{p}:{t:.2f}" for p, t in pass_ms))
-            log(f"[rank {rank}] pinned host allocations after each step: {host_allocs}")
-            log(f"[rank {rank}] host allocator stats: {dict(torch.cuda.host_memory_stats())}")
+    # every rank's step min / median / max and clock, gathered for the line (one all_gather of 5 floats)
+    mine = [float(per_step.min()), float(np.median(per_step)), float(per_step.max())] if len(per_step) else [0.0] * 3
+    mine += [float(sclk["median"]) if sclk else -1.0, float(sclk["min"]) if sclk else -1.0]
+    timed_phases = np.asarray(phases[-len(per_step):]) if phases else np.zeros((0, 3))
+    mine += [float(x) for x in np.median(timed_phases, axis=0)] if len(timed_phases) else [-1.0] * 3
+    per_rank = [mine]
+    if sharded:
+        tt = torch.tensor(mine, dtype=torch.float64, device=device)
+        ts = [torch.zeros_like(tt) for _ in range(world)]
+        dist.all_gather(ts, tt)
+        per_rank = [[float(x) for x in t.tolist()] for t in ts]
+    # each timed step's device passes (HIP events around every launch): the descriptor pass and the main pass, so
+    # that a slow step shows whether the device or the host took the extra time
+    step_desc = [round(t, 3) for p_, t in pass_ms if p_ == _lib.SMG_PASS_DESC]
+    step_main = [round(t, 3) for p_, t in pass_ms if p_ == _lib.SMG_PASS_MAIN]
+    if os.environ.get("SMG_BENCH_VERBOSE"):
+        log(f"[rank {rank}] steps: " + " ".join(f"{x:.1f}" for x in per_step))
+        log(f"[rank {rank}] pass launches (pass:ms): " + " ".join(f"{p}:{t:.2f}" for p, t in pass_ms))
+        log(f"[rank {rank}] pinned host allocations after each step: {host_allocs}")
+        log(f"[rank {rank}] host allocator stats: {dict(torch.cuda.host_memory_stats())}")
     # one more search with the host-side caches dropped (the theoretical-intensity alignment and the shard's
     # global row index are reused between steps while the ion keys are unchanged): a cold first search of a
     # new formula table in a warm process
@@ -362,6 +404,18 @@ def main():
             "cold_cache_step_ms": cold_ms,
             "step_ms_min_median_max": ([float(per_step.min()), float(np.median(per_step)), float(per_step.max())]
                                        if len(per_step) else None),
+            "steps_ms": [round(float(x), 3) for x in per_step],
+            "steps_sclk_mhz": step_clk,
+            # KFD's queue-eviction time of this process per step (ms; None where sysfs does not show it)
+            "steps_evicted_ms": ([b - a for a, b in zip(ev_marks[:-1], ev_marks[1:])]
+                                 if None not in ev_marks else None),
+            "numa_balancing": {"kernel": hostmem.numa_balancing_enabled(), "process_opted_out": NUMA_OPTOUT},
+            "steps_desc_pass_ms": step_desc if len(step_desc) == len(per_step) else None,
+            "steps_main_pass_ms": step_main if len(step_main) == len(per_step) else None,
+            "per_rank": [{"rank": r, "step_ms_min_median_max": v[:3],
+                          "sclk_mhz_median_min": None if v[3] < 0 else v[3:5],
+                          "median_ms_rows_gather_assembly": None if v[5] < 0 else v[5:8]}
+                         for r, v in enumerate(per_rank)],
             "device_chain": chain,
             "roofline": roofline,
             "passes": passes,
@@ -417,6 +471,7 @@ class ClockSampler:
         elif len(cands) == 1:
             self.path = cands[0][0]
         self.samples = []
+        self.times = []
         self._stop = threading.Event()
         self._thr = None
 
@@ -435,6 +490,7 @@ class ClockSampler:
                 v = None
             if v is not None:
                 self.samples.append(v)
+                self.times.append(time.perf_counter())
             self._stop.wait(0.02)
 
     def start(self):
@@ -451,6 +507,18 @@ class ClockSampler:
             return None
         v = np.asarray(self.samples)
         return {"min": float(v.min()), "median": float(np.median(v)), "max": float(v.max()), "samples": int(v.size)}
+
+    def over(self, t0, t1):
+        """The clock over [t0, t1] (perf_counter seconds): the lowest sample inside it, else the nearest one; None
+        without samples."""
+        if not self.samples:
+            return None
+        t = np.asarray(self.times)
+        v = np.asarray(self.samples)
+        inside = (t >= t0) & (t <= t1)
+        if inside.any():
+            return float(v[inside].min())
+        return float(v[np.argmin(np.minimum(np.abs(t - t0), np.abs(t - t1)))])
 
 
 def _assembly_seconds(D, plan, peaks, ds_config, reps=3):

@@ -28,7 +28,8 @@ L.smg_debug_sparse_stamps(buf, 16)
 names = ["top: ticket, descriptor checks", "build: filter, bucket counts, directory", "entries, values, side sums",
          "ticket barrier, stats, levels", "tail stream", "issue next ion, tail barrier", "duplicate table",
          "(unused)", "chaos screen (bands)", "exact eL", "kruskal", "record, clear, loop barrier"]
-extra = {12: "(tail stream: in counted waits)"}
+extra = {12: "(tail stream: in counted waits)", 13: "(tail stream: parked events resolved)",
+         14: "(tail stream: events handled in place)", 15: "(tail stream: refills issued)"}
 f = m.flags.cpu().numpy()
 n = int(((f & 0x41) == 0x41).sum())
 tot = sum(buf[i] for i in range(len(names)))

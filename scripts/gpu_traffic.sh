@@ -12,7 +12,10 @@ for c in FETCH_SIZE WRITE_SIZE; do
   cp $(find /tmp/tr_$c -name "*counter_collection.csv" | head -1) gpurun_out/$TAG/$c.csv
 done
 n=$(grep "calibration bytes" gpurun_out/$TAG/FETCH_SIZE.log | awk '{print $3/8}')
-python3 scripts/traffic_summary.py gpurun_out/$TAG/FETCH_SIZE.csv gpurun_out/$TAG/WRITE_SIZE.csv $n gpurun_out/$TAG/traffic.json
+# the main pass's kernel (KERNEL=ion_pipe_kernel[512] with SMG_MAIN_KERNEL=0); config 3's algorithmic bytes are
+# 12 B x 6,439,292,385 window points
+python3 scripts/traffic_summary.py gpurun_out/$TAG/FETCH_SIZE.csv gpurun_out/$TAG/WRITE_SIZE.csv $n gpurun_out/$TAG/traffic.json \
+  "${KERNEL:-ion_sparse_kernel}" config3 77271508620
 rc=$?
 rm -f gpurun_out/$TAG/FETCH_SIZE.csv gpurun_out/$TAG/WRITE_SIZE.csv  # large; the summary keeps what is used
 exit $rc

@@ -186,11 +186,24 @@ print("assembly parts (ms): " + ", ".join(f"{k} {v*1e3:.2f}" for k, v in parts.i
 same = df1 is not None and df.index.equals(df1.index) and np.allclose(df.to_numpy(), df1.to_numpy(), rtol=0,
                                                                        atol=1e-12)
 print(f"assembly (rank 0) {t_asm:.2f} ms; table identical to 1 GPU: {same}")
-gather_est = n_max * 40 / 50e9 * 1e3 + 0.05  # W-1 blocks over W-1 xGMI links into rank 0 at once, ~50 GB/s each
+# the gather's payload: W blocks of n_max rows x 5 f64 into rank 0 (RCCL gather).  One GPU cannot run the
+# collective; what it can time is the payload's own device copy (HBM to HBM, a floor) -- the xGMI leg is estimated
+# from it: W-1 blocks over W-1 point-to-point links into rank 0 at once, ~50 GB/s achieved per link, plus RCCL's
+# launch latency (~50 us).  bench.py --gpus N prints every rank's measured gather median on the driver's node.
+payload = W * n_max * 5 * 8
+src = torch.empty(W * n_max * 5, dtype=torch.float64, device="cuda")
+dst = torch.empty_like(src)
+t_copy, _ = timed(lambda: dst.copy_(src), reps=5)
+gather_est = (n_max * 40) / 50e9 * 1e3 + 0.05
+print(f"gather payload {payload / 1e6:.2f} MB ({W} x {n_max:,} rows x 40 B): device copy of it {t_copy:.3f} ms; "
+      f"xGMI estimate {gather_est:.3f} ms")
 est1 = worst + gather_est + t_asm
 others = max(times[1:]) * 1e3
 est = max(times[0] * 1e3 + t_asm, others) + gather_est
-print(f"one search alone {est1:.2f} ms = max rank {worst:.2f} + gather ~{gather_est:.2f} + assembly {t_asm:.2f}")
+print(f"one search alone {est1:.2f} ms = max rank {worst:.2f} + gather ~{gather_est:.2f} + assembly {t_asm:.2f}; "
+      f"strong-scaling efficiency {t1 / (W * est1):.2f}")
 print(f"estimated {W}-GPU step (back to back) {est:.2f} ms = max(rank 0 {times[0] * 1e3:.2f} + assembly "
       f"{t_asm:.2f}, other ranks {others:.2f}) + gather ~{gather_est:.2f}; strong-scaling efficiency "
       f"{t1 / (W * est):.2f}")
+print("(both efficiencies assume every rank runs at the clock it had alone on this GPU; eight busy GPUs of one "
+      "node may run slower)")

@@ -5,3 +5,4 @@ Ion-image generation (``formula_imager_segm.compute_sf_images``) and MSM scoring
 Python interface.  See DESIGN.md.
 """
 __version__ = "0.2.0"  # = the library's smg_version() (smg_prep.hip)
+

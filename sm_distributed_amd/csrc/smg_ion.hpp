@@ -275,23 +275,31 @@ __device__ __forceinline__ int home_xcd() {
   }
 }
 
+// A ticket is resolved against the counter it was drawn from (``home``, recorded at issue): a workgroup may move to
+// another XCD between the two -- a queue eviction saves and restores its waves, possibly elsewhere -- and a ticket of
+// one XCD's counter read against another XCD's range names a position that counter never handed out.  Two workgroups
+// then score the same position, and one of them may read the other's IonRec (written over the descriptor) as a
+// descriptor: window bases made of sums, a load from a wild address (round 5: a memory-aperture fault in a bench run
+// that coincided with a KFD eviction of the process's queues).
 template <int SRC>
-__device__ __forceinline__ uint32_t sched_issue(const Sched& S) {
-  if constexpr (SRC == SRC_RANGES) return atomicAdd(&S.ctr[home_xcd() * CTR_STRIDE], 1u);
+__device__ __forceinline__ uint32_t sched_issue(const Sched& S, int& home) {
+  home = home_xcd();
+  if constexpr (SRC == SRC_RANGES) return atomicAdd(&S.ctr[home * CTR_STRIDE], 1u);
   else return atomicAdd(S.ctr, 1u);
 }
 // the same ticket, asynchronously (see atomic_add_rtn_async); valid after the counted wait
 template <int SRC>
-__device__ __forceinline__ void sched_issue_async(const Sched& S, uint32_t& t) {
-  if constexpr (SRC == SRC_RANGES) atomic_add_rtn_async(t, &S.ctr[home_xcd() * CTR_STRIDE], 1u);
+__device__ __forceinline__ void sched_issue_async(const Sched& S, uint32_t& t, int& home) {
+  home = home_xcd();
+  if constexpr (SRC == SRC_RANGES) atomic_add_rtn_async(t, &S.ctr[home * CTR_STRIDE], 1u);
   else atomic_add_rtn_async(t, S.ctr, 1u);
 }
 
-// resolves a ticket of sched_issue into a position (-1: no work left)
+// resolves a ticket of sched_issue, drawn from XCD ``home``'s counter, into a position (-1: no work left); further
+// tickets come from the next XCDs' counters in turn
 template <int SRC>
-__device__ __forceinline__ int64_t sched_resolve(const Sched& S, uint32_t t) {
+__device__ __forceinline__ int64_t sched_resolve(const Sched& S, uint32_t t, int home) {
   if constexpr (SRC == SRC_RANGES) {
-    const int home = home_xcd();
     for (int i = 0; i < XCDS; ++i) {
       const int x = (home + i) % XCDS;
       const int64_t a = S.n * x / XCDS, b = S.n * (x + 1) / XCDS;
@@ -311,10 +319,14 @@ __device__ __forceinline__ int64_t uni64(int64_t v) {
   return ((int64_t)hi << 32) | (uint32_t)lo;
 }
 
+// (a position some pass already scored holds an IonRec, state 1 -- pad[7] of a descriptor is 0: never read its
+// sums as window bases, whatever hands such a position out twice)
 __device__ __forceinline__ bool desc_lds_ok(const IonDesc* D, int capc) {
   const int K = D->K;
-  return K >= 1 && K <= MAXK && D->end[0] <= capc && D->ngroups >= 0;
+  return K >= 1 && K <= MAXK && D->end[0] <= capc && D->ngroups >= 0 &&
+         reinterpret_cast<const IonRec*>(D)->state == 0u;
 }
+static_assert(offsetof(IonRec, state) == offsetof(IonDesc, pad) + 7 * sizeof(int32_t), "IonRec::state over pad[7]");
 
 // (key, f64 sum) open-addressing table in LDS (empty key 0xFFFFFFFF): adds v to key's sum; false when full
 template <int NSLOT>

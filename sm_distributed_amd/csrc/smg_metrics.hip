@@ -949,7 +949,11 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     }
   };
   clear_set_vals(tid, BLOCK);
-  if (tid == 0) ctr[C_NEXT] = (int)sched_resolve<SRC>(S, sched_issue<SRC>(S));
+  if (tid == 0) {
+    int h0;
+    const uint32_t t0 = sched_issue<SRC>(S, h0);
+    ctr[C_NEXT] = (int)sched_resolve<SRC>(S, t0, h0);
+  }
   __syncthreads();
   int64_t pos = -1;  // ion scored in this iteration (-1: none; the first iteration only issues loads)
   int64_t npos = uni(ctr[C_NEXT]);
@@ -967,10 +971,11 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     // the ticket of the ion after npos: issued now, consumed after phase 1 (wave 0 issues after it exactly one
     // descriptor load, and the 2*RC loads of tail chunks 2 and 3 unless this iteration skips)
     uint32_t ticket = 0;
+    int thome = 0;  // the XCD whose counter the ticket came from
     if constexpr (ASYNC) {
-      if (tid == 0) sched_issue_async<SRC>(S, ticket);
+      if (tid == 0) sched_issue_async<SRC>(S, ticket, thome);
     } else {
-      if (tid == 0) ticket = sched_issue<SRC>(S);
+      if (tid == 0) ticket = sched_issue<SRC>(S, thome);
     }
     // npos's descriptor: one async word per lane of wave 0 (exactly one load per lane, clamped), waited in
     // phase 2 behind the 2*RC loads of tail chunks 2 and 3
@@ -1079,7 +1084,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         vm_wait1<2 * RC>(ticket);
         vm_wait1<2 * RC>(dword);
       }
-      if (tid == 0) ctr[C_NEXT] = (int)sched_resolve<SRC>(S, ticket);
+      if (tid == 0) ctr[C_NEXT] = (int)sched_resolve<SRC>(S, ticket, thome);
       if (npos >= 0 && lane < DESC_QWORDS) reinterpret_cast<uint64_t*>(DN)[lane] = dword;
     }
     __syncthreads();

@@ -62,12 +62,21 @@ __device__ unsigned long long g_sp_stamps[16];
   do {                                                             \
     if (threadIdx.x == 0) _sacc[12] += __builtin_amdgcn_s_memtime() - _tw0; \
   } while (0)
+// wave 0's cycles in a marked region (inside a phase) into slot i (13: the parked events' resolution, 14: the
+// in-place event handling inside the tail stream, 15: the tail stream's refills)
+#define SP_MARK_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define SP_MARK_END(v, i)                                          \
+  do {                                                             \
+    if (threadIdx.x == 0) _sacc[i] += __builtin_amdgcn_s_memtime() - v; \
+  } while (0)
 #else
 #define SP_STAMP_DECL()
 #define SP_STAMP(i)
 #define SP_STAMP_FLUSH()
 #define SP_WAIT_BEGIN()
 #define SP_WAIT_END()
+#define SP_MARK_BEGIN(v)
+#define SP_MARK_END(v, i)
 #endif
 
 namespace {
@@ -302,7 +311,11 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
     }
   };
   clear_fc(tid, BLOCK);
-  if (tid == 0) ctr[S_NEXT] = (int)sched_resolve<SRC_RANGES>(S, sched_issue<SRC_RANGES>(S));
+  if (tid == 0) {
+    int h0;
+    const uint32_t t0 = sched_issue<SRC_RANGES>(S, h0);
+    ctr[S_NEXT] = (int)sched_resolve<SRC_RANGES>(S, t0, h0);
+  }
   __syncthreads();
   int64_t pos = -1;  // ion scored in this iteration (-1: none; the first iteration only issues loads)
   int64_t npos = uni(ctr[S_NEXT]);
@@ -315,7 +328,8 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
     // the ticket of the ion after npos, consumed after the principal build (wave 0 issues after it exactly one
     // descriptor load, then the 2*RC loads of tail chunks 2 and 3 or their stand-ins)
     uint32_t ticket = 0;
-    if (tid == 0) sched_issue_async<SRC_RANGES>(S, ticket);
+    int thome = 0;  // the XCD whose counter the ticket came from (sched_resolve)
+    if (tid == 0) sched_issue_async<SRC_RANGES>(S, ticket, thome);
     uint64_t dword = 0;
     if ((tid >> 6) == 0)
       ld8_async_wave0(dword, reinterpret_cast<const uint64_t*>(desc + (npos >= 0 ? npos : 0)) +
@@ -554,7 +568,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
     if ((tid >> 6) == 0) {
       vm_wait1<2 * RC>(ticket);
       vm_wait1<2 * RC>(dword);
-      if (tid == 0) ctr[S_NEXT] = (int)sched_resolve<SRC_RANGES>(S, ticket);
+      if (tid == 0) ctr[S_NEXT] = (int)sched_resolve<SRC_RANGES>(S, ticket, thome);
       if (npos >= 0 && lane < DESC_QWORDS) reinterpret_cast<uint64_t*>(DN)[lane] = dword;
     }
     __syncthreads();
@@ -674,7 +688,11 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
             }
             const bool ovf = evt && nev >= SP_NPARK;
             nev += evt ? 1 : 0;
-            if (__ballot(ovf)) handle(ovf, h, curk, in);
+            if (__ballot(ovf)) {
+              SP_MARK_BEGIN(_th0);
+              handle(ovf, h, curk, in);
+              SP_MARK_END(_th0, 14);
+            }
           }
         }
       };
@@ -685,6 +703,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       int ik = 1, ign = uni(D->gs[2]), iend = uni(D->end[1]);
       int64_t ibase = uni64(D->base[1]);
       auto refill = [&](int c, Reg (&buf)[RC]) {
+        SP_MARK_BEGIN(_tr0);
 #pragma unroll
         for (int j = 0; j < RC; ++j) {
           const int Gi = c * GPC + j * NW + wid;
@@ -697,6 +716,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
           const int64_t idx = Gi < ng ? ibase + (int64_t)Gi * 64 + min(lane, iend - Gi * 64 - 1) : 0;
           ld8_async_v(buf[j], hits.h + idx);
         }
+        SP_MARK_END(_tr0, 15);
       };
       for (int c = 0; c * GPC < ng; c += 4) {
         {
@@ -732,6 +752,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         refill(c + 7, pd);
       }
       // the parked events, all at once
+      SP_MARK_BEGIN(_tp0);
       if (__ballot(nev > 0)) {
         int r[SP_NPARK];
 #pragma unroll
@@ -754,6 +775,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         }
       }
       if (lane == 0) dcnt[wid] = nd;
+      SP_MARK_END(_tp0, 13);
     }
     SP_STAMP(4);
     // ---- the registers of ion b are dead: ion b+1's principal window and first two chunks go in flight
