@@ -450,6 +450,12 @@ class ClockSampler:
     def __init__(self, props):
         import glob
         self.path = None
+        self.samples = []
+        self.times = []
+        self._stop = threading.Event()
+        self._thr = None
+        if os.environ.get("SMG_BENCH_NO_CLOCK"):  # A/B: no sysfs polling during the timed steps
+            return
         cands = []
         for dev in sorted(glob.glob("/sys/class/drm/card*/device")):
             f = os.path.join(dev, "pp_dpm_sclk")

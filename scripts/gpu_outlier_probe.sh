@@ -30,8 +30,10 @@ EOF3
 echo "our gpu_id: $OURS"
 echo "numa_balancing $(cat /proc/sys/kernel/numa_balancing 2>&1); THP $(cat /sys/kernel/mm/transparent_hugepage/enabled 2>&1); khugepaged defrag $(cat /sys/kernel/mm/transparent_hugepage/khugepaged/defrag 2>&1)"
 for run in ${RUNS:-1}; do
-# runs named a*: the default memory policy (SMG_NUMA_OPTOUT=0); others: the process opted out of NUMA balancing
-case $run in a*) export SMG_NUMA_OPTOUT=0 ;; *) export SMG_NUMA_OPTOUT=1 ;; esac
+# runs named a* / c*: the default memory policy (SMG_NUMA_OPTOUT=0); b*: the process opted out of NUMA balancing
+case $run in a*|c*) export SMG_NUMA_OPTOUT=0 ;; *) export SMG_NUMA_OPTOUT=1 ;; esac
+# runs named c*: no shader-clock polling (pp_dpm_sclk) by the bench
+case $run in c*) export SMG_BENCH_NO_CLOCK=1 ;; *) unset SMG_BENCH_NO_CLOCK ;; esac
 SMG_BENCH_VERBOSE=1 timeout -k 10 400 python -u bench.py --steps 60 --warmup 3 --no-cpu-baseline --chain-steps 0 \
   > $OUT/bench_$run.json 2> $OUT/bench_err_$run.txt &
 TPID=$!

@@ -199,6 +199,22 @@ def make_case(name: str):
         ds = syn.make_dataset_np(250, 1000, 3, seed=173, ions=ions, plant_fraction=1.0, plant_seed=174,
                                  blob_sigma=(4.0, 10.0))
         return add_duplicates(ds, 0.02, 175), ions, 20.0, {}
+    if name == "clip_ties":    # the clip's radix selects down every path: intensities from five values, three of
+        # them one f32 ulp apart (the select runs to its last byte, many ties: the pair pass), windows whose positive
+        # values are all equal (no pass), a value alone in its top byte (fetch + next order statistic in one pass)
+        ds, ions, ppm, _ = make_case("long_tail")
+        rng = np.random.default_rng(181)
+        one = np.float32(1.0)
+        vals = np.array([one, np.nextafter(one, np.float32(2)), np.nextafter(np.nextafter(one, np.float32(2)),
+                                                                              np.float32(2)), 2.5, 1e6, 0.0],
+                        dtype=np.float32)
+        pick = rng.choice(len(vals), size=ds.ints.size, p=[0.45, 0.2, 0.1, 0.12, 0.03, 0.1])
+        ints = vals[pick]
+        # every point of the first ion's windows the same value: all-equal sets (lo == hi)
+        lo_mz, hi_mz = float(ions.peak_mz[ions.win_off[0]]) * (1 - 2e-4), float(ions.peak_mz[ions.win_off[1] - 1]) * (1 + 2e-4)
+        ints[(ds.mz >= lo_mz) & (ds.mz <= hi_mz)] = np.float32(3.0)
+        return (syn.SpectraSet(sp_off=ds.sp_off, mz=ds.mz, ints=ints, coords=ds.coords), ions, ppm,
+                {"do_preprocessing": True, "q": 75.0})
     if name == "boundary":
         ds = syn.make_dataset_np(16, 16, 300, seed=71)
         return ds, boundary_ions(ds, 5.0, 40, 72), 5.0, {}
@@ -207,7 +223,7 @@ def make_case(name: str):
 
 CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels", "nlevels1", "big_window", "huge_window",
          "large_image", "xl_image", "large_blobs", "boundary", "long_tail", "dups_heavy", "kmix", "clip99", "clip_q50_conn8",
-         "clip_dups_heavy", "clip_large", "wide_range", "wide_overflow", "nlevels100", "bands"]
+         "clip_dups_heavy", "clip_large", "wide_range", "wide_overflow", "nlevels100", "bands", "clip_ties"]
 
 
 def oracle_run(ds, ions, ppm, nlevels=30, connectivity=4, erosion_border=0, q=99.0, do_preprocessing=False):

@@ -177,7 +177,7 @@ def test_legacy_main_pass_matches_oracle(name):
 # every LDS-path case again with the two-level pixel set forced (smg_debug_force_two_level)
 TWO_LEVEL_CASES = ["basic", "zeros_rect", "dups", "row", "column", "row_border1", "conn8_border1", "nlevels",
                    "big_window", "boundary", "long_tail", "dups_heavy", "kmix", "clip99", "clip_q50_conn8",
-                   "clip_dups_heavy"]
+                   "clip_dups_heavy", "clip_ties"]
 
 
 @pytest.mark.parametrize("name", TWO_LEVEL_CASES)
