@@ -2,6 +2,7 @@
 import csv, re, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 def short(n):
+    n = n.replace("(anonymous namespace)::", "")
     n = re.sub(r"\(.*", "", n)
     n = re.sub(r"<.*>", "<..>", n)
     return n[:90]
