@@ -27,16 +27,13 @@ struct Params {
 };
 
 // row and column of pixel p < 2^24 from a float reciprocal: the estimate is off by at most one row
+// (branch-free: the correction is two compares and selects)
 __device__ __forceinline__ void rowcol(int p, const Params& P, int& r, int& c) {
   r = (int)((float)p * P.inv_ncols);
   c = p - r * P.ncols;
-  if (c < 0) {
-    --r;
-    c += P.ncols;
-  } else if (c >= P.ncols) {
-    ++r;
-    c -= P.ncols;
-  }
+  const int adj = c < 0 ? -1 : (c >= P.ncols ? 1 : 0);
+  r += adj;
+  c -= adj * P.ncols;
 }
 
 template <int FMT>

@@ -62,7 +62,7 @@ __device__ unsigned long long g_sp_stamps[16];
   do {                                                             \
     if (threadIdx.x == 0) _sacc[12] += __builtin_amdgcn_s_memtime() - _tw0; \
   } while (0)
-// wave 0's cycles in a marked region (inside a phase) into slot i (13: the parked events' resolution, 14: the
+// wave 0's cycles in a marked region (inside a phase) into slot i (13: the marked events' resolution, 14: the
 // in-place event handling inside the tail stream, 15: the tail stream's refills)
 #define SP_MARK_BEGIN(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define SP_MARK_END(v, i)                                          \
@@ -84,10 +84,14 @@ namespace {
 #ifndef SMG_SP_RC
 #define SMG_SP_RC 2  // tail points per thread per chunk (four chunks in flight)
 #endif
-#ifndef SMG_SP_NPARK
-#define SMG_SP_NPARK 4  // tail events parked in registers per thread (later ones are handled in place)
+// timing ablations (wrong results; diagnostic builds only): 1 no chaos, 2 no tail stream, 4 no levels
+#ifndef SMG_SP_ABL
+#define SMG_SP_ABL 0
 #endif
-constexpr int SP_NPARK = SMG_SP_NPARK;
+#ifndef SMG_SP_EVB
+#define SMG_SP_EVB 2  // tail events per lane resolved per round (their points read again together)
+#endif
+constexpr int SP_EVB = SMG_SP_EVB;
 constexpr int SP_BLOCK = 256, SP_RMAX = 10, SP_RC = SMG_SP_RC, SP_WPE = 4, SP_WGPCU = 4;
 constexpr int SP_NW = SP_BLOCK / WAVE;
 constexpr int SP_CAPC = SP_BLOCK * SP_RMAX;  // principal points per ion (more: the big-ion pass)
@@ -221,7 +225,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
   static_assert(SP_NBMAX == 16 * WAVE, "sixteen bucket counters per lane of wave 0");
   static_assert(CAPC <= 4096, "window positions in 12 bits of the sort key");
   using LY = SpLay;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // static LDS (the kernel's only variable besides the stamps' accumulators): its offset is a compile-time constant,
+  // so LDS addresses fold into the instructions' offsets (dynamic LDS costs an add of a relocated base per access)
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SP_LDS_BYTES];
   uint32_t* ekey = reinterpret_cast<uint32_t*>(smem + LY::o_ekey);
   uint8_t* L8 = smem + LY::o_L;
   uint16_t* dir = reinterpret_cast<uint16_t*>(smem + LY::o_dir);
@@ -265,8 +271,8 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
   // every slot issues exactly one load (clamped to the window's last point, or hit 0 for an empty window), so that
   // the counted waits hold on every path
   auto issue_principal = [&](const IonDesc* D) {
-    const int n0 = D->end[0];
-    const int64_t a = D->base[0];
+    const int n0 = uni(D->end[0]);
+    const int64_t a = uni64(D->base[0]);
 #pragma unroll
     for (int j = 0; j < RMAX; ++j) {
       const int i = tid + j * BLOCK;
@@ -274,19 +280,19 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
     }
   };
   // tail chunk c: groups [c*GPC, (c+1)*GPC); slot j of wave w holds group c*GPC + j*NW + w; exactly RC loads
-  auto issue_chunk = [&](const IonDesc* D, int c, Reg (&buf)[RC]) {
-    const int ng = D->ngroups;
+  auto issue_chunk = [&](const IonDesc* D, int c, Reg (&buf)[RC]) {  // (descriptor fields and group uniform: scalar)
+    const int ng = uni(D->ngroups);
     int gsv[MAXK];
 #pragma unroll
-    for (int kk = 2; kk < MAXK; ++kk) gsv[kk] = D->gs[kk];
+    for (int kk = 2; kk < MAXK; ++kk) gsv[kk] = uni(D->gs[kk]);
 #pragma unroll
     for (int j = 0; j < RC; ++j) {
       const int Gi = c * GPC + j * NW + wid;
       int k = 1;
 #pragma unroll
       for (int kk = 2; kk < MAXK; ++kk) k += (Gi >= gsv[kk]) ? 1 : 0;
-      const int64_t bk = D->base[k];
-      const int ek = D->end[k];
+      const int64_t bk = uni64(D->base[k]);
+      const int ek = uni(D->end[k]);
       const int64_t idx = Gi < ng ? bk + (int64_t)Gi * 64 + min(lane, ek - Gi * 64 - 1) : 0;
       ld8_async_v(buf[j], hits.h + idx);
     }
@@ -600,10 +606,10 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       npx_pos = t[3];
       vmax = t[4];
     }
-    const bool chaos_ok = !skip && (sx > 0.0) && (npx_pos >= 4.0);
+    const bool chaos_ok = !skip && (sx > 0.0) && (npx_pos >= 4.0) && !(SMG_SP_ABL & 1);
     // the level index per entry, for the chaos phase (the values' space later holds its candidate hash): computed here,
     // while tail chunks 2 and 3 are in flight (a hole not yet marked gets a level nobody reads)
-    if (chaos_ok) {
+    if (chaos_ok && !(SMG_SP_ABL & 4)) {
       const double rcp = 1.0 / vmax;
       for (int i = tid; i < n0; i += BLOCK) {
         const uint32_t w = ekey[i];
@@ -614,7 +620,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
 
     // ---- tail windows, one stream of window-aligned 64-point groups ------------------------------------------------
     if (!skip) {
-      const int ng = uni(D->ngroups);
+      const int ng = (SMG_SP_ABL & 2) ? 0 : uni(D->ngroups);
       int curk = 1;
       int nd = 0;  // this wave's deferred flagged points (uniform)
       uint32_t* wdkey = dkey + wid * SP_DSEG;
@@ -622,17 +628,12 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       int gnext = uni(D->gs[2]);
       int wend = uni(D->end[1]);
       // Events: a filter positive (the point's pixel may be principal: Σxy, Σy[x>0]) or a flagged point (summed per
-      // (pixel, window) before squaring).  SP_NPARK per lane are parked in registers (the raw hit and its window, bit 4:
-      // a filter positive) and resolved after the stream for all lanes at once; a lane's third and later events are
-      // handled in place.  Partials: part[k][wid], written only by this wave, lanes of one instruction in hardware
-      // order -- deterministic.
-      Reg ev[SP_NPARK];
-      int evk[SP_NPARK], nev = 0;
-#pragma unroll
-      for (int q = 0; q < SP_NPARK; ++q) {
-        ev[q] = 0ull;
-        evk[q] = 0;
-      }
+      // (pixel, window) before squaring).  The stream only marks them: bit t of the lane's event mask = its t-th point
+      // (chunk t / RC, slot t % RC) is an event.  After the stream the events are resolved lane by lane in stream
+      // order, the i-th round taking every lane's i-th event, each point read again (an L2 hit: streamed just now).
+      // A lane's points beyond the 64th are handled in place.  Partials: part[k][wid], written only by this wave,
+      // lanes of one instruction in hardware order -- deterministic.
+      uint32_t evlo = 0u, evhi = 0u;
       auto add_x = [&](bool hit, int r, const Reg& h, int k) {
         if (__ballot(hit)) {
           if (hit) {
@@ -678,19 +679,16 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
             }
             const bool valid = lane < wend - Gi * 64;
             const Reg h = buf[j];
-            const bool in = valid && (fw[j] & fm[j]) == fm[j];
+            const bool in = valid && (fw[j] & fm[j]) != 0u;
             const bool evt = in || (valid && H::dup(h));
-#pragma unroll
-            for (int q = 0; q < SP_NPARK; ++q) {
-              const bool sq = evt && nev == q;
-              ev[q] = sq ? h : ev[q];
-              evk[q] = sq ? (curk | (in ? 16 : 0)) : evk[q];
-            }
-            const bool ovf = evt && nev >= SP_NPARK;
-            nev += evt ? 1 : 0;
-            if (__ballot(ovf)) {
+            const int t = c * RC + j;  // (uniform)
+            if (t < 32) {
+              evlo |= evt ? 1u << t : 0u;
+            } else if (t < 64) {
+              evhi |= evt ? 1u << (t - 32) : 0u;
+            } else if (__ballot(evt)) {
               SP_MARK_BEGIN(_th0);
-              handle(ovf, h, curk, in);
+              handle(evt, h, curk, in);
               SP_MARK_END(_th0, 14);
             }
           }
@@ -751,26 +749,48 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         process(c + 3, pd);
         refill(c + 7, pd);
       }
-      // the parked events, all at once
+      // the marked events, the i-th round taking every lane's i-th
       SP_MARK_BEGIN(_tp0);
-      if (__ballot(nev > 0)) {
-        int r[SP_NPARK];
+      if (__ballot((evlo | evhi) != 0u)) {
+        int gsv[MAXK];
 #pragma unroll
-        for (int q = 0; q < SP_NPARK; ++q) r[q] = (nev > q && (evk[q] & 16)) ? sp_lookup(ekey, dir, H::pix(ev[q]), bs) : -1;
-#pragma unroll
-        for (int q = 0; q < SP_NPARK; ++q) add_x(r[q] >= 0, r[q], ev[q], evk[q] & 15);
+        for (int kk = 2; kk < MAXK; ++kk) gsv[kk] = uni(D->gs[kk]);
         const uint64_t below = (1ull << lane) - 1ull;
+        // rounds of SP_EVB events per lane, their points read together (one latency per round)
+        while (__ballot((evlo | evhi) != 0u)) {
+          Reg hq[SP_EVB];
+          int kq[SP_EVB];
+          bool hasq[SP_EVB];
 #pragma unroll
-        for (int q = 0; q < SP_NPARK; ++q) {
-          const bool dq = nev > q && H::dup(ev[q]);
-          const uint64_t mq = __ballot(dq);
-          if (mq) {
-            const int e = nd + (int)__popcll(mq & below);
-            if (dq && e < SP_DSEG) {
-              wdkey[e] = (H::pix(ev[q]) << 3) | (uint32_t)(evk[q] & 15);
-              wdval[e] = H::val(ev[q]);
+          for (int q = 0; q < SP_EVB; ++q) {
+            hasq[q] = (evlo | evhi) != 0u;
+            const int t = evlo ? __builtin_ctz(evlo) : (evhi ? 32 + __builtin_ctz(evhi) : 0);
+            if (evlo) evlo &= evlo - 1u;
+            else evhi &= evhi - 1u;
+            const int Gi = (t / RC) * GPC + (t % RC) * NW + wid;
+            int k = 1;
+#pragma unroll
+            for (int kk = 2; kk < MAXK; ++kk) k += (Gi >= gsv[kk]) ? 1 : 0;
+            kq[q] = k;
+            hq[q] = hasq[q] ? hits.h[D->base[k] + (int64_t)Gi * 64 + lane] : 0ull;
+          }
+#pragma unroll
+          for (int q = 0; q < SP_EVB; ++q) {
+            const Reg h = hq[q];
+            const uint32_t p = H::pix(h);
+            const bool in = hasq[q] && (F[sp_fword(p)] & sp_fmask(p)) != 0u;
+            const int r = in ? sp_lookup(ekey, dir, p, bs) : -1;
+            add_x(r >= 0, r, h, kq[q]);
+            const bool dq = hasq[q] && H::dup(h);
+            const uint64_t mq = __ballot(dq);
+            if (mq) {
+              const int e = nd + (int)__popcll(mq & below);
+              if (dq && e < SP_DSEG) {
+                wdkey[e] = (p << 3) | (uint32_t)kq[q];
+                wdval[e] = H::val(h);
+              }
+              nd += (int)__popcll(mq);
             }
-            nd += (int)__popcll(mq);
           }
         }
       }
@@ -831,32 +851,37 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       //     candidate (erosion border 0); the others go to the wave's own survivor list, and pass B (the wave's own
       //     list: no barrier between the passes) runs the full screen over them, appending candidates (owned pixels
       //     of the dilated-covered boxes) to the chaos list.
-      // presence of row `row`, columns c0 .. c0+6 (c0 >= -3) masked by cv, from bitmap bm whose bit 0 is pixel org;
-      // 0 outside the image.  Bits outside the image's columns are masked, so the words around the bitmap may hold
-      // anything.
-      auto bmrow7 = [&](const uint32_t* bm, int org, int rdef, int row, int c0, uint32_t cv) -> uint32_t {
-        const bool rv = (unsigned)row < (unsigned)nr;
-        const int st = (rv ? row : rdef) * ncl + c0 - org;  // >= -3
-        const int w = st >> 5;
-        const uint32_t v = __builtin_amdgcn_alignbit(bm[w + 1], bm[w], (uint32_t)(st & 31)) & cv;
-        return rv ? v : 0u;
-      };
       auto rowcv = [&](int s, int& rs, int& cs, uint32_t& cv) {
         rowcol(s, P, rs, cs);
         const int clo = 3 - cs > 0 ? 3 - cs : 0, chi = ncl - cs + 3 < 7 ? ncl - cs + 3 : 7;
         cv = ((1u << chi) - 1u) & ~((1u << clo) - 1u);
       };
-      auto sparse = [&](const uint32_t (&Hh)[7]) {
-        return !P.erosion_border && (__popc(Hh[0]) + __popc(Hh[1]) + __popc(Hh[2]) + __popc(Hh[3]) +
-                                     __popc(Hh[4]) + __popc(Hh[5]) + __popc(Hh[6])) < 3;
-      };
-      // passes A and B over the entries [i0, i1) whose pixels lie in [q0, q1), rows read from bm (origin org, rows
-      // rdef.. present)
-      auto screen_range = [&](const uint32_t* bm, int org, int rdef, int i0, int i1, uint32_t q0, uint32_t q1) {
+      // passes A and B over the entries [i0, i1) whose pixels lie in [q0, q1), rows read from bm (origin org)
+      auto screen_range = [&](const uint32_t* bm, int org, int wmax, int i0, int i1, uint32_t q0, uint32_t q1) {
+        // presence rows rs-3 .. rs+3 of pixel s, columns cs-3 .. cs+3 (masked by cv; 0 outside the image), from bm
+        // whose bit 0 is pixel org.  The bit of column cs-3 in row rs is st0 = s - 3 - org, row rs+e's is st0 + e*ncl;
+        // word indices are clamped into [-1, wmax] (a row outside the image reads some word of the bitmap's space and
+        // is zeroed by its row mask).  Branch-free.  Bits
+        // outside the image's columns are masked, so the words around the bitmap may hold anything.
         auto rows7 = [&](int s, int& rs, int& cs, uint32_t& cv, uint32_t (&Hh)[7]) {
           rowcv(s, rs, cs, cv);
+          const int st0 = s - 3 - org;
+          const int dlo = 3 - rs > 0 ? 3 - rs : 0, dhi = nr + 2 - rs < 6 ? nr + 2 - rs : 6;
+          const uint32_t vmask = ((2u << dhi) - 1u) & ~((1u << dlo) - 1u);  // rows d in [dlo, dhi] lie in the image
+          uint32_t a[7], b[7];
+          int st[7];
 #pragma unroll
-          for (int d = 0; d < 7; ++d) Hh[d] = bmrow7(bm, org, rdef, rs - 3 + d, cs - 3, cv);
+          for (int d = 0; d < 7; ++d) {
+            st[d] = st0 + (d - 3) * ncl;
+            const int w = min(max(st[d] >> 5, -1), wmax);
+            a[d] = bm[w];
+            b[d] = bm[w + 1];
+          }
+#pragma unroll
+          for (int d = 0; d < 7; ++d) {
+            const uint32_t rm = (uint32_t)((int)(vmask << (31 - d)) >> 31);  // all ones if row d is in the image
+            Hh[d] = __builtin_amdgcn_alignbit(b[d], a[d], (uint32_t)st[d]) & cv & rm;
+          }
         };
         // pass B on this wave's survivors wsurv[0, wcnt) (lane i takes survivor i)
         auto screen = [&](int wcnt) {
@@ -915,10 +940,27 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
           const int i = ob + tid;
           const uint32_t w = i < i1 ? ekey[i] >> 12 : 0xFFFFFFFFu;  // the pixel (a hole's: >= 2^19)
           const bool ok = w >= q0 && w < q1;
-          int rs, cs;
-          uint32_t cv, Hh[7];
-          rows7(ok ? (int)w : (int)q0, rs, cs, cv, Hh);
-          const bool surv = ok && !sparse(Hh);
+          // pass A counts the 7x7 window's bits without the column and row masks: a window at the image's left or
+          // right edge also counts bits of the neighbouring row, one at its top or bottom whatever its clamped reads
+          // find -- only ever more, never fewer, so a pixel it lets through gets the exact screen in pass B, and
+          // one it drops has fewer than three principal pixels in its 7x7
+          bool surv = ok;
+          if (!P.erosion_border) {  // (uniform)
+            const int st0 = (ok ? (int)w : (int)q0) - 3 - org;
+            uint32_t a[7], b[7];
+            int st[7];
+#pragma unroll
+            for (int d = 0; d < 7; ++d) {
+              st[d] = st0 + (d - 3) * ncl;
+              const int wd = min(max(st[d] >> 5, -1), wmax);
+              a[d] = bm[wd];
+              b[d] = bm[wd + 1];
+            }
+            int cnt = 0;
+#pragma unroll
+            for (int d = 0; d < 7; ++d) cnt += __popc(__builtin_amdgcn_alignbit(b[d], a[d], (uint32_t)st[d]) & 0x7Fu);
+            surv = ok && cnt >= 3;
+          }
           const uint64_t m = __ballot(surv);
           const int c = (int)__popcll(m);
           if (wcnt + c > WAVE) {
@@ -931,7 +973,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         if (wcnt > 0) screen(wcnt);
       };
       if (P.npx <= SP_FWORDS * 32) {  // F is the principal image's presence bitmap
-        screen_range(F, 0, 0, 0, n0, 0u, (uint32_t)P.npx);
+        screen_range(F, 0, SP_FWORDS - 2, 0, n0, 0u, (uint32_t)P.npx);
         __syncthreads();
       } else {
         const int B = G.band_rows;
@@ -951,7 +993,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
           }
           __syncthreads();
           const uint32_t q0 = (uint32_t)(r0 * ncl), q1 = (uint32_t)(r1 * ncl);
-          screen_range(band, org, rb, dir[q0 >> bs], dir[((q1 - 1) >> bs) + 1], q0, q1);
+          screen_range(band, org, SpLay::band_bits / 32 - 2, dir[q0 >> bs], dir[((q1 - 1) >> bs) + 1], q0, q1);
           __syncthreads();
         }
       }
@@ -1188,12 +1230,11 @@ int launch_sparse_main(Hits<SMG_HITS_PACKED_F32> hits, IonDesc* desc, Sched S, c
                        uint32_t* rej_count, int cus, hipStream_t st) {
   const SpGeo G = sparse_geo(P);
   auto k = &ion_sparse_kernel<SP_BLOCK, SP_RMAX, SP_RC, SP_WPE>;
-  SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)SP_LDS_BYTES));
+
   // SP_WGPCU resident workgroups per CU, a multiple of the XCD count
   int64_t nwg = (int64_t)cus * SP_WGPCU;
   if (nwg > S.n) nwg = ((S.n + XCDS - 1) / XCDS) * XCDS;
-  hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(SP_BLOCK), SP_LDS_BYTES, st, hits, desc, S, P, G, oc, osp, osc, omsm,
+  hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(SP_BLOCK), 0, st, hits, desc, S, P, G, oc, osp, osc, omsm,
                      oflags, rej_list, rej_count);
   SMG_LAUNCH_CHECK();
   return SMG_OK;
