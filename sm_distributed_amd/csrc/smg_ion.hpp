@@ -299,7 +299,7 @@ __device__ __forceinline__ int64_t sched_resolve(const Sched& S, uint32_t t, int
   if constexpr (SRC == SRC_RANGES) {
     for (int i = 0; i < XCDS; ++i) {
       const int x = (home + i) % XCDS;
-      const int64_t a = S.n * x / XCDS, b = S.n * (x + 1) / XCDS;
+      const int64_t a = (int64_t)((uint64_t)(S.n * x) / XCDS), b = (int64_t)((uint64_t)(S.n * (x + 1)) / XCDS);
       if (i > 0) t = atomicAdd(&S.ctr[x * CTR_STRIDE], 1u);
       if ((int64_t)t < b - a) return a + (int64_t)t;
     }

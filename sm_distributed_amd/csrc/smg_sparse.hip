@@ -199,6 +199,12 @@ __device__ __forceinline__ int sp_level(double v, double vmax, double rcp, const
   const int n = P.nlevels;
   if (!(v > 0.0)) return 0;  // (vmax > 0 whenever levels are needed)
   if (n == 1) return 1;
+  if (n <= 2048) {  // f32 first: x = v/vmax (n-1) to ~2.4e-7 relative (<= 5e-4 absolute here); away from an integer
+                    // by 1e-3 and below the top level it decides alone
+    const float xf = (float)v * (float)rcp * (float)(n - 1);
+    const float jf = floorf(xf), fr = xf - jf;
+    if (fr > 1e-3f && fr < 1.0f - 1e-3f && xf < (float)(n - 1) - 1.0f) return (int)jf + 1;
+  }
   const double na = v * rcp;
   const double tol = na * 1e-15;
   int j = (int)(na * (double)(n - 1)) + 1;
@@ -367,22 +373,21 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
     // the principal statistics (sum x, sum x^2, sum x[x>0], #(x>0), max) over the image's pixels, per thread in a fixed
     // order: single-point pixels from the registers, summed pixels by their first entry
     double acc[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
+    int npos_l = 0;  // #(x > 0) of this lane (acc[3] after an integer wave sum)
     auto stat = [&](double v) {
       acc[0] += v;
       acc[1] += v * v;
       if (v > 0.0) {
         acc[2] += v;
-        acc[3] += 1.0;
+        ++npos_l;
       }
       acc[4] = v > acc[4] ? v : acc[4];
     };
-    uint32_t aw[(RMAX + 1) / 2];  // u16 pairs: a point's arrival index in its bucket, later its sorted entry index
+    uint32_t aw[RMAX];  // a point's arrival index in its bucket, later its entry index (a register each)
 #pragma unroll
-    for (int j = 0; j < (RMAX + 1) / 2; ++j) aw[j] = 0u;
-    auto aw_get = [&](int j) -> uint32_t { return (aw[j >> 1] >> ((j & 1) * 16)) & 0xFFFFu; };
-    auto aw_set = [&](int j, uint32_t v) {
-      aw[j >> 1] = (aw[j >> 1] & ~(0xFFFFu << ((j & 1) * 16))) | (v << ((j & 1) * 16));
-    };
+    for (int j = 0; j < RMAX; ++j) aw[j] = 0u;
+    auto aw_get = [&](int j) -> uint32_t { return aw[j]; };
+    auto aw_set = [&](int j, uint32_t v) { aw[j] = v; };
     // the principal window was issued before this ion's tail chunks 0 and 1.  Waited on every path (a skipped
     // position has nothing older in flight; the wait only gets stricter), so that the wait dominates every use of
     // the principal registers in the separate blocks below
@@ -403,7 +408,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
           } else {
             // a filter bit set twice: the two points may share a pixel (only those scan their bucket below)
             if (atomicOr(&F[sp_fword(p)], sp_fmask(p)) & sp_fmask(p)) atomicOr(&coll[sp_fword(p)], sp_fmask(p));
-            aw_set(j, atomicAdd(&cnt[p >> bs], 1u) & 0xFFFFu);
+            aw_set(j, atomicAdd(&cnt[p >> bs], 1u));
           }
         }
       }
@@ -561,7 +566,8 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
     // the statistics' per-wave sums into red (every thread reads them after the ticket barrier)
     if (!skip) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q] = wave_sum_dpp(acc[q]);
+      for (int q = 0; q < 3; ++q) acc[q] = wave_sum_dpp(acc[q]);
+      acc[3] = (double)__builtin_amdgcn_readlane(wave_incl_scan_dpp(npos_l), 63);
       acc[4] = wave_max_dpp(acc[4]);
       if (lane == 0) {
 #pragma unroll
