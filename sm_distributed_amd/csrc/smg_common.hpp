@@ -155,4 +155,23 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* scratch) {
   __syncthreads();
 }
 
+#ifndef SMG_XCDS
+#define SMG_XCDS 8  // XCDs of the device (gfx950: 8); diagnostic 1 = no XCD locality (one range, no hwreg read)
+#endif
+constexpr int XCDS = SMG_XCDS;
+
+// The XCD this workgroup runs on (HW_REG_XCC_ID, 0-7).  Blocks are observed to be dealt round-robin over the XCDs,
+// but which XCD a block lands on is not fixed, and with other work resident (a copy kernel on another stream) the
+// deal can skip an XCD, so blockIdx % 8 no longer groups the blocks of one XCD; the register is exact.  Speed only:
+// any range may be scored by any workgroup (the ion passes' ranges, the sort's tiles).
+__device__ __forceinline__ int home_xcd() {
+  if constexpr (XCDS == 1) {
+    return 0;
+  } else {
+    int x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    return x % XCDS;
+  }
+}
+
 }  // namespace smg

@@ -239,10 +239,6 @@ static_assert(sizeof(IonRec) == sizeof(IonDesc) && offsetof(IonRec, theor) == of
 //    workgroup whose range is exhausted steals from the other ranges.
 //  SRC_LIST: a device list of positions (the rejects of the previous pass) with a global cursor.
 enum { SRC_RANGES = 0, SRC_LIST = 1 };
-#ifndef SMG_XCDS
-#define SMG_XCDS 8  // diagnostic: 1 = one global range (no XCD locality)
-#endif
-constexpr int XCDS = SMG_XCDS;
 #ifndef SMG_SCREEN2P
 #define SMG_SCREEN2P 1  // chaos screen in two passes (pre-filtered survivors, then the full screen over them)
 #endif
@@ -257,20 +253,6 @@ struct Sched {
   const uint32_t* list;   // SRC_LIST
   const uint32_t* count;  // SRC_LIST
 };
-
-// The XCD this workgroup runs on (HW_REG_XCC_ID, 0-7).  Blocks are observed to be dealt round-robin over the XCDs,
-// but which XCD a block lands on is not fixed, and with other work resident (a copy kernel on another stream) the
-// deal can skip an XCD, so blockIdx % 8 no longer groups the blocks of one XCD; the register is exact.  Speed only:
-// any range may be scored by any workgroup.
-__device__ __forceinline__ int home_xcd() {
-  if constexpr (XCDS == 1) {
-    return 0;
-  } else {
-    int x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
-    return x % XCDS;
-  }
-}
 
 // A ticket is resolved against the counter it was drawn from (``home``, recorded at issue): a workgroup may move to
 // another XCD between the two -- a queue eviction saves and restores its waves, possibly elsewhere -- and a ticket of

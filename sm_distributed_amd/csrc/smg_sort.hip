@@ -404,11 +404,10 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
     if (offsets == nullptr) {
       s_tile = atomicAdd(ticket, 1u);
     } else {
-      int home;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(home));
-      const int64_t nt = gridDim.x, q = nt / 8, r = nt % 8;
-      for (int i = 0; i < 8; ++i) {
-        const int64_t x = (home + i) % 8, a = x * q + (x < r ? x : r), len = q + (x < r ? 1 : 0);
+      const int home = home_xcd();
+      const int64_t nt = gridDim.x, q = nt / XCDS, r = nt % XCDS;
+      for (int i = 0; i < XCDS; ++i) {
+        const int64_t x = (home + i) % XCDS, a = x * q + (x < r ? x : r), len = q + (x < r ? 1 : 0);
         const unsigned k = atomicAdd(ticket + x, 1u);
         if ((int64_t)k < len) {
           s_tile = (unsigned)(a + k);
@@ -734,7 +733,7 @@ static int run_passes(const SortPlan& P, const uint32_t* mz, const uint64_t* hit
     } else if (p >= 2) {
       SMG_HIP(hipMemsetAsync(sp, 0, region * sizeof(S), st));  // pass p - 2's look-back words
     }
-    unsigned* tk_p = rts ? tickets + 8 * p : tickets + p;  // (reduce-then-scan: one counter per XCD and pass)
+    unsigned* tk_p = rts ? tickets + XCDS * p : tickets + p;  // (reduce-then-scan: one counter per XCD and pass)
     if (flag && p == 0)
       hipLaunchKernelGGL((sort_pass_kernel<S, true>), dim3((unsigned)P.ntiles), dim3(SRT_T), 0, st, ki, vi, kdst,
                          vdst, n, p * P.dbits, P.dbits, binbase + p * SRT_BINS, sp, tk_p, flagbits, offs);

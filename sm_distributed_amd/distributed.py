@@ -180,8 +180,13 @@ def slice_peaks(peaks, plan, cache=True):
     The slice is a function of the resident dataset and the plan only, so it is made once per (plan bounds, ppm)
     and kept on the DevicePeaks, the way the single-GPU search keeps the whole dataset resident: every search still
     flags (the copy did), sorts and prefix-sums it (compute_sf_images), as the single-GPU search does the whole
-    dataset.  ``cache=False`` copies it anew."""
-    key = (float(plan.mz_lo), float(plan.mz_hi), float(plan.ppm))
+    dataset.  ``cache=False`` copies it anew.
+
+    The key names the data as well as the plan: the resident arrays (their device addresses and length) and
+    ``peaks.version`` (bumped by every flag pass or sort of them), so that replaced or re-flagged resident data
+    is sliced again.  One slice is kept per rank (a new key drops the old one); it holds ~1/N of the dataset."""
+    key = (float(plan.mz_lo), float(plan.mz_hi), float(plan.ppm), int(peaks.n_points), int(peaks.version),
+           int(peaks.mz.data_ptr()), int(peaks.hits.data_ptr()))
     store = peaks.__dict__.setdefault("_slices", {})
     if cache and key in store:
         return store[key]

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 import warnings
 
 import numpy as np
@@ -299,22 +300,33 @@ def device_frame(ion_keys, cols, idx, cols_compact=False):
     return pd.DataFrame(host[2].numpy().T, index=mi, columns=METRIC_COLUMNS, copy=False)
 
 
-_STAGE = {}  # device -> [copy stream, ring index, two grow-only pinned uint8 buffers]
+_STAGE = {}  # device -> [copy stream, free pinned uint8 buffers, lock]
+_STAGE_LOCK = threading.Lock()
 
 
 def _stage_buffers(device, n):
-    """A persistent pinned host buffer of >= n bytes (ring of two per device, grow-only) and the device's copy
-    stream: the per-step row mask never allocates pinned memory."""
+    """A pinned host buffer of >= n bytes taken from the device's pool of free staging buffers (allocated only when
+    none is free: the per-step row mask never allocates pinned memory in steady state) and the device's copy stream.
+    The buffer belongs to the caller until ``_release_stage_buffer``: a pending frame's mask is never overwritten,
+    whatever the thread or the number of stages in flight."""
     import torch
     key = str(device)
-    ent = _STAGE.get(key)
-    if ent is None:
-        ent = _STAGE[key] = [torch.cuda.Stream(device=device), 0, [None, None]]
-    ent[1] ^= 1
-    buf = ent[2][ent[1]]
-    if buf is None or buf.numel() < n:
-        buf = ent[2][ent[1]] = torch.empty(max(int(n), 1 << 20), dtype=torch.uint8, pin_memory=True)
-    return ent[0], buf
+    with _STAGE_LOCK:
+        ent = _STAGE.get(key)
+        if ent is None:
+            ent = _STAGE[key] = [torch.cuda.Stream(device=device), [], threading.Lock()]
+    with ent[2]:
+        for i, b in enumerate(ent[1]):
+            if b.numel() >= n:
+                return ent[0], ent[1].pop(i)
+    return ent[0], torch.empty(max(int(n), 1 << 20), dtype=torch.uint8, pin_memory=True)
+
+
+def _release_stage_buffer(device, buf):
+    ent = _STAGE.get(str(device))
+    if ent is not None and buf is not None:
+        with ent[2]:
+            ent[1].append(buf)
 
 
 class FrameIndex:
@@ -336,6 +348,7 @@ class FrameIndex:
             n = keep.numel()
             main = torch.cuda.current_stream(keep.device)
             _, buf = _stage_buffers(keep.device, n)
+            self._stage_buf = buf
             buf[:n].copy_(keep.view(torch.uint8), non_blocking=True)
             self.ev = torch.cuda.Event()
             self.ev.record(main)
@@ -345,15 +358,17 @@ class FrameIndex:
             n = keep.numel()
             main = torch.cuda.current_stream(keep.device)
             cs, buf = _stage_buffers(keep.device, n)
+            self._stage_buf = buf
             cs.wait_stream(main)
             with torch.cuda.stream(cs):
                 buf[:n].copy_(keep.view(torch.uint8), non_blocking=True)
                 self.ev = torch.cuda.Event()
                 self.ev.record(cs)
             keep.record_stream(cs)
-            # the compute stream waits for the copy: the copy may run as a blit kernel, and one queued beside the
-            # persistent ion kernel (every CU's LDS held) was seen to time-slice it (35 -> 53-73 ms per launch, in
-            # ~10 ms steps, after the first ~8 steps of a bench)
+            # the compute stream waits for the copy (no copy runs beside the persistent ion kernel).  The 10-ms
+            # step quanta once blamed on such a copy are KFD queue evictions of the whole process (round 5:
+            # evicted_ms grows by exactly those quanta, and a pending copy, barrier or kernel on a second queue
+            # was measured not to stall a CU-filling kernel, scripts/queue_slice_probe.hip)
             main.wait_event(self.ev)
             self.keep_host = buf[:n]
             # the DataFrame's own pinned block (caching host allocator: reused once an earlier frame is freed),
@@ -373,6 +388,8 @@ class FrameIndex:
             return pd.DataFrame(cols[:, idx].numpy().T, index=mi, columns=METRIC_COLUMNS, copy=False)
         self.ev.synchronize()  # the mask was copied before the kernel ran: ready while it runs
         idx = np.flatnonzero(self.keep_host.numpy())
+        self.keep_host = None
+        _release_stage_buffer(keep.device, self.__dict__.pop("_stage_buf", None))  # (the mask is read)
         m = len(idx)
         _, sfc, adc = self.ion_keys.level_codes()
         mi = self.ion_keys.multi_index_from_codes(sfc[idx], adc[idx])

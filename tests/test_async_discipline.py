@@ -41,10 +41,16 @@ def test_async_load_registers_are_never_touched_in_flight(tmp_path):
         assert (n_loads, n_bad, n_guarded) == (0, 0, 0), out
     n_loads, n_bad, n_guarded, out = _check(asm, "_ZN3smg15ion_pipe_kernelILi0ELi512")
     assert n_loads > 0 and n_bad == 0, out
-    # every guarded report is one of the tagged wave-0 loads (two per instantiation at most)
+    # every guarded report is one of the tagged wave-0 loads, pinned exactly: the ticket atomic and the
+    # descriptor load of each of the two 512-thread instantiations, once each -- a new guarded path fails here
     guarded = [l for l in out.split("\n") if l.startswith("GUARDED")]
     assert all("smg:wave0" in l for l in guarded), out
-    assert n_guarded <= 4, out
+    assert n_guarded == 4, out
+    per = {}
+    for l in guarded:
+        inst, op = l.split()[1], ("atomic" if "global_atomic" in l else "load")
+        per[(inst, op)] = per.get((inst, op), 0) + 1
+    assert len({k[0] for k in per}) == 2 and all(v == 1 for v in per.values()), out
 
 
 @pytest.mark.timeout(600)

@@ -322,3 +322,28 @@ def test_device_iso_image_rows_reference_kat():
     torch.cuda.synchronize()
     assert cnt.tolist() == [1, 1] and pix[:2].tolist() == [0, 5] and val[:2].tolist() == [100.0, 10.0]
     assert mn.tolist() == [0.0, 0.0] and mx.tolist() == [100.0, 10.0]
+
+
+@pytest.mark.gpu
+def test_frame_index_stages_in_flight_do_not_share_a_buffer():
+    """Three FrameIndex stages queued before any frame() (the staging ring had two buffers and no
+    ownership): each frame() returns exactly its own mask's rows, framed in reverse order."""
+    import torch
+
+    from sm_distributed_amd.formula_imager_segm import FrameIndex, IonKeys
+    dev = torch.device("cuda", 0)
+    n = 5000
+    keys = np.arange(n, dtype=np.int64) * 3  # sf codes 0..n-1, adduct 0 of 3
+    ik = IonKeys(keys, ["+H", "+K", "+Na"])
+    rng = np.random.default_rng(7)
+    masks = [rng.random(n) < f for f in (0.2, 0.5, 0.8)]
+    cols = [torch.from_numpy(rng.random((4, n))).to(dev) for _ in masks]
+    fis = []
+    for m in masks:
+        fi = FrameIndex(ik)
+        fi.stage(torch.from_numpy(m).to(dev))
+        fis.append(fi)
+    for fi, m, c in reversed(list(zip(fis, masks, cols))):
+        df = fi.frame(c)
+        assert len(df) == int(m.sum())
+        np.testing.assert_array_equal(df.to_numpy(), c.cpu().numpy()[:, m].T)
