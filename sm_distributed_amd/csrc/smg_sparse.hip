@@ -84,7 +84,8 @@ namespace {
 #ifndef SMG_SP_RC
 #define SMG_SP_RC 2  // tail points per thread per chunk (four chunks in flight)
 #endif
-// timing ablations (wrong results; diagnostic builds only): 1 no chaos, 2 no tail stream, 4 no levels
+// timing ablations (wrong results; diagnostic builds only): 1 no chaos, 2 no tail stream, 4 no levels, 8 no chaos
+// pass B (no candidates), 16 no band bitmaps, 32 no chaos screen, 64 no eL / Kruskal
 #ifndef SMG_SP_ABL
 #define SMG_SP_ABL 0
 #endif
@@ -154,6 +155,8 @@ struct SpLay {
   static_assert(o_hash >= o_F + SP_FWORDS * 4 && o_par + SP_CCAP * 4 <= o_wsurv, "hash + union-find between F and the lists");
   static_assert(o_F + SP_FWORDS * 4 <= o_wsurv && o_cnt + SP_NBMAX * 4 <= o_wsurv, "cleared words below the lists");
   static_assert(SP_LDS_BYTES % 512 == 0 && 4 * SP_LDS_BYTES <= 160 * 1024, "four workgroups per CU");
+  static_assert(SP_NW == 4, "the chaos screen merges four partial survivor lists");
+  static_assert(o_U + SP_NW * WAVE * 8 <= o_wsurv && SP_NW * WAVE * 8 <= SP_FWORDS * 4 && SP_NW * WAVE >= 2 * WAVE, "eL row blocks over the screen's bitmaps, the small Kruskal's hash over the survivor lists");
 };
 
 struct SpGeo {
@@ -254,6 +257,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
   uint32_t* clist = reinterpret_cast<uint32_t*>(smem + LY::o_clist);
   uint8_t* cel = smem + LY::o_cel;
   uint32_t* wsurv = reinterpret_cast<uint32_t*>(smem + LY::o_wsurv) + (threadIdx.x >> 6) * WAVE;
+  int* wsc = reinterpret_cast<int*>(smem + LY::o_wsc);  // the chaos screen's partial survivor counts per wave
   uint32_t* band = reinterpret_cast<uint32_t*>(smem + LY::o_band);
   uint32_t* htab = reinterpret_cast<uint32_t*>(smem + LY::o_hash);
   uint32_t* par = reinterpret_cast<uint32_t*>(smem + LY::o_par);
@@ -854,9 +858,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       //     p for pixel p), else band bitmaps of image rows rebuilt in the LDS the values and the flagged-point lists
       //     leave behind (two bands at 500x500 px): the band's words zeroed, then a bit set per entry.  Pass A: a
       //     principal pixel with fewer than three principal pixels in its 7x7 (itself included) cannot own a
-      //     candidate (erosion border 0); the others go to the wave's own survivor list, and pass B (the wave's own
-      //     list: no barrier between the passes) runs the full screen over them, appending candidates (owned pixels
-      //     of the dilated-covered boxes) to the chaos list.
+      //     candidate (erosion border 0); the others go to the wave's own survivor list, and pass B runs the full
+      //     screen over each full list (no barrier) and over the waves' partial lists together at the range's end
+      //     (after one), appending candidates (owned pixels of the dilated-covered boxes) to the chaos list.
       auto rowcv = [&](int s, int& rs, int& cs, uint32_t& cv) {
         rowcol(s, P, rs, cs);
         const int clo = 3 - cs > 0 ? 3 - cs : 0, chi = ncl - cs + 3 < 7 ? ncl - cs + 3 : 7;
@@ -889,11 +893,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
             Hh[d] = __builtin_amdgcn_alignbit(b[d], a[d], (uint32_t)st[d]) & cv & rm;
           }
         };
-        // pass B on this wave's survivors wsurv[0, wcnt) (lane i takes survivor i)
-        auto screen = [&](int wcnt) {
-          __builtin_amdgcn_wave_barrier();  // (the survivor list was written by this wave's lanes)
-          const bool ok = lane < wcnt;
-          const int s = ok ? (int)wsurv[lane] : (int)q0;
+        // pass B on survivor s of each lane where ok (wave-uniform call)
+        auto screen_s = [&](const bool ok, const int s) {
+          if constexpr ((SMG_SP_ABL & 8) != 0) return;
           int rs, cs;
           uint32_t cv, Hh[7];
           rows7(s, rs, cs, cv, Hh);
@@ -939,6 +941,12 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
               ++idx;
             }
           }
+        };
+        // pass B on this wave's full survivor list wsurv[0, wcnt) (lane i takes survivor i)
+        auto screen = [&](int wcnt) {
+          __builtin_amdgcn_wave_barrier();  // (the survivor list was written by this wave's lanes)
+          const bool ok = lane < wcnt;
+          screen_s(ok, ok ? (int)wsurv[lane] : (int)q0);
           __builtin_amdgcn_wave_barrier();  // (the list is refilled after this)
         };
         int wcnt = 0;  // (wave-uniform)
@@ -976,10 +984,22 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
           if (surv) wsurv[wcnt + (int)__popcll(m & ((1ull << lane) - 1ull))] = w;
           wcnt += c;
         }
-        if (wcnt > 0) screen(wcnt);
+        // the waves' partial lists (up to 63 survivors each) are screened together: their counts, a barrier, then
+        // wave w takes survivors [64w, 64w + 64) of the four lists laid end to end -- one pass B per range and
+        // chunk of 64 survivors rather than one per wave
+        if (lane == 0) wsc[wid] = wcnt;
+        __syncthreads();
+        const int c0 = wsc[0], c1 = c0 + wsc[1], c2 = c1 + wsc[2], tot = c2 + wsc[3];
+        const uint32_t* wall = reinterpret_cast<const uint32_t*>(smem + SpLay::o_wsurv);
+        if (wid * WAVE < tot) {  // (wave-uniform)
+          const int g = wid * WAVE + lane;
+          const int at = g < c0 ? g : g < c1 ? WAVE + g - c0 : g < c2 ? 2 * WAVE + g - c1 : 3 * WAVE + g - c2;
+          const bool ok = g < tot;
+          screen_s(ok, ok ? (int)wall[at] : (int)q0);
+        }
       };
       if (P.npx <= SP_FWORDS * 32) {  // F is the principal image's presence bitmap
-        screen_range(F, 0, SP_FWORDS - 2, 0, n0, 0u, (uint32_t)P.npx);
+        if (!(SMG_SP_ABL & 32)) screen_range(F, 0, SP_FWORDS - 2, 0, n0, 0u, (uint32_t)P.npx);
         __syncthreads();
       } else {
         const int B = G.band_rows;
@@ -990,21 +1010,23 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
           // rows fall outside)
           const uint32_t span = (uint32_t)(re * ncl - org);
           const int nw4 = (int)((span + 127u) >> 7);
-          for (int k = tid; k < nw4; k += BLOCK) reinterpret_cast<uint4*>(band)[k] = make_uint4(0u, 0u, 0u, 0u);
+          for (int k = tid; k < nw4 && !(SMG_SP_ABL & 16); k += BLOCK)
+            reinterpret_cast<uint4*>(band)[k] = make_uint4(0u, 0u, 0u, 0u);
           __syncthreads();
-          const int e1 = dir[b1 + 1];
+          const int e1 = (SMG_SP_ABL & 16) ? 0 : dir[b1 + 1];
           for (int i = dir[b0] + tid; i < e1; i += BLOCK) {
             const uint32_t q = (ekey[i] >> 12) - (uint32_t)org;
             if (q < span) atomicOr(&band[q >> 5], 1u << (q & 31u));
           }
           __syncthreads();
           const uint32_t q0 = (uint32_t)(r0 * ncl), q1 = (uint32_t)(r1 * ncl);
-          screen_range(band, org, SpLay::band_bits / 32 - 2, dir[q0 >> bs], dir[((q1 - 1) >> bs) + 1], q0, q1);
+          if (!(SMG_SP_ABL & 32))
+            screen_range(band, org, SpLay::band_bits / 32 - 2, dir[q0 >> bs], dir[((q1 - 1) >> bs) + 1], q0, q1);
           __syncthreads();
         }
       }
       SP_STAMP(8);
-      const int ncand = ctr[S_NE];
+      const int ncand = (SMG_SP_ABL & 64) ? 0 : ctr[S_NE];
       if (ctr[S_ABORT] || ncand > SP_CCAP) {  // more candidates than the list holds: the big-ion pass
         reject();
         skip = true;
@@ -1014,15 +1036,19 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         //      its 5x5 neighbourhood's principal pixels found in the directory (entries are in pixel order), packed 8
         //      bits per column
         int emax_local = 0;
-        for (int c = tid; c < ncand; c += BLOCK) {
-          const int p = (int)clist[c];
-          int rp, cp;
-          rowcol(p, P, rp, cp);
-          uint64_t Lrow[5];
-#pragma unroll
-          for (int d = 0; d < 5; ++d) {
-            const int row = rp - 2 + d;
-            uint64_t packed = 0;
+        // one lane per (candidate, window row), so that the five rows' directory scans run side by side: wave w
+        // takes candidates w, w + 4, ... in rounds of 12; the rows meet in a wave-private block where the screen's
+        // bitmaps were (free now: F is cleared whole by the next ion's build)
+        uint64_t* lrow = reinterpret_cast<uint64_t*>(smem + SpLay::o_U) + wid * WAVE;
+        const int eslot = lane % 12, erow = lane / 12;  // lanes 60..63 idle
+        for (int cb = 0; cb < ncand; cb += SP_NW * 12) {  // uniform trip count
+          const int c = cb + eslot * SP_NW + wid;
+          uint64_t packed = 0;
+          if (erow < 5 && c < ncand) {
+            const int p = (int)clist[c];
+            int rp, cp;
+            rowcol(p, P, rp, cp);
+            const int row = rp - 2 + erow;
             if ((unsigned)row < (unsigned)nr) {
               const int base = row * ncl + cp - 2;  // pixel of window column 0
               const uint32_t lo = (uint32_t)(row * ncl + max(cp - 2, 0)), hi = (uint32_t)(row * ncl + min(cp + 2, ncl - 1));
@@ -1032,34 +1058,45 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
                 if (w >= lo && w <= hi) packed |= (uint64_t)L8[i] << (8 * (int)(w - (uint32_t)base));
               }
             }
-            Lrow[d] = packed;
           }
+          lrow[lane] = packed;
+          __builtin_amdgcn_wave_barrier();
+          const int c2 = cb + lane * SP_NW + wid;
+          if (lane < 12 && c2 < ncand) {
+            const int p = (int)clist[c2];
+            int rp, cp;
+            rowcol(p, P, rp, cp);
+            uint64_t Lrow[5];
+#pragma unroll
+            for (int d = 0; d < 5; ++d) Lrow[d] = lrow[d * 12 + lane];
 #define SP_L(r, cc) ((int)((Lrow[r] >> (8 * (cc))) & 0xFFull))
-          int mn = 1 << 20;
-          bool outside = false;
+            int mn = 1 << 20;
+            bool outside = false;
 #pragma unroll
-          for (int a2 = -1; a2 <= 1; ++a2) {
+            for (int a2 = -1; a2 <= 1; ++a2) {
 #pragma unroll
-            for (int b2 = -1; b2 <= 1; ++b2) {
-              const int rq = rp + a2, cq = cp + b2;
-              if (rq < 0 || rq >= nr || cq < 0 || cq >= ncl) {
-                outside = true;
-                continue;
+              for (int b2 = -1; b2 <= 1; ++b2) {
+                const int rq = rp + a2, cq = cp + b2;
+                if (rq < 0 || rq >= nr || cq < 0 || cq >= ncl) {
+                  outside = true;
+                  continue;
+                }
+                const int R = 2 + a2, C = 2 + b2;
+                int dl = SP_L(R, C);
+                dl = max(dl, SP_L(R - 1, C));
+                dl = max(dl, SP_L(R + 1, C));
+                dl = max(dl, SP_L(R, C - 1));
+                dl = max(dl, SP_L(R, C + 1));
+                mn = min(mn, dl);
               }
-              const int R = 2 + a2, C = 2 + b2;
-              int dl = SP_L(R, C);
-              dl = max(dl, SP_L(R - 1, C));
-              dl = max(dl, SP_L(R + 1, C));
-              dl = max(dl, SP_L(R, C - 1));
-              dl = max(dl, SP_L(R, C + 1));
-              mn = min(mn, dl);
             }
-          }
 #undef SP_L
-          if (outside && !P.erosion_border) mn = 0;
-          if (mn >= (1 << 20)) mn = 0;
-          cel[c] = (uint8_t)mn;
-          emax_local = max(emax_local, mn);
+            if (outside && !P.erosion_border) mn = 0;
+            if (mn >= (1 << 20)) mn = 0;
+            cel[c2] = (uint8_t)mn;
+            emax_local = max(emax_local, mn);
+          }
+          __builtin_amdgcn_wave_barrier();  // (the block is rewritten next round)
         }
         if (emax_local > 0) atomicMax(&ctr[S_EMAX], emax_local);
         __syncthreads();
@@ -1068,8 +1105,8 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         double sum_c = 0.0;
         const int emax_all = ctr[S_EMAX];
         if (emax_all > 0 && ncand <= WAVE) {
-          // few candidates (most noise images): wave 0 alone, one candidate per lane, forward neighbours found by
-          // comparing pixel indices across lanes; no barrier (only wave 0 needs the result)
+          // few candidates (most noise images): wave 0 alone, one candidate per lane; no barrier (only wave 0 needs
+          // the result)
           if (wid == 0) {
             uint32_t* upar = reinterpret_cast<uint32_t*>(red);  // 64 entries (red is free until the record)
             const bool act = lane < ncand;
@@ -1078,15 +1115,33 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
             int rp = 0, cp = 0;
             rowcol(p < 0 ? 0 : p, P, rp, cp);
             int nb[4] = {-1, -1, -1, -1};
-            for (int j = 0; j < ncand; ++j) {
-              const int pj = __shfl(p, j, WAVE), ej = __shfl(e, j, WAVE);
-              if (e >= 1 && ej >= 1) {
-                if (cp + 1 < ncl && pj == p + 1) nb[0] = j;
-                if (rp + 1 < nr) {
-                  if (pj == p + ncl) nb[1] = j;
-                  if (P.connectivity == 8 && cp > 0 && pj == p + ncl - 1) nb[2] = j;
-                  if (P.connectivity == 8 && cp + 1 < ncl && pj == p + ncl + 1) nb[3] = j;
-                }
+            // forward neighbours through a 128-slot pixel -> lane hash over the survivor lists (the other waves clear
+            // F and the counters meanwhile; the lists are rewritten only after the ion's last barrier)
+            uint32_t* kt = reinterpret_cast<uint32_t*>(smem + SpLay::o_wsurv);
+            kt[lane] = SP_EMPTY;
+            kt[lane + WAVE] = SP_EMPTY;
+            __builtin_amdgcn_wave_barrier();
+            auto kslot = [](uint32_t q) { return (q * 2654435761u) >> 25; };
+            if (act && e >= 1) {
+              uint32_t h = kslot((uint32_t)p);
+              while (atomicCAS(&kt[h], SP_EMPTY, ((uint32_t)p << 6) | (uint32_t)lane) != SP_EMPTY) h = (h + 1) & 127u;
+            }
+            __builtin_amdgcn_wave_barrier();
+            auto kfind = [&](int q) -> int {
+              uint32_t h = kslot((uint32_t)q);
+              while (true) {
+                const uint32_t k = kt[h];
+                if (k == SP_EMPTY) return -1;
+                if ((k >> 6) == (uint32_t)q) return (int)(k & 63u);
+                h = (h + 1) & 127u;
+              }
+            };
+            if (act && e >= 1) {
+              if (cp + 1 < ncl) nb[0] = kfind(p + 1);
+              if (rp + 1 < nr) {
+                nb[1] = kfind(p + ncl);
+                if (P.connectivity == 8 && cp > 0) nb[2] = kfind(p + ncl - 1);
+                if (P.connectivity == 8 && cp + 1 < ncl) nb[3] = kfind(p + ncl + 1);
               }
             }
             int eq[4];
