@@ -90,7 +90,7 @@ namespace {
 #define SMG_SP_ABL 0
 #endif
 #ifndef SMG_SP_EVB
-#define SMG_SP_EVB 2  // tail events per lane resolved per round (their points read again together)
+#define SMG_SP_EVB 1  // rounds of 64 listed tail events resolved together (their points read again together)
 #endif
 constexpr int SP_EVB = SMG_SP_EVB;
 constexpr int SP_BLOCK = 256, SP_RMAX = 10, SP_RC = SMG_SP_RC, SP_WPE = 4, SP_WGPCU = 4;
@@ -101,6 +101,7 @@ constexpr int SP_FWORDS = 1024;              // Bloom filter: 2^15 bits
 constexpr int SP_DSEG = 64;                  // deferred flagged tail points per wave
 constexpr int SP_DTBL = 256;                 // their (pixel, window)-keyed sums
 constexpr int SP_SIDE = 336;                 // f64 sums of pixels with >= 2 principal points
+constexpr int SP_EVCAP = 192;               // tail events listed per wave (resolved when it fills)
 constexpr int SP_CCAP = 768;                 // chaos survivors + candidates
 constexpr int SP_HSZ = 2048;                 // Kruskal: candidate hash
 constexpr int SP_BMAX = 128;                 // points per bucket (more: the big-ion pass)
@@ -156,6 +157,8 @@ struct SpLay {
   static_assert(o_F + SP_FWORDS * 4 <= o_wsurv && o_cnt + SP_NBMAX * 4 <= o_wsurv, "cleared words below the lists");
   static_assert(SP_LDS_BYTES % 512 == 0 && 4 * SP_LDS_BYTES <= 160 * 1024, "four workgroups per CU");
   static_assert(SP_NW == 4, "the chaos screen merges four partial survivor lists");
+  static_assert(SP_NW * SP_EVCAP * 4 == SP_DTBL * 12 && o_tval == o_tkey + SP_DTBL * 4 && SP_EVCAP % WAVE == 0,
+                "the event lists tile the dup table's space");
   static_assert(o_U + SP_NW * WAVE * 8 <= o_wsurv && SP_NW * WAVE * 8 <= SP_FWORDS * 4 && SP_NW * WAVE >= 2 * WAVE, "eL row blocks over the screen's bitmaps, the small Kruskal's hash over the survivor lists");
 };
 
@@ -320,10 +323,13 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
     for (int i = t0; i < SP_FWORDS / 4; i += nt) zl[i] = make_uint4(0, 0, 0, 0);
     if (t0 < S_NCTR && t0 != S_NEXT) ctr[t0] = 0;
   };
+  // the dup table (keys all ones, values zero), cleared by each wave over the words of its own tail-event list (the
+  // two share the space), so that a wave done with its stream never touches the list of one still streaming
   auto clear_table = [&]() {
-    for (int i = tid; i < SP_DTBL; i += BLOCK) {
-      tkey[i] = 0xFFFFFFFFu;
-      tval[i] = 0.0;
+#pragma unroll
+    for (int q = 0; q < SP_EVCAP / WAVE; ++q) {
+      const int i = wid * SP_EVCAP + q * WAVE + (int)(threadIdx.x & 63u);
+      tkey[i] = i < SP_DTBL ? 0xFFFFFFFFu : 0u;
     }
   };
   clear_fc(tid, BLOCK);
@@ -638,12 +644,18 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       int gnext = uni(D->gs[2]);
       int wend = uni(D->end[1]);
       // Events: a filter positive (the point's pixel may be principal: Σxy, Σy[x>0]) or a flagged point (summed per
-      // (pixel, window) before squaring).  The stream only marks them: bit t of the lane's event mask = its t-th point
-      // (chunk t / RC, slot t % RC) is an event.  After the stream the events are resolved lane by lane in stream
-      // order, the i-th round taking every lane's i-th event, each point read again (an L2 hit: streamed just now).
-      // A lane's points beyond the 64th are handled in place.  Partials: part[k][wid], written only by this wave,
-      // lanes of one instruction in hardware order -- deterministic.
-      uint32_t evlo = 0u, evhi = 0u;
+      // (pixel, window) before squaring).  The stream only lists them, compacted over the wave's lanes (one list entry
+      // per event, so that resolving them takes ceil(events / 64) rounds rather than the busiest lane's count); the
+      // list is resolved when it fills and after the stream.  Partials: part[k][wid], written only by this wave, lanes
+      // of one instruction in hardware order -- deterministic.
+      // the wave's event list (t << 7 | in << 6 | lane, t = chunk * RC + slot), in the dup table's space (written only
+      // after the stream; the filter collisions overlapping it were read before the ticket barrier)
+      uint32_t* evl = tkey + wid * SP_EVCAP;
+      int nev = 0;  // (uniform)
+      const uint64_t below = (1ull << lane) - 1ull;
+      int gsv[MAXK];
+#pragma unroll
+      for (int kk = 2; kk < MAXK; ++kk) gsv[kk] = uni(D->gs[kk]);
       auto add_x = [&](bool hit, int r, const Reg& h, int k) {
         if (__ballot(hit)) {
           if (hit) {
@@ -655,20 +667,47 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
           }
         }
       };
-      auto handle = [&](bool pred, const Reg& h, int k, bool inb) {
-        const uint32_t p = H::pix(h);
-        const int r = (pred && inb) ? sp_lookup(ekey, dir, p, bs) : -1;
-        add_x(r >= 0, r, h, k);
-        const bool dup = pred && H::dup(h);
-        const uint64_t dm = __ballot(dup);
-        if (dm) {
-          const int e = nd + (int)__popcll(dm & ((1ull << lane) - 1ull));
-          if (dup && e < SP_DSEG) {
-            wdkey[e] = (p << 3) | (uint32_t)k;
-            wdval[e] = H::val(h);
+      // the listed events, SP_EVB rounds of 64 together (their points read again, an L2 hit: streamed just now), in
+      // list order -- stream order, then lane order
+      auto resolve = [&]() {
+        __builtin_amdgcn_wave_barrier();  // (the list was written by this wave's lanes)
+        for (int e0 = 0; e0 < nev; e0 += SP_EVB * WAVE) {  // uniform
+          Reg hq[SP_EVB];
+          int kq[SP_EVB];
+          bool hasq[SP_EVB], inq[SP_EVB];
+#pragma unroll
+          for (int q = 0; q < SP_EVB; ++q) {
+            const int e = e0 + q * WAVE + lane;
+            hasq[q] = e < nev;
+            const uint32_t ent = hasq[q] ? evl[e] : 0u;
+            const int t = (int)(ent >> 7);
+            inq[q] = (ent & 64u) != 0u;
+            const int Gi = (t / RC) * GPC + (t % RC) * NW + wid;
+            int k = 1;
+#pragma unroll
+            for (int kk = 2; kk < MAXK; ++kk) k += (Gi >= gsv[kk]) ? 1 : 0;
+            kq[q] = k;
+            hq[q] = hasq[q] ? hits.h[D->base[k] + (int64_t)Gi * 64 + (ent & 63u)] : 0ull;
           }
-          nd += (int)__popcll(dm);
+#pragma unroll
+          for (int q = 0; q < SP_EVB; ++q) {
+            const Reg h = hq[q];
+            const uint32_t p = H::pix(h);
+            const int r = inq[q] ? sp_lookup(ekey, dir, p, bs) : -1;
+            add_x(r >= 0, r, h, kq[q]);
+            const bool dq = hasq[q] && H::dup(h);
+            const uint64_t mq = __ballot(dq);
+            if (mq) {
+              const int e = nd + (int)__popcll(mq & below);
+              if (dq && e < SP_DSEG) {
+                wdkey[e] = (p << 3) | (uint32_t)kq[q];
+                wdval[e] = H::val(h);
+              }
+              nd += (int)__popcll(mq);
+            }
+          }
         }
+        nev = 0;
       };
       auto process = [&](int c, Reg (&buf)[RC]) {
         uint32_t fw[RC], fm[RC];
@@ -691,15 +730,16 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
             const Reg h = buf[j];
             const bool in = valid && (fw[j] & fm[j]) != 0u;
             const bool evt = in || (valid && H::dup(h));
-            const int t = c * RC + j;  // (uniform)
-            if (t < 32) {
-              evlo |= evt ? 1u << t : 0u;
-            } else if (t < 64) {
-              evhi |= evt ? 1u << (t - 32) : 0u;
-            } else if (__ballot(evt)) {
-              SP_MARK_BEGIN(_th0);
-              handle(evt, h, curk, in);
-              SP_MARK_END(_th0, 14);
+            const uint64_t em = __ballot(evt);
+            if (em) {  // (uniform)
+              const uint32_t t = (uint32_t)(c * RC + j);
+              if (evt) evl[nev + (int)__popcll(em & below)] = (t << 7) | (in ? 64u : 0u) | (uint32_t)lane;
+              nev += (int)__popcll(em);
+              if (nev > SP_EVCAP - WAVE) {
+                SP_MARK_BEGIN(_th0);
+                resolve();
+                SP_MARK_END(_th0, 14);
+              }
             }
           }
         }
@@ -759,51 +799,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         process(c + 3, pd);
         refill(c + 7, pd);
       }
-      // the marked events, the i-th round taking every lane's i-th
+      // the events still listed
       SP_MARK_BEGIN(_tp0);
-      if (__ballot((evlo | evhi) != 0u)) {
-        int gsv[MAXK];
-#pragma unroll
-        for (int kk = 2; kk < MAXK; ++kk) gsv[kk] = uni(D->gs[kk]);
-        const uint64_t below = (1ull << lane) - 1ull;
-        // rounds of SP_EVB events per lane, their points read together (one latency per round)
-        while (__ballot((evlo | evhi) != 0u)) {
-          Reg hq[SP_EVB];
-          int kq[SP_EVB];
-          bool hasq[SP_EVB];
-#pragma unroll
-          for (int q = 0; q < SP_EVB; ++q) {
-            hasq[q] = (evlo | evhi) != 0u;
-            const int t = evlo ? __builtin_ctz(evlo) : (evhi ? 32 + __builtin_ctz(evhi) : 0);
-            if (evlo) evlo &= evlo - 1u;
-            else evhi &= evhi - 1u;
-            const int Gi = (t / RC) * GPC + (t % RC) * NW + wid;
-            int k = 1;
-#pragma unroll
-            for (int kk = 2; kk < MAXK; ++kk) k += (Gi >= gsv[kk]) ? 1 : 0;
-            kq[q] = k;
-            hq[q] = hasq[q] ? hits.h[D->base[k] + (int64_t)Gi * 64 + lane] : 0ull;
-          }
-#pragma unroll
-          for (int q = 0; q < SP_EVB; ++q) {
-            const Reg h = hq[q];
-            const uint32_t p = H::pix(h);
-            const bool in = hasq[q] && (F[sp_fword(p)] & sp_fmask(p)) != 0u;
-            const int r = in ? sp_lookup(ekey, dir, p, bs) : -1;
-            add_x(r >= 0, r, h, kq[q]);
-            const bool dq = hasq[q] && H::dup(h);
-            const uint64_t mq = __ballot(dq);
-            if (mq) {
-              const int e = nd + (int)__popcll(mq & below);
-              if (dq && e < SP_DSEG) {
-                wdkey[e] = (p << 3) | (uint32_t)kq[q];
-                wdval[e] = H::val(h);
-              }
-              nd += (int)__popcll(mq);
-            }
-          }
-        }
-      }
+      if (nev) resolve();
       if (lane == 0) dcnt[wid] = nd;
       SP_MARK_END(_tp0, 13);
     }
