@@ -85,7 +85,7 @@ namespace {
 #define SMG_SP_RC 2  // tail points per thread per chunk (four chunks in flight)
 #endif
 // timing ablations (wrong results; diagnostic builds only): 1 no chaos, 2 no tail stream, 4 no levels, 8 no chaos
-// pass B (no candidates), 16 no band bitmaps, 32 no chaos screen, 64 no eL / Kruskal
+// pass B (no candidates), 16 no band bitmaps, 32 no chaos screen, 64 no eL / Kruskal, 128 no collision scans
 #ifndef SMG_SP_ABL
 #define SMG_SP_ABL 0
 #endif
@@ -101,6 +101,7 @@ constexpr int SP_FWORDS = 1024;              // Bloom filter: 2^15 bits
 constexpr int SP_DSEG = 64;                  // deferred flagged tail points per wave
 constexpr int SP_DTBL = 256;                 // their (pixel, window)-keyed sums
 constexpr int SP_SIDE = 336;                 // f64 sums of pixels with >= 2 principal points
+constexpr int SP_CLW = 2 * WAVE;               // colliding principal points listed per wave
 constexpr int SP_EVCAP = 192;               // tail events listed per wave (resolved when it fills)
 constexpr int SP_CCAP = 768;                 // chaos survivors + candidates
 constexpr int SP_HSZ = 2048;                 // Kruskal: candidate hash
@@ -140,6 +141,7 @@ struct SpLay {
   static constexpr uint32_t o_tval = c16(o_tkey + SP_DTBL * 4);
   static constexpr uint32_t o_side = c16(o_tval + SP_DTBL * 8);  // read until the levels are computed
   static constexpr uint32_t o_tend = c16(o_side + SP_SIDE * 8);
+  static constexpr uint32_t o_clw = c16(o_coll + SP_FWORDS * 4);  // colliding points' work lists (entries phase)
   // chaos view
   static constexpr uint32_t o_cel = SP_LDS_BYTES - SP_CCAP;
   static constexpr uint32_t o_clist = o_cel - SP_CCAP * 4;
@@ -157,6 +159,7 @@ struct SpLay {
   static_assert(o_F + SP_FWORDS * 4 <= o_wsurv && o_cnt + SP_NBMAX * 4 <= o_wsurv, "cleared words below the lists");
   static_assert(SP_LDS_BYTES % 512 == 0 && 4 * SP_LDS_BYTES <= 160 * 1024, "four workgroups per CU");
   static_assert(SP_NW == 4, "the chaos screen merges four partial survivor lists");
+  static_assert(o_clw + SP_NW * SP_CLW * 4 <= o_side, "collision work lists between the collision bits and the side table");
   static_assert(SP_NW * SP_EVCAP * 4 == SP_DTBL * 12 && o_tval == o_tkey + SP_DTBL * 4 && SP_EVCAP % WAVE == 0,
                 "the event lists tile the dup table's space");
   static_assert(o_U + SP_NW * WAVE * 8 <= o_wsurv && SP_NW * WAVE * 8 <= SP_FWORDS * 4 && SP_NW * WAVE >= 2 * WAVE, "eL row blocks over the screen's bitmaps, the small Kruskal's hash over the survivor lists");
@@ -471,9 +474,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       }
     }
     SP_STAMP(1);
-    uint32_t hole_slots = 0;  // bit j: point j is a later point of its pixel (marked in ekey after the ticket barrier)
     if (!skip) {
-      // every point's key (pixel << 12 | window position) and value at its bucket's arrival slot (entry index) ...
+      // every point's key (pixel << 12 | window position) and value at its bucket's arrival slot (entry index); its
+      // hole mark (L8, until the levels overwrite it) cleared
 #pragma unroll
       for (int j = 0; j < RMAX; ++j) {
         const int i = tid + j * BLOCK;
@@ -482,59 +485,43 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
           const int f = (int)dir[p >> bs] + (int)aw_get(j);
           ekey[f] = (p << 12) | (uint32_t)i;
           evals[f] = (uint32_t)(hs(j) >> 32);
+          L8[f] = 0;
           aw_set(j, (uint32_t)f);
         }
       }
       __syncthreads();
       // ... then each point whose filter bit was set twice scans its bucket for points of its pixel: none (a single
-      // point, like every point with a filter bit of its own: its value enters the
-      // statistics), only later ones (the pixel's first point: it sums them all, in window order as coo.toarray()
-      // does, into the side table), or an earlier one (a hole).  The scans of five slots run together.
-#pragma unroll
-      for (int g = 0; g < RMAX; g += 5) {
-        constexpr int GS = 5;
-        uint32_t sl[GS], st[GS];
-        int mlen = 0;
-#pragma unroll
-        for (int jj = 0; jj < GS; ++jj) {
-          const int j = g + jj;
-          sl[jj] = 0u;
-          st[jj] = 0u;
-          if (j < RMAX && tid + j * BLOCK < n0) {
-            const uint32_t p = H::pix(hs(j));
-            if (coll[sp_fword(p)] & sp_fmask(p)) {  // (else no other point has its pixel: a single point)
-              const uint32_t b = p >> bs;
-              const uint32_t s0 = dir[b], s1 = dir[b + 1];
-              sl[jj] = s0 | ((s1 - s0) << 16);
-              mlen = max(mlen, (int)(s1 - s0));
-            }
-          }
+      // point, like every point with a filter bit of its own: its value enters the statistics), only later ones (the
+      // pixel's first point: it sums them all, in window order as coo.toarray() does, into the side table), or an
+      // earlier one (a hole: L8 = 1, marked in ekey after the ticket barrier).  The colliding points are listed per
+      // wave (entry indices, compacted over the lanes by ballot) and scanned 64 at a time, one per lane.
+      uint32_t* wcl = reinterpret_cast<uint32_t*>(smem + LY::o_clw) + wid * SP_CLW;
+      const uint64_t below = (1ull << lane) - 1ull;
+      auto coll_round = [&](int cnt) {  // lanes < cnt take wcl[lane] (cnt uniform)
+        __builtin_amdgcn_wave_barrier();  // (the list was written by this wave's lanes)
+        const bool ok = lane < cnt;
+        const uint32_t f = ok ? wcl[lane] : 0u;
+        const uint32_t key = ekey[f], p = key >> 12;
+        int b0 = 0, b1 = 0;
+        if (ok) {
+          b0 = dir[p >> bs];
+          b1 = dir[(p >> bs) + 1];
         }
-        for (int k = 0; k < mlen; ++k) {
-#pragma unroll
-          for (int jj = 0; jj < GS; ++jj) {
-            const int j = g + jj;
-            if (j < RMAX && k < (int)(sl[jj] >> 16)) {
-              const uint32_t p = H::pix(hs(j)), key = (p << 12) | (uint32_t)(tid + j * BLOCK);
-              const uint32_t w = ekey[(sl[jj] & 0xFFFFu) + k];
-              const bool same = (w >> 12) == p;
-              st[jj] |= (same && w < key ? 2u : 0u) | (same && w > key ? 1u : 0u);
-            }
-          }
+        uint32_t st = 0u;
+        for (int k = b0; k < b1; ++k) {
+          const uint32_t w = ekey[k];
+          const bool same = (w >> 12) == p;
+          st |= (same && w < key ? 2u : 0u) | (same && w > key ? 1u : 0u);
         }
-#pragma unroll
-        for (int jj = 0; jj < GS; ++jj) {
-          const int j = g + jj;
-          if (j >= RMAX || tid + j * BLOCK >= n0) continue;
-          if (st[jj] & 2u) {
-            hole_slots |= 1u << j;
-          } else if (st[jj] == 0u) {
-            stat((double)__uint_as_float((uint32_t)(hs(j) >> 32)));
+        if (ok) {
+          const float v0 = __uint_as_float(evals[f]);
+          if (st & 2u) {
+            L8[f] = 1;
+          } else if (st == 0u) {
+            stat((double)v0);
           } else {  // the first point of a pixel with several: their sum in window order
-            const uint32_t p = H::pix(hs(j));
-            const int b0 = (int)(sl[jj] & 0xFFFFu), b1 = b0 + (int)(sl[jj] >> 16);
-            double sum = (double)__uint_as_float((uint32_t)(hs(j) >> 32));
-            uint32_t last = (p << 12) | (uint32_t)(tid + j * BLOCK);
+            double sum = (double)v0;
+            uint32_t last = key;
             while (true) {  // the next point of the pixel by window position
               uint32_t nk = 0xFFFFFFFFu;
               int ni = -1;
@@ -552,14 +539,37 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
             const int slot = atomicAdd(&ctr[S_SIDE], 1);
             if (slot < SP_SIDE) {
               side[slot] = sum;
-              evals[aw_get(j)] = SP_SIDEREF | (uint32_t)slot;
+              evals[f] = SP_SIDEREF | (uint32_t)slot;
             } else {
               ctr[S_ABORT] = 1;
             }
             stat(sum);
           }
         }
+        __builtin_amdgcn_wave_barrier();  // (the list is rewritten after this)
+      };
+      int ncw = 0;  // (uniform)
+#pragma unroll
+      for (int j = 0; j < RMAX; ++j) {
+        const int i = tid + j * BLOCK;
+        bool col = false;
+        if (i < n0) {
+          const uint32_t p = H::pix(hs(j));
+          col = !(SMG_SP_ABL & 128) && (coll[sp_fword(p)] & sp_fmask(p)) != 0u;
+          if (!col) stat((double)__uint_as_float((uint32_t)(hs(j) >> 32)));  // (no other point has its pixel)
+        }
+        const uint64_t m = __ballot(col);
+        if (m) {  // (uniform)
+          if (col) wcl[ncw + (int)__popcll(m & below)] = aw_get(j);
+          ncw += (int)__popcll(m);
+          if (ncw >= WAVE) {
+            coll_round(WAVE);
+            ncw -= WAVE;
+            if (lane < ncw) wcl[lane] = wcl[WAVE + lane];
+          }
+        }
       }
+      if (ncw > 0) coll_round(ncw);
     }
     // the principal registers are consumed: tail chunks 2 and 3 go in flight (or the same number of stand-in loads, so
     // that the waits below count 2*RC younger loads on every path)
@@ -599,13 +609,6 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       reject();
       skip = true;
     }
-    // the holes mark their entries (no scan reads the keys any more; a lookup before the mark sees the pixel's first
-    // point anyway: it takes the lowest window position)
-    if (!skip && hole_slots) {
-#pragma unroll
-      for (int j = 0; j < RMAX; ++j)
-        if ((hole_slots >> j) & 1u) ekey[aw_get(j)] |= SP_HOLE;
-    }
     // the principal statistics (per-wave sums, in wave order)
     double sx = 0.0, sxx = 0.0, s0 = 0.0, npx_pos = 0.0, vmax = 0.0;
     if (!skip) {
@@ -623,13 +626,16 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       vmax = t[4];
     }
     const bool chaos_ok = !skip && (sx > 0.0) && (npx_pos >= 4.0) && !(SMG_SP_ABL & 1);
-    // the level index per entry, for the chaos phase (the values' space later holds its candidate hash): computed here,
-    // while tail chunks 2 and 3 are in flight (a hole not yet marked gets a level nobody reads)
-    if (chaos_ok && !(SMG_SP_ABL & 4)) {
-      const double rcp = 1.0 / vmax;
+    // the holes (L8 = 1) mark their entries (no scan reads the keys any more; a lookup before the mark sees the
+    // pixel's first point anyway: it takes the lowest window position), and the other entries get their level index
+    // for the chaos phase (the values' space later holds its candidate hash): computed here, while tail chunks 2 and
+    // 3 are in flight
+    if (!skip) {
+      const bool lv = chaos_ok && !(SMG_SP_ABL & 4);
+      const double rcp = lv ? 1.0 / vmax : 0.0;
       for (int i = tid; i < n0; i += BLOCK) {
-        const uint32_t w = ekey[i];
-        if (!(w & SP_HOLE)) L8[i] = (uint8_t)sp_level(sp_val(evals[i], side), vmax, rcp, P);
+        if (L8[i]) ekey[i] |= SP_HOLE;
+        else if (lv) L8[i] = (uint8_t)sp_level(sp_val(evals[i], side), vmax, rcp, P);
       }
     }
     SP_STAMP(3);
