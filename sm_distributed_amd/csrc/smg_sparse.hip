@@ -170,6 +170,11 @@ struct SpGeo {
   int32_t band_rows;  // image rows screened per chaos band (images above 2^15 pixels)
 };
 
+// the number of lanes below this one whose bit is set in the wave mask m (v_mbcnt)
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // the filter F: bit p mod 2^15 for every principal pixel p (direct-mapped: a row segment of pixels is a run of bits, so
 // the chaos pre-filter reads it too)
 __device__ __forceinline__ uint32_t sp_fword(uint32_t p) { return (p >> 5) & (uint32_t)(SP_FWORDS - 1); }
@@ -496,7 +501,6 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       // earlier one (a hole: L8 = 1, marked in ekey after the ticket barrier).  The colliding points are listed per
       // wave (entry indices, compacted over the lanes by ballot) and scanned 64 at a time, one per lane.
       uint32_t* wcl = reinterpret_cast<uint32_t*>(smem + LY::o_clw) + wid * SP_CLW;
-      const uint64_t below = (1ull << lane) - 1ull;
       auto coll_round = [&](int cnt) {  // lanes < cnt take wcl[lane] (cnt uniform)
         __builtin_amdgcn_wave_barrier();  // (the list was written by this wave's lanes)
         const bool ok = lane < cnt;
@@ -560,7 +564,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         }
         const uint64_t m = __ballot(col);
         if (m) {  // (uniform)
-          if (col) wcl[ncw + (int)__popcll(m & below)] = aw_get(j);
+          if (col) wcl[ncw + (int)lanes_below(m)] = aw_get(j);
           ncw += (int)__popcll(m);
           if (ncw >= WAVE) {
             coll_round(WAVE);
@@ -654,11 +658,10 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       // per event, so that resolving them takes ceil(events / 64) rounds rather than the busiest lane's count); the
       // list is resolved when it fills and after the stream.  Partials: part[k][wid], written only by this wave, lanes
       // of one instruction in hardware order -- deterministic.
-      // the wave's event list (t << 7 | in << 6 | lane, t = chunk * RC + slot), in the dup table's space (written only
+      // the wave's event list (t << 6 | lane, t = chunk * RC + slot), in the dup table's space (written only
       // after the stream; the filter collisions overlapping it were read before the ticket barrier)
       uint32_t* evl = tkey + wid * SP_EVCAP;
       int nev = 0;  // (uniform)
-      const uint64_t below = (1ull << lane) - 1ull;
       int gsv[MAXK];
 #pragma unroll
       for (int kk = 2; kk < MAXK; ++kk) gsv[kk] = uni(D->gs[kk]);
@@ -680,14 +683,13 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         for (int e0 = 0; e0 < nev; e0 += SP_EVB * WAVE) {  // uniform
           Reg hq[SP_EVB];
           int kq[SP_EVB];
-          bool hasq[SP_EVB], inq[SP_EVB];
+          bool hasq[SP_EVB];
 #pragma unroll
           for (int q = 0; q < SP_EVB; ++q) {
             const int e = e0 + q * WAVE + lane;
             hasq[q] = e < nev;
             const uint32_t ent = hasq[q] ? evl[e] : 0u;
-            const int t = (int)(ent >> 7);
-            inq[q] = (ent & 64u) != 0u;
+            const int t = (int)(ent >> 6);
             const int Gi = (t / RC) * GPC + (t % RC) * NW + wid;
             int k = 1;
 #pragma unroll
@@ -699,12 +701,13 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
           for (int q = 0; q < SP_EVB; ++q) {
             const Reg h = hq[q];
             const uint32_t p = H::pix(h);
-            const int r = inq[q] ? sp_lookup(ekey, dir, p, bs) : -1;
+            const bool in = hasq[q] && (F[sp_fword(p)] & sp_fmask(p)) != 0u;  // (tested again: not in the entry)
+            const int r = in ? sp_lookup(ekey, dir, p, bs) : -1;
             add_x(r >= 0, r, h, kq[q]);
             const bool dq = hasq[q] && H::dup(h);
             const uint64_t mq = __ballot(dq);
             if (mq) {
-              const int e = nd + (int)__popcll(mq & below);
+              const int e = nd + (int)lanes_below(mq);
               if (dq && e < SP_DSEG) {
                 wdkey[e] = (p << 3) | (uint32_t)kq[q];
                 wdval[e] = H::val(h);
@@ -739,7 +742,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
             const uint64_t em = __ballot(evt);
             if (em) {  // (uniform)
               const uint32_t t = (uint32_t)(c * RC + j);
-              if (evt) evl[nev + (int)__popcll(em & below)] = (t << 7) | (in ? 64u : 0u) | (uint32_t)lane;
+              if (evt) evl[nev + (int)lanes_below(em)] = (t << 6) | (uint32_t)lane;
               nev += (int)__popcll(em);
               if (nev > SP_EVCAP - WAVE) {
                 SP_MARK_BEGIN(_th0);
@@ -985,7 +988,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
             screen(wcnt);
             wcnt = 0;
           }
-          if (surv) wsurv[wcnt + (int)__popcll(m & ((1ull << lane) - 1ull))] = w;
+          if (surv) wsurv[wcnt + (int)lanes_below(m)] = w;
           wcnt += c;
         }
         // the waves' partial lists (up to 63 survivors each) are screened together: their counts, a barrier, then
