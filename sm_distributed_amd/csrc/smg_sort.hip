@@ -440,12 +440,17 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
 
   uint32_t fmask = 0;  // FLAG: bit u = the duplicate-candidate flag of the thread's point u
   if constexpr (FLAG) {
-    // the flags were computed by the histogram pass (one bit per dataset position, in flagbits)
-    static_assert(SRT_IPT <= 32, "one flag bit per point in a 32-bit mask");
+    // the flags were computed by the histogram pass (one bit per dataset position, in flagbits).  The wave's
+    // SRT_IPT rows of 64 points are 2 * SRT_IPT consecutive flag words: one load (a word per lane), then row u's
+    // word comes from lane 2u + (lane >> 5) -- one memory instruction instead of one per row (the pass was bound
+    // by its memory instructions; bits past n are never stored)
+    static_assert(SRT_IPT <= 32 && 2 * SRT_IPT <= 64, "one flag bit per point in a 32-bit mask, one word per lane");
+    const int64_t fw0 = wbase >> 5, nfw = (n + 31) >> 5;
+    const uint32_t fw = (lane < 2 * SRT_IPT && fw0 + lane < nfw) ? flagbits[fw0 + lane] : 0u;
 #pragma unroll
     for (int u = 0; u < SRT_IPT; ++u) {
-      const int64_t i = wbase + u * 64 + lane;
-      if (i < n) fmask |= ((flagbits[i >> 5] >> (i & 31)) & 1u) << u;
+      const uint32_t word = (uint32_t)__shfl((int)fw, 2 * u + (lane >> 5), 64);
+      fmask |= ((word >> (lane & 31)) & 1u) << u;
     }
   }
 

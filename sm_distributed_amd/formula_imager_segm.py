@@ -656,8 +656,9 @@ def _side_stream(device):
 def compute_sf_images(sc, ds, sf_peak_df, ppm):
     """formula_imager_segm.py:142-161.  ``sc`` is accepted for signature compatibility and ignored.
 
-    Device order: the resident peaks are flagged, sorted and prefix-summed on the current stream while the
-    ion layout is uploaded and built on a side stream; the window search joins both."""
+    Device order: the resident peaks are flagged and sorted on the current stream while the ion layout is
+    uploaded and built on a side stream; the window search follows both on the side stream, beside the prefix
+    sums on the current one (a latency-bound search beside a bandwidth-bound read); the current stream joins."""
     import torch
 
     from .dataset import spectra_from_duck
@@ -673,11 +674,14 @@ def compute_sf_images(sc, ds, sf_peak_df, ppm):
     side = _side_stream(peaks.device) if os.environ.get("SMG_LAYOUT_SIDE", "1") != "0" else main
     side.wait_stream(main)  # the side stream may reuse memory the main stream released
     peaks.flag_and_sort(ppm)
-    peaks.prefix_sums()
     keys, dions, K = device_layout(sf_peak_df, peaks.device, side)
+    # the window search on the side stream after the sort; lo / hi are allocated on the main stream (the side
+    # stream waits for everything queued on it so far, so memory the main stream released is free)
+    side.wait_stream(main)
+    lo, hi = window_bounds(peaks, dions, ppm, stream=side)
+    peaks.prefix_sums()
     main.wait_stream(side)
     for t in (dions.win_off, dions.peak_mz, dions.win_order, dions.ion_order, K, keys.keys_dev):
         if t is not None:
             t.record_stream(main)
-    lo, hi = window_bounds(peaks, dions, ppm)
     return IonImageSet(peaks, keys, dions, K, lo, hi, ds.get_dims(), ppm)
