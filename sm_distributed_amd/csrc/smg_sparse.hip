@@ -192,11 +192,17 @@ __device__ __forceinline__ int sp_lookup(const uint32_t* ekey, const uint16_t* d
   const int s0 = dir[b], e = dir[b + 1];
   int r = -1;
   uint32_t best = 0xFFFFFFFFu;
-  for (int i = s0; i < e; ++i) {
-    const uint32_t w = ekey[i];
-    if ((w >> 12) == p && w < best) {
-      best = w;
+  // two entries per step, read together (one LDS round trip per pair: the loop is bound by their latency); the
+  // second of a bucket with an odd count is the next bucket's or the level bytes' and is not tested
+  for (int i = s0; i < e; i += 2) {
+    const uint32_t w0 = ekey[i], w1 = ekey[i + 1];
+    if ((w0 >> 12) == p && w0 < best) {
+      best = w0;
       r = i;
+    }
+    if (i + 1 < e && (w1 >> 12) == p && w1 < best) {
+      best = w1;
+      r = i + 1;
     }
   }
   return r;
@@ -512,10 +518,11 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
           b1 = dir[(p >> bs) + 1];
         }
         uint32_t st = 0u;
-        for (int k = b0; k < b1; ++k) {
-          const uint32_t w = ekey[k];
-          const bool same = (w >> 12) == p;
-          st |= (same && w < key ? 2u : 0u) | (same && w > key ? 1u : 0u);
+        for (int k = b0; k < b1; k += 2) {  // (pairs read together, as in sp_lookup)
+          const uint32_t w0 = ekey[k], w1 = ekey[k + 1];
+          const bool same0 = (w0 >> 12) == p, same1 = k + 1 < b1 && (w1 >> 12) == p;
+          st |= (same0 && w0 < key ? 2u : 0u) | (same0 && w0 > key ? 1u : 0u);
+          st |= (same1 && w1 < key ? 2u : 0u) | (same1 && w1 > key ? 1u : 0u);
         }
         if (ok) {
           const float v0 = __uint_as_float(evals[f]);
@@ -1060,9 +1067,11 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
               const int base = row * ncl + cp - 2;  // pixel of window column 0
               const uint32_t lo = (uint32_t)(row * ncl + max(cp - 2, 0)), hi = (uint32_t)(row * ncl + min(cp + 2, ncl - 1));
               const int e1 = dir[(hi >> bs) + 1];
-              for (int i = dir[lo >> bs]; i < e1; ++i) {
-                const uint32_t w = ekey[i] >> 12;  // (a hole's: >= 2^19, outside the range)
-                if (w >= lo && w <= hi) packed |= (uint64_t)L8[i] << (8 * (int)(w - (uint32_t)base));
+              for (int i = dir[lo >> bs]; i < e1; i += 2) {  // (pairs read together, as in sp_lookup)
+                const uint32_t w0 = ekey[i] >> 12, w1 = ekey[i + 1] >> 12;  // (a hole's: >= 2^19, outside the range)
+                const uint64_t l0 = L8[i], l1 = L8[i + 1];
+                if (w0 >= lo && w0 <= hi) packed |= l0 << (8 * (int)(w0 - (uint32_t)base));
+                if (i + 1 < e1 && w1 >= lo && w1 <= hi) packed |= l1 << (8 * (int)(w1 - (uint32_t)base));
               }
             }
           }
