@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes
 import os
 
-# SMG_LIB overrides the path (diagnostic builds of the same C-ABI, e.g. scripts/variants.sh)
+# SMG_LIB overrides the path (diagnostic builds of the same C-ABI, e.g. scripts/build_sparse_variant.sh)
 LIB_PATH = os.environ.get("SMG_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsmg.so")
 
 SMG_OK = 0
