@@ -563,7 +563,7 @@ __device__ __forceinline__ double2 block_part(const Hits<FMT>& hits, int64_t i) 
   if constexpr (FMT == SMG_HITS_PACKED_F32) {  // 16-byte loads: two hits per load (a is even)
     const ulonglong2* h2 = reinterpret_cast<const ulonglong2*>(hits.h + a);
     const int m = (int)(i - a);
-#pragma unroll 8
+#pragma unroll 4  // (8 spilled 20 VGPRs in ion_desc8_kernel; 4 fits in 90, no scratch: ion stage -0.35 ms at config 3)
     for (int q = 0; q < (m >> 1); ++q) {
       const ulonglong2 hh = h2[q];
       const double v0 = Hits<FMT>::val(hh.x), v1 = Hits<FMT>::val(hh.y);
@@ -665,10 +665,10 @@ __global__ void ion_desc_kernel(Hits<FMT> hits, const int64_t* __restrict__ lo, 
 // The same descriptors with eight lanes per ion, lane k = window k (k >= 8: the has-hits test of windows 8..31):
 // the two partial 64-point blocks of every window are summed in parallel instead of one window after another.
 template <int FMT>
-__global__ void ion_desc8_kernel(Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
-                                 const int64_t* __restrict__ ion_off, const double* __restrict__ theor,
-                                 const DD4* __restrict__ cum, const int64_t* __restrict__ ion_order, int64_t n_ions,
-                                 IonDesc* __restrict__ out) {
+__global__ void __launch_bounds__(256)
+    ion_desc8_kernel(Hits<FMT> hits, const int64_t* __restrict__ lo, const int64_t* __restrict__ hi,
+                     const int64_t* __restrict__ ion_off, const double* __restrict__ theor, const DD4* __restrict__ cum,
+                     const int64_t* __restrict__ ion_order, int64_t n_ions, IonDesc* __restrict__ out) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t b = t >> 3;
   const int k = (int)(t & 7);

@@ -438,22 +438,6 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
     }
   }
 
-  uint32_t fmask = 0;  // FLAG: bit u = the duplicate-candidate flag of the thread's point u
-  if constexpr (FLAG) {
-    // the flags were computed by the histogram pass (one bit per dataset position, in flagbits).  The wave's
-    // SRT_IPT rows of 64 points are 2 * SRT_IPT consecutive flag words: one load (a word per lane), then row u's
-    // word comes from lane 2u + (lane >> 5) -- one memory instruction instead of one per row (the pass was bound
-    // by its memory instructions; bits past n are never stored)
-    static_assert(SRT_IPT <= 32 && 2 * SRT_IPT <= 64, "one flag bit per point in a 32-bit mask, one word per lane");
-    const int64_t fw0 = wbase >> 5, nfw = (n + 31) >> 5;
-    const uint32_t fw = (lane < 2 * SRT_IPT && fw0 + lane < nfw) ? flagbits[fw0 + lane] : 0u;
-#pragma unroll
-    for (int u = 0; u < SRT_IPT; ++u) {
-      const uint32_t word = (uint32_t)__shfl((int)fw, 2 * u + (lane >> 5), 64);
-      fmask |= ((word >> (lane & 31)) & 1u) << u;
-    }
-  }
-
   // ranking: each wave counts its rows in order (row u, lane) -- the stable order of its points -- into its own
   // u16 histogram; the lanes of one digit find each other with one ballot per digit bit
   uint32_t rk[SRT_IPT];
@@ -553,6 +537,21 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
     if (j < nvalid) kout[s_gbase[dd] + j] = kk;
   }
   auto slot_digit = [&](int u) { return (dj[u >> 1] >> ((u & 1) * 16)) & 0xFFFFu; };
+  // FLAG: the duplicate-candidate flags were computed by the histogram pass (one bit per dataset position, in
+  // flagbits).  The wave's SRT_IPT rows of 64 points are 2 * SRT_IPT consecutive flag words: one load (a word per
+  // lane) beside the values', then row u's word comes from lane 2u + (lane >> 5).  Read here, after the keys are
+  // out of registers (held from the start, they spilled), and as one memory instruction instead of one per row
+  // (bits past n are never stored)
+  static_assert(SRT_IPT <= 32 && 2 * SRT_IPT <= 64, "a flag word per lane");
+  uint32_t fw = 0u;
+  if constexpr (FLAG) {
+    const int64_t fw0 = wbase >> 5, nfw = (n + 31) >> 5;
+    fw = (lane < 2 * SRT_IPT && fw0 + lane < nfw) ? flagbits[fw0 + lane] : 0u;
+  }
+  auto flag_of = [&](int u) -> bool {
+    const uint32_t word = (uint32_t)__shfl((int)fw, 2 * u + (lane >> 5), 64);
+    return ((word >> (lane & 31)) & 1u) != 0u;
+  };
 
   if constexpr (!SPLIT) {
     // the values (not loaded before: with the keys they would spill)
@@ -571,7 +570,7 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
 #pragma unroll
     for (int u = 0; u < SRT_IPT; ++u) {
       uint64_t x = v[u];
-      if constexpr (FLAG) x = ((fmask >> u) & 1u) ? (x | 0x80000000ull) : (x & ~0x80000000ull);
+      if constexpr (FLAG) x = flag_of(u) ? (x | 0x80000000ull) : (x & ~0x80000000ull);
       xbuf[rk[u]] = x;
     }
     __syncthreads();
@@ -600,7 +599,7 @@ __global__ void __launch_bounds__(SRT_T, SMG_SRT_WPE) sort_pass_kernel(const uin
 #pragma unroll
       for (int u = 0; u < SRT_IPT; ++u) {
         uint32_t x = v[u];
-        if (FLAG && half == 0) x = ((fmask >> u) & 1u) ? (x | 0x80000000u) : (x & ~0x80000000u);
+        if (FLAG && half == 0) x = flag_of(u) ? (x | 0x80000000u) : (x & ~0x80000000u);
         xk[rk[u]] = x;
       }
       __syncthreads();
