@@ -38,16 +38,17 @@ import sys
 import threading
 import time
 
-import numpy as np
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # KFD queue evictions of this process (each stops every running kernel for >= one 10-ms tick) are counted per step
 # (sm_distributed_amd/hostmem.py); SMG_NUMA_OPTOUT=1 takes the process out of NUMA-balancing scans, one trigger of
-# them, before torch starts its threads (the pool's boxes run with numa_balancing = 0)
+# them.  A thread inherits the policy when it is created, so this runs before numpy (its BLAS pool) and torch start
+# any thread: hostmem imports only the standard library (the package's __init__ imports nothing else)
 from sm_distributed_amd import hostmem  # noqa: E402
 
 NUMA_OPTOUT = hostmem.numa_balancing_optout() if os.environ.get("SMG_NUMA_OPTOUT") == "1" else False
+
+import numpy as np  # noqa: E402
 
 METRIC = "MSM-scored ions/sec (HMDB×3 adducts, 250k-px synth) + imaging-kernel HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -225,21 +226,12 @@ def main():
             plan = D.rebalance(plan, formulas, peaks, times, head_seconds=head)
             log(f"[rank {rank}] rebalanced from measured shard times (ms) {[round(x * 1e3, 2) for x in times]}, "
                 f"rank-0 assembly {head * 1e3:.2f} ms: counts {plan.counts}")
-        phases = []  # per step: this rank's rows, gather (its wait for the slowest rank included), assembly (ms)
+        # per step: timing events of this rank's rows, gather (its wait for the slowest rank included) and assembly,
+        # recorded by score_sharded itself on the stream (no synchronisation added), read after the timed steps
+        phases = []
 
         def step_fn():
-            # D.score_sharded's body with a clock between its three parts (a device synchronisation after the
-            # rows: the gather needs them anyway), so that each rank's line says where its step went
-            t_a = time.perf_counter()
-            rows, _ = D._device_rows(plan, peaks, ds_config)
-            torch.cuda.synchronize()
-            t_b = time.perf_counter()
-            table = D.gather_rows(rows, plan)
-            torch.cuda.synchronize()
-            t_c = time.perf_counter()
-            df = D.rows_to_frame(table, plan.global_keys) if table is not None else None
-            phases.append(((t_b - t_a) * 1e3, (t_c - t_b) * 1e3, (time.perf_counter() - t_c) * 1e3))
-            return df
+            return D.score_sharded(plan, peaks, ds_config, phases=phases)[0]
         my_formulas = plan.formulas
     elif shard_only:
         # one rank of an N-way plan measured alone on this GPU: its slice, images, scores and row block (the
@@ -324,7 +316,8 @@ def main():
     # every rank's step min / median / max and clock, gathered for the line (one all_gather of 5 floats)
     mine = [float(per_step.min()), float(np.median(per_step)), float(per_step.max())] if len(per_step) else [0.0] * 3
     mine += [float(sclk["median"]) if sclk else -1.0, float(sclk["min"]) if sclk else -1.0]
-    timed_phases = np.asarray(phases[-len(per_step):]) if phases else np.zeros((0, 3))
+    timed_phases = (np.asarray([D.phase_ms(e) for e in phases[-len(per_step):]]) if phases and len(per_step)
+                    else np.zeros((0, 3)))
     mine += [float(x) for x in np.median(timed_phases, axis=0)] if len(timed_phases) else [-1.0] * 3
     per_rank = [mine]
     if sharded:
@@ -422,6 +415,8 @@ def main():
             "cpu_baseline": cpu,
             "lib": _lib.version(),
         }
+        if _lib.check_build():  # the -DSMG_CHECK diagnostic library (SMG_LIB): its counters over the whole run
+            line["check"] = _lib.check_counters()
         print(json.dumps(line), file=json_out, flush=True)
     if sharded:
         dist.destroy_process_group()

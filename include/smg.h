@@ -213,6 +213,16 @@ int smg_debug_main_kernel(int32_t which);
  * reset on read; SMG_ERR_UNSUPPORTED in the shipped build. */
 int smg_debug_stamps(unsigned long long* host_out, int n);
 int smg_debug_sparse_stamps(unsigned long long* host_out, int n);
+/* Diagnostic build only (-DSMG_CHECK, `make check` -> libsmg_check.so): every ion pass checks each position it scores
+ * -- claimed once per pass, its descriptor equal to what lo / hi / ion_win_off / ion_order give, every hit index it
+ * loads inside its window and inside [0, n_points), every reject inside its list -- and counts failures (printing the
+ * first few).  smg_debug_check_points sets the resident hit count the next smg_ion_metrics calls are checked
+ * against (every build accepts it; only the check build uses it).  smg_debug_check_read waits for the device, writes
+ * up to n counters (positions claimed, descriptor mismatches, loads outside their window, double hand-outs, records
+ * read as descriptors, reject-list overflows, windows outside [0, n_points], descriptors checked) and resets them;
+ * SMG_ERR_UNSUPPORTED in the shipped build. */
+int smg_debug_check_points(int64_t n_points);
+int smg_debug_check_read(unsigned long long* host_out, int32_t n);
 
 /* passes of smg_ion_metrics, as reported by smg_debug_pass_times */
 #define SMG_PASS_DESC 0   /* ion descriptors (ion_desc8_kernel) */

@@ -62,6 +62,8 @@ PROTOTYPES = {
     "smg_debug_main_kernel": (ctypes.c_int, [_I32]),
     "smg_debug_stamps": (ctypes.c_int, [_P, ctypes.c_int]),
     "smg_debug_sparse_stamps": (ctypes.c_int, [_P, ctypes.c_int]),
+    "smg_debug_check_points": (ctypes.c_int, [_I64]),
+    "smg_debug_check_read": (ctypes.c_int, [_P, _I32]),
     "smg_debug_time_main_pass": (ctypes.c_int, [_I32]),
     "smg_debug_main_pass_times": (ctypes.c_int, [_P, _I32, ctypes.POINTER(_I32)]),
     "smg_debug_pass_times": (ctypes.c_int, [_P, _P, _I32, ctypes.POINTER(_I32)]),
@@ -109,3 +111,24 @@ def check(rc: int, what: str = "smg call"):
 
 def version() -> str:
     return lib().smg_version().decode()
+
+
+CHECK_NAMES = ("positions_claimed", "descriptor_mismatches", "loads_outside_window", "double_hand_outs",
+               "records_read_as_descriptors", "reject_list_overflows", "windows_out_of_range", "descriptors_checked")
+_check_build = None
+
+
+def check_build() -> bool:
+    """True when the loaded library is the -DSMG_CHECK diagnostic build (libsmg_check.so)."""
+    global _check_build
+    if _check_build is None:
+        buf = (ctypes.c_ulonglong * 8)()
+        _check_build = lib().smg_debug_check_read(ctypes.cast(buf, ctypes.c_void_p), 0) == SMG_OK
+    return _check_build
+
+
+def check_counters() -> dict:
+    """The check build's counters since the last read (smg_debug_check_read), by name; reset on read."""
+    buf = (ctypes.c_ulonglong * 8)()
+    check(lib().smg_debug_check_read(ctypes.cast(buf, ctypes.c_void_p), 8), "smg_debug_check_read")
+    return dict(zip(CHECK_NAMES, (int(x) for x in buf)))

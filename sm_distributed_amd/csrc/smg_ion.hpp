@@ -252,7 +252,79 @@ struct Sched {
   uint32_t* ctr;          // SRC_RANGES: XCDS counters; SRC_LIST: cursor
   const uint32_t* list;   // SRC_LIST
   const uint32_t* count;  // SRC_LIST
+  uint32_t rej_cap;       // entries the pass's reject list holds (n_ions): a reject beyond it is dropped and counted
 };
+
+// ---- SMG_CHECK: the diagnostic build `make check` (-> libsmg_check.so, never the product) --------------------------
+// Every ion pass checks, per position it scores: that no other workgroup took the same position in this pass (a
+// claimed bit per position, set with atomicOr); that the 384-B descriptor it read equals what lo / hi / ion_off /
+// ion_order say for that position (so a record or stale bytes read as a descriptor are caught); that every global
+// index it loads lies inside its window and inside [0, n_points); and that no reject overflows its list.  Failures are
+// counted (smg_debug_check_read) and the first few printed with their position.
+// counters: positions claimed, descriptor mismatches, loads out of their window, double hand-outs, records read as
+// descriptors, reject-list overflows, windows outside [0, n_points], descriptors checked
+enum { CHK_IONS = 0, CHK_DESC, CHK_INDEX, CHK_DOUBLE, CHK_STATE, CHK_REJ, CHK_WINDOW, CHK_DESCS, CHK_N = 8 };
+struct ChkCtx {
+  const int64_t* lo;         // the scored windows (lo2 / hi2 of smg_ion_metrics)
+  const int64_t* hi;
+  const int64_t* ion_off;    // windows per ion (theoretical peaks)
+  const int64_t* ion_order;  // position -> ion
+  uint32_t* claim;           // bit per position and pass (zeroed per launch), pass p at claim + p * words
+  int64_t words;
+  int64_t n_points;          // resident hits (smg_debug_check_points)
+  unsigned long long* cnt;   // CHK_N counters (persistent, read and reset by smg_debug_check_read)
+};
+#ifdef SMG_CHECK
+#define SMG_CHK_PARAM , ::smg::ChkCtx CK
+#define SMG_CHK_ARG(c) , (c)
+__device__ __forceinline__ bool chk(const ChkCtx& C, bool ok, int code, int64_t a, int64_t b) {
+  if (!ok) {
+    const unsigned long long k = atomicAdd(&C.cnt[code], 1ull);
+    if (k < 4) printf("SMG_CHECK failure %d: %lld %lld (wg %d, tid %d)\n", code, (long long)a, (long long)b,
+                      (int)blockIdx.x, (int)threadIdx.x);
+  }
+  return ok;
+}
+// a load of hit `idx` for window k of ion `ion` (idx 0 stands for a group past the tail: a stand-in load)
+__device__ __forceinline__ void chk_load(const ChkCtx& C, int64_t ion, int k, int64_t idx, bool standin) {
+  if (standin) {
+    chk(C, idx == 0, CHK_INDEX, ion, idx);
+    return;
+  }
+  const int64_t w = C.ion_off[ion] + k;
+  chk(C, idx >= C.lo[w] && idx < C.hi[w] && idx >= 0 && idx < C.n_points, CHK_INDEX, ion * 64 + k, idx);
+}
+// claims position `pos` for pass `pass`; wave-uniform call, lane 0 acts
+__device__ __forceinline__ void chk_claim(const ChkCtx& C, int pass, int64_t pos) {
+  if ((threadIdx.x & 63) == 0) {
+    const uint32_t b = 1u << (pos & 31);
+    chk(C, !(atomicOr(&C.claim[pass * C.words + (pos >> 5)], b) & b), CHK_DOUBLE, pass, pos);
+    atomicAdd(&C.cnt[CHK_IONS], 1ull);
+  }
+}
+// the descriptor D (LDS copy) of position pos against the arrays it was made from; wave-uniform call, lane k checks
+// window k
+__device__ __forceinline__ void chk_desc(const ChkCtx& C, int64_t pos, const IonDesc* D) {
+  const int lane = threadIdx.x & 63;
+  const int64_t ion = C.ion_order ? C.ion_order[pos] : pos;
+  const int64_t w0 = C.ion_off[ion];
+  const int K = (int)(C.ion_off[ion + 1] - w0);
+  if (lane == 0) {
+    chk(C, D->ion == ion && D->K == K, CHK_DESC, pos, ((int64_t)D->ion << 8) | (D->K & 255));
+    atomicAdd(&C.cnt[CHK_DESCS], 1ull);
+  }
+  if (lane < K && lane < MAXK) {
+    const int64_t a = C.lo[w0 + lane], b = C.hi[w0 + lane];
+    chk(C, a >= 0 && b >= a && b <= C.n_points, CHK_WINDOW, pos * 64 + lane, a);
+    const int64_t g = lane == 0 ? 0 : (int64_t)D->gs[lane] * 64;
+    chk(C, D->base[lane] + g == a && (int64_t)D->end[lane] - g == b - a, CHK_DESC, pos * 64 + lane,
+        D->base[lane] + g - a);
+  }
+}
+#else
+#define SMG_CHK_PARAM
+#define SMG_CHK_ARG(c)
+#endif
 
 // A ticket is resolved against the counter it was drawn from (``home``, recorded at issue): a workgroup may move to
 // another XCD between the two -- a queue eviction saves and restores its waves, possibly elsewhere -- and a ticket of
@@ -329,7 +401,7 @@ __device__ __forceinline__ bool tbl_add(uint32_t* keys, double* vals, uint32_t k
 bool sparse_main_fits(const Params& P);
 int launch_sparse_main(Hits<SMG_HITS_PACKED_F32> hits, IonDesc* desc, Sched S, const Params& P, double* oc,
                        double* osp, double* osc, double* omsm, uint32_t* oflags, uint32_t* rej_list,
-                       uint32_t* rej_count, int cus, hipStream_t st);
+                       uint32_t* rej_count, int cus, hipStream_t st, const ChkCtx& ck);
 int sparse_read_stamps(unsigned long long* host_out, int n);
 
 }  // namespace smg

@@ -759,7 +759,7 @@ template <int FMT, int LB, int LRMAX, int LRC, int WPE, int SRC, bool TWO, bool 
 __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     Hits<FMT> hits, IonDesc* __restrict__ desc, Sched S, Params P, double* __restrict__ oc,
     double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags,
-    uint32_t* __restrict__ rej_list, uint32_t* __restrict__ rej_count) {
+    uint32_t* __restrict__ rej_list, uint32_t* __restrict__ rej_count SMG_CHK_PARAM) {
   constexpr int BLOCK = LB;
   constexpr int NW = LB / WAVE;
   constexpr int RMAX = LRMAX;
@@ -889,12 +889,18 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
 #pragma unroll
       for (int j = 0; j < RMAX; ++j) {
         const int i = tid + j * BLOCK;
+#ifdef SMG_CHECK
+        chk_load(CK, D->ion, 0, n0 > 0 ? a + min(i, n0 - 1) : 0, n0 <= 0);
+#endif
         ld8_async_v(hs(j), hits.h + (n0 > 0 ? a + min(i, n0 - 1) : 0));
       }
     } else {
 #pragma unroll
       for (int j = 0; j < RMAX; ++j) {
         const int i = tid + j * BLOCK;
+#ifdef SMG_CHECK
+        if (i < n0) chk_load(CK, D->ion, 0, a + i, false);
+#endif
         if (i < n0) hs(j) = hits.load(a, i);
       }
     }
@@ -918,11 +924,17 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         const int64_t bk = D->base[k];
         const int ek = D->end[k];
         const int64_t idx = G < ng ? bk + (int64_t)G * 64 + min(lane, ek - G * 64 - 1) : 0;
+#ifdef SMG_CHECK
+        chk_load(CK, D->ion, k, idx, G >= ng);
+#endif
         ld8_async_v(buf[j], hits.h + idx);
       } else {
         buf[j] = Hits<FMT>::zero();
         if (G < ng) {
           const int i = G * 64 + lane;
+#ifdef SMG_CHECK
+          if (i < D->end[k]) chk_load(CK, D->ion, k, D->base[k] + i, false);
+#endif
           if (i < D->end[k]) buf[j] = hits.load(D->base[k] + i);
         }
       }
@@ -991,9 +1003,19 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
     STAMP_INIT();
     bool skip = pos < 0;
     int K = 0, ion = 0, n0 = 0;
+    // a reject beyond the list's capacity (impossible while every position is handed out once) is dropped
     auto reject = [&]() {
-      if (tid == 0) rej_list[atomicAdd(rej_count, 1u)] = (SRC == SRC_RANGES) ? (uint32_t)pos : (uint32_t)ion;
+      if (tid == 0) {
+        const uint32_t r = atomicAdd(rej_count, 1u);
+        if (r < S.rej_cap) rej_list[r] = (SRC == SRC_RANGES) ? (uint32_t)pos : (uint32_t)ion;
+#ifdef SMG_CHECK
+        chk(CK, r < S.rej_cap, CHK_REJ, pos, r);
+#endif
+      }
     };
+#ifdef SMG_CHECK
+    if (!skip && wid == 0) chk_claim(CK, SRC == SRC_RANGES ? 0 : 1, pos);
+#endif
     if (!skip) {
       K = uni(D->K);
       ion = uni(D->ion);
@@ -1005,9 +1027,17 @@ __global__ void __launch_bounds__(LB, WPE) ion_pipe_kernel(
         }
         skip = true;
       } else if (!desc_lds_ok(D, CAPC)) {
+#ifdef SMG_CHECK
+        if (tid == 0) chk(CK, reinterpret_cast<const IonRec*>(D)->state == 0u, CHK_STATE, pos, 0);
+#endif
         reject();
         skip = true;
       }
+#ifdef SMG_CHECK
+      else if (wid == 0) {
+        chk_desc(CK, pos, D);
+      }
+#endif
     }
 
     const bool began = !skip;  // this ion uses the LDS structures (cleared again at its end)
@@ -3992,10 +4022,27 @@ static size_t slot_bytes_for(int npx) {
   return a > b ? a : b;
 }
 
+// SMG_CHECK builds: two claimed-bit sets (main pass, big-ion pass) behind the slots, zeroed per launch
+static size_t chk_words(int64_t n_ions) { return (size_t)((n_ions + 31) / 32 + 1); }
+static size_t chk_bytes(int64_t n_ions) {
+#ifdef SMG_CHECK
+  return al16(2 * chk_words(n_ions) * 4);
+#else
+  (void)n_ions;
+  return 0;
+#endif
+}
+
 static size_t ws_bytes_for(int64_t n_ions, int npx) {
   return WS_HEADER + 2 * al16((size_t)n_ions * 4) + (size_t)n_ions * sizeof(IonDesc) +
-         (size_t)DENSE_SLOTS * slot_bytes_for(npx);
+         (size_t)DENSE_SLOTS * slot_bytes_for(npx) + chk_bytes(n_ions);
 }
+
+// SMG_CHECK: the counters (persistent device buffer) and the hit count the checks index against
+#ifdef SMG_CHECK
+static unsigned long long* g_chk_cnt = nullptr;
+#endif
+static int64_t g_chk_points = INT64_MAX;
 
 using MainLay = Lay<MAIN_BLOCK / WAVE, MAIN_BLOCK * MAIN_RMAX>;
 using BigLay = Lay<BIG_BLOCK / WAVE, BIG_BLOCK * BIG_RMAX>;
@@ -4095,6 +4142,16 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   unsigned char* slots = reinterpret_cast<unsigned char*>(desc) + (size_t)n_ions * sizeof(IonDesc);
   const size_t slot_bytes = slot_bytes_for(P.npx);
   SMG_HIP(hipMemsetAsync(ws, 0, WS_HEADER, st));
+  ChkCtx ck{lo, hi, ion_off, ion_order, nullptr, (int64_t)chk_words(n_ions), g_chk_points, nullptr};
+#ifdef SMG_CHECK
+  if (!g_chk_cnt) {
+    SMG_HIP(hipMalloc(&g_chk_cnt, CHK_N * sizeof(unsigned long long)));
+    SMG_HIP(hipMemset(g_chk_cnt, 0, CHK_N * sizeof(unsigned long long)));
+  }
+  ck.cnt = g_chk_cnt;
+  ck.claim = reinterpret_cast<uint32_t*>(slots + (size_t)DENSE_SLOTS * slot_bytes);
+  SMG_HIP(hipMemsetAsync(ck.claim, 0, chk_bytes(n_ions), st));
+#endif
   // images above NPX_LDS_MAX pixels (or forced, smg_debug_force_two_level) take the two-level LDS passes
   const bool two = (P.npx > NPX_LDS_MAX || g_force_two_level) && P.npx <= NPX_TWO_MAX;
   Params PM = P, PB = P;
@@ -4138,14 +4195,14 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
     SMG_LAUNCH_CHECK();
   }
   if (main_ok && sparse) {
-    Sched SA{n_ions, hdr + HDR_XCD, nullptr, nullptr};
+    Sched SA{n_ions, hdr + HDR_XCD, nullptr, nullptr, (uint32_t)n_ions};
     PassTimer tm(SMG_PASS_MAIN, st);
     if constexpr (FMT == SMG_HITS_PACKED_F32) {
-      const int rc = launch_sparse_main(hits, desc, SA, P, oc, osp, osc, omsm, oflags, list_a, hdr + 0, cus, st);
+      const int rc = launch_sparse_main(hits, desc, SA, P, oc, osp, osc, omsm, oflags, list_a, hdr + 0, cus, st, ck);
       if (rc != SMG_OK) return rc;
     }
   } else if (main_ok) {
-    Sched SA{n_ions, hdr + HDR_XCD, nullptr, nullptr};
+    Sched SA{n_ions, hdr + HDR_XCD, nullptr, nullptr, (uint32_t)n_ions};
     auto k1 =P.clip ? (two ? &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, true, true>
                             : &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, false, true>)
                      : (two ? &ion_pipe_kernel<FMT, MAIN_BLOCK, MAIN_RMAX, MAIN_RC, MAIN_WPE, SRC_RANGES, true>
@@ -4157,7 +4214,7 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
     if (nwg > n_ions) nwg = ((n_ions + XCDS - 1) / XCDS) * XCDS;
     PassTimer tm(SMG_PASS_MAIN, st);
     hipLaunchKernelGGL(k1, dim3((unsigned)nwg), dim3(MAIN_BLOCK), lds_main, st, hits, desc, SA, PM, oc, osp, osc,
-                       omsm, oflags, list_a, hdr + 0);
+                       omsm, oflags, list_a, hdr + 0 SMG_CHK_ARG(ck));
     SMG_LAUNCH_CHECK();
   } else if (big_ok) {
     hipLaunchKernelGGL(list_positions_kernel, dim3((unsigned)((n_ions + 255) / 256)), dim3(256), 0, st, list_a,
@@ -4165,7 +4222,7 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
     SMG_LAUNCH_CHECK();
   }
   if (big_ok) {
-    Sched SB{0, hdr + 1, list_a, hdr + 0};
+    Sched SB{0, hdr + 1, list_a, hdr + 0, (uint32_t)n_ions};
     auto k2 = P.clip ? (two ? &ion_pipe_kernel<FMT, BIG_BLOCK, BIG2_RMAX, BIG_RC, 1, SRC_LIST, true, true>
                             : &ion_pipe_kernel<FMT, BIG_BLOCK, BIG_RMAX, BIG_RC, 1, SRC_LIST, false, true>)
                      : (two ? &ion_pipe_kernel<FMT, BIG_BLOCK, BIG2_RMAX, BIG_RC, 1, SRC_LIST, true>
@@ -4175,7 +4232,7 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
     const int nwg2 = (int)(n_ions < cus ? n_ions : cus);
     PassTimer tm(SMG_PASS_BIG, st);
     hipLaunchKernelGGL(k2, dim3((unsigned)nwg2), dim3(BIG_BLOCK), lds_big, st, hits, desc, SB, PB, oc, osp, osc,
-                       omsm, oflags, list_b, hdr + 2);
+                       omsm, oflags, list_b, hdr + 2 SMG_CHK_ARG(ck));
     SMG_LAUNCH_CHECK();
   } else if (main_ok) {
     hipLaunchKernelGGL(pos_to_ion_kernel, dim3(64), dim3(256), 0, st, desc, list_a, hdr + 0, list_b, hdr + 2);
@@ -4260,6 +4317,33 @@ int smg_debug_wide_check(unsigned long long* host_out) {
   return SMG_OK;
 }
 #endif
+
+int smg_debug_check_points(int64_t n_points) {
+  SMG_CHECK_ARG(n_points >= 0, "negative n_points");
+  g_chk_points = n_points;
+  return SMG_OK;
+}
+
+int smg_debug_check_read(unsigned long long* host_out, int32_t n) {
+#ifdef SMG_CHECK
+  SMG_CHECK_ARG(host_out != nullptr && n >= 0, "bad arguments");
+  unsigned long long z[CHK_N] = {0};
+  if (!g_chk_cnt) {  // no checked launch yet
+    for (int i = 0; i < n && i < CHK_N; ++i) host_out[i] = 0;
+    return SMG_OK;
+  }
+  SMG_HIP(hipDeviceSynchronize());
+  SMG_HIP(hipMemcpy(z, g_chk_cnt, sizeof(z), hipMemcpyDeviceToHost));
+  for (int i = 0; i < n && i < CHK_N; ++i) host_out[i] = z[i];
+  SMG_HIP(hipMemset(g_chk_cnt, 0, sizeof(z)));
+  return SMG_OK;
+#else
+  (void)host_out;
+  (void)n;
+  set_error("library built without -DSMG_CHECK");
+  return SMG_ERR_UNSUPPORTED;
+#endif
+}
 
 int smg_debug_main_kernel(int32_t which) {
   SMG_CHECK_ARG(which == 0 || which == 1, "main kernel must be 0 (ion_pipe_kernel) or 1 (ion_sparse_kernel)");

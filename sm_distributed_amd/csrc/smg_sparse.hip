@@ -238,7 +238,7 @@ template <int LB, int RMAX, int RC, int WPE>
 __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
     Hits<SMG_HITS_PACKED_F32> hits, IonDesc* __restrict__ desc, Sched S, Params P, SpGeo G, double* __restrict__ oc,
     double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags,
-    uint32_t* __restrict__ rej_list, uint32_t* __restrict__ rej_count) {
+    uint32_t* __restrict__ rej_list, uint32_t* __restrict__ rej_count SMG_CHK_PARAM) {
   using H = Hits<SMG_HITS_PACKED_F32>;
   using Reg = uint64_t;
   constexpr int BLOCK = LB;
@@ -303,7 +303,11 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
 #pragma unroll
     for (int j = 0; j < RMAX; ++j) {
       const int i = tid + j * BLOCK;
-      ld8_async_v(hs(j), hits.h + (n0 > 0 ? a + min(i, n0 - 1) : 0));
+      const int64_t idx = n0 > 0 ? a + min(i, n0 - 1) : 0;
+#ifdef SMG_CHECK
+      chk_load(CK, D->ion, 0, idx, n0 <= 0);
+#endif
+      ld8_async_v(hs(j), hits.h + idx);
     }
   };
   // tail chunk c: groups [c*GPC, (c+1)*GPC); slot j of wave w holds group c*GPC + j*NW + w; exactly RC loads
@@ -321,6 +325,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       const int64_t bk = uni64(D->base[k]);
       const int ek = uni(D->end[k]);
       const int64_t idx = Gi < ng ? bk + (int64_t)Gi * 64 + min(lane, ek - Gi * 64 - 1) : 0;
+#ifdef SMG_CHECK
+      chk_load(CK, D->ion, k, idx, Gi >= ng);
+#endif
       ld8_async_v(buf[j], hits.h + idx);
     }
   };
@@ -372,9 +379,20 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
                                  (lane < DESC_QWORDS ? lane : 0));
     bool skip = pos < 0;
     int K = 0, ion = 0, n0 = 0;
+    // a reject beyond the list's capacity (impossible while every position is handed out once) is dropped, never
+    // written past the list
     auto reject = [&]() {
-      if (tid == 0) rej_list[atomicAdd(rej_count, 1u)] = (uint32_t)pos;
+      if (tid == 0) {
+        const uint32_t r = atomicAdd(rej_count, 1u);
+        if (r < S.rej_cap) rej_list[r] = (uint32_t)pos;
+#ifdef SMG_CHECK
+        chk(CK, r < S.rej_cap, CHK_REJ, pos, r);
+#endif
+      }
     };
+#ifdef SMG_CHECK
+    if (!skip && wid == 0) chk_claim(CK, 0, pos);
+#endif
     if (!skip) {
       K = uni(D->K);
       ion = uni(D->ion);
@@ -386,9 +404,17 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         }
         skip = true;
       } else if (!desc_lds_ok(D, CAPC)) {
+#ifdef SMG_CHECK
+        if (tid == 0) chk(CK, reinterpret_cast<const IonRec*>(D)->state == 0u, CHK_STATE, pos, 0);
+#endif
         reject();
         skip = true;
       }
+#ifdef SMG_CHECK
+      else if (wid == 0) {
+        chk_desc(CK, pos, D);
+      }
+#endif
     }
     const bool began = !skip;  // this ion uses the filter and the counters (cleared again at its end)
     SP_STAMP(0);
@@ -702,13 +728,18 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
 #pragma unroll
             for (int kk = 2; kk < MAXK; ++kk) k += (Gi >= gsv[kk]) ? 1 : 0;
             kq[q] = k;
+#ifdef SMG_CHECK
+            if (hasq[q]) chk_load(CK, ion, k, D->base[k] + (int64_t)Gi * 64 + (ent & 63u), false);
+#endif
             hq[q] = hasq[q] ? hits.h[D->base[k] + (int64_t)Gi * 64 + (ent & 63u)] : 0ull;
           }
 #pragma unroll
           for (int q = 0; q < SP_EVB; ++q) {
             const Reg h = hq[q];
             const uint32_t p = H::pix(h);
-            const bool in = hasq[q] && (F[sp_fword(p)] & sp_fmask(p)) != 0u;  // (tested again: not in the entry)
+            // (tested again: not in the entry; a pixel outside the image -- only a caller-supplied hit can carry one --
+            // is no principal pixel and never indexes the directory)
+            const bool in = hasq[q] && p < (uint32_t)P.npx && (F[sp_fword(p)] & sp_fmask(p)) != 0u;
             const int r = in ? sp_lookup(ekey, dir, p, bs) : -1;
             add_x(r >= 0, r, h, kq[q]);
             const bool dq = hasq[q] && H::dup(h);
@@ -778,6 +809,9 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
             ibase = uni64(D->base[ik]);
           }
           const int64_t idx = Gi < ng ? ibase + (int64_t)Gi * 64 + min(lane, iend - Gi * 64 - 1) : 0;
+#ifdef SMG_CHECK
+          chk_load(CK, ion, ik, idx, Gi >= ng);
+#endif
           ld8_async_v(buf[j], hits.h + idx);
         }
         SP_MARK_END(_tr0, 15);
@@ -1304,7 +1338,8 @@ bool sparse_main_fits(const Params& P) {
 
 int launch_sparse_main(Hits<SMG_HITS_PACKED_F32> hits, IonDesc* desc, Sched S, const Params& P, double* oc,
                        double* osp, double* osc, double* omsm, uint32_t* oflags, uint32_t* rej_list,
-                       uint32_t* rej_count, int cus, hipStream_t st) {
+                       uint32_t* rej_count, int cus, hipStream_t st, const ChkCtx& ck) {
+  (void)ck;
   const SpGeo G = sparse_geo(P);
   auto k = &ion_sparse_kernel<SP_BLOCK, SP_RMAX, SP_RC, SP_WPE>;
 
@@ -1312,7 +1347,7 @@ int launch_sparse_main(Hits<SMG_HITS_PACKED_F32> hits, IonDesc* desc, Sched S, c
   int64_t nwg = (int64_t)cus * SP_WGPCU;
   if (nwg > S.n) nwg = ((S.n + XCDS - 1) / XCDS) * XCDS;
   hipLaunchKernelGGL(k, dim3((unsigned)nwg), dim3(SP_BLOCK), 0, st, hits, desc, S, P, G, oc, osp, osc, omsm,
-                     oflags, rej_list, rej_count);
+                     oflags, rej_list, rej_count SMG_CHK_ARG(ck));
   SMG_LAUNCH_CHECK();
   return SMG_OK;
 }

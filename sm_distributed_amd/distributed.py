@@ -297,15 +297,36 @@ def rows_to_frame(table, global_keys):
     return df
 
 
-def score_sharded(plan, peaks, ds_config, group=None, score_local=None):
+def score_sharded(plan, peaks, ds_config, group=None, score_local=None, phases=None):
     """compute_sf_images + sf_image_metrics over all ranks: returns (the reference metrics table on rank 0,
     None elsewhere; this rank's IonImageSet).  ``score_local(plan, peaks, ds_config) -> (rows, images)``
-    replaces the device scorer (tests on CPU ranks)."""
-    import torch.distributed as dist
+    replaces the device scorer (tests on CPU ranks).
+
+    ``phases`` (diagnostics, GPU ranks): a list to which this call appends four timing events recorded on the
+    current stream at its start, after the rows, after the gather and after the assembly -- no synchronisation is
+    added; ``phase_ms`` turns them into the (rows, gather, assembly) split once they have completed."""
+    import torch
+    ev = None
+    if phases is not None and torch.cuda.is_available() and peaks.device.type == "cuda":
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record()
     rows, ims = (score_local or _device_rows)(plan, peaks, ds_config)
+    if ev:
+        ev[1].record()
     table = gather_rows(rows, plan, group)
+    if ev:
+        ev[2].record()
     df = rows_to_frame(table, plan.global_keys) if table is not None else None
+    if ev:
+        ev[3].record()
+        phases.append(ev)
     return df, ims
+
+
+def phase_ms(ev):
+    """(rows, gather, assembly) milliseconds of one score_sharded call's ``phases`` events (waits for them)."""
+    ev[3].synchronize()
+    return tuple(ev[j].elapsed_time(ev[j + 1]) for j in range(3))
 
 
 def search(plan, peaks, formulas, fdr, ds_config, group=None, score_local=None):

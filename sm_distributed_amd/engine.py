@@ -345,6 +345,8 @@ def ion_metrics_raw(hit_format: int, hits: torch.Tensor, hit_vals, hit_cum, lo, 
     check(lib().smg_ion_metrics_workspace_size(n_ions, nrows, ncols, ctypes.byref(sz)),
           "smg_ion_metrics_workspace_size")
     ws = workspace(sz.value, device, "metrics")
+    if _lib.check_build():  # the diagnostic build checks every hit index against the resident count
+        check(lib().smg_debug_check_points(int(hits.numel())), "smg_debug_check_points")
     check(lib().smg_ion_metrics(hit_format, _p(hits), _p(hit_vals), _p(hit_cum), _p(lo), _p(hi), _p(win_off),
                                 _p(theor),
                                 _p(ion_order), n_ions, nrows, ncols, nlevels, float(q), int(bool(do_preprocessing)),

@@ -151,6 +151,30 @@ def test_bands_case_reaches_the_hash_kruskal_and_two_bands():
     sparse = ((m["flags"] & 0x41) == 0x41)
     assert sparse.sum() >= 8
     assert (df.chaos > 0).sum() >= 4  # real structure, not only isolated noise
+    # the image is screened in more than one band: above 2^15 pixels the screen reads band bitmaps of
+    # SpGeo.band_rows rows (smg_sparse.hip sparse_geo: the bitmap space below the survivor lists, 18,624 B, less
+    # two buckets of 2^bs pixels and 128 bits, over ncols, minus 6)
+    nrows, ncols = peaks.nrows, peaks.ncols
+    npx = nrows * ncols
+    assert npx > 1 << 15
+    bs = max((npx - 1).bit_length() - 10, 0)
+    band_rows = (18624 * 8 - 2 * (1 << bs) - 128) // ncols - 6
+    assert 8 <= band_rows < nrows, (band_rows, nrows)
+    # ... and some sparse-pass ion has more than 64 chaos candidates (the block's hash Kruskal, not wave 0's): a
+    # candidate is a pixel of erode_box(dilate_cross(principal presence)) (eL >= 1), border 0
+    from scipy import ndimage
+    from oracle.msm_oracle import BOX, CROSS
+    hits = peaks.hits_sorted.cpu().numpy().view(np.uint64)
+    pix = (hits & np.uint64(0x7FFFFFFF)).astype(np.int64)
+    most = 0
+    for i in np.nonzero(sparse)[0]:
+        w = ions.win_off[i]
+        pres = np.zeros(npx, bool)
+        pres[pix[lo[w]:hi[w]]] = True
+        bw = ndimage.binary_dilation(pres.reshape(nrows, ncols), structure=CROSS, border_value=0)
+        bw = ndimage.binary_erosion(bw, structure=BOX, border_value=0)
+        most = max(most, int(bw.sum()))
+    assert most > 64, most
 
 
 @pytest.mark.parametrize("name", SPARSE_CASES)
