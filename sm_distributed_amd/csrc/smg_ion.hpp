@@ -73,6 +73,21 @@ struct PixVal {
 // The destination is an in/out operand: its previous value counts as used by the next load into it, so
 // a register with a load in flight is never reallocated to another value, even when that load's data end
 // up unused (a refill past the tail, or an ion that is handed to another pass).
+#ifdef SMG_CHECK
+// The check build's extra code spills registers (the compiler cannot know that a register with one of these loads
+// in flight must not be read -- a spill reads it), so there every asynchronous load is a compiler-tracked one and the
+// counted waits are empty: slower, and immune to that hazard, which only scripts/check_async_regs.py rules out in
+// the shipped ISA.
+__device__ __forceinline__ void ld8_async(uint64_t& r, const void* sbase, uint32_t voff) {
+  r = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(sbase) + voff);
+}
+__device__ __forceinline__ void ld8_async_v(uint64_t& r, const void* addr) { r = *reinterpret_cast<const uint64_t*>(addr); }
+__device__ __forceinline__ void ld4_async_v(uint32_t& r, const void* addr) { r = *reinterpret_cast<const uint32_t*>(addr); }
+template <int N>
+__device__ __forceinline__ void vm_wait1(uint64_t&) {}
+template <int N>
+__device__ __forceinline__ void vm_wait1(uint32_t&) {}
+#else
 __device__ __forceinline__ void ld8_async(uint64_t& r, const void* sbase, uint32_t voff) {
   asm volatile("global_load_dwordx2 %0, %1, %2" : "+v"(r) : "v"(voff), "s"(sbase) : "memory");
 }
@@ -92,11 +107,20 @@ __device__ __forceinline__ void vm_wait1(uint32_t& r) {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
   asm volatile("" : "+v"(r));
 }
+#endif
 // Returning atomic add issued like the async loads: the compiler would wait for its result with
 // s_waitcnt vmcnt(0) right away -- i.e. for every prefetch load of the wave in flight -- so it is waited
 // for with a counted vm_wait1 where the ticket is consumed.
 // Tagged "smg:wave0" in the ISA: issued by wave 0 only and waited by wave 0 only (scripts/check_async_regs.py
 // accepts a path that skips its wait only through an exec-zero branch, i.e. in another wave).
+#ifdef SMG_CHECK
+__device__ __forceinline__ void atomic_add_rtn_async(uint32_t& r, uint32_t* addr, uint32_t v) { r = atomicAdd(addr, v); }
+__device__ __forceinline__ void ld8_async_wave0(uint64_t& r, const void* addr) {
+  r = *reinterpret_cast<const uint64_t*>(addr);
+}
+template <int N, int M>
+__device__ __forceinline__ void vm_wait(uint64_t (&)[M]) {}
+#else
 __device__ __forceinline__ void atomic_add_rtn_async(uint32_t& r, uint32_t* addr, uint32_t v) {
   asm volatile("global_atomic_add %0, %1, %2, off sc0 ; smg:wave0" : "+v"(r) : "v"(addr), "v"(v) : "memory");
 }
@@ -110,6 +134,7 @@ __device__ __forceinline__ void vm_wait(uint64_t (&r)[M]) {
 #pragma unroll
   for (int j = 0; j < M; ++j) asm volatile("" : "+v"(r[j]));
 }
+#endif
 template <int N, int M>
 __device__ __forceinline__ void vm_wait(PixVal (&)[M]) {}  // split-format hits use compiler-tracked loads
 

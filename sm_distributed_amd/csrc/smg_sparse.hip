@@ -93,14 +93,32 @@ namespace {
 #define SMG_SP_EVB 1  // rounds of 64 listed tail events resolved together (their points read again together)
 #endif
 constexpr int SP_EVB = SMG_SP_EVB;
-constexpr int SP_BLOCK = 256, SP_RMAX = 10, SP_RC = SMG_SP_RC, SP_WPE = 4, SP_WGPCU = 4;
+// geometry (diagnostic variants override it): principal points per thread, resident workgroups per CU (also the
+// launch bound's waves per SIMD), LDS bytes per workgroup, filter words, side-table entries
+#ifndef SMG_SP_RMAX
+#define SMG_SP_RMAX 10
+#endif
+#ifndef SMG_SP_WGPCU
+#define SMG_SP_WGPCU 4
+#endif
+#ifndef SMG_SP_LDS
+#define SMG_SP_LDS 40448
+#endif
+#ifndef SMG_SP_FWORDS
+#define SMG_SP_FWORDS 1024
+#endif
+#ifndef SMG_SP_SIDE
+#define SMG_SP_SIDE 336
+#endif
+constexpr int SP_BLOCK = 256, SP_RMAX = SMG_SP_RMAX, SP_RC = SMG_SP_RC, SP_WPE = SMG_SP_WGPCU,
+              SP_WGPCU = SMG_SP_WGPCU;
 constexpr int SP_NW = SP_BLOCK / WAVE;
 constexpr int SP_CAPC = SP_BLOCK * SP_RMAX;  // principal points per ion (more: the big-ion pass)
 constexpr int SP_NBMAX = 1024;               // bucket directory entries
-constexpr int SP_FWORDS = 1024;              // Bloom filter: 2^15 bits
+constexpr int SP_FWORDS = SMG_SP_FWORDS;     // Bloom filter: 2^15 bits
 constexpr int SP_DSEG = 64;                  // deferred flagged tail points per wave
 constexpr int SP_DTBL = 256;                 // their (pixel, window)-keyed sums
-constexpr int SP_SIDE = 336;                 // f64 sums of pixels with >= 2 principal points
+constexpr int SP_SIDE = SMG_SP_SIDE;         // f64 sums of pixels with >= 2 principal points
 constexpr int SP_CLW = 2 * WAVE;               // colliding principal points listed per wave
 constexpr int SP_EVCAP = 192;               // tail events listed per wave (resolved when it fills)
 constexpr int SP_CCAP = 768;                 // chaos survivors + candidates
@@ -109,7 +127,7 @@ constexpr int SP_BMAX = 128;                 // points per bucket (more: the big
 constexpr uint32_t SP_HOLE = 0x80000000u;
 constexpr uint32_t SP_SIDEREF = 0xFFF00000u;  // an f32 NaN pattern: the entry's value is side[w & 0xFFFFF]
 constexpr uint32_t SP_EMPTY = 0xFFFFFFFFu;
-constexpr uint32_t SP_LDS_BYTES = 40448;      // 4 x 40,448 B <= 160 KiB: four workgroups per CU
+constexpr uint32_t SP_LDS_BYTES = SMG_SP_LDS;  // 4 x 40,448 B <= 160 KiB: four workgroups per CU
 enum { S_NE = 0, S_EMAX, S_ABORT, S_SIDE, S_NEXT, S_MAXB, S_NCTR = 8 };
 
 constexpr uint32_t c16(uint32_t x) { return (x + 15u) & ~15u; }
@@ -157,7 +175,7 @@ struct SpLay {
                 "collision bits below the chaos lists");
   static_assert(o_hash >= o_F + SP_FWORDS * 4 && o_par + SP_CCAP * 4 <= o_wsurv, "hash + union-find between F and the lists");
   static_assert(o_F + SP_FWORDS * 4 <= o_wsurv && o_cnt + SP_NBMAX * 4 <= o_wsurv, "cleared words below the lists");
-  static_assert(SP_LDS_BYTES % 512 == 0 && 4 * SP_LDS_BYTES <= 160 * 1024, "four workgroups per CU");
+  static_assert(SP_LDS_BYTES % 512 == 0 && SP_WGPCU * SP_LDS_BYTES <= 160 * 1024, "SP_WGPCU workgroups per CU");
   static_assert(SP_NW == 4, "the chaos screen merges four partial survivor lists");
   static_assert(o_clw + SP_NW * SP_CLW * 4 <= o_side, "collision work lists between the collision bits and the side table");
   static_assert(SP_NW * SP_EVCAP * 4 == SP_DTBL * 12 && o_tval == o_tkey + SP_DTBL * 4 && SP_EVCAP % WAVE == 0,

@@ -18,7 +18,12 @@ def pytest_sessionfinish(session, exitstatus):
     mod = sys.modules.get("sm_distributed_amd._lib")
     if mod is None or mod._lib is None or not mod.check_build():
         return
-    c = mod.check_counters()
+    try:
+        c = mod.check_counters()
+    except Exception as e:  # a device fault earlier in the session: report it, keep the test reports
+        print(f"\nSMG_CHECK counters unreadable: {e}")
+        session.exitstatus = 1
+        return
     bad = {k: v for k, v in c.items() if k not in ("positions_claimed", "descriptors_checked") and v}
     line = f"SMG_CHECK counters over the session: {c}"
     print("\n" + line)
