@@ -73,6 +73,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rebalance", action="store_true",
                     help="N > 1: keep the cost model's cut (default: re-cut once from every rank's measured time)")
+    ap.add_argument("--rebalance-rounds", type=int, default=3,
+                    help="N > 1: at most this many re-cuts, until the ranks' measured times agree within 3 %%")
     ap.add_argument("--no-head-cut", action="store_true",
                     help="N > 1: re-cut without rank 0's assembly time (default: rank 0's shard is cut smaller by "
                          "it, since the other ranks start the next search while rank 0 assembles the table)")
@@ -214,18 +216,26 @@ def main():
     if sharded:
         plan = D.plan_shards(formulas, peaks, args.ppm, world, rank)
         if not args.no_rebalance:
-            # the cut re-made from every rank's measured shard time (one all_gather of N floats): the cost model's
-            # per-rank residuals would otherwise set the slowest rank's time
-            t_rank = _rank_seconds(D, plan, peaks, ds_config)
-            t_head = 0.0 if args.no_head_cut else _assembly_seconds(D, plan, peaks, ds_config)
-            tt = torch.tensor([t_rank, t_head], dtype=torch.float64, device=device)
-            ts = [torch.zeros_like(tt) for _ in range(world)]
-            dist.all_gather(ts, tt)
-            times = [float(x[0].item()) for x in ts]
-            head = float(ts[0][1].item())  # rank 0's
-            plan = D.rebalance(plan, formulas, peaks, times, head_seconds=head)
-            log(f"[rank {rank}] rebalanced from measured shard times (ms) {[round(x * 1e3, 2) for x in times]}, "
-                f"rank-0 assembly {head * 1e3:.2f} ms: counts {plan.counts}")
+            # the cut re-made from every rank's measured shard time (one all_gather of 2 floats per rank): the cost
+            # model's per-rank residuals would otherwise set the slowest rank's time.  Re-cut until the ranks (rank
+            # 0 with its assembly) agree within 3 %, at most --rebalance-rounds times
+            for it in range(args.rebalance_rounds):
+                t_rank = _rank_seconds(D, plan, peaks, ds_config)
+                t_head = 0.0 if args.no_head_cut else _assembly_seconds(D, plan, peaks, ds_config)
+                tt = torch.tensor([t_rank, t_head], dtype=torch.float64, device=device)
+                ts = [torch.zeros_like(tt) for _ in range(world)]
+                dist.all_gather(ts, tt)
+                times = [float(x[0].item()) for x in ts]
+                head = float(ts[0][1].item())  # rank 0's
+                loads = [times[0] + head] + times[1:]
+                spread = max(loads) / min(loads) - 1.0
+                if spread <= 0.03:
+                    log(f"[rank {rank}] shard times (ms) {[round(x * 1e3, 2) for x in times]}, rank-0 assembly "
+                        f"{head * 1e3:.2f} ms: within {spread * 100:.1f} %, cut kept after {it} re-cuts")
+                    break
+                plan = D.rebalance(plan, formulas, peaks, times, head_seconds=head)
+                log(f"[rank {rank}] re-cut {it + 1} from measured shard times (ms) {[round(x * 1e3, 2) for x in times]}"
+                    f" (spread {spread * 100:.1f} %), rank-0 assembly {head * 1e3:.2f} ms: counts {plan.counts}")
         # per step: timing events of this rank's rows, gather (its wait for the slowest rank included) and assembly,
         # recorded by score_sharded itself on the stream (no synchronisation added), read after the timed steps
         phases = []

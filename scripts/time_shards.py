@@ -146,9 +146,16 @@ D.rows_to_frame(table, plans[0].global_keys)
 t_head, _ = timed(lambda: D.rows_to_frame(table, plans[0].global_keys))
 NO_HEAD = bool(os.environ.get("NO_HEAD"))
 print(f"rank-0 assembly of the cost-model table {t_head:.2f} ms (head cut {'off' if NO_HEAD else 'on'})", flush=True)
-plans = [D.rebalance(p, formulas, peaks, times, head_seconds=0.0 if NO_HEAD else t_head * 1e-3) for p in plans]
-print("rebalanced counts", plans[0].counts, flush=True)
-rows_all, worst, times = run_ranks(plans, "rebalanced")
+# re-cut until the ranks (rank 0 with its assembly) agree within 3 %, at most ROUNDS times (bench.py does the same)
+for it in range(int(os.environ.get("ROUNDS", "3"))):
+    loads = [times[0] + (0.0 if NO_HEAD else t_head * 1e-3)] + times[1:]
+    spread = max(loads) / min(loads) - 1.0
+    print(f"re-cut round {it}: spread {spread * 100:.1f} %", flush=True)
+    if spread <= 0.03:
+        break
+    plans = [D.rebalance(p, formulas, peaks, times, head_seconds=0.0 if NO_HEAD else t_head * 1e-3) for p in plans]
+    print("rebalanced counts", plans[0].counts, flush=True)
+    rows_all, worst, times = run_ranks(plans, f"rebalanced {it + 1}")
 print(f"max rank: cost model {worst0:.2f} ms, rebalanced {worst:.2f} ms", flush=True)
 table, n_max = table_of(rows_all)
 plan0 = plans[0]

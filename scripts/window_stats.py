@@ -42,3 +42,7 @@ show("principal points", n0, [1536, 2048, 2304, 2560])
 show("principal flagged points", f0, [64, 128, 168, 336])
 show("tail points", ntail, [2048, 4096, 8192])
 show("tail flagged points (4 waves' deferred lists)", ftail, [64, 128, 192, 256])
+ch = m.chaos.cpu().numpy()
+fl = m.flags.cpu().numpy()
+print(f"ions with chaos != 0 (some chaos candidate): {(ch[sparse] != 0).mean() * 100:.2f}% of the sparse-pass ions; "
+      f"chaos NaN flag: {((fl[sparse] & 4) != 0).mean() * 100:.2f}%")

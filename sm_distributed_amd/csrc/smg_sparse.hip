@@ -89,6 +89,13 @@ namespace {
 #ifndef SMG_SP_ABL
 #define SMG_SP_ABL 0
 #endif
+// The points that may share a pixel with another point of the principal window: 1 (round 6) its duplicate-candidate
+// points (the hit's flag: every pair of points of one pixel inside a window carries it; ~1.2% of the points at config
+// 3, against ~5% whose filter bit was set twice), 0 the filter's collision bits (round 5; A/B: 27.15 vs 26.46 ms for
+// the ion stage at config 3, profiles/round6/r6var1_variants.txt)
+#ifndef SMG_SP_DUPCOLL
+#define SMG_SP_DUPCOLL 1
+#endif
 #ifndef SMG_SP_EVB
 #define SMG_SP_EVB 1  // rounds of 64 listed tail events resolved together (their points read again together)
 #endif
@@ -359,7 +366,8 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
     uint4* zl = reinterpret_cast<uint4*>(coll);
     for (int i = t0; i < SP_FWORDS / 4; i += nt) zf[i] = make_uint4(0, 0, 0, 0);
     for (int i = t0; i < SP_NBMAX / 4; i += nt) zc[i] = make_uint4(0, 0, 0, 0);
-    for (int i = t0; i < SP_FWORDS / 4; i += nt) zl[i] = make_uint4(0, 0, 0, 0);
+    if (!SMG_SP_DUPCOLL)
+      for (int i = t0; i < SP_FWORDS / 4; i += nt) zl[i] = make_uint4(0, 0, 0, 0);
     if (t0 < S_NCTR && t0 != S_NEXT) ctr[t0] = 0;
   };
   // the dup table (keys all ones, values zero), cleared by each wave over the words of its own tail-event list (the
@@ -475,7 +483,8 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
             bad = true;
           } else {
             // a filter bit set twice: the two points may share a pixel (only those scan their bucket below)
-            if (atomicOr(&F[sp_fword(p)], sp_fmask(p)) & sp_fmask(p)) atomicOr(&coll[sp_fword(p)], sp_fmask(p));
+            if (SMG_SP_DUPCOLL) atomicOr(&F[sp_fword(p)], sp_fmask(p));
+            else if (atomicOr(&F[sp_fword(p)], sp_fmask(p)) & sp_fmask(p)) atomicOr(&coll[sp_fword(p)], sp_fmask(p));
             aw_set(j, atomicAdd(&cnt[p >> bs], 1u));
           }
         }
@@ -610,7 +619,8 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         bool col = false;
         if (i < n0) {
           const uint32_t p = H::pix(hs(j));
-          col = !(SMG_SP_ABL & 128) && (coll[sp_fword(p)] & sp_fmask(p)) != 0u;
+          col = !(SMG_SP_ABL & 128) &&
+                (SMG_SP_DUPCOLL ? H::dup(hs(j)) : (coll[sp_fword(p)] & sp_fmask(p)) != 0u);
           if (!col) stat((double)__uint_as_float((uint32_t)(hs(j) >> 32)));  // (no other point has its pixel)
         }
         const uint64_t m = __ballot(col);

@@ -55,6 +55,7 @@ class ShardPlan:
     bounds: list                   # [(first, last) principal-order positions] per rank
     global_keys: object            # IonKeys of the whole table (rank 0 builds the DataFrame from codes)
     est_cost: list = field(default_factory=list)  # estimated seconds per rank
+    costs: np.ndarray = None       # per-ion seconds in principal order that made this cut (rebalance scales them)
     _sf_peak_df: object = None
     _glob: object = None           # (shard ion keys, device f64 global index of each): reused while they match
 
@@ -141,8 +142,14 @@ def rebalance(plan, formulas, peaks_or_mz, rank_seconds, bins=8192, head_seconds
     ``head_seconds``: rank 0's assembly of the gathered table (rows_to_frame), which the other ranks do not wait
     for -- they return after the gather and start the next search -- so rank 0's shard is cut that much smaller
     (shard_bounds' head) and every rank reaches the next gather together.
-    Deterministic: every rank computes the same cut from the same times.  Returns this rank's new ShardPlan."""
+    Deterministic: every rank computes the same cut from the same times.  Returns this rank's new ShardPlan.
+
+    Repeated calls refine the cut: the costs of a rebalanced plan (``plan.costs``) are scaled again, so each
+    call multiplies every ion's cost by its current rank's measured/estimated ratio (bench.py re-cuts until the
+    ranks' times agree within a few per cent)."""
     order, cost = _principal_costs(formulas, peaks_or_mz, plan.ppm, bins)
+    if plan.costs is not None and len(plan.costs) == len(cost):
+        cost = plan.costs
     t = np.asarray(rank_seconds, dtype=np.float64)
     if len(t) != plan.world or not np.all(np.isfinite(t)) or not np.all(t > 0):
         raise ValueError("rank_seconds: one positive time per rank")
@@ -171,7 +178,8 @@ def _plan_from_costs(formulas, order, cost, ppm, world, rank, head=0.0):
     keys = formulas.ion_sf.astype(np.int64) * max(len(formulas.adducts), 1) + formulas.ion_adduct_code
     return ShardPlan(rank=rank, world=world, ion_idx=mine, formulas=shard, mz_lo=mz_lo, mz_hi=mz_hi, ppm=ppm,
                      counts=[int(y - x) for x, y in bounds], bounds=bounds,
-                     global_keys=IonKeys(keys, formulas.adducts), est_cost=[float(cost[x:y].sum()) for x, y in bounds])
+                     global_keys=IonKeys(keys, formulas.adducts), est_cost=[float(cost[x:y].sum()) for x, y in bounds],
+                     costs=np.asarray(cost, dtype=np.float64))
 
 
 def slice_peaks(peaks, plan, cache=True):

@@ -270,6 +270,44 @@ def device_layout(sf_peak_df: pd.DataFrame, device, stream=None):
     return IonKeys(keys, cats, sf_levels, keys_dev=uniq, codes=codes, codes_dev=codes_dev), ions, K
 
 
+# The ion layout of an sf_peak_df is a function of its four columns only, and a search per dataset runs over the same
+# formula table (the reference keeps it in Postgres, formulas_segm.py:14-33): the last few layouts are kept, addressed
+# by a hash of the columns' contents (not by object identity), so an edited or new table always gets its own layout.
+_LAYOUT_CACHE = {}
+_LAYOUT_KEEP = 4
+
+
+def _layout_key(sf_peak_df, device):
+    """xxh3-128 of the sf_id / peak_i / mz columns and the adduct column's categories + codes (None -- no caching --
+    for a non-Categorical adduct column or non-integer sf ids: those take the slow path anyway).  ~1 ms per 1M rows,
+    on the host while the device sorts."""
+    import xxhash
+    adduct = sf_peak_df["adduct"]
+    sf = sf_peak_df["sf_id"].to_numpy()
+    if not isinstance(adduct.dtype, pd.CategoricalDtype) or sf.dtype.kind not in "iu":
+        return None
+    h = xxhash.xxh3_128()
+    for a in (sf, sf_peak_df["peak_i"].to_numpy(), sf_peak_df["mz"].to_numpy(), adduct.cat.codes.to_numpy()):
+        a = np.ascontiguousarray(a)
+        h.update(f"{a.dtype.str}{a.shape}".encode())
+        h.update(a.view(np.uint8).reshape(-1) if a.size else b"")
+    h.update("\x00".join(str(c) for c in adduct.cat.categories).encode())
+    return (h.hexdigest(), str(device))
+
+
+def cached_device_layout(sf_peak_df, device, stream=None):
+    """device_layout(sf_peak_df, device, stream), reused while a table with the same contents comes again."""
+    key = _layout_key(sf_peak_df, device)
+    if key is not None and key in _LAYOUT_CACHE:
+        return _LAYOUT_CACHE[key]
+    out = device_layout(sf_peak_df, device, stream)
+    if key is not None:
+        while len(_LAYOUT_CACHE) >= _LAYOUT_KEEP:
+            _LAYOUT_CACHE.pop(next(iter(_LAYOUT_CACHE)))
+        _LAYOUT_CACHE[key] = out
+    return out
+
+
 METRIC_COLUMNS = ["chaos", "spatial", "spectral", "msm"]
 
 
@@ -657,8 +695,9 @@ def compute_sf_images(sc, ds, sf_peak_df, ppm):
     """formula_imager_segm.py:142-161.  ``sc`` is accepted for signature compatibility and ignored.
 
     Device order: the resident peaks are flagged and sorted on the current stream while the ion layout is
-    uploaded and built on a side stream; the window search follows both on the side stream, beside the prefix
-    sums on the current one (a latency-bound search beside a bandwidth-bound read); the current stream joins."""
+    uploaded and built on a side stream (or taken from the layout cache when the same table comes again:
+    ``cached_device_layout``); the window search follows both on the side stream, beside the prefix sums on the
+    current one (a latency-bound search beside a bandwidth-bound read); the current stream joins."""
     import torch
 
     from .dataset import spectra_from_duck
@@ -674,7 +713,7 @@ def compute_sf_images(sc, ds, sf_peak_df, ppm):
     side = _side_stream(peaks.device) if os.environ.get("SMG_LAYOUT_SIDE", "1") != "0" else main
     side.wait_stream(main)  # the side stream may reuse memory the main stream released
     peaks.flag_and_sort(ppm)
-    keys, dions, K = device_layout(sf_peak_df, peaks.device, side)
+    keys, dions, K = cached_device_layout(sf_peak_df, peaks.device, side)
     # the window search on the side stream after the sort; lo / hi are allocated on the main stream (the side
     # stream waits for everything queued on it so far, so memory the main stream released is free)
     side.wait_stream(main)

@@ -122,7 +122,7 @@ def _theor_arrays(ims, sf_ints, device):
         # (a search per step over the same formula table), without its synchronisations
         last = cache.get(("last",) + sig)
         if (last is not None and last[4] is ik.sf_levels and len(last[0]) == n
-                and np.array_equal(last[0], ik.keys)):
+                and (last[5] is ik.keys or np.array_equal(last[0], ik.keys))):
             return last[1], last[2], last[3]
         n_pk = len(sf_ints.sf_ids)
         if (sig not in cache and ik.sf_levels is None and n_pk == n and n > 0 and
@@ -135,7 +135,7 @@ def _theor_arrays(ims, sf_ints, device):
                 vals = torch.from_numpy(np.ascontiguousarray(sf_ints.values, np.float64)).to(device)
                 out = (off_t[1:] - off_t[:-1], vals, off_t)
                 cache.clear()
-                cache[("last",) + sig] = (np.array(ik.keys, copy=True),) + out + (ik.sf_levels,)
+                cache[("last",) + sig] = (np.array(ik.keys, copy=True),) + out + (ik.sf_levels, ik.keys)
                 return out
         if sig not in cache:
             k, ok = ik.encode_codes(sf_ints.sf_ids, sf_ints.adduct_codes, sf_ints.adducts)
@@ -168,7 +168,7 @@ def _theor_arrays(ims, sf_ints, device):
         k_in = torch.arange(n_t, device=device) - off_t[owner]
         out = (Kt, pk_val[pk_off[row][owner] + k_in], off_t)
         cache.pop(("last",) + sig, None)
-        cache[("last",) + sig] = (np.array(ik.keys, copy=True),) + out + (ik.sf_levels,)
+        cache[("last",) + sig] = (np.array(ik.keys, copy=True),) + out + (ik.sf_levels, ik.keys)
         return out
     vals = [sf_ints[k] for k in ims.keys]
     Kt = np.array([len(v) for v in vals], dtype=np.int64)

@@ -151,3 +151,30 @@ def test_theor_alignment_identity_fast_path_matches_generic():
         np.testing.assert_array_equal(Kt.numpy(), [len(e) for e in exp])
         np.testing.assert_array_equal(vals.numpy(), np.concatenate(exp))
         np.testing.assert_array_equal(off.numpy(), np.concatenate([[0], np.cumsum([len(e) for e in exp])]))
+
+
+def test_layout_cache_is_content_addressed():
+    """cached_device_layout: a table with the same contents (another object, e.g. a copy) gets the cached layout; an
+    edited table (even in place, same object and buffers) or another adduct category order gets its own; a table with
+    a non-Categorical adduct column is never cached."""
+    from sm_distributed_amd import formula_imager_segm as FIS
+    from sm_distributed_amd.formulas import FormulasSegm
+    FIS._LAYOUT_CACHE.clear()
+    ions = syn.make_ion_table(200, seed=5, decoy_seed=6)
+    df = FormulasSegm.from_ion_table(ions, 2.0).get_sf_peak_df()
+    a = FIS.cached_device_layout(df, "cpu")
+    assert FIS.cached_device_layout(df.copy(), "cpu") is a
+    edited = df.copy()
+    mz = edited["mz"].to_numpy()
+    mz[5] += 1e-9  # in place: same object, same buffer, other contents
+    b = FIS.cached_device_layout(edited, "cpu")
+    assert b is not a and not np.array_equal(a[1].peak_mz.numpy(), b[1].peak_mz.numpy())
+    renamed = df.copy()
+    renamed["adduct"] = renamed["adduct"].cat.rename_categories(lambda c: c + "x")
+    assert FIS.cached_device_layout(renamed, "cpu") is not a
+    plain = df.copy()
+    plain["adduct"] = plain["adduct"].astype(object)
+    assert FIS._layout_key(plain, "cpu") is None
+    c = FIS.cached_device_layout(plain, "cpu")
+    assert np.array_equal(c[0].keys, a[0].keys) and c is not FIS.cached_device_layout(plain, "cpu")
+    assert len(FIS._LAYOUT_CACHE) <= FIS._LAYOUT_KEEP
