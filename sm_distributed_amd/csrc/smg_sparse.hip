@@ -19,16 +19,17 @@
 //  * values: f32 per entry (the packed hits carry f32 intensities, so a single point's value is exact); a pixel
 //    with several points keeps its f64 sum -- summed in window order, as coo.toarray() adds them -- in a side table
 //    its entry points to;
-//  * a direct-mapped filter F (bit p mod 2^15 for principal pixel p, 4 KB) answers the tail stream's membership test
-//    with one LDS read; its positives (~4% false at 500x500 px) are resolved exactly after the stream, as
+//  * a direct-mapped filter F (bit p mod 2^16 for principal pixel p, 8 KB) answers the tail stream's membership test
+//    with one LDS read; its positives (~2% false at 500x500 px) are resolved exactly after the stream, as
 //    ion_pipe_kernel resolves its parked principal hits;
-//  * chaos: the level index per entry (u8); the 7x7 screen's sparsity pre-filter reads its rows from F (a superset
-//    of the principal image whose row segments are runs of bits), the few survivors' rows come exactly from the
-//    directory; candidates' exact eL and the Kruskal pass look pixels up in the directory / a candidate hash, never
-//    in an image-sized array.
+//  * chaos: the level index per entry (u8); the 7x7 screen reads presence rows from F where F is exact (images up to
+//    2^16 pixels), else from band bitmaps of image rows rebuilt in the LDS; candidates' exact eL and the Kruskal pass
+//    look pixels up in the directory / a candidate hash, never in an image-sized array.
 // Everything else (software pipeline with counted waits, the tail stream of window-aligned 64-point groups with
 // parked events, the flagged-point lists and table, the threshold-decomposition chaos, the record for
 // ion_finalize_kernel) is ion_pipe_kernel's.
+#include <type_traits>
+
 #include "smg_common.hpp"
 #include "smg_ion.hpp"
 
@@ -108,21 +109,32 @@ constexpr int SP_EVB = SMG_SP_EVB;
 #ifndef SMG_SP_WGPCU
 #define SMG_SP_WGPCU 4
 #endif
+// round 6: a 2^16-bit filter (half the tail stream's false positives; ion stage 26.46 -> 25.97 ms at config 3,
+// profiles/round6/r6var3_variants.txt), paid for by a 48-entry side table (the principal windows of config 3 have at most
+// 38 pixels with two or more points), f32 deferred values and the whole 40 KiB of LDS a workgroup can have at four per CU
 #ifndef SMG_SP_LDS
-#define SMG_SP_LDS 40448
+#define SMG_SP_LDS 40960
 #endif
 #ifndef SMG_SP_FWORDS
-#define SMG_SP_FWORDS 1024
+#define SMG_SP_FWORDS 2048
+#endif
+#ifndef SMG_SP_HASH_AT_F
+#define SMG_SP_HASH_AT_F 1
 #endif
 #ifndef SMG_SP_SIDE
-#define SMG_SP_SIDE 336
+#define SMG_SP_SIDE 48
 #endif
+// deferred flagged tail points' values as f32 (exact: packed hits carry f32 intensities) instead of f64
+#ifndef SMG_SP_DV32
+#define SMG_SP_DV32 1
+#endif
+using SpDv = std::conditional_t<SMG_SP_DV32 != 0, float, double>;
 constexpr int SP_BLOCK = 256, SP_RMAX = SMG_SP_RMAX, SP_RC = SMG_SP_RC, SP_WPE = SMG_SP_WGPCU,
               SP_WGPCU = SMG_SP_WGPCU;
 constexpr int SP_NW = SP_BLOCK / WAVE;
 constexpr int SP_CAPC = SP_BLOCK * SP_RMAX;  // principal points per ion (more: the big-ion pass)
 constexpr int SP_NBMAX = 1024;               // bucket directory entries
-constexpr int SP_FWORDS = SMG_SP_FWORDS;     // Bloom filter: 2^15 bits
+constexpr int SP_FWORDS = SMG_SP_FWORDS;     // Bloom filter: 2^16 bits
 constexpr int SP_DSEG = 64;                  // deferred flagged tail points per wave
 constexpr int SP_DTBL = 256;                 // their (pixel, window)-keyed sums
 constexpr int SP_SIDE = SMG_SP_SIDE;         // f64 sums of pixels with >= 2 principal points
@@ -134,7 +146,7 @@ constexpr int SP_BMAX = 128;                 // points per bucket (more: the big
 constexpr uint32_t SP_HOLE = 0x80000000u;
 constexpr uint32_t SP_SIDEREF = 0xFFF00000u;  // an f32 NaN pattern: the entry's value is side[w & 0xFFFFF]
 constexpr uint32_t SP_EMPTY = 0xFFFFFFFFu;
-constexpr uint32_t SP_LDS_BYTES = SMG_SP_LDS;  // 4 x 40,448 B <= 160 KiB: four workgroups per CU
+constexpr uint32_t SP_LDS_BYTES = SMG_SP_LDS;  // 4 x 40,960 B = 160 KiB: four workgroups per CU
 enum { S_NE = 0, S_EMAX, S_ABORT, S_SIDE, S_NEXT, S_MAXB, S_NCTR = 8 };
 
 constexpr uint32_t c16(uint32_t x) { return (x + 15u) & ~15u; }
@@ -161,26 +173,30 @@ struct SpLay {
   static constexpr uint32_t o_dkey = c16(o_evals + SP_CAPC * 4);
   static constexpr uint32_t o_coll = o_dkey;  // filter collisions: build only (the tail's lists are written after)
   static constexpr uint32_t o_dval = c16(o_dkey + SP_NW * SP_DSEG * 4);
-  static constexpr uint32_t o_dcnt = c16(o_dval + SP_NW * SP_DSEG * 8);
+  static constexpr uint32_t o_dcnt = c16(o_dval + SP_NW * SP_DSEG * sizeof(SpDv));
   static constexpr uint32_t o_tkey = c16(o_dcnt + SP_NW * 4);
   static constexpr uint32_t o_tval = c16(o_tkey + SP_DTBL * 4);
   static constexpr uint32_t o_side = c16(o_tval + SP_DTBL * 8);  // read until the levels are computed
   static constexpr uint32_t o_tend = c16(o_side + SP_SIDE * 8);
-  static constexpr uint32_t o_clw = c16(o_coll + SP_FWORDS * 4);  // colliding points' work lists (entries phase)
+  // colliding points' work lists (entries phase): behind the collision bits, or at their place without them
+  static constexpr uint32_t o_clw = SMG_SP_DUPCOLL ? o_dkey : c16(o_coll + SP_FWORDS * 4);
   // chaos view
   static constexpr uint32_t o_cel = SP_LDS_BYTES - SP_CCAP;
   static constexpr uint32_t o_clist = o_cel - SP_CCAP * 4;
   static constexpr uint32_t o_wsurv = o_clist - SP_NW * WAVE * 4;  // per-wave survivor lists (chaos screen)
-  static constexpr uint32_t o_band = o_U;                          // band bitmaps (images above 2^15 pixels)
+  static constexpr uint32_t o_band = o_U;                          // band bitmaps (images above 2^16 pixels)
   static constexpr int band_bits = (int)(o_wsurv - o_band) * 8;
   static_assert(o_band % 16 == 0, "band bitmaps are zeroed as uint4");
-  static constexpr uint32_t o_hash = o_evals;  // (the filter F stays intact for the chaos pre-filter)
+  // the Kruskal's candidate hash: after the screen (which reads F for images up to SP_FWORDS * 32 pixels), so it may
+  // start at F (SMG_SP_HASH_AT_F) or behind it
+  static constexpr uint32_t o_hash = SMG_SP_HASH_AT_F ? o_F : o_evals;
   static constexpr uint32_t o_par = o_hash + SP_HSZ * 4;
   static_assert(o_tend <= SP_LDS_BYTES, "principal / tail view fits");
   static_assert(o_cnt + SP_NBMAX * 4 <= o_dkey, "bucket counters inside the values' space");
-  static_assert(o_coll + SP_FWORDS * 4 <= o_tval + 8 * 8 && o_coll + SP_FWORDS * 4 <= SP_LDS_BYTES - SP_CCAP * 5 - SP_NW * WAVE * 4,
+  static_assert(SMG_SP_DUPCOLL || (o_coll + SP_FWORDS * 4 <= o_tval + 8 * 8 &&
+                                   o_coll + SP_FWORDS * 4 <= SP_LDS_BYTES - SP_CCAP * 5 - SP_NW * WAVE * 4),
                 "collision bits below the chaos lists");
-  static_assert(o_hash >= o_F + SP_FWORDS * 4 && o_par + SP_CCAP * 4 <= o_wsurv, "hash + union-find between F and the lists");
+  static_assert(o_hash >= o_F && o_par + SP_CCAP * 4 <= o_wsurv, "hash + union-find below the lists");
   static_assert(o_F + SP_FWORDS * 4 <= o_wsurv && o_cnt + SP_NBMAX * 4 <= o_wsurv, "cleared words below the lists");
   static_assert(SP_LDS_BYTES % 512 == 0 && SP_WGPCU * SP_LDS_BYTES <= 160 * 1024, "SP_WGPCU workgroups per CU");
   static_assert(SP_NW == 4, "the chaos screen merges four partial survivor lists");
@@ -192,7 +208,7 @@ struct SpLay {
 
 struct SpGeo {
   int32_t bs;         // bucket = pixel >> bs
-  int32_t band_rows;  // image rows screened per chaos band (images above 2^15 pixels)
+  int32_t band_rows;  // image rows screened per chaos band (images above 2^16 pixels)
 };
 
 // the number of lanes below this one whose bit is set in the wave mask m (v_mbcnt)
@@ -200,7 +216,7 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// the filter F: bit p mod 2^15 for every principal pixel p (direct-mapped: a row segment of pixels is a run of bits, so
+// the filter F: bit p mod 2^16 for every principal pixel p (direct-mapped: a row segment of pixels is a run of bits, so
 // the chaos pre-filter reads it too)
 __device__ __forceinline__ uint32_t sp_fword(uint32_t p) { return (p >> 5) & (uint32_t)(SP_FWORDS - 1); }
 __device__ __forceinline__ uint32_t sp_fmask(uint32_t p) { return 1u << (p & 31u); }
@@ -292,7 +308,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
   uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + LY::o_cnt);
   uint32_t* coll = reinterpret_cast<uint32_t*>(smem + LY::o_coll);
   uint32_t* dkey = reinterpret_cast<uint32_t*>(smem + LY::o_dkey);
-  double* dval = reinterpret_cast<double*>(smem + LY::o_dval);
+  SpDv* dval = reinterpret_cast<SpDv*>(smem + LY::o_dval);
   int* dcnt = reinterpret_cast<int*>(smem + LY::o_dcnt);
   uint32_t* tkey = reinterpret_cast<uint32_t*>(smem + LY::o_tkey);
   double* tval = reinterpret_cast<double*>(smem + LY::o_tval);
@@ -711,7 +727,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
       int curk = 1;
       int nd = 0;  // this wave's deferred flagged points (uniform)
       uint32_t* wdkey = dkey + wid * SP_DSEG;
-      double* wdval = dval + wid * SP_DSEG;
+      SpDv* wdval = dval + wid * SP_DSEG;
       int gnext = uni(D->gs[2]);
       int wend = uni(D->end[1]);
       // Events: a filter positive (the point's pixel may be principal: Σxy, Σy[x>0]) or a flagged point (summed per
@@ -776,7 +792,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
               const int e = nd + (int)lanes_below(mq);
               if (dq && e < SP_DSEG) {
                 wdkey[e] = (p << 3) | (uint32_t)kq[q];
-                wdval[e] = H::val(h);
+                wdval[e] = (SpDv)H::val(h);
               }
               nd += (int)__popcll(mq);
             }
@@ -905,7 +921,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
         reject();
         skip = true;
       } else if (nd_tot > 0) {
-        if ((tid % SP_DSEG) < dcnt[tid / SP_DSEG] && !tbl_add<SP_DTBL>(tkey, tval, dkey[tid], dval[tid]))
+        if ((tid % SP_DSEG) < dcnt[tid / SP_DSEG] && !tbl_add<SP_DTBL>(tkey, tval, dkey[tid], (double)dval[tid]))
           ctr[S_ABORT] = 1;
         __syncthreads();
         if (ctr[S_ABORT]) {
@@ -930,7 +946,7 @@ __global__ void __launch_bounds__(LB, WPE) ion_sparse_kernel(
     uint32_t flags = 0;
     if (!skip && chaos_ok) {
       SP_STAMP(7);
-      // (i) the 7x7 screen over presence bitmaps: the filter F itself where it is exact (images up to 2^15 pixels: bit
+      // (i) the 7x7 screen over presence bitmaps: the filter F itself where it is exact (images up to 2^16 pixels: bit
       //     p for pixel p), else band bitmaps of image rows rebuilt in the LDS the values and the flagged-point lists
       //     leave behind (two bands at 500x500 px): the band's words zeroed, then a bit set per entry.  Pass A: a
       //     principal pixel with fewer than three principal pixels in its 7x7 (itself included) cannot own a

@@ -151,14 +151,14 @@ def test_bands_case_reaches_the_hash_kruskal_and_two_bands():
     sparse = ((m["flags"] & 0x41) == 0x41)
     assert sparse.sum() >= 8
     assert (df.chaos > 0).sum() >= 4  # real structure, not only isolated noise
-    # the image is screened in more than one band: above 2^15 pixels the screen reads band bitmaps of
-    # SpGeo.band_rows rows (smg_sparse.hip sparse_geo: the bitmap space below the survivor lists, 18,624 B, less
+    # the image is screened in more than one band: above 2^16 pixels the screen reads band bitmaps of
+    # SpGeo.band_rows rows (smg_sparse.hip sparse_geo: the bitmap space below the survivor lists, 19,136 B, less
     # two buckets of 2^bs pixels and 128 bits, over ncols, minus 6)
     nrows, ncols = peaks.nrows, peaks.ncols
     npx = nrows * ncols
-    assert npx > 1 << 15
+    assert npx > 1 << 16  # (images up to 2^16 pixels screen from the filter itself)
     bs = max((npx - 1).bit_length() - 10, 0)
-    band_rows = (18624 * 8 - 2 * (1 << bs) - 128) // ncols - 6
+    band_rows = (19136 * 8 - 2 * (1 << bs) - 128) // ncols - 6
     assert 8 <= band_rows < nrows, (band_rows, nrows)
     # ... and some sparse-pass ion has more than 64 chaos candidates (the block's hash Kruskal, not wave 0's): a
     # candidate is a pixel of erode_box(dilate_cross(principal presence)) (eL >= 1), border 0
