@@ -124,6 +124,11 @@ constexpr int SP_EVB = SMG_SP_EVB;
 #ifndef SMG_SP_SIDE
 #define SMG_SP_SIDE 48
 #endif
+// the level index's f32 test: 1 (round 6) a margin of (n-1) * 1e-6 and the top interval included, 0 a margin of 1e-3
+// with the top interval sent to the f64 test (the lanes of a wave with an entry in the top interval all waited for it)
+#ifndef SMG_SP_LVM
+#define SMG_SP_LVM 0
+#endif
 // deferred flagged tail points' values as f32 (exact: packed hits carry f32 intensities) instead of f64
 #ifndef SMG_SP_DV32
 #define SMG_SP_DV32 1
@@ -260,11 +265,19 @@ __device__ __forceinline__ int sp_level(double v, double vmax, double rcp, const
   const int n = P.nlevels;
   if (!(v > 0.0)) return 0;  // (vmax > 0 whenever levels are needed)
   if (n == 1) return 1;
-  if (n <= 2048) {  // f32 first: x = v/vmax (n-1) to ~2.4e-7 relative (<= 5e-4 absolute here); away from an integer
-                    // by 1e-3 and below the top level it decides alone
+  if (n <= 2048) {  // f32 first: x = v/vmax (n-1) to ~2.4e-7 relative, i.e. (n-1) * 2.4e-7 absolute; farther than
+                    // SMG_SP_LVM = (n-1) * 1e-6 from an integer and from n-1 itself (the top interval (n-2, n-1) is
+                    // the count n-1 like any other) it decides alone
+#if SMG_SP_LVM
+    const float xf = (float)v * (float)rcp * (float)(n - 1);
+    const float jf = floorf(xf), fr = xf - jf;
+    const float mg = (float)(n - 1) * 1e-6f;
+    if (fr > mg && fr < 1.0f - mg && xf < (float)(n - 1) - mg) return (int)jf + 1;
+#else
     const float xf = (float)v * (float)rcp * (float)(n - 1);
     const float jf = floorf(xf), fr = xf - jf;
     if (fr > 1e-3f && fr < 1.0f - 1e-3f && xf < (float)(n - 1) - 1.0f) return (int)jf + 1;
+#endif
   }
   const double na = v * rcp;
   const double tol = na * 1e-15;
