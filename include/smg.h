@@ -208,6 +208,10 @@ int smg_debug_sort_impl(int32_t which);
  * to 2^18 pixels), 0 = ion_pipe_kernel<512> for every image (kept for A/B timing and
  * so that the parity suite covers both).  Process-wide; returns 0. */
 int smg_debug_main_kernel(int32_t which);
+/* The rank-indexed wide pass: 1 = ion_wide_join_kernel where it applies (default: packed f32 hits, no hot-spot clip;
+ * no per-pixel arrays in global memory), 0 = ion_wide_kernel for every image (kept for A/B timing and so that the
+ * parity suite covers both).  Process-wide; returns 0, -1 for another value. */
+int smg_debug_wide_impl(int32_t which);
 /* Diagnostic builds only (-DSMG_STAMPS, libsmg_stamps.so): per-phase cycles of the main passes summed over their
  * workgroups since the last call (ion_pipe_kernel: smg_debug_stamps; ion_sparse_kernel: smg_debug_sparse_stamps),
  * reset on read; SMG_ERR_UNSUPPORTED in the shipped build. */

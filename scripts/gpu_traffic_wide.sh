@@ -13,7 +13,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
 done
 n=$(grep "calibration bytes" gpurun_out/$TAG/FETCH_SIZE.log | awk '{print $3/8}')
 alg=$(grep "sum window points" gpurun_out/$TAG/FETCH_SIZE.log | awk '{for(i=1;i<=NF;i++) if($i=="points" && $(i-1)=="window") print $(i+1)*12}')
-python3 scripts/traffic_summary.py gpurun_out/$TAG/FETCH_SIZE.csv gpurun_out/$TAG/WRITE_SIZE.csv $n gpurun_out/$TAG/traffic_wide.json ion_wide_kernel config5 $alg
+python3 scripts/traffic_summary.py gpurun_out/$TAG/FETCH_SIZE.csv gpurun_out/$TAG/WRITE_SIZE.csv $n gpurun_out/$TAG/traffic_wide.json ${KERN:-ion_wide_join_kernel} config5 $alg
 rc=$?
 rm -f gpurun_out/$TAG/FETCH_SIZE.csv gpurun_out/$TAG/WRITE_SIZE.csv
 exit $rc

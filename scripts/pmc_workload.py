@@ -22,6 +22,8 @@ if which == "c5shard":
     peaks = D.slice_peaks(full, plan)
     f = plan.formulas
     dions = E.DeviceIons.from_arrays(f.ion_off, f.peak_mz, f.peak_int)
+    if os.environ.get("SMG_WIDE_IMPL"):  # 1 = ion_wide_join_kernel (default), 0 = ion_wide_kernel
+        _lib.lib().smg_debug_wide_impl(int(os.environ["SMG_WIDE_IMPL"]))
     m, lo, hi = E.run_hot_path(peaks, dions, 2.0, 30)
     for _ in range(2):
         m = E.ion_metrics(peaks, dions, lo, hi, nlevels=30)

@@ -5,7 +5,7 @@ must be calibrated otherwise).  FETCH_SIZE counts L2 -> fabric requests (Infinit
 
 usage: traffic_summary.py FETCH.csv WRITE.csv n_points out.json [kernel-key config alg_bytes]
   kernel-key: ion_pipe_kernel[512] (default) | ion_sparse_kernel | ion_pipe_kernel[1024] | ion_wave_kernel |
-              ion_wide_kernel | ion_dense_kernel
+              ion_wide_kernel | ion_wide_join_kernel | ion_dense_kernel
 """
 import csv, json, re, sys
 from collections import defaultdict
@@ -19,7 +19,7 @@ def per_kernel(path, counter):
         name = r.get("Kernel_Name") or ""
         m = re.search(r"ion_pipe_kernel<[^,]*, (\d+)", name)
         key = f"ion_pipe_kernel[{m.group(1)}]" if m else ("stream_read" if "stream_read_kernel" in name else None)
-        for k in ("ion_sparse_kernel", "ion_wave_kernel", "ion_wide_kernel", "ion_dense_kernel"):
+        for k in ("ion_sparse_kernel", "ion_wave_kernel", "ion_wide_join_kernel", "ion_wide_kernel", "ion_dense_kernel"):
             if key is None and k in name:
                 key = k
         if key:

@@ -60,6 +60,7 @@ PROTOTYPES = {
     "smg_debug_force_dense": (ctypes.c_int, [_I32]),
     "smg_debug_sort_impl": (ctypes.c_int, [_I32]),
     "smg_debug_main_kernel": (ctypes.c_int, [_I32]),
+    "smg_debug_wide_impl": (ctypes.c_int, [_I32]),
     "smg_debug_stamps": (ctypes.c_int, [_P, ctypes.c_int]),
     "smg_debug_sparse_stamps": (ctypes.c_int, [_P, ctypes.c_int]),
     "smg_debug_check_points": (ctypes.c_int, [_I64]),

@@ -3983,6 +3983,748 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
   STAMP_FLUSH();
 }
 
+// ---------------------------------------------------------------------------------------------
+// wide pass without per-pixel arrays in global memory (round 6): ion_wide_join_kernel
+// ---------------------------------------------------------------------------------------------
+// ion_wide_kernel keeps the principal image's values, pixel list and levels at the pixels' ranks in its slot: at
+// config 5 (~8.5k principal pixels per ion) that is ~110 KB stored per ion, 77 GB per rank-0 launch
+// (profiles/round4/traffic_wide_r4.json), of which only ~450 values per ion are ever read back -- the tail's hits on
+// principal pixels (mean 386) and the principal pixels within two of a chaos candidate (mean 59;
+// profiles/round6/r6c5s_c5_stats.txt).  This pass stores none of them.  Per ion:
+//  1. one stream over the principal window: presence bits (LDS bitmap), the statistics of the unflagged points (each
+//     alone on its pixel, smg_flag_duplicates), the flagged points summed per pixel in an LDS table (PD), then the
+//     statistics of PD's pixels;
+//  2. the tail stream of ion_wide_kernel; a lane parks its first two hits on principal pixels in registers, later
+//     ones go to a list in the slot; flagged tail points into the LT table (+ the slot's table) for Σy²;
+//  3. the chaos screen, per principal pixel p walked from the bitmap (per-wave work lists in the LT table's space):
+//     from presence rows r-4 .. r+4 it lists the candidates on p's 4-cross (as ion_wide_kernel) and marks p needed
+//     when a candidate lies within p's 5x5 (corners excluded: the reach of a candidate's eL);
+//  4. a hash (JH) over the dead bitmap / rank / LT space holds the needed pixels and the tail hits' pixels; a second
+//     stream over the principal window fills each entry's x (an unflagged point's value, a flagged pixel's PD sum);
+//  5. the hits' Σxy and Σy[x>0] from JH; each candidate's eL from its 5x5's levels through JH; Kruskal as in
+//     ion_wide_kernel (candidate bitmap + ranks over the bitmap's space, arrays in the slot).
+// An ion whose tables overflow goes to the pixel-indexed kernel (rej_list), as from ion_wide_kernel.
+// LDS (fixed, WJ_LDS): [bitmap n64p*8][superblock bases][group prefixes][LT 12 KB] ... [PD at the end];
+// JH = keys (u32) then x (f64), WJ_JH entries over [0, PD); images of up to WJ_JH * 12 / 8 pixels index x by pixel
+// instead (every pixel's x, absent pixels 0), so that no image of that size overflows JH.  PD takes what JH and the
+// LT table leave (1024 .. 8192 entries: 1024 at 2^20 pixels, 8192 on small images, whose flagged pixels can be many).
+constexpr size_t WJ_LDS = 160 * 1024 - 4096;  // dynamic LDS of the join pass (static arrays ~3 KB)
+constexpr int WJ_JH_LOG2 = 13;
+constexpr int WJ_JH = 1 << WJ_JH_LOG2;       // needed + hit pixels per ion
+constexpr int WJ_WL = 128;                   // per-wave work list entries (principal pixels of the screen)
+static_assert(DNW * WJ_WL * 4 <= WIDE_LT * 12, "work lists in the LT space");
+
+__host__ __device__ static inline size_t wj_lt_off(int npx) {  // offset of the LT table: bitmap, sb, pf before it
+  const size_t n64 = ((size_t)npx + 63) / 64, n64p = wide_n64p(npx);
+  return n64p * 8 + ((((n64 + 1023) / 1024) * 4 + 15) & ~(size_t)15) + (((n64p / 4) * 2 + 15) & ~(size_t)15);
+}
+struct WjGeom {
+  bool jdirect;  // x by pixel
+  int pd_log2;   // PD entries (log2)
+  size_t pd_off;
+};
+__host__ __device__ static inline WjGeom wj_geom(int npx) {
+  WjGeom g;
+  g.jdirect = (size_t)npx * 8 <= (size_t)WJ_JH * 12;
+  const size_t lt_end = wj_lt_off(npx) + (size_t)WIDE_LT * 12, jh = g.jdirect ? (size_t)npx * 8 : (size_t)WJ_JH * 12;
+  const size_t used = lt_end > jh ? lt_end : jh;
+  const size_t room = used < WJ_LDS ? WJ_LDS - used : 0;
+  g.pd_log2 = 0;
+  while (g.pd_log2 < 13 && ((size_t)12 << (g.pd_log2 + 1)) <= room) ++g.pd_log2;
+  g.pd_off = WJ_LDS - ((size_t)12 << g.pd_log2);
+  return g;
+}
+// the join pass applies where its layout leaves PD >= 1024 entries and build_rank covers the bitmap (n64 <= DNW * 1024)
+static inline bool wide_join_fits(int npx) {
+  return ((size_t)npx + 63) / 64 <= (size_t)DNW * 1024 && wj_geom(npx).pd_log2 >= 10 &&
+         wj_lt_off(npx) + (size_t)WIDE_LT * 12 <= wj_geom(npx).pd_off;
+}
+
+// open-addressing u32 -> slot hash in LDS (empty WIDE_EMPTY): the slot of key or of its insertion (-1: full)
+__device__ __forceinline__ int wj_insert(uint32_t* keys, int cap_log2, uint32_t key) {
+  const int cap = 1 << cap_log2;
+  uint32_t h = (key * 0x9E3779B1u) >> (32 - cap_log2);
+  for (int t = 0; t < cap; ++t) {
+    const uint32_t old = atomicCAS(&keys[h], WIDE_EMPTY, key);
+    if (old == WIDE_EMPTY || old == key) return (int)h;
+    h = (h + 1) & (uint32_t)(cap - 1);
+  }
+  return -1;
+}
+__device__ __forceinline__ int wj_find(const uint32_t* keys, int cap_log2, uint32_t key) {
+  const int cap = 1 << cap_log2;
+  uint32_t h = (key * 0x9E3779B1u) >> (32 - cap_log2);
+  for (int t = 0; t < cap; ++t) {
+    const uint32_t k = keys[h];
+    if (k == key) return (int)h;
+    if (k == WIDE_EMPTY) return -1;
+    h = (h + 1) & (uint32_t)(cap - 1);
+  }
+  return -1;
+}
+
+// presence bits of columns c0-4 .. c0+4 of row r from the LDS bitmap (bit j = column c0-4+j; 0 outside the image);
+// one zero word follows the bitmap
+__device__ __forceinline__ uint32_t wj_row9(const uint32_t* w, int r, int c0, int nr, int nc) {
+  if (r < 0 || r >= nr) return 0u;
+  const int lc = c0 - 4;
+  const int64_t g = (int64_t)r * nc + lc;
+  uint32_t v;
+  if (g >= 0) {
+    const int wi = (int)(g >> 5);
+    v = __builtin_amdgcn_alignbit(w[wi + 1], w[wi], (uint32_t)(g & 31));
+  } else {
+    v = w[0] << (uint32_t)(-g);
+  }
+  uint32_t cm = 0x1FFu;
+  if (lc < 0) cm &= 0x1FFu << (uint32_t)(-lc);
+  if (c0 + 4 >= nc) cm &= 0x1FFu >> (uint32_t)(c0 + 4 - (nc - 1));
+  return v & cm;
+}
+
+__global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
+    Hits<SMG_HITS_PACKED_F32> hits, const DD4* __restrict__ cum, const int64_t* __restrict__ lo,
+    const int64_t* __restrict__ hi, const int64_t* __restrict__ ion_off, const double* __restrict__ theor, Params P,
+    const uint32_t* __restrict__ list, const uint32_t* __restrict__ count, uint32_t* next, uint32_t* rej_list,
+    uint32_t* rej_count, uint32_t rej_cap, unsigned char* scratch, size_t slot_bytes, double* __restrict__ oc,
+    double* __restrict__ osp, double* __restrict__ osc, double* __restrict__ omsm, uint32_t* __restrict__ oflags) {
+  using H = Hits<SMG_HITS_PACKED_F32>;
+  extern __shared__ __attribute__((aligned(16))) uint64_t wide_dyn[];
+  __shared__ double red[8 * DNW];
+  __shared__ double kst[4 * MAXK_DENSE];
+  __shared__ uint32_t sc[DNW];
+  __shared__ int sh_ion;
+  __shared__ int sh_ctr[4];  // candidates with eL >= 1, max eL, listed flagged tail points, overflow (-> pixel kernel)
+  __shared__ int sh_nown;    // claimed global table entries
+  __shared__ int sh_ncand;   // screened chaos candidates (listed in S.epr)
+  __shared__ int sh_anyfl;   // the tail stream met a flagged point
+  __shared__ int sh_nov;     // tail hits beyond the registers (listed in the slot)
+  __shared__ int sh_need;    // needed principal pixels (listed in S.par)
+  __shared__ int sh_anyhit;  // some lane parked a hit
+  __shared__ int sh_rs;      // the hit list overflowed on an image with x by pixel: the tail is streamed again
+  __shared__ double sh_st[5];  // principal sums: x, x^2, x[x > 0], #(x > 0); max
+  __shared__ int64_t sh_tb[MAXK_DENSE + 1];
+  __shared__ int64_t sh_tlo[MAXK_DENSE];
+  __shared__ int64_t sh_tn[MAXK_DENSE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int npx = P.npx, n64 = (npx + 63) / 64, nsb = (n64 + 1023) / 1024;
+  const int n64p = (int)wide_n64p(npx);
+  unsigned char* const lds = reinterpret_cast<unsigned char*>(wide_dyn);
+  uint64_t* bm = wide_dyn;
+  uint32_t* bm32 = reinterpret_cast<uint32_t*>(bm);
+  uint32_t* sb = reinterpret_cast<uint32_t*>(lds + (size_t)n64p * 8);
+  uint16_t* pf = reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(sb) + (((size_t)nsb * 4 + 15) & ~(size_t)15));
+  uint32_t* ltkey = reinterpret_cast<uint32_t*>(lds + wj_lt_off(npx));
+  double* ltval = reinterpret_cast<double*>(ltkey + WIDE_LT);
+  const WjGeom G = wj_geom(npx);
+  const int pd_log2 = G.pd_log2, npd = 1 << pd_log2;
+  uint32_t* pdkey = reinterpret_cast<uint32_t*>(lds + G.pd_off);
+  double* pdval = reinterpret_cast<double*>(pdkey + npd);
+  uint32_t* wlist = ltkey + wid * WJ_WL;  // the screen's work lists (LT space)
+  // JH (after the screen), or x by pixel on small images
+  const bool jdirect = G.jdirect;
+  uint32_t* jkey = reinterpret_cast<uint32_t*>(lds);
+  double* jx = reinterpret_cast<double*>(lds + (jdirect ? (size_t)0 : (size_t)WJ_JH * 4));
+  auto jslot = [&](uint32_t p) -> int { return jdirect ? (int)p : wj_find(jkey, WJ_JH_LOG2, p); };
+  const RankBits R{bm, pf, sb};
+  WideSlot S = wide_slot(scratch + (size_t)blockIdx.x * slot_bytes, npx);
+  uint64_t* ovh = reinterpret_cast<uint64_t*>(S.vals);  // tail hits beyond the registers (their windows in S.L)
+  uint32_t* need = S.par;                               // needed principal pixels
+  const uint32_t total = *count;
+  for (int i = tid; i < WIDE_HT; i += DBLOCK) {
+    S.hkey[i] = WIDE_EMPTY;
+    S.hval[i] = 0.0;
+  }
+  for (int i = tid; i < WIDE_LT; i += DBLOCK) {
+    ltkey[i] = WIDE_EMPTY;
+    ltval[i] = 0.0;
+  }
+  for (int i = tid; i < npd; i += DBLOCK) {
+    pdkey[i] = WIDE_EMPTY;
+    pdval[i] = 0.0;
+  }
+  slot_sync();
+  const int nr = P.nrows, nc = P.ncols;
+
+  while (true) {
+    if (tid == 0) {
+      const uint32_t k = atomicAdd(next, 1u);
+      sh_ion = (k < total) ? (int)list[k] : -1;
+      sh_ctr[0] = sh_ctr[1] = sh_ctr[2] = sh_ctr[3] = 0;
+      sh_nown = 0;
+      sh_ncand = 0;
+      sh_anyfl = 0;
+      sh_nov = 0;
+      sh_need = 0;
+      sh_anyhit = 0;
+      sh_rs = 0;
+    }
+    __syncthreads();
+    const int64_t ion = sh_ion;
+    if (ion < 0) break;
+    const int64_t w0 = ion_off[ion];
+    const int K = (int)(ion_off[ion + 1] - w0);
+    uint32_t flags = SMG_ION_DENSE | SMG_ION_WIDE;
+    for (int k = 0; k < K && k < MAXK_DENSE; ++k)
+      if (hi[w0 + k] > lo[w0 + k]) flags |= SMG_ION_HAS_HITS;
+    if (K > MAXK_DENSE || K == 0) {
+      if (tid == 0) {
+        oc[ion] = osp[ion] = osc[ion] = omsm[ion] = 0.0;
+        oflags[ion] = (K == 0) ? 0u : (flags | 0x80000000u);
+      }
+      __syncthreads();
+      continue;
+    }
+    // ---- 1. principal image: presence bits, statistics, flagged pixels summed in PD ----------------------------
+    for (int w = tid; w < n64p; w += DBLOCK) bm[w] = 0ull;
+    __syncthreads();
+    const int64_t a0 = lo[w0], b0 = hi[w0];
+    double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // Σx, Σx², Σx[x>0], #(x>0), #pixels
+    double mx = -INFINITY;
+    auto stat = [&](double v) {
+      acc[0] += v;
+      acc[1] += v * v;
+      if (v > 0.0) {
+        acc[2] += v;
+        acc[3] += 1.0;
+      }
+      acc[4] += 1.0;
+      mx = v > mx ? v : mx;
+    };
+    for (int64_t i0 = a0; i0 < b0; i0 += (int64_t)DBLOCK * WDU) {
+      uint64_t r[WDU];
+#pragma unroll
+      for (int u = 0; u < WDU; ++u) {
+        const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
+        r[u] = hits.load(i < b0 ? i : b0 - 1);
+      }
+#pragma unroll
+      for (int u = 0; u < WDU; ++u) {
+        const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
+        if (i < b0) {
+          const uint32_t p = H::pix(r[u]);
+          if (p >= (uint32_t)npx) {  // (only a caller-supplied hit can carry one)
+            sh_ctr[3] = 1;
+            continue;
+          }
+          atomicOr(&bm32[p >> 5], 1u << (p & 31));
+          const double v = H::val(r[u]);
+          if (H::dup(r[u])) {
+            const int s = wj_insert(pdkey, pd_log2, p);
+            if (s >= 0) atomicAdd(&pdval[s], v);
+            else sh_ctr[3] = 1;
+          } else {
+            stat(v);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    for (int s = tid; s < npd; s += DBLOCK)
+      if (pdkey[s] != WIDE_EMPTY) stat(pdval[s]);
+    dblock_sum<5>(acc, red);
+    if (acc[4] < (double)npx) mx = mx > 0.0 ? mx : 0.0;  // pixels outside the principal image are zero
+    {
+      const double vmax = block_max<DNW>(mx, red);
+      if (tid == 0) {
+        sh_st[0] = acc[0];
+        sh_st[1] = acc[1];
+        sh_st[2] = acc[2];
+        sh_st[3] = acc[3];
+        sh_st[4] = vmax;
+      }
+    }
+    // ---- 2. tail windows (ion_wide_kernel's packed stream; hits parked, none gathered) -------------------------
+    constexpr int64_t TSTEP = (int64_t)DBLOCK * TDU;
+    if (tid < 4 * MAXK_DENSE) kst[tid] = 0.0;
+    if (tid <= K - 1) {
+      int64_t n = 0;
+      for (int k = 1; k <= tid; ++k) n += (hi[w0 + k] - lo[w0 + k] + TSTEP - 1) / TSTEP * TSTEP;
+      sh_tb[tid] = n;
+      if (tid < K - 1) {
+        sh_tlo[tid] = lo[w0 + 1 + tid];
+        sh_tn[tid] = hi[w0 + 1 + tid] - lo[w0 + 1 + tid];
+      }
+    }
+    __syncthreads();
+    if (tid < K - 1) {
+      const double2 ws = window_sums<SMG_HITS_PACKED_F32>(hits, cum, lo[w0 + 1 + tid], hi[w0 + 1 + tid]);
+      kst[1 * MAXK_DENSE + tid + 1] = ws.x;
+      kst[2 * MAXK_DENSE + tid + 1] = ws.y;
+    }
+    const int64_t T = sh_tb[K - 1];
+    uint32_t fk[WIDE_FLR];
+    float fv[WIDE_FLR];
+    int fc = 0;
+#pragma unroll
+    for (int j = 0; j < WIDE_FLR; ++j) {
+      fk[j] = 0u;
+      fv[j] = 0.0f;
+    }
+    auto append = [&](uint32_t flm, int kw, const uint64_t (&rs)[TDU]) {
+      for (int u = 0; u < TDU; ++u)
+        if ((flm >> u) & 1u) {
+          const uint32_t key = (uint32_t)kw * (uint32_t)npx + H::pix(rs[u]);
+          const float y = __uint_as_float((uint32_t)(rs[u] >> 32));
+          if (fc < WIDE_FLR) {
+#pragma unroll
+            for (int j = 0; j < WIDE_FLR; ++j)
+              if (fc == j) {
+                fk[j] = key;
+                fv[j] = y;
+              }
+          } else {
+            const int idx = atomicAdd(&sh_ctr[2], 1);
+            if (idx < WIDE_DL) {
+              S.dkey[idx] = key;
+              S.dval[idx] = (double)y;
+            } else {
+              sh_ctr[3] = 1;
+            }
+          }
+          ++fc;
+          sh_anyfl = 1;
+        }
+    };
+    const uint64_t* hb = hits.h;
+    uint64_t rA[TDU], rB[TDU];
+#pragma unroll
+    for (int u = 0; u < TDU; ++u) rA[u] = rB[u] = 0ull;
+    uint64_t ev0 = 0ull, ev1 = 0ull;
+    int evk0 = 0, evk1 = 0, nev = 0;
+    int ki = 0;
+    auto issue = [&](int64_t v0, uint64_t (&r)[TDU]) -> int {
+      while (v0 >= sh_tb[ki + 1]) ++ki;
+      ki = __builtin_amdgcn_readfirstlane(ki);
+      const int64_t off = v0 - sh_tb[ki], n = sh_tn[ki], a = sh_tlo[ki];
+#pragma unroll
+      for (int u = 0; u < TDU; ++u) {
+        const int64_t lv = off + (int64_t)u * DBLOCK + tid;
+        r[u] = hb[a + (lv < n ? lv : n - 1)];
+      }
+      return ki;
+    };
+    auto batch = [&](int64_t v0, uint64_t (&r)[TDU], int kb, uint64_t (&rn)[TDU], int& kn) {
+      if (v0 + TSTEP < T) kn = issue(v0 + TSTEP, rn);
+      const int64_t off = v0 - sh_tb[kb], n = sh_tn[kb];
+      uint32_t flm = 0u;
+#pragma unroll
+      for (int u = 0; u < TDU; ++u) {
+        const uint32_t p = H::pix(r[u]);
+        const bool valid = off + (int64_t)u * DBLOCK + tid < n && p < (uint32_t)npx;
+        const bool pr = valid && R.test(p);
+        const bool s0 = pr && nev == 0, s1 = pr && nev == 1;
+        ev0 = s0 ? r[u] : ev0;
+        evk0 = s0 ? kb : evk0;
+        ev1 = s1 ? r[u] : ev1;
+        evk1 = s1 ? kb : evk1;
+        nev += pr ? 1 : 0;
+        flm |= (uint32_t)(valid && H::dup(r[u])) << u;
+        flm |= (uint32_t)(pr && nev > 2) << (16 + u);
+      }
+      if (__ballot((flm >> 16) != 0u)) {  // a lane's third and later hits: listed in the slot (rare)
+#pragma unroll
+        for (int u = 0; u < TDU; ++u)
+          if ((flm >> (16 + u)) & 1u) {
+            const int idx = atomicAdd(&sh_nov, 1);
+            if (idx < npx) {
+              ovh[idx] = r[u];
+              S.L[idx] = (uint8_t)kb;
+            } else if (jdirect) {
+              sh_rs = 1;
+            } else {
+              sh_ctr[3] = 1;
+            }
+          }
+      }
+      append(flm & 0xFFFFu, kb, r);
+    };
+    int kA = 0, kB = 0;
+    if (T > 0) kA = issue(0, rA);
+    for (int64_t v0 = 0; v0 < T; v0 += 2 * TSTEP) {
+      batch(v0, rA, kA, rB, kB);
+      if (v0 + TSTEP >= T) break;
+      batch(v0 + TSTEP, rB, kB, rA, kA);
+    }
+    if (nev > 0) sh_anyhit = 1;
+    __syncthreads();
+    // flagged tail points summed per (window, pixel): LDS table, then the slot's table; (Σy)² of each entry into Σy²
+    const int nd = min(sh_ctr[2], WIDE_DL);
+    if (sh_anyfl) {
+      if (nd > 0) slot_sync();
+      auto insert_global = [&](uint32_t key, double y) {
+        uint32_t h = (key * 0x9E3779B1u) >> (32 - WIDE_HT_LOG2);
+        bool own = false, done = false;
+        for (int t = 0; t < WIDE_PROBES; ++t) {
+          const uint32_t old = atomicCAS(&S.hkey[h], WIDE_EMPTY, key);
+          if (old == WIDE_EMPTY || old == key) {
+            atomicAdd(&S.hval[h], y);
+            own = old == WIDE_EMPTY;
+            done = true;
+            break;
+          }
+          h = (h + 1) & (WIDE_HT - 1);
+        }
+        if (!done) sh_ctr[3] = 1;
+        return own ? (int)h : -1;
+      };
+      auto insert = [&](bool act, uint32_t key, double y) {
+        bool placed = !act;
+        if (act) {
+          uint32_t h = (key * 0x9E3779B1u) >> (32 - WIDE_LT_LOG2);
+          for (int t = 0; t < WIDE_LT_PROBES; ++t) {
+            const uint32_t old = atomicCAS(&ltkey[h], WIDE_EMPTY, key);
+            if (old == WIDE_EMPTY || old == key) {
+              atomicAdd(&ltval[h], y);
+              placed = true;
+              break;
+            }
+            h = (h + 1) & (WIDE_LT - 1);
+          }
+        }
+        int gh = -1;
+        if (__ballot(!placed)) {
+          if (!placed) gh = insert_global(key, y);
+        }
+        const int idx = wave_append(gh >= 0, &sh_nown);
+        if (gh >= 0) S.hown[idx] = (uint32_t)gh;
+      };
+#pragma unroll
+      for (int j = 0; j < WIDE_FLR; ++j) insert(j < fc, fk[j], (double)fv[j]);
+      for (int j0 = 0; j0 < nd; j0 += DBLOCK) {
+        const int j = j0 + tid;
+        insert(j < nd, j < nd ? ld_agent(&S.dkey[j]) : 0u, j < nd ? ld_agent(&S.dval[j]) : 0.0);
+      }
+      slot_sync();
+      for (int i = tid; i < WIDE_LT; i += DBLOCK) {
+        const uint32_t key = ltkey[i];
+        if (key != WIDE_EMPTY) {
+          const double y = ltval[i];
+          atomicAdd(&kst[2 * MAXK_DENSE + key / (uint32_t)npx + 1], y * y);
+          ltkey[i] = WIDE_EMPTY;
+          ltval[i] = 0.0;
+        }
+      }
+      const int no = sh_nown;
+      for (int j = tid; j < no; j += DBLOCK) {
+        const uint32_t s = S.hown[j];
+        const uint32_t key = ld_agent(&S.hkey[s]);
+        const double y = ld_agent(&S.hval[s]);
+        atomicAdd(&kst[2 * MAXK_DENSE + key / (uint32_t)npx + 1], y * y);
+        S.hkey[s] = WIDE_EMPTY;
+        S.hval[s] = 0.0;
+      }
+      __syncthreads();
+    }
+    if (sh_ctr[3]) {  // an overflow: the pixel-indexed kernel scores this ion
+      if (tid == 0) {
+        const uint32_t r = atomicAdd(rej_count, 1u);
+        if (r < rej_cap) rej_list[r] = (uint32_t)ion;
+      }
+      for (int s = tid; s < npd; s += DBLOCK) {
+        pdkey[s] = WIDE_EMPTY;
+        pdval[s] = 0.0;
+      }
+      __syncthreads();
+      continue;
+    }
+    // ---- 3. chaos screen per principal pixel, walked from the bitmap -------------------------------------------
+    const double npos = sh_st[3];
+    const bool chaos_ok = (sh_st[0] > 0.0) && (npos >= 4.0);
+    if (chaos_ok) {
+      // uniform call: candidates on p's 4-cross (listed by the first principal pixel on their cross, as in
+      // ion_wide_kernel) and whether a candidate lies within p's 5x5 minus its corners, from presence rows r-4 .. r+4
+      auto screen_px = [&](bool act, int p) {
+        uint32_t cm = 0u;
+        bool nd_ = false;
+        int r0 = 0, c0 = 0;
+        if (act) {
+          rowcol(p, P, r0, c0);
+          uint32_t B[9], IM[9];
+          uint32_t imc = 0x1FFu;  // columns c0-4 .. c0+4 inside the image
+          if (c0 - 4 < 0) imc &= 0x1FFu << (uint32_t)(4 - c0);
+          if (c0 + 4 >= nc) imc &= 0x1FFu >> (uint32_t)(c0 + 4 - (nc - 1));
+          int cnt = 0;
+#pragma unroll
+          for (int k = 0; k < 9; ++k) {
+            B[k] = wj_row9(bm32, r0 + k - 4, c0, nr, nc);
+            IM[k] = (r0 + k - 4 >= 0 && r0 + k - 4 < nr) ? imc : 0u;
+            cnt += __popc(B[k]);
+          }
+          // a candidate's 3x3 box is covered by 4-crosses of principal pixels only if >= 3 of them lie in its 5x5
+          if (P.erosion_border || cnt >= 3) {
+            uint32_t Eh[9], E[9];
+#pragma unroll
+            for (int k = 1; k <= 7; ++k) {  // D = dilate_cross(presence) (valid columns 1..7), its 3-wide erosion
+              const uint32_t d = B[k] | (B[k] << 1) | (B[k] >> 1) | B[k - 1] | B[k + 1];
+              const uint32_t dm = (P.erosion_border ? (d | ~IM[k]) : (d & IM[k])) & 0x1FFu;
+              Eh[k] = dm & (dm << 1) & (dm >> 1);  // (valid columns 2..6)
+            }
+#pragma unroll
+            for (int k = 2; k <= 6; ++k) E[k] = Eh[k - 1] & Eh[k] & Eh[k + 1] & IM[k];  // candidates, rows r-2 .. r+2
+            nd_ = (((E[2] | E[6]) & 0x38u) | ((E[3] | E[4] | E[5]) & 0x7Cu)) != 0u;
+            auto prb = [&](int k, int j) -> uint32_t { return (B[k] >> j) & 1u; };
+#pragma unroll
+            for (int t = 0; t < 5; ++t) {
+              const int qr = (t == 1) ? -1 : (t == 2) ? 1 : 0, qc = (t == 3) ? -1 : (t == 4) ? 1 : 0;
+              const int wr = qr + 4, wc = qc + 4;
+              int orr = 9, occ = 9;  // the first principal pixel among q-nc, q-1, q, q+1, q+nc must be p
+              if (prb(wr + 1, wc)) orr = 1, occ = 0;
+              if (prb(wr, wc + 1)) orr = 0, occ = 1;
+              if (prb(wr, wc)) orr = 0, occ = 0;
+              if (prb(wr, wc - 1)) orr = 0, occ = -1;
+              if (prb(wr - 1, wc)) orr = -1, occ = 0;
+              if (qr + orr == 0 && qc + occ == 0 && ((E[wr] >> wc) & 1u)) cm |= 1u << t;
+            }
+          }
+        }
+        const int ni = wave_append(nd_, &sh_need);
+        if (nd_) need[ni] = (uint32_t)p;  // (each principal pixel once: at most np <= npx entries)
+        const int cnt = __popc(cm);
+        const int incl = wave_incl_scan_dpp(cnt);
+        int wbase = 0;
+        if (lane == 63 && incl > 0) wbase = atomicAdd(&sh_ncand, incl);
+        wbase = __shfl(wbase, 63);
+        int idx = wbase + incl - cnt;
+        while (cm != 0u) {
+          const int t = __ffs(cm) - 1;
+          const int qr = (t == 1) ? -1 : (t == 2) ? 1 : 0, qc = (t == 3) ? -1 : (t == 4) ? 1 : 0;
+          if (idx < npx) S.epr[idx] = (uint32_t)((r0 + qr) * nc + c0 + qc);
+          ++idx;
+          cm &= cm - 1u;
+        }
+      };
+      // each wave walks 64 bitmap words (4096 pixels) at a time: a lane pops its word's bits one per round into the
+      // wave's list, which is screened 64 entries (one per lane) at a time
+      int wn = 0;  // listed entries (uniform)
+      for (int w0w = wid * WAVE; w0w < n64; w0w += DBLOCK) {
+        const int w = w0w + lane;
+        uint64_t bits = w < n64 ? bm[w] : 0ull;
+        while (true) {
+          const bool has = bits != 0ull;
+          const uint64_t m = __ballot(has);
+          if (m == 0ull) break;
+          if (has) {
+            const int b = __ffsll((unsigned long long)bits) - 1;
+            bits &= bits - 1ull;
+            wlist[wn + (int)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)(w * 64 + b);
+          }
+          wn += (int)__popcll(m);
+          if (wn >= WAVE) {
+            __builtin_amdgcn_wave_barrier();
+            screen_px(true, (int)wlist[lane]);
+            __builtin_amdgcn_wave_barrier();
+            wn -= WAVE;
+            const uint32_t mv = lane < wn ? wlist[WAVE + lane] : 0u;
+            __builtin_amdgcn_wave_barrier();
+            if (lane < wn) wlist[lane] = mv;
+            __builtin_amdgcn_wave_barrier();
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (wn > 0) screen_px(lane < wn, lane < wn ? (int)wlist[lane] : 0);
+    }
+    slot_sync();  // (candidates and needed pixels listed in L2; every bitmap reader done)
+    const int nscr = chaos_ok ? min(sh_ncand, npx) : 0;
+    const int nneed = chaos_ok ? min(sh_need, npx) : 0;
+    // ---- 4. JH over the dead bitmap / rank / LT space: the needed and the hit pixels, x from a second stream ----
+    const int nov = min(sh_nov, npx);
+    const bool rs = sh_rs != 0;
+    const bool anyhit = sh_anyhit != 0 || nov > 0 || rs;
+    if (anyhit || nneed > 0 || nscr > 0) {
+      if (jdirect) {
+        for (int i = tid; i < npx; i += DBLOCK) jx[i] = 0.0;
+      } else {
+        for (int i = tid; i < WJ_JH; i += DBLOCK) jkey[i] = WIDE_EMPTY;
+        __syncthreads();
+        if (nev > 0 && wj_insert(jkey, WJ_JH_LOG2, H::pix(ev0)) < 0) sh_ctr[3] = 1;
+        if (nev > 1 && wj_insert(jkey, WJ_JH_LOG2, H::pix(ev1)) < 0) sh_ctr[3] = 1;
+        for (int j = tid; j < nov; j += DBLOCK)
+          if (wj_insert(jkey, WJ_JH_LOG2, H::pix(ld_agent(&ovh[j]))) < 0) sh_ctr[3] = 1;
+        for (int j = tid; j < nneed; j += DBLOCK)
+          if (wj_insert(jkey, WJ_JH_LOG2, ld_agent(&need[j])) < 0) sh_ctr[3] = 1;
+      }
+      __syncthreads();
+      for (int64_t i0 = a0; i0 < b0; i0 += (int64_t)DBLOCK * WDU) {
+        uint64_t r[WDU];
+#pragma unroll
+        for (int u = 0; u < WDU; ++u) {
+          const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
+          r[u] = hits.load(i < b0 ? i : b0 - 1);
+        }
+#pragma unroll
+        for (int u = 0; u < WDU; ++u) {
+          const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
+          if (i < b0) {
+            const uint32_t p = H::pix(r[u]);
+            const int s = jslot(p);
+            if (s >= 0) {
+              double x = H::val(r[u]);
+              if (H::dup(r[u])) {
+                const int t = wj_find(pdkey, pd_log2, p);
+                x = t >= 0 ? pdval[t] : 0.0;
+              }
+              jx[s] = x;  // (every point of a pixel stores the same value)
+            }
+          }
+        }
+      }
+      __syncthreads();
+      // ---- 5a. the hits' Σxy and Σy[x>0] -----------------------------------------------------------------------
+      auto hit = [&](uint64_t h, int kb) {
+        const int s = jslot(H::pix(h));
+        const double xv = s >= 0 ? jx[s] : 0.0;
+        const double y = H::val(h);
+        atomicAdd(&kst[3 * MAXK_DENSE + kb + 1], xv * y);
+        if (xv > 0.0) atomicAdd(&kst[0 * MAXK_DENSE + kb + 1], y);
+      };
+      if (!rs) {
+        if (nev > 0) hit(ev0, evk0);
+        if (nev > 1) hit(ev1, evk1);
+        for (int j = tid; j < nov; j += DBLOCK) hit(ld_agent(&ovh[j]), (int)S.L[j]);
+      } else {  // more hits than pixels (x by pixel, absent pixels 0): every tail point again, none listed
+        int kb = 0;
+        for (int64_t v0 = 0; v0 < T; v0 += TSTEP) {
+          while (v0 >= sh_tb[kb + 1]) ++kb;
+          kb = __builtin_amdgcn_readfirstlane(kb);
+          const int64_t off = v0 - sh_tb[kb], n = sh_tn[kb], a = sh_tlo[kb];
+          uint64_t r[TDU];
+#pragma unroll
+          for (int u = 0; u < TDU; ++u) {
+            const int64_t lv = off + (int64_t)u * DBLOCK + tid;
+            r[u] = hb[a + (lv < n ? lv : n - 1)];
+          }
+#pragma unroll
+          for (int u = 0; u < TDU; ++u)
+            if (off + (int64_t)u * DBLOCK + tid < n && H::pix(r[u]) < (uint32_t)npx && jx[H::pix(r[u])] != 0.0)
+              hit(r[u], kb);
+        }
+      }
+    }
+    // ---- 5b. eL of every screened candidate from its 5x5's levels (absent pixels: level 0), then Kruskal --------
+    double chaos_raw = NAN;
+    if (chaos_ok && !sh_ctr[3]) {
+      const double vmax = sh_st[4];
+      for (int i0 = 0; i0 < nscr; i0 += DBLOCK) {
+        const int i = i0 + tid;
+        const int q = (i < nscr) ? (int)ld_agent(&S.epr[i]) : -1;
+        int e = 0;
+        if (q >= 0) {
+          int r0, c0;
+          rowcol(q, P, r0, c0);
+          auto lev = [&](int rr, int cc) -> int {  // level of pixel (rr, cc); 0 outside the image or absent
+            if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) return 0;
+            const int s = jslot((uint32_t)(rr * nc + cc));
+            return s >= 0 ? level_fast(jx[s], vmax, P) : 0;
+          };
+          int Lv[5][5];
+#pragma unroll
+          for (int a = 0; a < 5; ++a)
+#pragma unroll
+            for (int b = 0; b < 5; ++b)
+              Lv[a][b] = ((a == 0 || a == 4) && (b == 0 || b == 4)) ? 0 : lev(r0 + a - 2, c0 + b - 2);
+          e = 1 << 20;
+#pragma unroll
+          for (int a = -1; a <= 1; ++a)
+#pragma unroll
+            for (int b = -1; b <= 1; ++b) {
+              const int rr = r0 + a, cc = c0 + b;
+              if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) {
+                if (!P.erosion_border) e = 0;
+                continue;
+              }
+              const int A = a + 2, Bc = b + 2;
+              const int t = max(max(Lv[A][Bc], Lv[A - 1][Bc]), max(max(Lv[A + 1][Bc], Lv[A][Bc - 1]), Lv[A][Bc + 1]));
+              e = min(e, t);
+            }
+          if (e >= (1 << 20)) e = 0;
+        }
+        const int idx = wave_append(e >= 1, &sh_ctr[0]);
+        if (e >= 1) {
+          S.epix[idx] = (uint32_t)q;
+          S.eL[idx] = (uint8_t)e;
+          atomicMax(&sh_ctr[1], e);
+        }
+      }
+      slot_sync();
+      const int m = sh_ctr[0];
+      const int emax = sh_ctr[1];
+      double esum = 0.0, wsum = 0.0;
+      for (int i = tid; i < m; i += DBLOCK) esum += (double)S.eL[i];
+      if (m > 0) {  // Kruskal over the candidates, indexed by their rank in a candidate bitmap (ion_wide_kernel's)
+        for (int w = tid; w < n64p; w += DBLOCK) bm[w] = 0ull;
+        __syncthreads();
+        for (int i = tid; i < m; i += DBLOCK) {
+          const uint32_t q = S.epix[i];
+          atomicOr(&bm32[q >> 5], 1u << (q & 31));
+        }
+        __syncthreads();
+        build_rank(bm, pf, sb, n64, sc);
+        for (int i = tid; i < m; i += DBLOCK) {
+          const uint32_t q = S.epix[i];
+          const uint32_t k = R.rank(q);
+          S.epr[k] = q;
+          S.eLr[k] = S.eL[i];
+          S.par[k] = k;
+        }
+        slot_sync();
+        for (int t = emax; t >= 1; --t) {
+          for (int i = tid; i < m; i += DBLOCK) {
+            const int e = S.eLr[i];
+            if (e < t) continue;
+            const int p = (int)S.epr[i];
+            const int r = p / nc, c = p - r * nc;
+            auto edge = [&](int q) {
+              if (!R.test((uint32_t)q)) return;
+              const uint32_t kq = R.rank((uint32_t)q);
+              const int eq = S.eLr[kq];
+              if ((e < eq ? e : eq) == t && guf_unite(S.par, (uint32_t)i, kq)) wsum += (double)t;
+            };
+            if (c + 1 < nc) edge(p + 1);
+            if (r + 1 < nr) {
+              edge(p + nc);
+              if (P.connectivity == 8) {
+                if (c > 0) edge(p + nc - 1);
+                if (c + 1 < nc) edge(p + nc + 1);
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+      double a3[2] = {esum, wsum};
+      dblock_sum<2>(a3, red);
+      chaos_raw = 1.0 - (a3[0] - a3[1]) / (double)P.nlevels / npos;
+    } else if (!chaos_ok) {
+      flags |= SMG_ION_CHAOS_NAN;
+    }
+    __syncthreads();  // (the hits' kst sums; every JH and LT-space reader done)
+    const bool over = sh_ctr[3] != 0;
+    // the LT space (work lists, JH) and PD back to empty for the next ion
+    for (int i = tid; i < WIDE_LT; i += DBLOCK) {
+      ltkey[i] = WIDE_EMPTY;
+      ltval[i] = 0.0;
+    }
+    for (int s = tid; s < npd; s += DBLOCK) {
+      pdkey[s] = WIDE_EMPTY;
+      pdval[s] = 0.0;
+    }
+    if (tid == 0) {
+      if (over) {  // JH or a list overflowed after the tail: the pixel-indexed kernel scores this ion
+        const uint32_t r = atomicAdd(rej_count, 1u);
+        if (r < rej_cap) rej_list[r] = (uint32_t)ion;
+      } else {
+        kst[0] = sh_st[2];
+        kst[1 * MAXK_DENSE] = kst[2 * MAXK_DENSE] = kst[3 * MAXK_DENSE] = 0.0;
+        finalize_ion(K, theor + w0, kst, sh_st[0], sh_st[1], kst + MAXK_DENSE, kst + 2 * MAXK_DENSE,
+                     kst + 3 * MAXK_DENSE, (double)npx, chaos_raw, ion, flags, oc, osp, osc, omsm, oflags);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void list_all_kernel(uint32_t* list, uint32_t* count, const int64_t* ion_order, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) list[i] = (uint32_t)(ion_order ? ion_order[i] : i);
@@ -4053,6 +4795,7 @@ using Big2Lay = Lay2<BIG_BLOCK / WAVE, BIG_BLOCK * BIG2_RMAX>;
 static int g_main_kernel = 1;      // smg_debug_main_kernel: 1 the sparse main pass where it applies, 0 ion_pipe_kernel
 static int g_force_two_level = 0;  // smg_debug_force_two_level: two-level passes for every image size
 static int g_force_dense = 0;      // smg_debug_force_dense: 1 every ion on the dense path, 2 pixel-indexed only
+static int g_wide_impl = 1;        // smg_debug_wide_impl: 1 ion_wide_join_kernel where it applies, 0 ion_wide_kernel
 // smg_debug_time_main_pass: HIP events recorded on the launch stream around every pass launch of
 // smg_ion_metrics (descriptors, main LDS pass, big-ion pass, wide pass, pixel-indexed pass), so a benchmark
 // measures each kernel itself and prices each pass's own window points against its own time
@@ -4172,7 +4915,9 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   // two-level pass spent 6.7 ms rejecting every ion, profiles/round3/r3c5_*); smg_debug_force_two_level keeps
   // the two-level passes for the parity suite
   const size_t wide_max = P.clip ? WIDE_LDS_MAX_CLIP : WIDE_LDS_MAX;
-  const bool wide_fits = g_force_dense != 2 && wide_lds_bytes(P.npx) <= wide_max;
+  // (build_rank ranks at most DNW * 1024 bitmap words: images up to 2^20 pixels)
+  const bool wide_fits = g_force_dense != 2 && wide_lds_bytes(P.npx) <= wide_max &&
+                         ((int64_t)P.npx + 63) / 64 <= (int64_t)DNW * 1024;
   const bool lds_ok = two ? (!wide_fits || g_force_two_level) : P.npx <= NPX_LDS_MAX;
   // the main pass: ion_sparse_kernel (four 256-thread workgroups per CU, a sparse principal set) where it applies,
   // else ion_pipe_kernel<512>; either hands its rejects (positions) to the big-ion pass
@@ -4255,7 +5000,23 @@ static int launch_metrics(Hits<FMT> hits, const double* hit_cum, const int64_t* 
   uint32_t* dcount = hdr + 2;
   uint32_t* dnext = hdr + 3;
   const size_t wide_lds = wide_lds_bytes(P.npx);
-  if (wide_fits) {
+  // packed hits without the clip: the join variant (no per-pixel arrays in the slot) where its LDS fits
+  const bool wide_join = FMT == SMG_HITS_PACKED_F32 && !P.clip && g_wide_impl == 1 && wide_join_fits(P.npx);
+  if (wide_fits && wide_join) {
+    if constexpr (FMT == SMG_HITS_PACKED_F32) {
+      const size_t jl = WJ_LDS;
+      SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&ion_wide_join_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)jl));
+      PassTimer tm(SMG_PASS_WIDE, st);
+      hipLaunchKernelGGL(ion_wide_join_kernel, dim3((unsigned)nslots), dim3(DBLOCK), jl, st, hits,
+                         reinterpret_cast<const DD4*>(hit_cum), lo, hi, ion_off, theor, P, list_b, hdr + 2, hdr + 3,
+                         list_a, hdr + 4, (uint32_t)n_ions, slots, slot_bytes, oc, osp, osc, omsm, oflags);
+      SMG_LAUNCH_CHECK();
+    }
+    dlist = list_a;
+    dcount = hdr + 4;
+    dnext = hdr + 5;
+  } else if (wide_fits) {
     auto kw = P.clip ? &ion_wide_kernel<FMT, true> : &ion_wide_kernel<FMT, false>;
     SMG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kw), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)wide_lds));
@@ -4410,6 +5171,12 @@ int smg_debug_pass_times(int32_t* pass, double* ms, int32_t cap, int32_t* n) {
 
 int smg_debug_force_dense(int32_t on) {
   g_force_dense = (on == 1 || on == 2) ? on : 0;
+  return SMG_OK;
+}
+
+int smg_debug_wide_impl(int32_t which) {
+  SMG_CHECK_ARG(which == 0 || which == 1, "wide pass must be 0 (ion_wide_kernel) or 1 (ion_wide_join_kernel)");
+  g_wide_impl = which;
   return SMG_OK;
 }
 

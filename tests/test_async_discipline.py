@@ -2,8 +2,8 @@
 register with a load in flight before its counted wait, on any control-flow path, and no such register is spilled
 (scripts/check_async_regs.py).  CPU-only: compiles the kernels to assembly.
 
-* ion_wide_kernel and the big-ion pass (ion_pipe_kernel<1024>) use compiler-tracked loads only: no asynchronous
-  load at all.
+* ion_wide_kernel, ion_wide_join_kernel and the big-ion pass (ion_pipe_kernel<1024>) use compiler-tracked loads
+  only: no asynchronous load at all.
 * the main pass (ion_pipe_kernel<512>) keeps its asynchronous loads: zero violations.  Its two
   wave-0 loads (scheduling ticket, ion descriptor; tagged "smg:wave0") are waited by wave 0 only; paths that skip
   that wait through an exec-zero branch (the other waves, which issued no such load) are reported as guarded, and
@@ -36,7 +36,7 @@ def test_async_load_registers_are_never_touched_in_flight(tmp_path):
     asm = str(tmp_path / "smg_metrics.s")
     subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "--cuda-device-only",
                     "-S", src, "-o", asm], check=True, capture_output=True)
-    for kern in ("_ZN3smg15ion_wide_kernelILi0E", "_ZN3smg15ion_pipe_kernelILi0ELi1024"):
+    for kern in ("_ZN3smg15ion_wide_kernelILi0E", "_ZN3smg20ion_wide_join_kernel", "_ZN3smg15ion_pipe_kernelILi0ELi1024"):
         n_loads, n_bad, n_guarded, out = _check(asm, kern)
         assert (n_loads, n_bad, n_guarded) == (0, 0, 0), out
     n_loads, n_bad, n_guarded, out = _check(asm, "_ZN3smg15ion_pipe_kernelILi0ELi512")

@@ -227,20 +227,24 @@ def test_forced_two_level_matches_oracle(name):
 
 
 @pytest.mark.parametrize("name", CASES)
-@pytest.mark.parametrize("mode", [1, 2])
-def test_forced_dense_matches_oracle(name, mode):
+@pytest.mark.parametrize("mode,impl", [(1, 1), (1, 0), (2, 1)])
+def test_forced_dense_matches_oracle(name, mode, impl):
     """Every case again with every ion on the dense path (smg_debug_force_dense): mode 1 = the rank-indexed wide
-    pass where the image fits it (with the clip too; its rejects on the pixel-indexed kernel), mode 2 = the pixel-indexed
-    kernel alone (sparse scatter into the slot's pixel-sized images, owner lists, candidate-only chaos)."""
+    pass where the image fits it (with the clip too; its rejects on the pixel-indexed kernel) -- impl 1 its join
+    variant (ion_wide_join_kernel, packed hits without the clip; the default), impl 0 ion_wide_kernel everywhere
+    (smg_debug_wide_impl) --, mode 2 = the pixel-indexed kernel alone (sparse scatter into the slot's pixel-sized
+    images, owner lists, candidate-only chaos)."""
     from sm_distributed_amd import _lib
     ds, ions, ppm, kw, imgs, df, _, _, _, _ = _run_case(name)
     L = _lib.lib()
     L.smg_debug_force_dense(mode)
+    L.smg_debug_wide_impl(impl)
     try:
         _, m, _, _ = _device_run(ds, ions, ppm, **kw)
         _, m2, _, _ = _device_run(ds, ions, ppm, **kw)  # a second launch: slots start clean every launch
     finally:
         L.smg_debug_force_dense(0)
+        L.smg_debug_wide_impl(1)
     has = (m["flags"] & 1) != 0
     assert ((m["flags"][has] & 2) != 0).all()
     wide = (m["flags"] & 0x20) != 0

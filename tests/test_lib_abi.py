@@ -38,6 +38,7 @@ def test_version_and_argument_errors_without_gpu():
     assert b"gfx950" in L.smg_version()
     assert L.smg_version().decode().startswith(f"smg {sm_distributed_amd.__version__} ")  # one version
     assert L.smg_debug_main_kernel(2) == -1 and L.smg_debug_main_kernel(1) == 0
+    assert L.smg_debug_wide_impl(2) == -1 and L.smg_debug_wide_impl(1) == 0
     sz = ctypes.c_size_t(0)
     assert L.smg_ion_metrics_workspace_size(10, 0, 5, ctypes.byref(sz)) == -1  # bad shape -> SMG_ERR_INVALID
     assert b"bad arguments" in L.smg_last_error()
