@@ -23,6 +23,8 @@ a = sys.argv[1:]
 W = int(a[0]) if a else 8
 nrows, ncols, pk, n_sf = (int(a[1]), int(a[2]), float(a[3]), int(a[4])) if len(a) >= 5 else (500, 500, 2000.0, 20000)
 ppm = 2.0
+if os.environ.get("WIDE_IMPL"):  # 1 = ion_wide_join_kernel (default), 0 = ion_wide_kernel (A/B)
+    _lib.lib().smg_debug_wide_impl(int(os.environ["WIDE_IMPL"]))
 CONFIG5 = os.environ.get("CONFIG") == "5"
 if CONFIG5:
     nrows, ncols, pk, n_sf = 1000, 1000, 5000.0, 40000

@@ -3996,13 +3996,14 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
 //     statistics of PD's pixels;
 //  2. the tail stream of ion_wide_kernel; a lane parks its first two hits on principal pixels in registers, later
 //     ones go to a list in the slot; flagged tail points into the LT table (+ the slot's table) for Σy²;
-//  3. the chaos screen, per principal pixel p walked from the bitmap (per-wave work lists in the LT table's space):
-//     from presence rows r-4 .. r+4 it lists the candidates on p's 4-cross (as ion_wide_kernel) and marks p needed
-//     when a candidate lies within p's 5x5 (corners excluded: the reach of a candidate's eL);
-//  4. a hash (JH) over the dead bitmap / rank / LT space holds the needed pixels and the tail hits' pixels; a second
-//     stream over the principal window fills each entry's x (an unflagged point's value, a flagged pixel's PD sum);
-//  5. the hits' Σxy and Σy[x>0] from JH; each candidate's eL from its 5x5's levels through JH; Kruskal as in
-//     ion_wide_kernel (candidate bitmap + ranks over the bitmap's space, arrays in the slot).
+//  3. the chaos screen of ion_wide_kernel per principal pixel, the pixels walked from the bitmap (every DNW-th word
+//     per wave, per-wave work lists in the LT table's space, no barrier); candidates listed in the slot;
+//  4. a hash (JH) over the dead bitmap / rank / LT space holds the tail hits' pixels and every candidate's 5x5 minus
+//     its corners (images of up to 12,288 pixels index x by pixel instead); a second stream over the principal
+//     window fills each entry's x (an unflagged point's value, a flagged pixel's PD sum; 0 without a point);
+//  5. the hits' Σxy and Σy[x>0] from JH; JH's x replaced by levels; each candidate's eL from its 5x5; Kruskal as in
+//     ion_wide_kernel (candidate bitmap + ranks over the bitmap's space) with its arrays and union-find in the LDS
+//     (up to WJ_LK candidates, else in the slot), visiting only the levels some candidate has.
 // An ion whose tables overflow goes to the pixel-indexed kernel (rej_list), as from ion_wide_kernel.
 // LDS (fixed, WJ_LDS): [bitmap n64p*8][superblock bases][group prefixes][LT 12 KB] ... [PD at the end];
 // JH = keys (u32) then x (f64), WJ_JH entries over [0, PD); images of up to WJ_JH * 12 / 8 pixels index x by pixel
@@ -4010,8 +4011,10 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
 // LT table leave (1024 .. 8192 entries: 1024 at 2^20 pixels, 8192 on small images, whose flagged pixels can be many).
 constexpr size_t WJ_LDS = 160 * 1024 - 4096;  // dynamic LDS of the join pass (static arrays ~3 KB)
 constexpr int WJ_JH_LOG2 = 13;
-constexpr int WJ_JH = 1 << WJ_JH_LOG2;       // needed + hit pixels per ion
+constexpr int WJ_JH = 1 << WJ_JH_LOG2;       // hit pixels and candidates' neighbourhoods per ion
 constexpr int WJ_WL = 128;                   // per-wave work list entries (principal pixels of the screen)
+constexpr int WJ_LK = 1024;                  // candidates whose eL / Kruskal arrays stay in the LDS
+static_assert(WJ_LK * 9 <= WIDE_LT * 12 && WJ_LK * 5 <= 1024 * 12, "Kruskal arrays in LT, eL lists in PD");
 static_assert(DNW * WJ_WL * 4 <= WIDE_LT * 12, "work lists in the LT space");
 
 __host__ __device__ static inline size_t wj_lt_off(int npx) {  // offset of the LT table: bitmap, sb, pf before it
@@ -4019,15 +4022,20 @@ __host__ __device__ static inline size_t wj_lt_off(int npx) {  // offset of the 
   return n64p * 8 + ((((n64 + 1023) / 1024) * 4 + 15) & ~(size_t)15) + (((n64p / 4) * 2 + 15) & ~(size_t)15);
 }
 struct WjGeom {
-  bool jdirect;  // x by pixel
-  int pd_log2;   // PD entries (log2)
+  bool jdirect;   // x by pixel (over the bitmap's space)
+  bool jafter;    // JH after the bitmap (over the LT table's space): the bitmap stays live while JH is filled
+  int pd_log2;    // PD entries (log2)
+  size_t jh_off;  // JH's offset
   size_t pd_off;
 };
 __host__ __device__ static inline WjGeom wj_geom(int npx) {
   WjGeom g;
-  g.jdirect = (size_t)npx * 8 <= (size_t)WJ_JH * 12;
-  const size_t lt_end = wj_lt_off(npx) + (size_t)WIDE_LT * 12, jh = g.jdirect ? (size_t)npx * 8 : (size_t)WJ_JH * 12;
-  const size_t used = lt_end > jh ? lt_end : jh;
+  const size_t lt_off = wj_lt_off(npx), lt_end = lt_off + (size_t)WIDE_LT * 12, jhb = (size_t)WJ_JH * 12;
+  g.jdirect = (size_t)npx * 8 <= jhb;
+  g.jafter = !g.jdirect && lt_off + jhb + (size_t)12 * 1024 <= WJ_LDS;
+  g.jh_off = g.jafter ? lt_off : 0;
+  const size_t jh_end = g.jdirect ? (size_t)npx * 8 : g.jh_off + jhb;
+  const size_t used = lt_end > jh_end ? lt_end : jh_end;
   const size_t room = used < WJ_LDS ? WJ_LDS - used : 0;
   g.pd_log2 = 0;
   while (g.pd_log2 < 13 && ((size_t)12 << (g.pd_log2 + 1)) <= room) ++g.pd_log2;
@@ -4038,6 +4046,31 @@ __host__ __device__ static inline WjGeom wj_geom(int npx) {
 static inline bool wide_join_fits(int npx) {
   return ((size_t)npx + 63) / 64 <= (size_t)DNW * 1024 && wj_geom(npx).pd_log2 >= 10 &&
          wj_lt_off(npx) + (size_t)WIDE_LT * 12 <= wj_geom(npx).pd_off;
+}
+
+// union-find over LDS parents (the join pass's Kruskal): find with path halving, unite the larger root under the smaller
+__device__ __forceinline__ uint32_t luf_find(uint32_t* par, uint32_t x) {
+  volatile uint32_t* vp = par;
+  while (true) {
+    const uint32_t p = vp[x];
+    if (p == x) return x;
+    const uint32_t g = vp[p];
+    if (g != p) vp[x] = g;
+    x = g;
+  }
+}
+__device__ __forceinline__ bool luf_unite(uint32_t* par, uint32_t a, uint32_t b) {
+  while (true) {
+    a = luf_find(par, a);
+    b = luf_find(par, b);
+    if (a == b) return false;
+    if (a < b) {
+      const uint32_t t = a;
+      a = b;
+      b = t;
+    }
+    if (atomicCAS(&par[a], a, b) == a) return true;
+  }
 }
 
 // open-addressing u32 -> slot hash in LDS (empty WIDE_EMPTY): the slot of key or of its insertion (-1: full)
@@ -4099,9 +4132,11 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
   __shared__ int sh_ncand;   // screened chaos candidates (listed in S.epr)
   __shared__ int sh_anyfl;   // the tail stream met a flagged point
   __shared__ int sh_nov;     // tail hits beyond the registers (listed in the slot)
-  __shared__ int sh_need;    // needed principal pixels (listed in S.par)
   __shared__ int sh_anyhit;  // some lane parked a hit
   __shared__ int sh_rs;      // the hit list overflowed on an image with x by pixel: the tail is streamed again
+  __shared__ uint32_t sh_lvm[8];  // the candidates' eL values (bit e)
+  __shared__ int sh_K;       // the ion's windows, first window, principal bounds (fetched during the previous ion)
+  __shared__ int64_t sh_w0, sh_a0, sh_b0;
   __shared__ double sh_st[5];  // principal sums: x, x^2, x[x > 0], #(x > 0); max
   __shared__ int64_t sh_tb[MAXK_DENSE + 1];
   __shared__ int64_t sh_tlo[MAXK_DENSE];
@@ -4120,16 +4155,16 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
   const int pd_log2 = G.pd_log2, npd = 1 << pd_log2;
   uint32_t* pdkey = reinterpret_cast<uint32_t*>(lds + G.pd_off);
   double* pdval = reinterpret_cast<double*>(pdkey + npd);
-  uint32_t* wlist = ltkey + wid * WJ_WL;  // the screen's work lists (LT space)
   // JH (after the screen), or x by pixel on small images
-  const bool jdirect = G.jdirect;
-  uint32_t* jkey = reinterpret_cast<uint32_t*>(lds);
-  double* jx = reinterpret_cast<double*>(lds + (jdirect ? (size_t)0 : (size_t)WJ_JH * 4));
+  const bool jdirect = G.jdirect, jafter = G.jafter;
+  uint32_t* jkey = reinterpret_cast<uint32_t*>(lds + G.jh_off);
+  double* jx = reinterpret_cast<double*>(lds + (jdirect ? (size_t)0 : G.jh_off + (size_t)WJ_JH * 4));
   auto jslot = [&](uint32_t p) -> int { return jdirect ? (int)p : wj_find(jkey, WJ_JH_LOG2, p); };
   const RankBits R{bm, pf, sb};
   WideSlot S = wide_slot(scratch + (size_t)blockIdx.x * slot_bytes, npx);
   uint64_t* ovh = reinterpret_cast<uint64_t*>(S.vals);  // tail hits beyond the registers (their windows in S.L)
-  uint32_t* need = S.par;                               // needed principal pixels
+  const PresenceBits<true> pres{bm32};
+  uint32_t* wlist = ltkey + wid * WJ_WL;  // the screen's per-wave work lists (LT space)
   const uint32_t total = *count;
   for (int i = tid; i < WIDE_HT; i += DBLOCK) {
     S.hkey[i] = WIDE_EMPTY;
@@ -4145,40 +4180,84 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
   }
   slot_sync();
   const int nr = P.nrows, nc = P.ncols;
+  STAMP_DECL();
+  // the next ion (ticket, list entry, windows, principal bounds) is fetched by thread 0 one dependent load per phase
+  // of the current ion, so that the chain's round trips overlap its streams; nst = the last stage done
+  // (thread 0's state in the LDS: registers held across the ion by every lane would spill)
+  __shared__ uint32_t nx_k;
+  __shared__ int nx_ion, nx_st;
+  __shared__ int64_t nx_w0, nx_w1, nx_a0, nx_b0;
+  auto nx_start = [&]() {
+    nx_k = atomicAdd(next, 1u);
+    nx_ion = -1;
+    nx_w0 = nx_w1 = nx_a0 = nx_b0 = 0;
+    nx_st = 0;
+  };
+  auto nx_step = [&]() {
+    const int st = nx_st;
+    if (st == 0) {
+      const uint32_t k = nx_k;
+      nx_ion = k < total ? (int)list[k] : -1;
+    } else if (st == 1) {
+      const int i = nx_ion;
+      if (i >= 0) {
+        nx_w0 = ion_off[i];
+        nx_w1 = ion_off[i + 1];
+      }
+    } else if (st == 2) {
+      const int64_t w = nx_w0;
+      if (nx_ion >= 0 && nx_w1 > w) {
+        nx_a0 = lo[w];
+        nx_b0 = hi[w];
+      }
+    }
+    nx_st = st < 3 ? st + 1 : 3;
+  };
+  auto nx_publish = [&]() {
+    while (nx_st < 3) nx_step();
+    sh_ion = nx_ion;
+    sh_w0 = nx_w0;
+    sh_K = (int)(nx_w1 - nx_w0);
+    sh_a0 = nx_a0;
+    sh_b0 = nx_b0;
+  };
+  if (tid == 0) {
+    nx_start();
+    nx_publish();
+  }
 
   while (true) {
     if (tid == 0) {
-      const uint32_t k = atomicAdd(next, 1u);
-      sh_ion = (k < total) ? (int)list[k] : -1;
       sh_ctr[0] = sh_ctr[1] = sh_ctr[2] = sh_ctr[3] = 0;
       sh_nown = 0;
       sh_ncand = 0;
       sh_anyfl = 0;
       sh_nov = 0;
-      sh_need = 0;
       sh_anyhit = 0;
       sh_rs = 0;
     }
     __syncthreads();
     const int64_t ion = sh_ion;
     if (ion < 0) break;
-    const int64_t w0 = ion_off[ion];
-    const int K = (int)(ion_off[ion + 1] - w0);
+    const int64_t w0 = sh_w0, a0 = sh_a0, b0 = sh_b0;
+    const int K = sh_K;
+    if (tid == 0) nx_start();
     uint32_t flags = SMG_ION_DENSE | SMG_ION_WIDE;
-    for (int k = 0; k < K && k < MAXK_DENSE; ++k)
-      if (hi[w0 + k] > lo[w0 + k]) flags |= SMG_ION_HAS_HITS;
     if (K > MAXK_DENSE || K == 0) {
+      for (int k = 0; k < K && k < MAXK_DENSE; ++k)
+        if (hi[w0 + k] > lo[w0 + k]) flags |= SMG_ION_HAS_HITS;
       if (tid == 0) {
         oc[ion] = osp[ion] = osc[ion] = omsm[ion] = 0.0;
         oflags[ion] = (K == 0) ? 0u : (flags | 0x80000000u);
+        nx_publish();
       }
       __syncthreads();
       continue;
     }
+    STAMP(15);
     // ---- 1. principal image: presence bits, statistics, flagged pixels summed in PD ----------------------------
     for (int w = tid; w < n64p; w += DBLOCK) bm[w] = 0ull;
     __syncthreads();
-    const int64_t a0 = lo[w0], b0 = hi[w0];
     double acc[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // Σx, Σx², Σx[x>0], #(x>0), #pixels
     double mx = -INFINITY;
     auto stat = [&](double v) {
@@ -4219,6 +4298,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
         }
       }
     }
+    if (tid == 0) nx_step();
     __syncthreads();
     for (int s = tid; s < npd; s += DBLOCK)
       if (pdkey[s] != WIDE_EMPTY) stat(pdval[s]);
@@ -4234,6 +4314,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
         sh_st[4] = vmax;
       }
     }
+    STAMP(10);
     // ---- 2. tail windows (ion_wide_kernel's packed stream; hits parked, none gathered) -------------------------
     constexpr int64_t TSTEP = (int64_t)DBLOCK * TDU;
     if (tid < 4 * MAXK_DENSE) kst[tid] = 0.0;
@@ -4347,6 +4428,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
       batch(v0 + TSTEP, rB, kB, rA, kA);
     }
     if (nev > 0) sh_anyhit = 1;
+    if (tid == 0) nx_step();
     __syncthreads();
     // flagged tail points summed per (window, pixel): LDS table, then the slot's table; (Σy)² of each entry into Σy²
     const int nd = min(sh_ctr[2], WIDE_DL);
@@ -4420,6 +4502,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
       if (tid == 0) {
         const uint32_t r = atomicAdd(rej_count, 1u);
         if (r < rej_cap) rej_list[r] = (uint32_t)ion;
+        nx_publish();
       }
       for (int s = tid; s < npd; s += DBLOCK) {
         pdkey[s] = WIDE_EMPTY;
@@ -4428,58 +4511,63 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
       __syncthreads();
       continue;
     }
+    STAMP(12);
     // ---- 3. chaos screen per principal pixel, walked from the bitmap -------------------------------------------
     const double npos = sh_st[3];
     const bool chaos_ok = (sh_st[0] > 0.0) && (npos >= 4.0);
     if (chaos_ok) {
-      // uniform call: candidates on p's 4-cross (listed by the first principal pixel on their cross, as in
-      // ion_wide_kernel) and whether a candidate lies within p's 5x5 minus its corners, from presence rows r-4 .. r+4
+      // uniform call: the candidates on p's 4-cross, each listed by the first principal pixel on its cross (as in
+      // ion_wide_kernel), from presence rows r-3 .. r+3
       auto screen_px = [&](bool act, int p) {
+#ifdef SMG_STAMPS
+        {
+          const uint64_t am = __ballot(act);
+          if (lane == 0) {
+            atomicAdd(&_sacc[0], 1ull);
+            atomicAdd(&_sacc[1], (unsigned long long)__popcll(am));
+          }
+        }
+#endif
         uint32_t cm = 0u;
-        bool nd_ = false;
         int r0 = 0, c0 = 0;
         if (act) {
           rowcol(p, P, r0, c0);
-          uint32_t B[9], IM[9];
-          uint32_t imc = 0x1FFu;  // columns c0-4 .. c0+4 inside the image
-          if (c0 - 4 < 0) imc &= 0x1FFu << (uint32_t)(4 - c0);
-          if (c0 + 4 >= nc) imc &= 0x1FFu >> (uint32_t)(c0 + 4 - (nc - 1));
+          uint32_t B[7], IM[7];
+          uint32_t imc = 0x7Fu;  // columns c0-3 .. c0+3 inside the image
+          if (c0 - 3 < 0) imc &= 0x7Fu << (uint32_t)(3 - c0);
+          if (c0 + 3 >= nc) imc &= 0x7Fu >> (uint32_t)(c0 + 3 - (nc - 1));
           int cnt = 0;
 #pragma unroll
-          for (int k = 0; k < 9; ++k) {
-            B[k] = wj_row9(bm32, r0 + k - 4, c0, nr, nc);
-            IM[k] = (r0 + k - 4 >= 0 && r0 + k - 4 < nr) ? imc : 0u;
+          for (int k = 0; k < 7; ++k) {
+            B[k] = pres.row7(r0 + k - 3, c0, nr, nc);
+            IM[k] = (r0 + k - 3 >= 0 && r0 + k - 3 < nr) ? imc : 0u;
             cnt += __popc(B[k]);
           }
           // a candidate's 3x3 box is covered by 4-crosses of principal pixels only if >= 3 of them lie in its 5x5
           if (P.erosion_border || cnt >= 3) {
-            uint32_t Eh[9], E[9];
+            uint32_t Eh[7];
 #pragma unroll
-            for (int k = 1; k <= 7; ++k) {  // D = dilate_cross(presence) (valid columns 1..7), its 3-wide erosion
+            for (int k = 1; k <= 5; ++k) {
               const uint32_t d = B[k] | (B[k] << 1) | (B[k] >> 1) | B[k - 1] | B[k + 1];
-              const uint32_t dm = (P.erosion_border ? (d | ~IM[k]) : (d & IM[k])) & 0x1FFu;
-              Eh[k] = dm & (dm << 1) & (dm >> 1);  // (valid columns 2..6)
+              const uint32_t dm = (P.erosion_border ? (d | ~IM[k]) : (d & IM[k])) & 0x7Fu;
+              Eh[k] = dm & (dm << 1) & (dm >> 1);
             }
-#pragma unroll
-            for (int k = 2; k <= 6; ++k) E[k] = Eh[k - 1] & Eh[k] & Eh[k + 1] & IM[k];  // candidates, rows r-2 .. r+2
-            nd_ = (((E[2] | E[6]) & 0x38u) | ((E[3] | E[4] | E[5]) & 0x7Cu)) != 0u;
+            auto Ebit = [&](int k, int j) -> uint32_t { return (Eh[k - 1] & Eh[k] & Eh[k + 1] & IM[k]) >> j & 1u; };
             auto prb = [&](int k, int j) -> uint32_t { return (B[k] >> j) & 1u; };
 #pragma unroll
             for (int t = 0; t < 5; ++t) {
               const int qr = (t == 1) ? -1 : (t == 2) ? 1 : 0, qc = (t == 3) ? -1 : (t == 4) ? 1 : 0;
-              const int wr = qr + 4, wc = qc + 4;
+              const int wr = qr + 3, wc = qc + 3;
               int orr = 9, occ = 9;  // the first principal pixel among q-nc, q-1, q, q+1, q+nc must be p
               if (prb(wr + 1, wc)) orr = 1, occ = 0;
               if (prb(wr, wc + 1)) orr = 0, occ = 1;
               if (prb(wr, wc)) orr = 0, occ = 0;
               if (prb(wr, wc - 1)) orr = 0, occ = -1;
               if (prb(wr - 1, wc)) orr = -1, occ = 0;
-              if (qr + orr == 0 && qc + occ == 0 && ((E[wr] >> wc) & 1u)) cm |= 1u << t;
+              if (qr + orr == 0 && qc + occ == 0 && Ebit(wr, wc)) cm |= 1u << t;
             }
           }
         }
-        const int ni = wave_append(nd_, &sh_need);
-        if (nd_) need[ni] = (uint32_t)p;  // (each principal pixel once: at most np <= npx entries)
         const int cnt = __popc(cm);
         const int incl = wave_incl_scan_dpp(cnt);
         int wbase = 0;
@@ -4494,11 +4582,13 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
           cm &= cm - 1u;
         }
       };
-      // each wave walks 64 bitmap words (4096 pixels) at a time: a lane pops its word's bits one per round into the
-      // wave's list, which is screened 64 entries (one per lane) at a time
+      // each wave takes every DNW-th bitmap word (lane j of wave w: word c0 + j * DNW + w), so that a blob's rows are
+      // spread over all waves; a lane pops its word's bits one per round into the wave's list, which is screened 64
+      // entries (one per lane) at a time.  No barrier: the candidates' stores stay in flight until the slot_sync
+      // after the walk.
       int wn = 0;  // listed entries (uniform)
-      for (int w0w = wid * WAVE; w0w < n64; w0w += DBLOCK) {
-        const int w = w0w + lane;
+      for (int c0 = 0; c0 < n64; c0 += DBLOCK) {
+        const int w = c0 + lane * DNW + wid;
         uint64_t bits = w < n64 ? bm[w] : 0ull;
         while (true) {
           const bool has = bits != 0ull;
@@ -4525,25 +4615,40 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
       __builtin_amdgcn_wave_barrier();
       if (wn > 0) screen_px(lane < wn, lane < wn ? (int)wlist[lane] : 0);
     }
-    slot_sync();  // (candidates and needed pixels listed in L2; every bitmap reader done)
+    if (tid == 0) nx_step();
+    slot_sync();  // (candidates listed in L2; every bitmap reader done)
     const int nscr = chaos_ok ? min(sh_ncand, npx) : 0;
-    const int nneed = chaos_ok ? min(sh_need, npx) : 0;
+    STAMP(8);
     // ---- 4. JH over the dead bitmap / rank / LT space: the needed and the hit pixels, x from a second stream ----
     const int nov = min(sh_nov, npx);
     const bool rs = sh_rs != 0;
     const bool anyhit = sh_anyhit != 0 || nov > 0 || rs;
-    if (anyhit || nneed > 0 || nscr > 0) {
+    if (anyhit || nscr > 0) {
       if (jdirect) {
         for (int i = tid; i < npx; i += DBLOCK) jx[i] = 0.0;
       } else {
-        for (int i = tid; i < WJ_JH; i += DBLOCK) jkey[i] = WIDE_EMPTY;
+        for (int i = tid; i < WJ_JH; i += DBLOCK) {
+          jkey[i] = WIDE_EMPTY;
+          jx[i] = 0.0;  // (pixels of a candidate's neighbourhood without a point keep x = 0)
+        }
         __syncthreads();
         if (nev > 0 && wj_insert(jkey, WJ_JH_LOG2, H::pix(ev0)) < 0) sh_ctr[3] = 1;
         if (nev > 1 && wj_insert(jkey, WJ_JH_LOG2, H::pix(ev1)) < 0) sh_ctr[3] = 1;
         for (int j = tid; j < nov; j += DBLOCK)
           if (wj_insert(jkey, WJ_JH_LOG2, H::pix(ld_agent(&ovh[j]))) < 0) sh_ctr[3] = 1;
-        for (int j = tid; j < nneed; j += DBLOCK)
-          if (wj_insert(jkey, WJ_JH_LOG2, ld_agent(&need[j])) < 0) sh_ctr[3] = 1;
+        // every candidate's 5x5 minus its corners (what its eL reads), in the image (and present, while the bitmap
+        // lives: JH after it)
+        for (int j = tid; j < nscr * 21; j += DBLOCK) {
+          const int i = j / 21, o = j - i * 21;
+          const int oo = o + (o >= 18 ? 3 : o >= 3 ? 2 : 1);  // offsets 1..3, 5..19, 21..23 of 0..24
+          const int dr = oo / 5 - 2, dc = oo % 5 - 2;
+          int r0, c0;
+          rowcol((int)ld_agent(&S.epr[i]), P, r0, c0);
+          const int rr = r0 + dr, cc = c0 + dc;
+          if (rr >= 0 && rr < nr && cc >= 0 && cc < nc && (!jafter || pres.test((uint32_t)(rr * nc + cc))) &&
+              wj_insert(jkey, WJ_JH_LOG2, (uint32_t)(rr * nc + cc)) < 0)
+            sh_ctr[3] = 1;
+        }
       }
       __syncthreads();
       for (int64_t i0 = a0; i0 < b0; i0 += (int64_t)DBLOCK * WDU) {
@@ -4571,6 +4676,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
         }
       }
       __syncthreads();
+      STAMP(11);
       // ---- 5a. the hits' Σxy and Σy[x>0] -----------------------------------------------------------------------
       auto hit = [&](uint64_t h, int kb) {
         const int s = jslot(H::pix(h));
@@ -4602,10 +4708,31 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
         }
       }
     }
+    STAMP(13);
     // ---- 5b. eL of every screened candidate from its 5x5's levels (absent pixels: level 0), then Kruskal --------
+    // Up to WJ_LK candidates keep their arrays in the LDS: eL in discovery order over PD's space (dead after the join
+    // stream), the arrays by rank over the LT space (JH is dead by then), union-find with LDS atomics; more go to
+    // the slot.  Kruskal visits only the levels some candidate has (sh_lvm).
     double chaos_raw = NAN;
     if (chaos_ok && !sh_ctr[3]) {
       const double vmax = sh_st[4];
+      const bool lk = nscr <= WJ_LK;
+      uint32_t* lepix = pdkey;  // (PD: >= WJ_LK * 12 B)
+      uint8_t* leL = reinterpret_cast<uint8_t*>(pdkey + WJ_LK);
+      uint32_t* lepr = ltkey;   // (LT: 12 KB)
+      uint32_t* lpar = ltkey + WJ_LK;
+      uint8_t* leLr = reinterpret_cast<uint8_t*>(ltkey + 2 * WJ_LK);
+      if (tid < 8) sh_lvm[tid] = 0u;
+      if (nscr > 0) {  // every entry's x replaced by its level, once (the hits are done with x)
+        __syncthreads();
+        if (jdirect) {
+          for (int i = tid; i < npx; i += DBLOCK) jx[i] = (double)level_fast(jx[i], vmax, P);
+        } else {
+          for (int i = tid; i < WJ_JH; i += DBLOCK)
+            if (jkey[i] != WIDE_EMPTY) jx[i] = (double)level_fast(jx[i], vmax, P);
+        }
+        __syncthreads();
+      }
       for (int i0 = 0; i0 < nscr; i0 += DBLOCK) {
         const int i = i0 + tid;
         const int q = (i < nscr) ? (int)ld_agent(&S.epr[i]) : -1;
@@ -4616,7 +4743,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
           auto lev = [&](int rr, int cc) -> int {  // level of pixel (rr, cc); 0 outside the image or absent
             if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) return 0;
             const int s = jslot((uint32_t)(rr * nc + cc));
-            return s >= 0 ? level_fast(jx[s], vmax, P) : 0;
+            return s >= 0 ? (int)jx[s] : 0;
           };
           int Lv[5][5];
 #pragma unroll
@@ -4642,44 +4769,71 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
         }
         const int idx = wave_append(e >= 1, &sh_ctr[0]);
         if (e >= 1) {
-          S.epix[idx] = (uint32_t)q;
-          S.eL[idx] = (uint8_t)e;
-          atomicMax(&sh_ctr[1], e);
+          if (lk) {
+            lepix[idx] = (uint32_t)q;
+            leL[idx] = (uint8_t)e;
+          } else {
+            S.epix[idx] = (uint32_t)q;
+            S.eL[idx] = (uint8_t)e;
+          }
+          atomicOr(&sh_lvm[(e >> 5) & 7], 1u << (e & 31));
         }
       }
-      slot_sync();
+      if (lk) __syncthreads();
+      else slot_sync();
+      STAMP(14);
       const int m = sh_ctr[0];
-      const int emax = sh_ctr[1];
       double esum = 0.0, wsum = 0.0;
-      for (int i = tid; i < m; i += DBLOCK) esum += (double)S.eL[i];
+      for (int i = tid; i < m; i += DBLOCK) esum += (double)(lk ? leL[i] : S.eL[i]);
       if (m > 0) {  // Kruskal over the candidates, indexed by their rank in a candidate bitmap (ion_wide_kernel's)
         for (int w = tid; w < n64p; w += DBLOCK) bm[w] = 0ull;
         __syncthreads();
         for (int i = tid; i < m; i += DBLOCK) {
-          const uint32_t q = S.epix[i];
+          const uint32_t q = lk ? lepix[i] : S.epix[i];
           atomicOr(&bm32[q >> 5], 1u << (q & 31));
         }
         __syncthreads();
         build_rank(bm, pf, sb, n64, sc);
         for (int i = tid; i < m; i += DBLOCK) {
-          const uint32_t q = S.epix[i];
+          const uint32_t q = lk ? lepix[i] : S.epix[i];
           const uint32_t k = R.rank(q);
-          S.epr[k] = q;
-          S.eLr[k] = S.eL[i];
-          S.par[k] = k;
+          if (lk) {
+            lepr[k] = q;
+            leLr[k] = leL[i];
+            lpar[k] = k;
+          } else {
+            S.epr[k] = q;
+            S.eLr[k] = S.eL[i];
+            S.par[k] = k;
+          }
         }
-        slot_sync();
-        for (int t = emax; t >= 1; --t) {
+        if (lk) __syncthreads();
+        else slot_sync();
+        uint32_t lvm[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) lvm[j] = sh_lvm[j];
+        for (int t = 255; t >= 1; --t) {  // (uniform: the levels some candidate has, from the highest)
+          const int wj = t >> 5;
+          const uint32_t word = wj == 7 ? lvm[7] : wj == 6 ? lvm[6] : wj == 5 ? lvm[5] : wj == 4 ? lvm[4] :
+                                wj == 3 ? lvm[3] : wj == 2 ? lvm[2] : wj == 1 ? lvm[1] : lvm[0];
+          const uint32_t below = word & ((2u << (t & 31)) - 1u);  // levels <= t in this word (bit 31: 2u << 31 = 0 -> ~0)
+          if (below == 0u) {  // none at or below t in this word: jump to the word's start
+            t = wj * 32;
+            continue;
+          }
+          t = wj * 32 + 31 - __clz(below);  // the highest present level <= t
+          if (t < 1) break;
           for (int i = tid; i < m; i += DBLOCK) {
-            const int e = S.eLr[i];
+            const int e = lk ? leLr[i] : S.eLr[i];
             if (e < t) continue;
-            const int p = (int)S.epr[i];
+            const int p = (int)(lk ? lepr[i] : S.epr[i]);
             const int r = p / nc, c = p - r * nc;
             auto edge = [&](int q) {
               if (!R.test((uint32_t)q)) return;
               const uint32_t kq = R.rank((uint32_t)q);
-              const int eq = S.eLr[kq];
-              if ((e < eq ? e : eq) == t && guf_unite(S.par, (uint32_t)i, kq)) wsum += (double)t;
+              const int eq = lk ? leLr[kq] : S.eLr[kq];
+              if ((e < eq ? e : eq) == t && (lk ? luf_unite(lpar, (uint32_t)i, kq) : guf_unite(S.par, (uint32_t)i, kq)))
+                wsum += (double)t;
             };
             if (c + 1 < nc) edge(p + 1);
             if (r + 1 < nr) {
@@ -4710,7 +4864,11 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
       pdkey[s] = WIDE_EMPTY;
       pdval[s] = 0.0;
     }
+    bool hh = b0 > a0;
+    for (int j = 0; j < K - 1; ++j) hh = hh || sh_tn[j] > 0;
+    if (hh) flags |= SMG_ION_HAS_HITS;
     if (tid == 0) {
+      nx_publish();
       if (over) {  // JH or a list overflowed after the tail: the pixel-indexed kernel scores this ion
         const uint32_t r = atomicAdd(rej_count, 1u);
         if (r < rej_cap) rej_list[r] = (uint32_t)ion;
@@ -4723,6 +4881,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
     }
     __syncthreads();
   }
+  STAMP_FLUSH();
 }
 
 __global__ void list_all_kernel(uint32_t* list, uint32_t* count, const int64_t* ion_order, int64_t n) {
