@@ -54,7 +54,8 @@ names = {10: "pass1+rank", 11: "pass2+stats", 12: "tail windows", 13: "levels", 
          9: "screen: erode+list", 14: "candidates exact eL", 15: "kruskal+finalize+fetch"}
 if os.environ.get("WIDE_IMPL", "1") == "1" and not CLIP:  # ion_wide_join_kernel's phases
     names = {10: "principal stream+stats", 12: "tail windows", 8: "screen (bitmap walk)", 11: "JH + join stream",
-             13: "hits", 14: "candidates exact eL", 15: "kruskal+finalize+fetch"}
+             13: "hits", 14: "candidates exact eL", 9: "kruskal",
+             15: "finalize+cleanup+next ion"}
 tot = sum(buf[i] for i in names)
 for i, nm in names.items():
     print(f"  {nm:20s} {buf[i]/max(nw,1):10.0f} cycles/ion  {100*buf[i]/max(tot,1):5.1f}%")

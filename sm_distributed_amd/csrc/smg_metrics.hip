@@ -4001,7 +4001,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_kernel(
 //  4. a hash (JH) over the dead bitmap / rank / LT space holds the tail hits' pixels and every candidate's 5x5 minus
 //     its corners (images of up to 12,288 pixels index x by pixel instead); a second stream over the principal
 //     window fills each entry's x (an unflagged point's value, a flagged pixel's PD sum; 0 without a point);
-//  5. the hits' Σxy and Σy[x>0] from JH; JH's x replaced by levels; each candidate's eL from its 5x5; Kruskal as in
+//  5. the hits' Σxy and Σy[x>0] from JH; each candidate's eL from its 5x5's levels; Kruskal as in
 //     ion_wide_kernel (candidate bitmap + ranks over the bitmap's space) with its arrays and union-find in the LDS
 //     (up to WJ_LK candidates, else in the slot), visiting only the levels some candidate has.
 // An ion whose tables overflow goes to the pixel-indexed kernel (rej_list), as from ion_wide_kernel.
@@ -4135,6 +4135,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
   __shared__ int sh_anyhit;  // some lane parked a hit
   __shared__ int sh_rs;      // the hit list overflowed on an image with x by pixel: the tail is streamed again
   __shared__ uint32_t sh_lvm[8];  // the candidates' eL values (bit e)
+  __shared__ double sh_th[MAXK_DENSE];  // the ion's theoretical intensities (read during the tail, used by finalize)
   __shared__ int sh_K;       // the ion's windows, first window, principal bounds (fetched during the previous ion)
   __shared__ int64_t sh_w0, sh_a0, sh_b0;
   __shared__ double sh_st[5];  // principal sums: x, x^2, x[x > 0], #(x > 0); max
@@ -4235,6 +4236,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
       sh_nov = 0;
       sh_anyhit = 0;
       sh_rs = 0;
+      for (int j = 0; j < 8; ++j) sh_lvm[j] = 0u;
     }
     __syncthreads();
     const int64_t ion = sh_ion;
@@ -4328,6 +4330,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
       }
     }
     __syncthreads();
+    if (tid < K) sh_th[tid] = theor[w0 + tid];
     if (tid < K - 1) {
       const double2 ws = window_sums<SMG_HITS_PACKED_F32>(hits, cum, lo[w0 + 1 + tid], hi[w0 + 1 + tid]);
       kst[1 * MAXK_DENSE + tid + 1] = ws.x;
@@ -4582,13 +4585,14 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
           cm &= cm - 1u;
         }
       };
-      // each wave takes every DNW-th bitmap word (lane j of wave w: word c0 + j * DNW + w), so that a blob's rows are
-      // spread over all waves; a lane pops its word's bits one per round into the wave's list, which is screened 64
-      // entries (one per lane) at a time.  No barrier: the candidates' stores stay in flight until the slot_sync
-      // after the walk.
+      // each wave takes one word of every DNW (lane j of wave w: word c0 + j * DNW + ((w + j) mod DNW): a permutation
+      // within each group, so the lanes' 8-byte reads spread over the LDS banks), so that a blob's rows are spread
+      // over all waves; a lane pops its word's bits one per round into the wave's list, which is screened 64 entries
+      // (one per lane) at a time.  No barrier: the candidates' stores stay in flight until the slot_sync after the
+      // walk.
       int wn = 0;  // listed entries (uniform)
       for (int c0 = 0; c0 < n64; c0 += DBLOCK) {
-        const int w = c0 + lane * DNW + wid;
+        const int w = c0 + lane * DNW + ((wid + lane) & (DNW - 1));
         uint64_t bits = w < n64 ? bm[w] : 0ull;
         while (true) {
           const bool has = bits != 0ull;
@@ -4722,17 +4726,6 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
       uint32_t* lepr = ltkey;   // (LT: 12 KB)
       uint32_t* lpar = ltkey + WJ_LK;
       uint8_t* leLr = reinterpret_cast<uint8_t*>(ltkey + 2 * WJ_LK);
-      if (tid < 8) sh_lvm[tid] = 0u;
-      if (nscr > 0) {  // every entry's x replaced by its level, once (the hits are done with x)
-        __syncthreads();
-        if (jdirect) {
-          for (int i = tid; i < npx; i += DBLOCK) jx[i] = (double)level_fast(jx[i], vmax, P);
-        } else {
-          for (int i = tid; i < WJ_JH; i += DBLOCK)
-            if (jkey[i] != WIDE_EMPTY) jx[i] = (double)level_fast(jx[i], vmax, P);
-        }
-        __syncthreads();
-      }
       for (int i0 = 0; i0 < nscr; i0 += DBLOCK) {
         const int i = i0 + tid;
         const int q = (i < nscr) ? (int)ld_agent(&S.epr[i]) : -1;
@@ -4743,7 +4736,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
           auto lev = [&](int rr, int cc) -> int {  // level of pixel (rr, cc); 0 outside the image or absent
             if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) return 0;
             const int s = jslot((uint32_t)(rr * nc + cc));
-            return s >= 0 ? (int)jx[s] : 0;
+            return s >= 0 ? level_fast(jx[s], vmax, P) : 0;
           };
           int Lv[5][5];
 #pragma unroll
@@ -4853,6 +4846,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
     } else if (!chaos_ok) {
       flags |= SMG_ION_CHAOS_NAN;
     }
+    STAMP(9);
     __syncthreads();  // (the hits' kst sums; every JH and LT-space reader done)
     const bool over = sh_ctr[3] != 0;
     // the LT space (work lists, JH) and PD back to empty for the next ion
@@ -4875,7 +4869,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
       } else {
         kst[0] = sh_st[2];
         kst[1 * MAXK_DENSE] = kst[2 * MAXK_DENSE] = kst[3 * MAXK_DENSE] = 0.0;
-        finalize_ion(K, theor + w0, kst, sh_st[0], sh_st[1], kst + MAXK_DENSE, kst + 2 * MAXK_DENSE,
+        finalize_ion(K, sh_th, kst, sh_st[0], sh_st[1], kst + MAXK_DENSE, kst + 2 * MAXK_DENSE,
                      kst + 3 * MAXK_DENSE, (double)npx, chaos_raw, ion, flags, oc, osp, osc, omsm, oflags);
       }
     }
