@@ -622,7 +622,7 @@ def pass_roofline(args, pass_ms, chain, is_single):
     ms_charged = dom["ms_avg"] + fin_ms
     ach = ALG_BYTES_PER_POINT * dom["window_points"] / (ms_charged * 1e-3) / 1e9
     key = {1: "ion_pipe_kernel[512]" if legacy_main else "ion_sparse_kernel", 2: "ion_pipe_kernel[1024]",
-           3: "ion_wide_kernel", 4: "ion_dense_kernel"}
+           3: "ion_wide_join_kernel", 4: "ion_dense_kernel"}  # (no clip here: the wide pass is the join kernel)
     traffic, src = measured_traffic(key[dom["pass"]], "config5" if args.config == "5" else "config3") \
         if is_single else (None, None)
     roofline = {"bound": "hbm", "kernel": name, "achieved": ach, "peak": HBM_PEAK_GBS,

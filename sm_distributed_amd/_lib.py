@@ -25,7 +25,7 @@ SMG_HITS_SPLIT_F64 = 1
 # pass ids of smg_debug_pass_times
 SMG_PASS_DESC, SMG_PASS_MAIN, SMG_PASS_BIG, SMG_PASS_WIDE, SMG_PASS_DENSE, SMG_PASS_FINALIZE = range(6)
 PASS_NAMES = {0: "ion_desc8_kernel", 1: "ion_sparse_kernel (main LDS pass)",
-              2: "ion_pipe_kernel<1024> (big-ion LDS pass)", 3: "ion_wide_kernel (wide pass)",
+              2: "ion_pipe_kernel<1024> (big-ion LDS pass)", 3: "ion_wide_join_kernel (wide pass; ion_wide_kernel with the clip)",
               4: "ion_dense_kernel (pixel-indexed pass)", 5: "ion_finalize_kernel (LDS passes' scores)"}
 
 # every symbol include/smg.h declares, with its ctypes prototype
