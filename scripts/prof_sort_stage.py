@@ -1,0 +1,26 @@
+"""Diagnostic: the config-3 flag + sort + scan stage alone (DevicePeaks.flag_and_sort + prefix_sums, as the
+search runs it), 10 times after a warm-up, for rocprofv3 --kernel-trace --stats: per-kernel times of the stage.
+Also prints the stage's wall time per repetition (events around it)."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from sm_distributed_amd import engine as E, synthetic as syn
+
+ions = syn.make_ion_table(200, seed=43, decoy_seed=44)
+mz, hits, dims, info = syn.make_dataset_torch(500, 500, 2000.0, seed=42, device="cuda", ions=ions)
+peaks = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
+for _ in range(2):
+    peaks.flag_and_sort(2.0)
+    peaks.prefix_sums()
+torch.cuda.synchronize()
+ts = []
+for _ in range(10):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    peaks.flag_and_sort(2.0)
+    peaks.prefix_sums()
+    e1.record()
+    torch.cuda.synchronize()
+    ts.append(e0.elapsed_time(e1))
+ts.sort()
+print(f"{peaks.n_points:,} points: flag+sort+scan min {ts[0]:.3f} median {ts[len(ts)//2]:.3f} ms", flush=True)

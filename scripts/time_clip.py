@@ -29,7 +29,11 @@ def timed(reps=3, **kw):
 
 
 t_n, _ = timed()
+CFD = int(os.environ.get("CLIP_FORCE_DENSE", "0"))  # the clipped run on the dense path (1: wide pass, 2: pixel kernel)
+if CFD:
+    _lib.lib().smg_debug_force_dense(CFD)
 t_c, g = timed(do_preprocessing=True, q=q)
+_lib.lib().smg_debug_force_dense(0)
 cols = ("chaos", "spatial", "spectral", "msm")
 ref = os.path.join("gpurun_out", "clip_ref.npz")
 if os.path.exists(ref):
@@ -40,4 +44,4 @@ else:
     np.savez(ref, **{c: g[c] for c in cols})
     note = "reference"
 print(f"{os.path.basename(_lib.LIB_PATH)} {nrows}x{ncols}: normal {t_n:.2f} ms, clip q{q:g} {t_c:.2f} ms = "
-      f"{t_c / t_n:.2f}x ({note})", flush=True)
+      f"{t_c / t_n:.2f}x ({note}; clipped run forced dense {CFD})", flush=True)
