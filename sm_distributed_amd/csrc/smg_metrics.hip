@@ -4084,6 +4084,20 @@ __device__ __forceinline__ int wj_insert(uint32_t* keys, int cap_log2, uint32_t 
   }
   return -1;
 }
+__device__ __forceinline__ uint32_t wj_hash(uint32_t key, int cap_log2) { return (key * 0x9E3779B1u) >> (32 - cap_log2); }
+// wj_find with the first probe's slot h and key k0 already read
+__device__ __forceinline__ int wj_find_from(const uint32_t* keys, int cap_log2, uint32_t key, uint32_t h, uint32_t k0) {
+  if (k0 == key) return (int)h;
+  if (k0 == WIDE_EMPTY) return -1;
+  const int cap = 1 << cap_log2;
+  for (int t = 1; t < cap; ++t) {
+    h = (h + 1) & (uint32_t)(cap - 1);
+    const uint32_t k = keys[h];
+    if (k == key) return (int)h;
+    if (k == WIDE_EMPTY) return -1;
+  }
+  return -1;
+}
 __device__ __forceinline__ int wj_find(const uint32_t* keys, int cap_log2, uint32_t key) {
   const int cap = 1 << cap_log2;
   uint32_t h = (key * 0x9E3779B1u) >> (32 - cap_log2);
@@ -4096,23 +4110,29 @@ __device__ __forceinline__ int wj_find(const uint32_t* keys, int cap_log2, uint3
   return -1;
 }
 
-// presence bits of columns c0-4 .. c0+4 of row r from the LDS bitmap (bit j = column c0-4+j; 0 outside the image);
-// one zero word follows the bitmap
-__device__ __forceinline__ uint32_t wj_row9(const uint32_t* w, int r, int c0, int nr, int nc) {
-  if (r < 0 || r >= nr) return 0u;
-  const int lc = c0 - 4;
-  const int64_t g = (int64_t)r * nc + lc;
-  uint32_t v;
-  if (g >= 0) {
-    const int wi = (int)(g >> 5);
-    v = __builtin_amdgcn_alignbit(w[wi + 1], w[wi], (uint32_t)(g & 31));
-  } else {
-    v = w[0] << (uint32_t)(-g);
+// presence bits of columns c0-3 .. c0+3 of rows r0-3 .. r0+3 from the LDS bitmap (B[k]: row r0+k-3, bit j = column
+// c0-3+j; 0 outside the image), branch-free: the 14 words are read together (one wait), then aligned and masked.
+// One zero word follows the bitmap.
+__device__ __forceinline__ void wj_rows7(const uint32_t* w, int r0, int c0, int nr, int nc, uint32_t (&B)[7]) {
+  uint32_t lo[7], hi[7];
+  int g[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const int rr = r0 + k - 3;
+    g[k] = (rr >= 0 && rr < nr) ? rr * nc + c0 - 3 : 0;
+    const int wi = (g[k] > 0 ? g[k] : 0) >> 5;
+    lo[k] = w[wi];
+    hi[k] = w[wi + 1];
   }
-  uint32_t cm = 0x1FFu;
-  if (lc < 0) cm &= 0x1FFu << (uint32_t)(-lc);
-  if (c0 + 4 >= nc) cm &= 0x1FFu >> (uint32_t)(c0 + 4 - (nc - 1));
-  return v & cm;
+  uint32_t cm = 0x7Fu;  // columns inside the image
+  if (c0 - 3 < 0) cm &= 0x7Fu << (uint32_t)(3 - c0);
+  if (c0 + 3 >= nc) cm &= 0x7Fu >> (uint32_t)(c0 + 3 - (nc - 1));
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const int rr = r0 + k - 3;
+    const uint32_t v = g[k] >= 0 ? __builtin_amdgcn_alignbit(hi[k], lo[k], (uint32_t)(g[k] & 31)) : lo[k] << (uint32_t)(-g[k]);
+    B[k] = (rr >= 0 && rr < nr) ? (v & cm) : 0u;
+  }
 }
 
 __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
@@ -4533,6 +4553,9 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
 #endif
         uint32_t cm = 0u;
         int r0 = 0, c0 = 0;
+#ifdef SMG_WJ_ABL  // diagnostic (timing only, wrong chaos): the walk without the screen itself
+        act = act && (SMG_WJ_ABL == 0);
+#endif
         if (act) {
           rowcol(p, P, r0, c0);
           uint32_t B[7], IM[7];
@@ -4540,9 +4563,9 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
           if (c0 - 3 < 0) imc &= 0x7Fu << (uint32_t)(3 - c0);
           if (c0 + 3 >= nc) imc &= 0x7Fu >> (uint32_t)(c0 + 3 - (nc - 1));
           int cnt = 0;
+          wj_rows7(bm32, r0, c0, nr, nc, B);
 #pragma unroll
           for (int k = 0; k < 7; ++k) {
-            B[k] = pres.row7(r0 + k - 3, c0, nr, nc);
             IM[k] = (r0 + k - 3 >= 0 && r0 + k - 3 < nr) ? imc : 0u;
             cnt += __popc(B[k]);
           }
@@ -4662,12 +4685,19 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
           const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
           r[u] = hits.load(i < b0 ? i : b0 - 1);
         }
+        // every point's first probe read together (one wait), then the rare collisions probed on
+        uint32_t h0[WDU], k0[WDU];
+#pragma unroll
+        for (int u = 0; u < WDU; ++u) {
+          h0[u] = jdirect ? H::pix(r[u]) : wj_hash(H::pix(r[u]), WJ_JH_LOG2);
+          k0[u] = jdirect ? 0u : jkey[h0[u]];
+        }
 #pragma unroll
         for (int u = 0; u < WDU; ++u) {
           const int64_t i = i0 + (int64_t)u * DBLOCK + tid;
           if (i < b0) {
             const uint32_t p = H::pix(r[u]);
-            const int s = jslot(p);
+            const int s = jdirect ? (int)p : wj_find_from(jkey, WJ_JH_LOG2, p, h0[u], k0[u]);
             if (s >= 0) {
               double x = H::val(r[u]);
               if (H::dup(r[u])) {
@@ -4733,17 +4763,36 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
         if (q >= 0) {
           int r0, c0;
           rowcol(q, P, r0, c0);
-          auto lev = [&](int rr, int cc) -> int {  // level of pixel (rr, cc); 0 outside the image or absent
-            if (rr < 0 || rr >= nr || cc < 0 || cc >= nc) return 0;
-            const int s = jslot((uint32_t)(rr * nc + cc));
-            return s >= 0 ? level_fast(jx[s], vmax, P) : 0;
-          };
+          // the levels of q's 5x5 minus corners (0 outside the image or absent): the 21 first probes read together,
+          // then the rare collisions probed on, then the 21 values read together
           int Lv[5][5];
+          uint32_t pk[5][5], ph[5][5], pv[5][5];
+          int ps[5][5];
+#pragma unroll
+          for (int a = 0; a < 5; ++a)
+#pragma unroll
+            for (int b = 0; b < 5; ++b) {
+              const int rr = r0 + a - 2, cc = c0 + b - 2;
+              const bool in = rr >= 0 && rr < nr && cc >= 0 && cc < nc && !((a == 0 || a == 4) && (b == 0 || b == 4));
+              pk[a][b] = in ? (uint32_t)(rr * nc + cc) : WIDE_EMPTY;
+              ph[a][b] = jdirect ? (in ? pk[a][b] : 0u) : wj_hash(pk[a][b], WJ_JH_LOG2);
+              pv[a][b] = jdirect ? 0u : jkey[ph[a][b]];
+            }
 #pragma unroll
           for (int a = 0; a < 5; ++a)
 #pragma unroll
             for (int b = 0; b < 5; ++b)
-              Lv[a][b] = ((a == 0 || a == 4) && (b == 0 || b == 4)) ? 0 : lev(r0 + a - 2, c0 + b - 2);
+              ps[a][b] = pk[a][b] == WIDE_EMPTY ? -1 : jdirect ? (int)ph[a][b] :
+                         wj_find_from(jkey, WJ_JH_LOG2, pk[a][b], ph[a][b], pv[a][b]);
+          double xv[5][5];
+#pragma unroll
+          for (int a = 0; a < 5; ++a)
+#pragma unroll
+            for (int b = 0; b < 5; ++b) xv[a][b] = ps[a][b] >= 0 ? jx[ps[a][b]] : 0.0;
+#pragma unroll
+          for (int a = 0; a < 5; ++a)
+#pragma unroll
+            for (int b = 0; b < 5; ++b) Lv[a][b] = ps[a][b] >= 0 ? level_fast(xv[a][b], vmax, P) : 0;
           e = 1 << 20;
 #pragma unroll
           for (int a = -1; a <= 1; ++a)
@@ -4778,7 +4827,62 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
       const int m = sh_ctr[0];
       double esum = 0.0, wsum = 0.0;
       for (int i = tid; i < m; i += DBLOCK) esum += (double)(lk ? leL[i] : S.eL[i]);
-      if (m > 0) {  // Kruskal over the candidates, indexed by their rank in a candidate bitmap (ion_wide_kernel's)
+      if (m > 0 && lk && m <= WAVE) {
+        // up to 64 candidates: wave 0 alone, one candidate per lane, its forward neighbours found in a 128-slot
+        // pixel hash over the LT space (JH is dead), the levels in sequence without a block barrier
+        if (wid == 0) {
+          uint32_t* hk = ltkey;           // 128 keys
+          uint32_t* hv = ltkey + 2 * WAVE;  // their candidate indices
+          uint32_t* lp = ltkey + 4 * WAVE;  // union-find parents
+          hk[lane] = WIDE_EMPTY;
+          hk[lane + WAVE] = WIDE_EMPTY;
+          __builtin_amdgcn_wave_barrier();
+          const bool mine = lane < m;
+          const uint32_t q = mine ? lepix[lane] : 0u;
+          const int e = mine ? (int)leL[lane] : 0;
+          if (mine) {
+            const int h = wj_insert(hk, 7, q);
+            hv[h] = (uint32_t)lane;  // (distinct candidates: the table has room for all)
+            lp[lane] = (uint32_t)lane;
+          }
+          __builtin_amdgcn_wave_barrier();
+          const int r = mine ? (int)q / nc : 0, c = mine ? (int)q - r * nc : 0;
+          auto nbr = [&](bool ok, int qq) -> int {  // candidate index of pixel qq, -1 if none
+            if (!ok) return -1;
+            const int h = wj_find(hk, 7, (uint32_t)qq);
+            return h >= 0 ? (int)hv[h] : -1;
+          };
+          // the forward neighbours (right, down, and with 8-connectivity down-left, down-right), found once
+          const int n0 = nbr(mine && c + 1 < nc, (int)q + 1);
+          const int n1 = nbr(mine && r + 1 < nr, (int)q + nc);
+          const int n2 = nbr(mine && P.connectivity == 8 && r + 1 < nr && c > 0, (int)q + nc - 1);
+          const int n3 = nbr(mine && P.connectivity == 8 && r + 1 < nr && c + 1 < nc, (int)q + nc + 1);
+          const int e0 = n0 >= 0 ? (int)leL[n0] : 0, e1 = n1 >= 0 ? (int)leL[n1] : 0;
+          const int e2 = n2 >= 0 ? (int)leL[n2] : 0, e3 = n3 >= 0 ? (int)leL[n3] : 0;
+          uint32_t lvm[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) lvm[j] = sh_lvm[j];
+          for (int t = 255; t >= 1; --t) {  // (uniform: the levels some candidate has, from the highest)
+            const int wj = t >> 5;
+            const uint32_t word = wj == 7 ? lvm[7] : wj == 6 ? lvm[6] : wj == 5 ? lvm[5] : wj == 4 ? lvm[4] :
+                                  wj == 3 ? lvm[3] : wj == 2 ? lvm[2] : wj == 1 ? lvm[1] : lvm[0];
+            const uint32_t below = word & ((2u << (t & 31)) - 1u);
+            if (below == 0u) {
+              t = wj * 32;
+              continue;
+            }
+            t = wj * 32 + 31 - __clz(below);
+            if (t < 1) break;
+            if (mine && e >= t) {
+              if (n0 >= 0 && min(e, e0) == t && luf_unite(lp, (uint32_t)lane, (uint32_t)n0)) wsum += (double)t;
+              if (n1 >= 0 && min(e, e1) == t && luf_unite(lp, (uint32_t)lane, (uint32_t)n1)) wsum += (double)t;
+              if (n2 >= 0 && min(e, e2) == t && luf_unite(lp, (uint32_t)lane, (uint32_t)n2)) wsum += (double)t;
+              if (n3 >= 0 && min(e, e3) == t && luf_unite(lp, (uint32_t)lane, (uint32_t)n3)) wsum += (double)t;
+            }
+            __builtin_amdgcn_wave_barrier();
+          }
+        }
+      } else if (m > 0) {  // Kruskal over the candidates, indexed by their rank in a candidate bitmap (ion_wide_kernel's)
         for (int w = tid; w < n64p; w += DBLOCK) bm[w] = 0ull;
         __syncthreads();
         for (int i = tid; i < m; i += DBLOCK) {
