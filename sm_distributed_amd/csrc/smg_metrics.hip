@@ -4014,6 +4014,7 @@ constexpr int WJ_JH_LOG2 = 13;
 constexpr int WJ_JH = 1 << WJ_JH_LOG2;       // hit pixels and candidates' neighbourhoods per ion
 constexpr int WJ_WL = 128;                   // per-wave work list entries (principal pixels of the screen)
 constexpr int WJ_LK = 1024;                  // candidates whose eL / Kruskal arrays stay in the LDS
+constexpr int WJ_LC = (WIDE_LT * 12 - DNW * WJ_WL * 4) / 4;  // candidates staged in the LT space behind the work lists
 static_assert(WJ_LK * 9 <= WIDE_LT * 12 && WJ_LK * 5 <= 1024 * 12, "Kruskal arrays in LT, eL lists in PD");
 static_assert(DNW * WJ_WL * 4 <= WIDE_LT * 12, "work lists in the LT space");
 
@@ -4186,6 +4187,10 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
   uint64_t* ovh = reinterpret_cast<uint64_t*>(S.vals);  // tail hits beyond the registers (their windows in S.L)
   const PresenceBits<true> pres{bm32};
   uint32_t* wlist = ltkey + wid * WJ_WL;  // the screen's per-wave work lists (LT space)
+  // the first WJ_LC candidates also staged behind the work lists where JH does not cover that space (large images)
+  uint32_t* lcand = ltkey + DNW * WJ_WL;
+  const bool cand_lds = !G.jdirect && !G.jafter && wj_lt_off(npx) + (size_t)DNW * WJ_WL * 4 >= (size_t)WJ_JH * 12;
+  auto cand = [&](int i) -> uint32_t { return cand_lds && i < WJ_LC ? lcand[i] : ld_agent(&S.epr[i]); };
   const uint32_t total = *count;
   for (int i = tid; i < WIDE_HT; i += DBLOCK) {
     S.hkey[i] = WIDE_EMPTY;
@@ -4603,7 +4608,9 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
         while (cm != 0u) {
           const int t = __ffs(cm) - 1;
           const int qr = (t == 1) ? -1 : (t == 2) ? 1 : 0, qc = (t == 3) ? -1 : (t == 4) ? 1 : 0;
-          if (idx < npx) S.epr[idx] = (uint32_t)((r0 + qr) * nc + c0 + qc);
+          const uint32_t qq = (uint32_t)((r0 + qr) * nc + c0 + qc);
+          if (idx < npx) S.epr[idx] = qq;
+          if (cand_lds && idx < WJ_LC) lcand[idx] = qq;
           ++idx;
           cm &= cm - 1u;
         }
@@ -4670,7 +4677,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
           const int oo = o + (o >= 18 ? 3 : o >= 3 ? 2 : 1);  // offsets 1..3, 5..19, 21..23 of 0..24
           const int dr = oo / 5 - 2, dc = oo % 5 - 2;
           int r0, c0;
-          rowcol((int)ld_agent(&S.epr[i]), P, r0, c0);
+          rowcol((int)cand(i), P, r0, c0);
           const int rr = r0 + dr, cc = c0 + dc;
           if (rr >= 0 && rr < nr && cc >= 0 && cc < nc && (!jafter || pres.test((uint32_t)(rr * nc + cc))) &&
               wj_insert(jkey, WJ_JH_LOG2, (uint32_t)(rr * nc + cc)) < 0)
@@ -4758,7 +4765,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
       uint8_t* leLr = reinterpret_cast<uint8_t*>(ltkey + 2 * WJ_LK);
       for (int i0 = 0; i0 < nscr; i0 += DBLOCK) {
         const int i = i0 + tid;
-        const int q = (i < nscr) ? (int)ld_agent(&S.epr[i]) : -1;
+        const int q = (i < nscr) ? (int)cand(i) : -1;
         int e = 0;
         if (q >= 0) {
           int r0, c0;
