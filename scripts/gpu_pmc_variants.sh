@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 TAG=${1:-pmcv}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-CTRS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES"
+CTRS=${CTRS:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES"}
 for so in sm_distributed_amd/libsmg.so $(ls sm_distributed_amd/variants/*.so 2>/dev/null); do
   n=$(basename $so .so)
   rm -rf /tmp/pv_$n
