@@ -4014,7 +4014,7 @@ constexpr int WJ_JH_LOG2 = 13;
 constexpr int WJ_JH = 1 << WJ_JH_LOG2;       // hit pixels and candidates' neighbourhoods per ion
 constexpr int WJ_WL = 128;                   // per-wave work list entries (principal pixels of the screen)
 constexpr int WJ_LK = 1024;                  // candidates whose eL / Kruskal arrays stay in the LDS
-constexpr int WJ_LC = (WIDE_LT * 12 - DNW * WJ_WL * 4) / 4;  // candidates staged in the LT space behind the work lists
+static_assert(DNW * (WJ_WL + WAVE) * 4 <= WIDE_LT * 12, "work and survivor lists in the LT space");
 static_assert(WJ_LK * 9 <= WIDE_LT * 12 && WJ_LK * 5 <= 1024 * 12, "Kruskal arrays in LT, eL lists in PD");
 static_assert(DNW * WJ_WL * 4 <= WIDE_LT * 12, "work lists in the LT space");
 
@@ -4187,10 +4187,8 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
   uint64_t* ovh = reinterpret_cast<uint64_t*>(S.vals);  // tail hits beyond the registers (their windows in S.L)
   const PresenceBits<true> pres{bm32};
   uint32_t* wlist = ltkey + wid * WJ_WL;  // the screen's per-wave work lists (LT space)
-  // the first WJ_LC candidates also staged behind the work lists where JH does not cover that space (large images)
-  uint32_t* lcand = ltkey + DNW * WJ_WL;
-  const bool cand_lds = !G.jdirect && !G.jafter && wj_lt_off(npx) + (size_t)DNW * WJ_WL * 4 >= (size_t)WJ_JH * 12;
-  auto cand = [&](int i) -> uint32_t { return cand_lds && i < WJ_LC ? lcand[i] : ld_agent(&S.epr[i]); };
+  uint32_t* slist = ltkey + DNW * WJ_WL + wid * WAVE;  // the screen's per-wave survivor lists (LT space)
+  auto cand = [&](int i) -> uint32_t { return ld_agent(&S.epr[i]); };
   const uint32_t total = *count;
   for (int i = tid; i < WIDE_HT; i += DBLOCK) {
     S.hkey[i] = WIDE_EMPTY;
@@ -4610,10 +4608,37 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
           const int qr = (t == 1) ? -1 : (t == 2) ? 1 : 0, qc = (t == 3) ? -1 : (t == 4) ? 1 : 0;
           const uint32_t qq = (uint32_t)((r0 + qr) * nc + c0 + qc);
           if (idx < npx) S.epr[idx] = qq;
-          if (cand_lds && idx < WJ_LC) lcand[idx] = qq;
           ++idx;
           cm &= cm - 1u;
         }
+      };
+      // pass A of the screen (as in ion_sparse_kernel): a principal pixel with fewer than three principal pixels in its
+      // 7x7 (itself included) cannot list a candidate (erosion border 0); the survivors (~6 % at config 5) go to the
+      // wave's survivor list, which gets the full screen (screen_px) 64 at a time, so that its ~200 instructions do not
+      // run for every list of pixels with a survivor somewhere in it
+      int sn = 0;  // survivors listed (uniform)
+      auto screen_list = [&](bool act, int p) {
+        bool sv = act;
+        if (act && !P.erosion_border) {
+          int r0, c0;
+          rowcol(p, P, r0, c0);
+          uint32_t B[7];
+          wj_rows7(bm32, r0, c0, nr, nc, B);
+          int cnt = 0;
+#pragma unroll
+          for (int k = 0; k < 7; ++k) cnt += __popc(B[k]);
+          sv = cnt >= 3;
+        }
+        const uint64_t m = __ballot(sv);
+        const int c = (int)__popcll(m);
+        if (sn + c > WAVE) {
+          __builtin_amdgcn_wave_barrier();
+          screen_px(lane < sn, lane < sn ? (int)slist[lane] : 0);
+          __builtin_amdgcn_wave_barrier();
+          sn = 0;
+        }
+        if (sv) slist[sn + (int)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)p;
+        sn += c;
       };
       // each wave takes one word of every DNW (lane j of wave w: word c0 + j * DNW + ((w + j) mod DNW): a permutation
       // within each group, so the lanes' 8-byte reads spread over the LDS banks), so that a blob's rows are spread
@@ -4636,7 +4661,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
           wn += (int)__popcll(m);
           if (wn >= WAVE) {
             __builtin_amdgcn_wave_barrier();
-            screen_px(true, (int)wlist[lane]);
+            screen_list(true, (int)wlist[lane]);
             __builtin_amdgcn_wave_barrier();
             wn -= WAVE;
             const uint32_t mv = lane < wn ? wlist[WAVE + lane] : 0u;
@@ -4647,7 +4672,9 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
         }
       }
       __builtin_amdgcn_wave_barrier();
-      if (wn > 0) screen_px(lane < wn, lane < wn ? (int)wlist[lane] : 0);
+      if (wn > 0) screen_list(lane < wn, lane < wn ? (int)wlist[lane] : 0);
+      __builtin_amdgcn_wave_barrier();
+      if (sn > 0) screen_px(lane < sn, lane < sn ? (int)slist[lane] : 0);
     }
     if (tid == 0) nx_step();
     slot_sync();  // (candidates listed in L2; every bitmap reader done)
