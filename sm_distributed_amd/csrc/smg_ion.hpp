@@ -221,6 +221,49 @@ __device__ __forceinline__ int level_fast(double v, double vmax, const Params& P
   return j + ((1.0 < norm) ? 1 : 0);
 }
 
+// the level index's f32 test: 1 (round 6) a margin of (n-1) * 1e-6 and the top interval included, 0 a margin of 1e-3
+// with the top interval sent to the f64 test (the lanes of a wave with an entry in the top interval all waited for it;
+// ion stage 25.97 -> 25.82 ms at config 3, profiles/round6/r6var4_variants.txt).  Used by ion_sparse_kernel and the
+// join wide pass's eL (ion_wide_join_kernel)
+#ifndef SMG_SP_LVM
+#define SMG_SP_LVM 1
+#endif
+
+// the exact level index (divisions, loops), kept out of line so that the loops calling sp_level stay small
+static __device__ __noinline__ int sp_level_exact(double v, double vmax, const Params& P) { return level_fast(v, vmax, P); }
+
+// level_fast(v, vmax, P) = #{i <= n-2 : i*step < v/vmax} (+ [1 < v/vmax], 0 here: v <= vmax) with the division
+// replaced by v * (1/vmax) where that cannot change the answer.  With x = (v/vmax)(n-1) non-integer, the count is
+// floor(x) + 1 (capped at n-1); the two comparisons that decide it are checked against na = v*rcp with a margin above
+// na's error (<= 2 ulp), and anything closer (or v ~ vmax) takes the exact path.  Straight-line: no loops.
+__device__ __forceinline__ int sp_level(double v, double vmax, double rcp, const Params& P) {
+  const int n = P.nlevels;
+  if (!(v > 0.0)) return 0;  // (vmax > 0 whenever levels are needed)
+  if (n == 1) return 1;
+  if (n <= 2048) {  // f32 first: x = v/vmax (n-1) to ~2.4e-7 relative, i.e. (n-1) * 2.4e-7 absolute; farther than
+                    // SMG_SP_LVM = (n-1) * 1e-6 from an integer and from n-1 itself (the top interval (n-2, n-1) is
+                    // the count n-1 like any other) it decides alone
+#if SMG_SP_LVM
+    const float xf = (float)v * (float)rcp * (float)(n - 1);
+    const float jf = floorf(xf), fr = xf - jf;
+    const float mg = (float)(n - 1) * 1e-6f;
+    if (fr > mg && fr < 1.0f - mg && xf < (float)(n - 1) - mg) return (int)jf + 1;
+#else
+    const float xf = (float)v * (float)rcp * (float)(n - 1);
+    const float jf = floorf(xf), fr = xf - jf;
+    if (fr > 1e-3f && fr < 1.0f - 1e-3f && xf < (float)(n - 1) - 1.0f) return (int)jf + 1;
+#endif
+  }
+  const double na = v * rcp;
+  const double tol = na * 1e-15;
+  int j = (int)(na * (double)(n - 1)) + 1;
+  j = j > n - 1 ? n - 1 : j;
+  const bool lo_ok = (double)(j - 1) * P.step < na - tol;
+  const bool hi_ok = j == n - 1 || (double)j * P.step >= na + tol;
+  return (na < 1.0 - 1e-12 && lo_ok && hi_ok) ? j : sp_level_exact(v, vmax, P);
+}
+
+
 // ---------------------------------------------------------------------------------------------
 // Ion descriptors: one 256-B record per position of the processing order (ion_desc_kernel), so that a
 // workgroup reaches an ion's windows with one coalesced read instead of the ion_order -> ion_off -> lo/hi

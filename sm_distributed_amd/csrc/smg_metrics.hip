@@ -4783,7 +4783,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
     // the slot.  Kruskal visits only the levels some candidate has (sh_lvm).
     double chaos_raw = NAN;
     if (chaos_ok && !sh_ctr[3]) {
-      const double vmax = sh_st[4];
+      const double vmax = sh_st[4], rcp = 1.0 / vmax;  // (x <= vmax: sp_level's domain)
       const bool lk = nscr <= WJ_LK;
       uint32_t* lepix = pdkey;  // (PD: >= WJ_LK * 12 B)
       uint8_t* leL = reinterpret_cast<uint8_t*>(pdkey + WJ_LK);
@@ -4826,7 +4826,7 @@ __global__ void __launch_bounds__(DBLOCK) ion_wide_join_kernel(
 #pragma unroll
           for (int a = 0; a < 5; ++a)
 #pragma unroll
-            for (int b = 0; b < 5; ++b) Lv[a][b] = ps[a][b] >= 0 ? level_fast(xv[a][b], vmax, P) : 0;
+            for (int b = 0; b < 5; ++b) Lv[a][b] = ps[a][b] >= 0 ? sp_level(xv[a][b], vmax, rcp, P) : 0;
           e = 1 << 20;
 #pragma unroll
           for (int a = -1; a <= 1; ++a)
