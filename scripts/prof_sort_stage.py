@@ -6,8 +6,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 from sm_distributed_amd import engine as E, synthetic as syn
 
-ions = syn.make_ion_table(200, seed=43, decoy_seed=44)
-mz, hits, dims, info = syn.make_dataset_torch(500, 500, 2000.0, seed=42, device="cuda", ions=ions)
+ions = syn.make_ion_table(int(os.environ.get("N_SF", "200")), seed=43, decoy_seed=44)  # (bench.py: 20000)
+PLANT = float(os.environ.get("PLANT", "0"))  # bench.py's dataset plants 2 % of the formulas' peaks (PLANT=0.02)
+kw = dict(plant_fraction=PLANT, plant_seed=45) if PLANT > 0 else {}
+mz, hits, dims, info = syn.make_dataset_torch(500, 500, 2000.0, seed=42, device="cuda", ions=ions, **kw)
 peaks = E.DevicePeaks.from_device(mz, hits, dims, sp_off=info["sp_off"])
 for _ in range(2):
     peaks.flag_and_sort(2.0)
@@ -23,4 +25,4 @@ for _ in range(10):
     torch.cuda.synchronize()
     ts.append(e0.elapsed_time(e1))
 ts.sort()
-print(f"{peaks.n_points:,} points: flag+sort+scan min {ts[0]:.3f} median {ts[len(ts)//2]:.3f} ms", flush=True)
+print(f"plant {PLANT}: {peaks.n_points:,} points: flag+sort+scan min {ts[0]:.3f} median {ts[len(ts)//2]:.3f} ms", flush=True)
