@@ -83,7 +83,9 @@ __device__ unsigned long long g_sp_stamps[16];
 namespace {
 
 #ifndef SMG_SP_RC
-#define SMG_SP_RC 2  // tail points per thread per chunk (four chunks in flight)
+// tail points per thread per chunk (four chunks in flight): 1 since round 6 (ion stage 25.80 -> 25.47 ms at config 3,
+// profiles/round6/r6spv2_*, r6spv3_*; 3: 26.41 ms)
+#define SMG_SP_RC 1
 #endif
 // timing ablations (wrong results; diagnostic builds only): 1 no chaos, 2 no tail stream, 4 no levels, 8 no chaos
 // pass B (no candidates), 16 no band bitmaps, 32 no chaos screen, 64 no eL / Kruskal, 128 no collision scans
