@@ -2055,18 +2055,27 @@ __global__ void __launch_bounds__(256) ion_finalize_kernel(const IonRec* __restr
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t i = t >> 3;
   const int k = (int)(t & 7);
-  const bool live = i < n && rec[i].state == 1u;
-  const IonRec* R = rec + (live ? i : 0);
-  const int K = live ? R->K : 0;
+  // every field this lane uses is read at once, before the record's state and K are known (one memory round trip
+  // rather than three; k < 8 stays inside the record's arrays)
+  const bool inr = i < n;
+  const IonRec* R = rec + (inr ? i : 0);
+  const uint32_t st = R->state;
+  const int Kr = R->K;
+  const double tk0 = R->theor[k], sk0 = R->s[k], sx = R->sx, sxx = R->sxx;
+  const double sy = R->sy[k], syy = R->syy[k], sxy = R->sxy[k];
+  const double chaos0 = R->chaos;
+  const int32_t ion0 = R->ion;
+  const uint32_t flags0 = R->flags;
+  const bool live = inr && st == 1u;
+  const int K = live ? Kr : 0;
   const bool act = live && k < K;
-  const double tk = act ? R->theor[k] : 0.0, sk = act ? R->s[k] : 0.0;
+  const double tk = act ? tk0 : 0.0, sk = act ? sk0 : 0.0;
   double rt = 0.0;  // r_k * t_k of isotope_image_correlation (k >= 1)
   if (act && k >= 1 && K >= 2) {
-    const double sx = R->sx, n1 = npx - 1.0;
-    const double sd0 = sqrt((R->sxx - sx * sx / npx) / n1);
-    const double sy = R->sy[k];
-    const double syy_c = (R->syy[k] - sy * sy / npx) / n1;
-    const double sxy_c = (R->sxy[k] - sx * sy / npx) / n1;
+    const double n1 = npx - 1.0;
+    const double sd0 = sqrt((sxx - sx * sx / npx) / n1);
+    const double syy_c = (syy - sy * sy / npx) / n1;
+    const double sxy_c = (sxy - sx * sy / npx) / n1;
     double r = sxy_c / sqrt(syy_c) / sd0;
     if (!isnan(r)) r = r > 1.0 ? 1.0 : (r < -1.0 ? -1.0 : r);
     if (isinf(r)) r = 0.0;
@@ -2074,23 +2083,27 @@ __global__ void __launch_bounds__(256) ion_finalize_kernel(const IonRec* __restr
   }
   // gather the eight lanes' terms in lane 0 of the group (window order)
   const int g0 = (threadIdx.x & 63) & ~7;
-  double T[MAXK], S[MAXK], RT[MAXK];
+  double T[MAXK], S[MAXK], RT[MAXK], D[MAXK];
 #pragma unroll
   for (int j = 0; j < MAXK; ++j) {
     T[j] = __shfl(tk, g0 + j, 64);
     S[j] = __shfl(sk, g0 + j, 64);
     RT[j] = __shfl(rt, g0 + j, 64);
   }
-  if (!live || k != 0) return;
-  // isotope_pattern_match
+  // isotope_pattern_match: every lane of the group forms the two norms (same order, same values), lane k its own
+  // term |t_k / |t| - s_k / |s||, and lane 0 sums the terms in window order
   double tt = 0.0, ss = 0.0;
   for (int j = 0; j < K; ++j) {
     tt += T[j] * T[j];
     ss += S[j] * S[j];
   }
   const double nt = sqrt(tt), ns = sqrt(ss);
+  const double dk = act ? fabs(tk / nt - sk / ns) : 0.0;
+#pragma unroll
+  for (int j = 0; j < MAXK; ++j) D[j] = __shfl(dk, g0 + j, 64);
+  if (!live || k != 0) return;
   double acc = 0.0;
-  for (int j = 0; j < K; ++j) acc += fabs(T[j] / nt - S[j] / ns);
+  for (int j = 0; j < K; ++j) acc += D[j];
   double spectral = 1.0 - acc / (double)K;
   if (spectral == 1.0) spectral = 0.0;
   double spatial = 0.0;
@@ -2102,17 +2115,17 @@ __global__ void __launch_bounds__(256) ion_finalize_kernel(const IonRec* __restr
     }
     spatial = num / den;
   }
-  double chaos = R->chaos;
+  double chaos = chaos0;
   if (!isnan(chaos) && fabs(chaos - 1.0) <= 1e-8 + 1e-5) chaos = 0.0;  // np.isclose(moc, 1.0)
   chaos = clean(chaos);
   spatial = clean(spatial);
   spectral = clean(spectral);
-  const int64_t ion = R->ion;
+  const int64_t ion = ion0;
   oc[ion] = chaos;
   osp[ion] = spatial;
   osc[ion] = spectral;
   omsm[ion] = chaos * spatial * spectral;
-  oflags[ion] = R->flags;
+  oflags[ion] = flags0;
 }
 
 // position list -> ion list (when the big-ion pass is skipped, the dense kernel reads ion indices)

@@ -482,28 +482,29 @@ __global__ void __launch_bounds__(PS_T) chunk_sums_kernel(const void* __restrict
   }
 }
 
-// exclusive scan of the chunk totals in one workgroup: each thread a run of chunks, then the thread totals
+// exclusive scan of the chunk totals in one workgroup: each thread a run of chunks, the thread totals scanned in
+// each wave (shuffles, fixed order) and across the waves (the 16 wave totals in order, in LDS)
 constexpr int PSB_T = 1024;
 __global__ void __launch_bounds__(PSB_T) chunk_base_kernel(const DD4* __restrict__ ctot, int64_t nch,
                                                            DD4* __restrict__ cbase) {
-  __shared__ DD4 tt[PSB_T];
-  const int t = threadIdx.x;
+  __shared__ DD4 wt[PSB_T / 64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t per = (nch + PSB_T - 1) / PSB_T;
   const int64_t a = t * per, b = a + per < nch ? a + per : nch;
   DD4 s{0.0, 0.0, 0.0, 0.0};
   for (int64_t i = a; i < b; ++i) s = dd4_add(s, ctot[i]);
-  tt[t] = s;
-  __syncthreads();
-  if (t == 0) {  // exclusive prefix of the thread totals, in order
-    DD4 run{0.0, 0.0, 0.0, 0.0};
-    for (int i = 0; i < PSB_T; ++i) {
-      const DD4 x = tt[i];
-      tt[i] = run;
-      run = dd4_add(run, x);
-    }
+  DD4 incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const DD4 y = dd4_shfl_up(incl, o);
+    if (lane >= o) incl = dd4_add(y, incl);
   }
+  if (lane == 63) wt[w] = incl;
   __syncthreads();
-  DD4 run = tt[t];
+  DD4 run{0.0, 0.0, 0.0, 0.0};
+  for (int i = 0; i < w; ++i) run = dd4_add(run, wt[i]);
+  const DD4 ex = dd4_shfl_up(incl, 1);
+  if (lane > 0) run = dd4_add(run, ex);
   for (int64_t i = a; i < b; ++i) {
     cbase[i] = run;
     run = dd4_add(run, ctot[i]);
