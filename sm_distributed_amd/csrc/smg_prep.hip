@@ -358,7 +358,7 @@ __device__ __forceinline__ double rows16_sum(double v) {  // every lane: the sum
   return v;
 }
 __global__ void __launch_bounds__(PS_T) chunk_sums_packed_kernel(const uint64_t* __restrict__ hits, int64_t n,
-                                                                 DD4* __restrict__ bs, DD4* __restrict__ ctot) {
+                                                                 double2* __restrict__ bs, DD4* __restrict__ ctot) {
   __shared__ DD4 wt[PS_T / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t nblk = (n + 63) >> 6;
@@ -411,7 +411,7 @@ __global__ void __launch_bounds__(PS_T) chunk_sums_packed_kernel(const uint64_t*
     }
     if (lane < BPI && blk0 + lane < nblk) {
       const DD4 d{ma, 0.0, mb, 0.0};
-      bs[blk0 + lane] = d;
+      bs[blk0 + lane] = make_double2(ma, mb);
       acc = dd4_add(acc, d);
     }
   }
@@ -434,7 +434,7 @@ __global__ void __launch_bounds__(PS_T) chunk_sums_packed_kernel(const uint64_t*
 template <int FMT>
 __global__ void __launch_bounds__(PS_T) chunk_sums_kernel(const void* __restrict__ hits,
                                                           const double* __restrict__ hit_vals, int64_t n,
-                                                          DD4* __restrict__ bs, DD4* __restrict__ ctot) {
+                                                          double2* __restrict__ bs, DD4* __restrict__ ctot) {
   __shared__ DD4 wt[PS_T / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t nblk = (n + 63) >> 6;
@@ -467,7 +467,7 @@ __global__ void __launch_bounds__(PS_T) chunk_sums_kernel(const void* __restrict
       const double a = wave_sum_dpp(v[j]), b = wave_sum_dpp(dup[j] ? 0.0 : v[j] * v[j]);
       if (lane == 0 && blk0 + j < nblk) {
         const DD4 d{a, 0.0, b, 0.0};
-        bs[blk0 + j] = d;
+        bs[blk0 + j] = make_double2(a, b);
         acc = dd4_add(acc, d);
       }
     }
@@ -513,7 +513,7 @@ __global__ void __launch_bounds__(PSB_T) chunk_base_kernel(const DD4* __restrict
 
 // each chunk's inclusive prefixes from its base: a thread scans PS_BPT consecutive blocks, the thread totals are
 // combined in order through the waves and the LDS; out[b] = sums over blocks [0, b]
-__global__ void __launch_bounds__(PS_T) chunk_scan_kernel(const DD4* __restrict__ bs, const DD4* __restrict__ cbase,
+__global__ void __launch_bounds__(PS_T) chunk_scan_kernel(const double2* __restrict__ bs, const DD4* __restrict__ cbase,
                                                           int64_t nblk, DD4* __restrict__ out) {
   __shared__ DD4 wt[PS_T / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -522,7 +522,8 @@ __global__ void __launch_bounds__(PS_T) chunk_scan_kernel(const DD4* __restrict_
   DD4 s{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int j = 0; j < PS_BPT; ++j) {
-    const DD4 x = b0 + j < nblk ? bs[b0 + j] : DD4{0.0, 0.0, 0.0, 0.0};
+    const double2 q = b0 + j < nblk ? bs[b0 + j] : make_double2(0.0, 0.0);
+    const DD4 x{q.x, 0.0, q.y, 0.0};
     s = dd4_add(s, x);
     loc[j] = s;
   }
@@ -747,7 +748,7 @@ int smg_hit_prefix_sums(int32_t hit_format, const void* hits, const double* hit_
     return SMG_ERR_UNSUPPORTED;
   }
   unsigned char* p = reinterpret_cast<unsigned char*>(workspace) + 256;
-  DD4* bs = reinterpret_cast<DD4*>(p);
+  double2* bs = reinterpret_cast<double2*>(p);  // a block's two plain f64 sums (its DD4 with zero low parts)
   p += ((size_t)nblk * sizeof(DD4) + 255) / 256 * 256;
   DD4* ctot = reinterpret_cast<DD4*>(p);
   p += ((size_t)nch * sizeof(DD4) + 255) / 256 * 256;
