@@ -63,8 +63,11 @@ def test_sparse_main_pass_async_loads(tmp_path):
         pytest.skip("hipcc not available")
     src = os.path.join(ROOT, "sm_distributed_amd", "csrc", "smg_sparse.hip")
     asm = str(tmp_path / "smg_sparse.s")
+    # the flags the library's build gives this file (Makefile SPARSE_FLAGS: its instruction scheduler)
+    flags = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "sm_distributed_amd", "csrc"), "print-sparse-flags"],
+                           check=True, capture_output=True, text=True).stdout.split()
     subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "--cuda-device-only",
-                    "-S", src, "-o", asm], check=True, capture_output=True)
+                    *flags, "-S", src, "-o", asm], check=True, capture_output=True)
     n_loads, n_bad, n_guarded, out = _check(asm, "_ZN3smg12_GLOBAL__N_117ion_sparse_kernel")
     assert n_loads > 0 and n_bad == 0 and n_guarded == 0, out
 
